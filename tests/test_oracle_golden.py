@@ -1,0 +1,124 @@
+"""Pin the CPU restatement (oracle/rfx_oracle.c) to the reference's own outputs.
+
+Every fixture in tests/golden/ was produced by the *unmodified* reference
+sources compiled by oracle/Makefile (tools/gen_golden.py).  The restatement
+must reproduce them bit-exactly: f32 framebuffer and ARGB8.  Runs on CPU.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle as orc
+from reflaxman_amd import scenes
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+MANIFEST = json.load(open(os.path.join(GOLDEN, "manifest.json")))
+CASES = MANIFEST["cases"]
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def render_oracle(c, nthreads=8):
+    r = orc.OracleRender(scenes.get_scene(c["scene"]), c["sphere_seed"], c.get("jitter_seed", 0))
+    r.set_image_size(c["W"], c["H"])
+    for _ in range(c["frames"]):
+        r.render(c["depth"], c["ss"], c["additive"], nthreads=nthreads)
+    return r.image_pixels(), r.argb()
+
+
+def test_scene_generator_unchanged(tmp_path):
+    """The scene files the goldens were made from are reproduced bit-for-bit."""
+    for name, digest in MANIFEST["scene_sha256"].items():
+        p = scenes.get_scene(name).write(str(tmp_path))
+        assert hashlib.sha256(open(p, "rb").read()).hexdigest() == digest, name
+
+
+@pytest.mark.parametrize("key", sorted(k for k, c in CASES.items() if c["kind"] == "render" and c.get("stored")))
+def test_render_bitexact(key):
+    c = CASES[key]
+    rgb, argb = render_oracle(c)
+    g = np.load(os.path.join(GOLDEN, key + ".npz"))
+    assert np.array_equal(argb, g["argb"]), f"{key}: ARGB8 differs in {(argb != g['argb']).sum()} pixels"
+    assert rgb.tobytes() == g["rgb"].tobytes(), f"{key}: f32 framebuffer differs"
+    assert sha(rgb) == c["sha_f32"] and sha(argb) == c["sha_argb"]
+
+
+@pytest.mark.parametrize("key", ["hash_default_640x480_d4", "hash_default_1920x1080_d4",
+                                 "hash_synth16_3840x2160_d8", "hash_default_3840x2160_d8"])
+def test_full_size_hash(key):
+    c = CASES[key]
+    rgb, argb = render_oracle(c, nthreads=os.cpu_count() or 8)
+    assert sha(argb) == c["sha_argb"], key
+    assert sha(rgb) == c["sha_f32"], key
+
+
+def test_appendix_b_known_answers():
+    """default 640x480 d4 hashes and pixels (row 0 = bottom)."""
+    c = CASES["hash_default_640x480_d4"]
+    assert c["sha_argb"] == "7273c1a33a8f257326c9d89c49c7e492959cbbd3170a079d228ec8ad78a0510a"
+    assert c["sha_f32"] == "e54c47f650f89432c6ce7c705eb9891ec7a799badef0c009a6557f618f73f0a9"
+    rgb, argb = render_oracle(c)
+    assert argb[0, 0] == 0x00575754 and argb[240, 320] == 0x004D4D4B and argb[479, 639] == 0x007F7F7A
+    assert argb[300, 100] == 0x00E6E6DE and argb[200, 250] == 0x001866AD
+    assert rgb[200, 250].tolist() == pytest.approx([0.0971308202, 0.398656249, 0.678708553], rel=0, abs=1e-9)
+
+
+@pytest.mark.parametrize("key", sorted(k for k, c in CASES.items() if c["kind"] == "band"))
+def test_band_bitexact(key):
+    c = CASES[key]
+    rgb, argb = orc.render_band(scenes.get_scene(c["scene"]), c["W"], c["H"], c["depth"], c["y0"], c["rows"],
+                                c["sphere_seed"], nthreads=8)
+    g = np.load(os.path.join(GOLDEN, key + ".npz"))
+    assert np.array_equal(argb, g["argb"])
+    assert rgb.tobytes() == g["rgb"].tobytes()
+
+
+def test_rand_stream():
+    g = np.load(os.path.join(GOLDEN, "kat_rand.npz"))
+    dirs, _ = orc.rand_dirs(int(g["seed"][0]), g["dirs"].shape[0])
+    assert dirs.tobytes() == g["dirs"].tobytes()
+    # Appendix B first draws
+    assert dirs[0].tolist() == pytest.approx([0.108676434, -0.350688219, -0.13675344], abs=1e-9)
+
+
+@pytest.mark.parametrize("key,kind,textured", [
+    ("kat_sphere", "sphere", False), ("kat_plane", "plane", False), ("kat_triangle", "triangle", False),
+    ("kat_triangle_tex", "triangle", True), ("kat_triangle_checker", "triangle", True)])
+def test_primitive_kats(key, kind, textured):
+    g = np.load(os.path.join(GOLDEN, key + ".npz"))
+    tex = g["tex"] if "tex" in g.files else None
+    out = orc.kat(kind, g["inp"], tex=tex, textured=textured)
+    assert out.tobytes() == g["out"].tobytes(), f"{key}: {np.argwhere(out != g['out'])[:5]}"
+    assert g["out"][:, 0].sum() > 50  # the fixture really exercises hits
+
+
+@pytest.mark.parametrize("key,kind", [("kat_skybox_checker", "skybox"), ("kat_skybox_tex", "skybox"),
+                                      ("kat_texture_checker", "texture"), ("kat_texture_tex", "texture"),
+                                      ("kat_texture_tex24", "texture")])
+def test_sampling_kats(key, kind):
+    g = np.load(os.path.join(GOLDEN, key + ".npz"))
+    tex = g["tex"] if "tex" in g.files else None
+    out = orc.kat(kind, g["inp"], tex=tex)
+    assert out.tobytes() == g["out"].tobytes()
+
+
+def test_argb_kat():
+    g = np.load(os.path.join(GOLDEN, "kat_argb.npz"))
+    assert np.array_equal(orc.argb_of(g["inp"]), g["out"])
+
+
+def test_camera_kat():
+    g = np.load(os.path.join(GOLDEN, "kat_camera.npz"))
+    out = np.stack([orc.camera_view(r[0:3], r[3:6]) for r in g["inp"]])
+    assert out.tobytes() == g["out"].tobytes()
+
+
+def test_pow_kat_is_libm():
+    """The fixture's pow values are glibc powf; numpy's float32 power is NOT used anywhere."""
+    g = np.load(os.path.join(GOLDEN, "kat_pow.npz"))
+    assert g["out"].dtype == np.float32 and g["out"].shape[0] == g["inp"].shape[0]
