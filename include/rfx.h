@@ -1,0 +1,154 @@
+/*
+ * rfx.h -- C-ABI of the MI355X-native ReflaxMan trace loop (librfx.so).
+ *
+ * The reference has no plugin/FFI layer: its path sits behind the C++ class API
+ * of Render (src/common/Render.h:7-42), Scene (Scene.h:28-40), Camera
+ * (Camera.h:30-62), Material (Material.h:5-19), OmniLight and Texture.  Each
+ * entry point below replaces one of those calls (cited per function) so a
+ * host-side shim -- include/reflaxman/ (C++ headers), reflaxman_amd/render.py
+ * (Python/ctypes), or the cgo/JNI/ctypes stubs in INTEGRATION.md -- can drop in
+ * for the reference's CPU render() call.
+ *
+ * Conventions: plain pointers and sizes only; status codes (rfx_status) instead
+ * of the reference's assert()+silent clamps; colours are float RGB; ARGB texels
+ * are uint32 0xAARRGGBB; images are row-major, row 0 = bottom (the reference's
+ * ry < 0 looks down, Render.cpp:146-156).  Device pointers are HIP device
+ * memory of the renderer's device; `stream` arguments are hipStream_t (NULL =
+ * the renderer's stream).
+ */
+#ifndef RFX_H
+#define RFX_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RFX_ABI_VERSION 1
+
+typedef enum {
+  RFX_OK = 0,
+  RFX_ERR_ARG = -1,      /* invalid argument (reference: assert + clamp/fallback) */
+  RFX_ERR_HIP = -2,      /* HIP runtime failure; rfx_last_error() has the text */
+  RFX_ERR_STATE = -3,    /* call not valid in the current state */
+  RFX_ERR_IO = -4,       /* file could not be read/written (reference returns false) */
+  RFX_ERR_RNG = -5,      /* RNG pre-pass ran short of accepted triples (never expected) */
+  RFX_ERR_NODEV = -6     /* no HIP device */
+} rfx_status;
+
+enum { RFX_METAL = 0, RFX_DIELECTRIC = 1 };  /* Material::Type (Material.h:8) */
+
+typedef struct rfx_scene rfx_scene;
+typedef struct rfx_renderer rfx_renderer;
+
+int rfx_abi_version(void);
+const char *rfx_last_error(void);
+
+/* ---------------------------------------------------------------- Scene */
+/* Scene(const Color & diffLightColor, float diffLightPower)  -- Scene.cpp:10-15 */
+rfx_scene *rfx_scene_create(float diff_r, float diff_g, float diff_b, float diff_power);
+void rfx_scene_destroy(rfx_scene *scene);
+/* Scene::addSphere(center, radius, Material(type, color, reflectivity, transparency))
+ *   -- Scene.cpp:29-39, Sphere.cpp:9-20, Material.cpp:8-14.  Returns the object index (>= 0). */
+int rfx_scene_add_sphere(rfx_scene *scene, const float center[3], float radius, int material_type,
+                         const float rgb[3], float reflectivity, float transparency);
+/* Scene::addTriangle(v1, v2, v3, material) -- Scene.cpp:41-46, Triangle.cpp:11-21.  Returns the object index. */
+int rfx_scene_add_triangle(rfx_scene *scene, const float v1[3], const float v2[3], const float v3[3],
+                           int material_type, const float rgb[3], float reflectivity, float transparency);
+/* Triangle::setTexture(texture, u1, v1, u2, v2, u3, v3) -- Triangle.cpp:110-120.  uv = {u1,v1,u2,v2,u3,v3}. */
+int rfx_triangle_set_texture(rfx_scene *scene, int object_index, int texture_index, const float uv[6]);
+/* Scene::addLight(origin, radius, color, power) -- Scene.cpp:48-59, OmniLight.cpp:8-14.  Returns the light index. */
+int rfx_scene_add_light(rfx_scene *scene, const float origin[3], float radius, const float rgb[3], float power);
+/* Scene::addTexture -- Scene.cpp:61-66, from memory: argb == NULL or w*h == 0 is the reference's failed
+ * load (empty texture -> procedural checker, Texture.cpp:242-243).  Returns the texture index. */
+int rfx_scene_add_texture_argb(rfx_scene *scene, uint32_t width, uint32_t height, const uint32_t *argb);
+/* Scene::addTexture(fileName) -- TGA loader of Texture.cpp:34-108 (type 2, 24/32 bpp).  A file that does
+ * not load yields an empty texture, as in the reference; *loaded (optional) reports success. */
+int rfx_scene_add_texture_file(rfx_scene *scene, const char *path, int *loaded);
+/* Scene::setSkyboxTexture(fileName) -- Scene.cpp:68-71, Skybox.cpp:21-37.  Returns 1 if loaded, 0 if not
+ * (checker fallback, as the reference), < 0 on error. */
+int rfx_scene_set_skybox_file(rfx_scene *scene, const char *path);
+/* same, from memory (NULL -> checker) */
+int rfx_scene_set_skybox_argb(rfx_scene *scene, uint32_t width, uint32_t height, const uint32_t *argb);
+int rfx_scene_counts(const rfx_scene *scene, int *spheres, int *triangles, int *lights, int *textures);
+
+/* ---------------------------------------------------------------- Camera */
+/* Camera(eye, at, fov): view = [ox | oy | oz] columns, row-major _11.._33 -- Camera.cpp:24-38 */
+void rfx_camera_view(const float eye[3], const float at[3], float view[9]);
+/* rz = W / 2 / tanf(fov / 2) -- Render.cpp:148 (host libm tanf, as the reference) */
+float rfx_camera_rz(uint32_t width, float fov);
+
+/* ---------------------------------------------------------------- Images & files */
+/* Texture::loadFromTGAFile -- Texture.cpp:34-108.  Call with argb == NULL to query w/h. */
+int rfx_tga_load(const char *path, uint32_t *width, uint32_t *height, uint32_t *argb, size_t capacity);
+/* Texture::saveToTGAFile / saveToBMPFile -- Texture.cpp:110-173 (32 bpp, rows as stored) */
+int rfx_tga_save(const char *path, uint32_t width, uint32_t height, const uint32_t *argb);
+int rfx_bmp_save(const char *path, uint32_t width, uint32_t height, const uint32_t *argb);
+/* Color::argb over a host float RGB image (Color.cpp:114-117) -- Render::copyImage (Render.cpp:82-101) */
+void rfx_argb_from_rgb(const float *rgb, size_t pixels, uint32_t *argb);
+
+/* ---------------------------------------------------------------- Renderer (device) */
+int rfx_renderer_create(rfx_renderer **out, int device);
+void rfx_renderer_destroy(rfx_renderer *r);
+int rfx_renderer_device(const rfx_renderer *r);
+/* launches go to this stream (hipStream_t); NULL = a stream the renderer owns */
+int rfx_renderer_set_stream(rfx_renderer *r, void *hip_stream);
+/* upload the scene (host precompute already done by the builder calls) */
+int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *scene);
+/* The reference's two LCG streams (trace_math.h:34-39): Vector3.cpp's (randomInsideSphere) and
+ * Render.cpp's (additive jitter).  Both persist across frames exactly as the reference's would. */
+int rfx_renderer_set_rng(rfx_renderer *r, uint32_t sphere_seed, uint32_t jitter_seed);
+int rfx_renderer_get_rng(rfx_renderer *r, uint32_t *sphere_seed, uint32_t *jitter_seed); /* synchronises */
+
+typedef struct {
+  float eye[3];        /* Render::renderCameraEye  (Render.cpp:128) */
+  float view[9];       /* Render::renderCameraView (Render.cpp:127), row-major */
+  float fov;           /* Camera::fov -> rz = W/2/tanf(fov/2) (Render.cpp:148) */
+  uint32_t width, height;
+  int32_t reflect_num;      /* renderBegin reflectNum (> 0) */
+  int32_t sample_num;       /* renderBegin sampleNum: >0 SSAA n x n, <0 |n| block preview, 0 invalid */
+  int32_t additive;         /* renderBegin additive */
+  int32_t additive_counter; /* Render::additiveCounter after renderBegin (Render.cpp:130-133) */
+  uint32_t row_block;       /* strip partition: rows are dealt in blocks of row_block ...   */
+  uint32_t rank, nranks;    /* ... block b belongs to rank b % nranks (nranks == 1: whole frame) */
+  uint64_t pixel_begin;     /* raster span [pixel_begin, pixel_end) of this call: the Render::renderNext */
+  uint64_t pixel_end;       /* cursor span (Render.cpp:136-215); 0, 0 = the whole frame.  nranks == 1 only */
+} rfx_frame;
+
+/* rows of `frame` that `rank` owns under the block-cyclic strip partition */
+uint32_t rfx_strip_rows(uint32_t height, uint32_t row_block, uint32_t rank, uint32_t nranks);
+/* global row of compact strip row `r` */
+uint32_t rfx_strip_row_to_y(uint32_t r, uint32_t row_block, uint32_t rank, uint32_t nranks);
+
+/*
+ * One Render::renderBegin + renderNext(W*H) pass on the device (Render.cpp:116-215 + Scene::trace,
+ * Scene.cpp:73-236): RNG pre-pass, trace kernel, ARGB epilogue, all stream-ordered, no host sync.
+ *   d_rgb  : device float RGB, strip_rows x W x 3 (read-modify-write when additive_counter > 1)
+ *   d_argb : device uint32, strip_rows x W, Color::argb of the stored value (copyImage), or NULL
+ *   d_counters : device uint64[RFX_NCOUNTERS] accumulated event counters (stats kernel), or NULL
+ */
+#define RFX_NCOUNTERS 31
+int rfx_render_frame(rfx_renderer *r, const rfx_frame *frame, float *d_rgb, uint32_t *d_argb,
+                     uint64_t *d_counters, void *stream);
+
+/* host-buffer convenience for callers without device memory of their own (PCIe-inclusive):
+ * rgb: host W*H*3 (in/out), argb: host W*H or NULL.  Partitioning fields must be rank 0 of 1. */
+int rfx_render_frame_host(rfx_renderer *r, const rfx_frame *frame, float *rgb, uint32_t *argb,
+                          uint64_t *counters);
+
+/* device memory helpers for C/C++ hosts that have no allocator of their own */
+int rfx_device_alloc(rfx_renderer *r, size_t bytes, void **dptr);
+int rfx_device_free(rfx_renderer *r, void *dptr);
+int rfx_memcpy_d2h(rfx_renderer *r, void *dst, const void *src, size_t bytes);
+int rfx_memcpy_h2d(rfx_renderer *r, void *dst, const void *src, size_t bytes);
+int rfx_synchronize(rfx_renderer *r);
+
+/* Sample the RNG stream: the first n randomInsideSphere draws from `seed` (Vector3.cpp:176-188),
+ * computed by the device pre-pass, n x 3 floats to host.  *seed_out = state after them. */
+int rfx_rand_dirs(rfx_renderer *r, uint32_t seed, uint64_t n, float *out3, uint32_t *seed_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RFX_H */

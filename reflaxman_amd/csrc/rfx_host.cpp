@@ -1,0 +1,774 @@
+// Host side of librfx.so: the C-ABI of include/rfx.h.
+//
+// Scene builder calls restate the reference's constructors (host precompute in
+// strict IEEE, shared rfx_math.h), uploads go to SoA device arrays
+// (rfx_types.h), and rfx_render_frame enqueues the RNG pre-pass + trace kernel
+// on one HIP stream without any host synchronisation.
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/rfx.h"
+#include "rfx_math.h"
+#include "rfx_types.h"
+
+#pragma clang fp contract(off)
+
+namespace rfx {
+uint64_t rng_blocks_for(uint64_t traces);
+hipError_t launch_rng(const uint32_t *d_seed, uint32_t *d_next_seed, uint64_t traces, float *d_rd, uint64_t n_rd,
+                      uint32_t *d_blk_cnt, uint64_t *d_blk_off, int *d_err, hipStream_t st);
+hipError_t launch_trace(const DevScene &S, const FrameParams &P, bool stats, hipStream_t st);
+}  // namespace rfx
+
+using namespace rfx;
+
+static thread_local std::string g_last_error;
+
+static int fail(int code, const char *fmt, ...)
+{
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  return code;
+}
+
+#define HIP_CHECK(expr)                                                                  \
+  do {                                                                                   \
+    hipError_t e_ = (expr);                                                              \
+    if (e_ != hipSuccess) return fail(RFX_ERR_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+extern "C" int rfx_abi_version(void) { return RFX_ABI_VERSION; }
+extern "C" const char *rfx_last_error(void) { return g_last_error.c_str(); }
+
+// ============================================================== scene (host)
+struct HostTexture { uint32_t w = 0, h = 0; std::vector<uint32_t> texels; };
+struct HostMat { int dielectric; float r, g, b, refl, transp; };
+struct HostSphere { v3 center; float radius, sq_radius; HostMat mat; int obj; };
+struct HostTri {
+  v3 v0, norm;
+  m33 ax, tuv;
+  float tu0 = 0, tv0 = 0;
+  int tex = -1;
+  HostMat mat;
+  int obj;
+};
+struct HostLight { v3 origin; float radius; float r, g, b, power; };
+
+struct rfx_scene {
+  col diff, env;
+  float diff_power;
+  float half_tile_w, half_tile_h;
+  int skybox = -1;
+  std::vector<HostSphere> spheres;
+  std::vector<HostTri> tris;
+  std::vector<int> obj_kind, obj_idx;  // insertion order
+  std::vector<HostLight> lights;
+  std::vector<HostTexture> textures;
+};
+
+static void default_half_tiles(rfx_scene *s)  // Skybox.cpp:5-9 / failed load :32-33
+{
+  s->half_tile_w = 1.0f / 8.0f - kFltEpsilon;
+  s->half_tile_h = 1.0f / 6.0f - kFltEpsilon;
+}
+
+extern "C" rfx_scene *rfx_scene_create(float dr, float dg, float db, float dp)   // Scene.cpp:10-15
+{
+  rfx_scene *s = new rfx_scene();
+  s->diff = mkc(dr, dg, db);
+  s->diff_power = dp;
+  s->env = cscale(s->diff, dp);
+  default_half_tiles(s);
+  return s;
+}
+
+extern "C" void rfx_scene_destroy(rfx_scene *s) { delete s; }
+
+static HostMat make_mat(int type, const float rgb[3], float refl, float transp)      // Material.cpp:8-14
+{
+  HostMat m;
+  m.dielectric = type == RFX_DIELECTRIC;
+  m.r = rgb[0]; m.g = rgb[1]; m.b = rgb[2];
+  m.refl = clampf(refl, 0.0f, 1.0f);
+  m.transp = clampf(transp, 0.0f, 1.0f);
+  return m;
+}
+
+extern "C" int rfx_scene_add_sphere(rfx_scene *s, const float c[3], float radius, int type, const float rgb[3],
+                                    float refl, float transp)                          // Scene.cpp:29-39
+{
+  if (!s || !c || !rgb || (type != RFX_METAL && type != RFX_DIELECTRIC)) return fail(RFX_ERR_ARG, "add_sphere: bad args");
+  if (radius <= kVerySmall) radius = kVerySmall;
+  HostSphere sp;
+  sp.center = mk(c[0], c[1], c[2]);
+  sp.radius = radius;
+  sp.sq_radius = radius * radius;                                                    // Sphere.cpp:19
+  sp.mat = make_mat(type, rgb, refl, transp);
+  sp.obj = (int)s->obj_kind.size();
+  s->obj_kind.push_back(0);
+  s->obj_idx.push_back((int)s->spheres.size());
+  s->spheres.push_back(sp);
+  return sp.obj;
+}
+
+extern "C" int rfx_scene_add_triangle(rfx_scene *s, const float a[3], const float b[3], const float c[3], int type,
+                                      const float rgb[3], float refl, float transp)    // Triangle.cpp:11-21
+{
+  if (!s || !a || !b || !c || !rgb || (type != RFX_METAL && type != RFX_DIELECTRIC))
+    return fail(RFX_ERR_ARG, "add_triangle: bad args");
+  HostTri t;
+  const v3 v0 = mk(a[0], a[1], a[2]), v1 = mk(b[0], b[1], b[2]), v2 = mk(c[0], c[1], c[2]);
+  t.v0 = v0;
+  t.mat = make_mat(type, rgb, refl, transp);
+  t.norm = normalized(cross(sub(v1, v0), sub(v2, v0)));
+  t.ax = inverted(from_cols(sub(v2, v0), sub(v1, v0), neg(t.norm)));
+  memset(&t.tuv, 0, sizeof(t.tuv));
+  t.obj = (int)s->obj_kind.size();
+  s->obj_kind.push_back(1);
+  s->obj_idx.push_back((int)s->tris.size());
+  s->tris.push_back(t);
+  return t.obj;
+}
+
+extern "C" int rfx_triangle_set_texture(rfx_scene *s, int obj, int tex, const float uv[6])  // Triangle.cpp:110-120
+{
+  if (!s || !uv || obj < 0 || obj >= (int)s->obj_kind.size() || s->obj_kind[obj] != 1)
+    return fail(RFX_ERR_ARG, "set_texture: object %d is not a triangle", obj);
+  if (tex < 0 || tex >= (int)s->textures.size()) return fail(RFX_ERR_ARG, "set_texture: bad texture %d", tex);
+  HostTri &t = s->tris[s->obj_idx[obj]];
+  t.tex = tex;
+  t.tu0 = uv[0];
+  t.tv0 = uv[1];
+  const v3 p1 = mk(uv[0], uv[1], 0), p2 = mk(uv[2], uv[3], 0), p3 = mk(uv[4], uv[5], 0);
+  t.tuv = from_cols(sub(p3, p1), sub(p2, p1), mk(0, 0, -1));
+  return RFX_OK;
+}
+
+extern "C" int rfx_scene_add_light(rfx_scene *s, const float o[3], float radius, const float rgb[3], float power)
+{                                                                                     // Scene.cpp:48-59
+  if (!s || !o || !rgb) return fail(RFX_ERR_ARG, "add_light: bad args");
+  if (radius <= kVerySmall) radius = kVerySmall;
+  const col c = mkc(rgb[0], rgb[1], rgb[2]);
+  s->env = cadd(s->env, cscale(c, power));
+  HostLight l;
+  l.origin = mk(o[0], o[1], o[2]);
+  l.radius = radius;
+  l.r = c.r; l.g = c.g; l.b = c.b;
+  l.power = clampf(power, 0.0f, 1.0f);                                                // OmniLight.cpp:13
+  s->lights.push_back(l);
+  return (int)s->lights.size() - 1;
+}
+
+extern "C" int rfx_scene_add_texture_argb(rfx_scene *s, uint32_t w, uint32_t h, const uint32_t *argb)
+{
+  if (!s) return fail(RFX_ERR_ARG, "add_texture: null scene");
+  HostTexture t;
+  if (argb && w && h)
+  {
+    t.w = w; t.h = h;
+    t.texels.assign(argb, argb + (size_t)w * h);
+  }
+  s->textures.push_back(std::move(t));
+  return (int)s->textures.size() - 1;
+}
+
+// ---- TGA / BMP (Texture.cpp:34-173, image_headers.h) ----
+#pragma pack(push, 1)
+struct TgaHeader { int8_t idlen, colmptype, imagetype; int16_t cmorg, cmlen; int8_t cmbits; int16_t xoff, yoff, xsize, ysize; int8_t bpix, imagedesc; };
+struct BmpFileHeader { uint16_t bfType; uint32_t bfSize; uint16_t r1, r2; uint32_t bfOffBits; };
+struct BmpInfoHeader { uint32_t biSize; int32_t biWidth, biHeight; uint16_t biPlanes, biBitCount; uint32_t biCompression, biSizeImage; int32_t xppm, yppm; uint32_t clrUsed, clrImportant; };
+#pragma pack(pop)
+
+static bool tga_read(const char *path, uint32_t &w, uint32_t &h, std::vector<uint32_t> &out)
+{
+  w = h = 0;
+  out.clear();
+  FILE *f = fopen(path, "rb");
+  if (!f) return false;
+  TgaHeader hd;
+  bool ok = false;
+  if (fread(&hd, sizeof(hd), 1, f) == 1 && hd.imagetype == 2)
+  {
+    const uint32_t W = (uint32_t)(uint16_t)hd.xsize, H = (uint32_t)(uint16_t)hd.ysize;
+    const int bpp = hd.bpix;
+    const long off = (long)sizeof(hd) + hd.idlen + hd.cmlen * hd.cmbits / 8;
+    if (!fseek(f, off, SEEK_SET) && (bpp == 24 || bpp == 32) && W && H)
+    {
+      const size_t n = (size_t)W * H, ps = (size_t)bpp / 8;
+      std::vector<uint8_t> raw(n * ps);
+      if (fread(raw.data(), 1, raw.size(), f) == raw.size())
+      {
+        out.resize(n);
+        for (size_t i = 0; i < n; ++i)
+        {
+          const uint8_t *p = &raw[i * ps];
+          const uint32_t a = bpp == 32 ? p[3] : 0xFFu;
+          out[i] = a << 24 | (uint32_t)p[2] << 16 | (uint32_t)p[1] << 8 | p[0];
+        }
+        w = W; h = H;
+        ok = true;
+      }
+    }
+  }
+  fclose(f);
+  if (!ok) out.clear();
+  return ok;
+}
+
+static bool has_ext(const char *path, const char *ext)
+{
+  const char *dot = strrchr(path, '.');
+  return dot && !strcmp(dot, ext);
+}
+
+extern "C" int rfx_tga_load(const char *path, uint32_t *w, uint32_t *h, uint32_t *argb, size_t capacity)
+{
+  if (!path || !w || !h) return fail(RFX_ERR_ARG, "tga_load: bad args");
+  std::vector<uint32_t> px;
+  if (!tga_read(path, *w, *h, px)) return fail(RFX_ERR_IO, "tga_load: cannot read %s", path);
+  if (argb)
+  {
+    if (capacity < px.size()) return fail(RFX_ERR_ARG, "tga_load: capacity %zu < %zu", capacity, px.size());
+    memcpy(argb, px.data(), px.size() * 4);
+  }
+  return RFX_OK;
+}
+
+extern "C" int rfx_tga_save(const char *path, uint32_t w, uint32_t h, const uint32_t *argb)  // Texture.cpp:110-137
+{
+  if (!path || !argb || !w || !h) return fail(RFX_ERR_ARG, "tga_save: bad args");
+  FILE *f = fopen(path, "wb");
+  if (!f) return fail(RFX_ERR_IO, "tga_save: cannot open %s", path);
+  TgaHeader hd;
+  memset(&hd, 0, sizeof(hd));
+  hd.imagetype = 2; hd.xsize = (int16_t)w; hd.ysize = (int16_t)h; hd.bpix = 32;
+  bool ok = fwrite(&hd, sizeof(hd), 1, f) == 1 && fwrite(argb, (size_t)w * h * 4, 1, f) == 1;
+  fclose(f);
+  return ok ? RFX_OK : fail(RFX_ERR_IO, "tga_save: short write");
+}
+
+extern "C" int rfx_bmp_save(const char *path, uint32_t w, uint32_t h, const uint32_t *argb)  // Texture.cpp:139-173
+{
+  if (!path || !argb || !w || !h) return fail(RFX_ERR_ARG, "bmp_save: bad args");
+  FILE *f = fopen(path, "wb");
+  if (!f) return fail(RFX_ERR_IO, "bmp_save: cannot open %s", path);
+  BmpFileHeader fh;
+  BmpInfoHeader ih;
+  memset(&fh, 0, sizeof(fh));
+  memset(&ih, 0, sizeof(ih));
+  fh.bfType = ((uint16_t)'M' << 8) | (uint16_t)'B';
+  fh.bfSize = (uint32_t)(sizeof(fh) + sizeof(ih) + (size_t)w * h * 4);
+  fh.bfOffBits = sizeof(fh) + sizeof(ih);
+  ih.biSize = sizeof(ih); ih.biWidth = (int32_t)w; ih.biHeight = (int32_t)h; ih.biPlanes = 1; ih.biBitCount = 32;
+  bool ok = fwrite(&fh, sizeof(fh), 1, f) == 1 && fwrite(&ih, sizeof(ih), 1, f) == 1 &&
+            fwrite(argb, (size_t)w * h * 4, 1, f) == 1;
+  fclose(f);
+  return ok ? RFX_OK : fail(RFX_ERR_IO, "bmp_save: short write");
+}
+
+extern "C" int rfx_scene_add_texture_file(rfx_scene *s, const char *path, int *loaded)  // Scene.cpp:61-66
+{
+  if (!s || !path) return fail(RFX_ERR_ARG, "add_texture_file: bad args");
+  HostTexture t;
+  const bool ok = has_ext(path, ".tga") && tga_read(path, t.w, t.h, t.texels);     // Texture.cpp:175-189
+  if (loaded) *loaded = ok ? 1 : 0;
+  s->textures.push_back(std::move(t));
+  return (int)s->textures.size() - 1;
+}
+
+static void set_skybox_index(rfx_scene *s, int idx)                                   // Skybox.cpp:21-37
+{
+  s->skybox = idx;
+  const HostTexture &t = s->textures[idx];
+  if (t.w)
+  {
+    s->half_tile_w = 1.0f / 8.0f - 1.0f / (float)t.w - kFltEpsilon;
+    s->half_tile_h = 1.0f / 6.0f - 1.0f / (float)t.h - kFltEpsilon;
+  }
+  else
+    default_half_tiles(s);
+}
+
+extern "C" int rfx_scene_set_skybox_file(rfx_scene *s, const char *path)
+{
+  if (!s || !path) return fail(RFX_ERR_ARG, "set_skybox_file: bad args");
+  int loaded = 0;
+  const int idx = rfx_scene_add_texture_file(s, path, &loaded);
+  set_skybox_index(s, idx);
+  return loaded;
+}
+
+extern "C" int rfx_scene_set_skybox_argb(rfx_scene *s, uint32_t w, uint32_t h, const uint32_t *argb)
+{
+  if (!s) return fail(RFX_ERR_ARG, "set_skybox_argb: null scene");
+  const int idx = rfx_scene_add_texture_argb(s, w, h, argb);
+  set_skybox_index(s, idx);
+  return s->textures[idx].w ? 1 : 0;
+}
+
+extern "C" int rfx_scene_counts(const rfx_scene *s, int *ns, int *nt, int *nl, int *nx)
+{
+  if (!s) return fail(RFX_ERR_ARG, "counts: null scene");
+  if (ns) *ns = (int)s->spheres.size();
+  if (nt) *nt = (int)s->tris.size();
+  if (nl) *nl = (int)s->lights.size();
+  if (nx) *nx = (int)s->textures.size();
+  return RFX_OK;
+}
+
+// ============================================================== camera / images
+extern "C" void rfx_camera_view(const float e[3], const float a[3], float view[9])    // Camera.cpp:24-38
+{
+  const v3 eye = mk(e[0], e[1], e[2]), at = mk(a[0], a[1], a[2]);
+  const v3 up = mk(0.0f, 1.0f, 0.0f);
+  const v3 oz = normalized(sub(at, eye));
+  const v3 ox = normalized(cross(up, oz));
+  const v3 oy = normalized(cross(oz, ox));
+  const m33 m = from_cols(ox, oy, oz);
+  memcpy(view, &m, sizeof(m));
+}
+
+extern "C" float rfx_camera_rz(uint32_t width, float fov)                             // Render.cpp:148
+{
+  return (float)width / 2.0f / tanf(fov / 2.0f);
+}
+
+extern "C" void rfx_argb_from_rgb(const float *rgb, size_t n, uint32_t *out)
+{
+  for (size_t i = 0; i < n; ++i) out[i] = argb(mkc(rgb[i * 3], rgb[i * 3 + 1], rgb[i * 3 + 2]));
+}
+
+extern "C" uint32_t rfx_strip_rows(uint32_t H, uint32_t rb, uint32_t rank, uint32_t nranks)
+{
+  if (nranks <= 1) return H;
+  if (!rb || rank >= nranks) return 0;
+  const uint32_t full = H / rb, rem = H % rb;
+  uint32_t rows = (full / nranks) * rb;
+  const uint32_t extra = full % nranks;
+  if (rank < extra) rows += rb;
+  if (rem && full % nranks == rank) rows += rem;
+  return rows;
+}
+
+extern "C" uint32_t rfx_strip_row_to_y(uint32_t r, uint32_t rb, uint32_t rank, uint32_t nranks)
+{
+  if (nranks <= 1) return r;
+  return (r / rb * nranks + rank) * rb + r % rb;
+}
+
+// ============================================================== renderer
+struct rfx_renderer {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  // scene on device
+  DevScene dev{};
+  std::vector<void *> scene_allocs;
+  bool has_scene = false;
+  // RNG state: d_seed[0] current, d_seed[1] next; d_err
+  uint32_t *d_seed = nullptr;
+  int *d_err = nullptr;
+  uint32_t jitter_seed = 0;
+  // workspaces
+  float *d_rd = nullptr; uint64_t rd_cap = 0;
+  uint32_t *d_blk_cnt = nullptr; uint64_t *d_blk_off = nullptr; uint64_t blk_cap = 0;
+  // host staging for rfx_render_frame_host
+  float *d_img = nullptr; uint32_t *d_argb = nullptr; uint64_t *d_cnt = nullptr; size_t img_cap = 0;
+};
+
+static int set_dev(rfx_renderer *r)
+{
+  HIP_CHECK(hipSetDevice(r->device));
+  return RFX_OK;
+}
+
+extern "C" int rfx_renderer_create(rfx_renderer **out, int device)
+{
+  if (!out) return fail(RFX_ERR_ARG, "renderer_create: null out");
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(RFX_ERR_NODEV, "no HIP device");
+  if (device < 0 || device >= n) return fail(RFX_ERR_ARG, "device %d out of range (%d devices)", device, n);
+  rfx_renderer *r = new rfx_renderer();
+  r->device = device;
+  int rc;
+  if ((rc = set_dev(r)) != RFX_OK) { delete r; return rc; }
+  if (hipStreamCreateWithFlags(&r->own_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipMalloc(&r->d_seed, 2 * sizeof(uint32_t)) != hipSuccess || hipMalloc(&r->d_err, sizeof(int)) != hipSuccess)
+  {
+    delete r;
+    return fail(RFX_ERR_HIP, "renderer_create: HIP allocation failed");
+  }
+  r->stream = r->own_stream;
+  const uint32_t seeds[2] = {1350490027u, 1350490027u};
+  if (hipMemcpy(r->d_seed, seeds, sizeof(seeds), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemset(r->d_err, 0, sizeof(int)) != hipSuccess)
+  {
+    delete r;
+    return fail(RFX_ERR_HIP, "renderer_create: HIP init copy failed");
+  }
+  *out = r;
+  return RFX_OK;
+}
+
+static void free_scene(rfx_renderer *r)
+{
+  for (void *p : r->scene_allocs) (void)hipFree(p);
+  r->scene_allocs.clear();
+  r->has_scene = false;
+}
+
+extern "C" void rfx_renderer_destroy(rfx_renderer *r)
+{
+  if (!r) return;
+  (void)hipSetDevice(r->device);
+  (void)hipStreamSynchronize(r->stream);
+  free_scene(r);
+  (void)hipFree(r->d_seed); (void)hipFree(r->d_err); (void)hipFree(r->d_rd);
+  (void)hipFree(r->d_blk_cnt); (void)hipFree(r->d_blk_off);
+  (void)hipFree(r->d_img); (void)hipFree(r->d_argb); (void)hipFree(r->d_cnt);
+  if (r->own_stream) (void)hipStreamDestroy(r->own_stream);
+  delete r;
+}
+
+extern "C" int rfx_renderer_device(const rfx_renderer *r) { return r ? r->device : -1; }
+
+extern "C" int rfx_renderer_set_stream(rfx_renderer *r, void *s)
+{
+  if (!r) return fail(RFX_ERR_ARG, "set_stream: null renderer");
+  r->stream = s ? (hipStream_t)s : r->own_stream;
+  return RFX_OK;
+}
+
+template <class T>
+static int upload(rfx_renderer *r, const std::vector<T> &v, const T **dst)
+{
+  if (v.empty()) { *dst = nullptr; return RFX_OK; }
+  void *p = nullptr;
+  HIP_CHECK(hipMalloc(&p, v.size() * sizeof(T)));
+  r->scene_allocs.push_back(p);
+  HIP_CHECK(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+  *dst = (const T *)p;
+  return RFX_OK;
+}
+
+extern "C" int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *s)
+{
+  if (!r || !s) return fail(RFX_ERR_ARG, "set_scene: bad args");
+  int rc;
+  if ((rc = set_dev(r)) != RFX_OK) return rc;
+  HIP_CHECK(hipStreamSynchronize(r->stream));
+  free_scene(r);
+  std::vector<SphereGeo> sg;
+  std::vector<MatRec> sm, tm;
+  std::vector<int32_t> si;
+  for (const HostSphere &sp : s->spheres)
+  {
+    sg.push_back({sp.center.x, sp.center.y, sp.center.z, sp.sq_radius});
+    sm.push_back({sp.mat.r, sp.mat.g, sp.mat.b, sp.mat.refl});
+    si.push_back(sp.obj);
+    si.push_back(sp.mat.dielectric);
+  }
+  std::vector<TriGeo> tg;
+  std::vector<TriShade> ts;
+  for (const HostTri &t : s->tris)
+  {
+    TriGeo g{};
+    g.v0x = t.v0.x; g.v0y = t.v0.y; g.v0z = t.v0.z;
+    g.a11 = t.ax.m11; g.a12 = t.ax.m12; g.a13 = t.ax.m13;
+    g.a21 = t.ax.m21; g.a22 = t.ax.m22; g.a23 = t.ax.m23;
+    g.a31 = t.ax.m31; g.a32 = t.ax.m32; g.a33 = t.ax.m33;
+    tg.push_back(g);
+    TriShade h{};
+    h.nx = t.norm.x; h.ny = t.norm.y; h.nz = t.norm.z;
+    h.tu0 = t.tu0; h.tv0 = t.tv0;
+    h.t11 = t.tuv.m11; h.t12 = t.tuv.m12; h.t21 = t.tuv.m21; h.t22 = t.tuv.m22;
+    h.tex = t.tex; h.dielectric = t.mat.dielectric; h.obj = t.obj;
+    ts.push_back(h);
+    tm.push_back({t.mat.r, t.mat.g, t.mat.b, t.mat.refl});
+  }
+  std::vector<LightRec> lr;
+  for (const HostLight &l : s->lights) lr.push_back({l.origin.x, l.origin.y, l.origin.z, l.radius, l.r, l.g, l.b, l.power});
+  std::vector<TexRec> tr;
+  std::vector<uint32_t> pool;
+  for (const HostTexture &t : s->textures)
+  {
+    tr.push_back({(uint32_t)pool.size(), t.w, t.h, 0});
+    pool.insert(pool.end(), t.texels.begin(), t.texels.end());
+  }
+  DevScene d{};
+  if ((rc = upload(r, sg, &d.sph_geo)) || (rc = upload(r, sm, &d.sph_mat)) || (rc = upload(r, si, &d.sph_info)) ||
+      (rc = upload(r, tg, &d.tri_geo)) || (rc = upload(r, ts, &d.tri_shade)) || (rc = upload(r, tm, &d.tri_mat)) ||
+      (rc = upload(r, lr, &d.lights)) || (rc = upload(r, tr, &d.texs)) || (rc = upload(r, pool, &d.texels)))
+    return rc;
+  d.n_sph = (int32_t)sg.size();
+  d.n_tri = (int32_t)tg.size();
+  d.n_light = (int32_t)lr.size();
+  d.skybox_tex = s->skybox;
+  const col amb = cscale(s->diff, s->diff_power);                                    // Scene.cpp:186 (first factor)
+  d.amb_r = amb.r; d.amb_g = amb.g; d.amb_b = amb.b;
+  d.env_r = s->env.r; d.env_g = s->env.g; d.env_b = s->env.b;
+  d.half_tile_w = s->half_tile_w;
+  d.half_tile_h = s->half_tile_h;
+  r->dev = d;
+  r->has_scene = true;
+  return RFX_OK;
+}
+
+extern "C" int rfx_renderer_set_rng(rfx_renderer *r, uint32_t sphere_seed, uint32_t jitter_seed)
+{
+  if (!r) return fail(RFX_ERR_ARG, "set_rng: null renderer");
+  int rc;
+  if ((rc = set_dev(r)) != RFX_OK) return rc;
+  HIP_CHECK(hipMemcpyAsync(r->d_seed, &sphere_seed, sizeof(uint32_t), hipMemcpyHostToDevice, r->stream));
+  HIP_CHECK(hipStreamSynchronize(r->stream));
+  r->jitter_seed = jitter_seed;
+  return RFX_OK;
+}
+
+extern "C" int rfx_renderer_get_rng(rfx_renderer *r, uint32_t *sphere_seed, uint32_t *jitter_seed)
+{
+  if (!r) return fail(RFX_ERR_ARG, "get_rng: null renderer");
+  int rc;
+  if ((rc = set_dev(r)) != RFX_OK) return rc;
+  uint32_t s = 0;
+  int err = 0;
+  HIP_CHECK(hipMemcpyAsync(&s, r->d_seed, sizeof(uint32_t), hipMemcpyDeviceToHost, r->stream));
+  HIP_CHECK(hipMemcpyAsync(&err, r->d_err, sizeof(int), hipMemcpyDeviceToHost, r->stream));
+  HIP_CHECK(hipStreamSynchronize(r->stream));
+  if (err) return fail(RFX_ERR_RNG, "RNG pre-pass ran short of accepted triples");
+  if (sphere_seed) *sphere_seed = s;
+  if (jitter_seed) *jitter_seed = r->jitter_seed;
+  return RFX_OK;
+}
+
+static int ensure_rng_workspace(rfx_renderer *r, uint64_t traces)
+{
+  if (traces > r->rd_cap)
+  {
+    (void)hipFree(r->d_rd);
+    r->d_rd = nullptr;
+    r->rd_cap = 0;
+    HIP_CHECK(hipMalloc(&r->d_rd, traces * 3 * sizeof(float)));
+    r->rd_cap = traces;
+  }
+  const uint64_t nblk = rng_blocks_for(traces);
+  if (nblk > r->blk_cap)
+  {
+    (void)hipFree(r->d_blk_cnt); (void)hipFree(r->d_blk_off);
+    r->d_blk_cnt = nullptr; r->d_blk_off = nullptr; r->blk_cap = 0;
+    HIP_CHECK(hipMalloc(&r->d_blk_cnt, nblk * sizeof(uint32_t)));
+    HIP_CHECK(hipMalloc(&r->d_blk_off, nblk * sizeof(uint64_t)));
+    r->blk_cap = nblk;
+  }
+  return RFX_OK;
+}
+
+// sphere stream: d_seed[0] -> pre-pass -> d_seed[1] -> copy back to d_seed[0]
+static int enqueue_rng(rfx_renderer *r, uint64_t traces, hipStream_t st)
+{
+  int rc;
+  if ((rc = ensure_rng_workspace(r, traces)) != RFX_OK) return rc;
+  HIP_CHECK(launch_rng(r->d_seed, r->d_seed + 1, traces, r->d_rd, r->rd_cap, r->d_blk_cnt, r->d_blk_off, r->d_err, st));
+  HIP_CHECK(hipMemcpyAsync(r->d_seed, r->d_seed + 1, sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+  return RFX_OK;
+}
+
+extern "C" int rfx_render_frame(rfx_renderer *r, const rfx_frame *f, float *d_rgb, uint32_t *d_argb,
+                                uint64_t *d_counters, void *stream)
+{
+  if (!r || !f || !d_rgb) return fail(RFX_ERR_ARG, "render_frame: bad args");
+  if (!r->has_scene) return fail(RFX_ERR_STATE, "render_frame: no scene uploaded");
+  if (!f->width || !f->height || f->reflect_num <= 0 || f->sample_num == 0)
+    return fail(RFX_ERR_ARG, "render_frame: W=%u H=%u reflect_num=%d sample_num=%d", f->width, f->height,
+                f->reflect_num, f->sample_num);
+  const uint32_t nranks = f->nranks ? f->nranks : 1;
+  if (nranks > 1 && (f->sample_num < 0 || !f->row_block || f->rank >= nranks))
+    return fail(RFX_ERR_ARG, "render_frame: strip partition needs sample_num > 0, row_block > 0, rank < nranks");
+  if (f->sample_num > 256 || f->sample_num < -4096) return fail(RFX_ERR_ARG, "render_frame: sample_num out of range");
+  int rc;
+  if ((rc = set_dev(r)) != RFX_OK) return rc;
+  hipStream_t st = stream ? (hipStream_t)stream : r->stream;
+
+  const uint32_t W = f->width, H = f->height;
+  const uint64_t npx = (uint64_t)W * H;
+  uint64_t p0 = f->pixel_begin, p1 = f->pixel_end;
+  if (p0 == 0 && p1 == 0) p1 = npx;
+  if (p0 >= p1 || p1 > npx) return fail(RFX_ERR_ARG, "render_frame: pixel span [%llu, %llu) outside frame",
+                                        (unsigned long long)p0, (unsigned long long)p1);
+  if (nranks > 1 && (p0 != 0 || p1 != npx)) return fail(RFX_ERR_ARG, "render_frame: strips need the whole frame");
+  const uint32_t y0 = (uint32_t)(p0 / W), y1 = (uint32_t)((p1 - 1) / W);
+  uint64_t traces, trace_base = 0;
+  uint32_t grid_rows, row0;
+  if (f->sample_num < 0)
+  {
+    // block preview: corners (x % n == 0 && y % n == 0) inside the span, in raster order (Render.cpp:158-172)
+    const uint64_t n = (uint64_t)(-f->sample_num);
+    const uint64_t bw = (W + n - 1) / n;
+    auto corners_before = [&](uint64_t p) -> uint64_t {
+      const uint64_t y = p / W, x = p % W;
+      return (y + n - 1) / n * bw + (y % n == 0 ? (x + n - 1) / n : 0);
+    };
+    trace_base = corners_before(p0);
+    traces = corners_before(p1) - trace_base;
+    row0 = (uint32_t)(y0 / n);
+    grid_rows = (uint32_t)(y1 / n - y0 / n + 1);
+  }
+  else
+  {
+    traces = (p1 - p0) * (uint64_t)(f->sample_num * f->sample_num);
+    row0 = nranks > 1 ? 0 : y0;
+    grid_rows = nranks > 1 ? rfx_strip_rows(H, f->row_block, f->rank, nranks) : y1 - y0 + 1;
+  }
+  if (traces >= (1ull << 32)) return fail(RFX_ERR_ARG, "render_frame: %llu traces exceed 2^32", (unsigned long long)traces);
+  if (traces == 0) return RFX_OK;  // a span with no block corner traces nothing (and draws no randDir)
+  if ((rc = enqueue_rng(r, traces, st)) != RFX_OK) return rc;
+
+  FrameParams P{};
+  P.eye_x = f->eye[0]; P.eye_y = f->eye[1]; P.eye_z = f->eye[2];
+  P.v11 = f->view[0]; P.v12 = f->view[1]; P.v13 = f->view[2];
+  P.v21 = f->view[3]; P.v22 = f->view[4]; P.v23 = f->view[5];
+  P.v31 = f->view[6]; P.v32 = f->view[7]; P.v33 = f->view[8];
+  P.rz = rfx_camera_rz(W, f->fov);
+  P.wh = W / 2.0f;
+  P.hh = H / 2.0f;
+  P.W = W; P.H = H;
+  P.depth = f->reflect_num;
+  P.ss = f->sample_num;
+  P.accumulate = f->sample_num > 0 && f->additive_counter > 1;
+  P.additive = f->sample_num > 0 && f->additive;
+  P.jitter_seed = r->jitter_seed;
+  P.row_block = f->row_block ? f->row_block : 1;
+  P.rank = nranks > 1 ? f->rank : 0;
+  P.nranks = nranks;
+  P.grid_rows = grid_rows;
+  P.row0 = row0;
+  P.p_begin = p0;
+  P.p_end = p1;
+  P.trace_base = trace_base;
+  P.img = d_rgb;
+  P.argb = d_argb;
+  P.rd = r->d_rd;
+  P.n_rd = r->rd_cap;
+  P.counters = (unsigned long long *)d_counters;
+  if (grid_rows)
+    HIP_CHECK(launch_trace(r->dev, P, d_counters != nullptr, st));
+  if (P.additive)                                                                  // 2 draws per pixel, raster order
+    r->jitter_seed = lcg_jump(r->jitter_seed, 2ull * (p1 - p0));
+  return RFX_OK;
+}
+
+extern "C" int rfx_device_alloc(rfx_renderer *r, size_t bytes, void **p)
+{
+  if (!r || !p) return fail(RFX_ERR_ARG, "device_alloc: bad args");
+  int rc;
+  if ((rc = set_dev(r)) != RFX_OK) return rc;
+  HIP_CHECK(hipMalloc(p, bytes ? bytes : 1));
+  return RFX_OK;
+}
+
+extern "C" int rfx_device_free(rfx_renderer *r, void *p)
+{
+  if (!r) return fail(RFX_ERR_ARG, "device_free: null renderer");
+  int rc;
+  if ((rc = set_dev(r)) != RFX_OK) return rc;
+  HIP_CHECK(hipFree(p));
+  return RFX_OK;
+}
+
+extern "C" int rfx_memcpy_d2h(rfx_renderer *r, void *dst, const void *src, size_t n)
+{
+  if (!r) return fail(RFX_ERR_ARG, "memcpy: null renderer");
+  HIP_CHECK(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, r->stream));
+  HIP_CHECK(hipStreamSynchronize(r->stream));
+  return RFX_OK;
+}
+
+extern "C" int rfx_memcpy_h2d(rfx_renderer *r, void *dst, const void *src, size_t n)
+{
+  if (!r) return fail(RFX_ERR_ARG, "memcpy: null renderer");
+  HIP_CHECK(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, r->stream));
+  HIP_CHECK(hipStreamSynchronize(r->stream));
+  return RFX_OK;
+}
+
+extern "C" int rfx_synchronize(rfx_renderer *r)
+{
+  if (!r) return fail(RFX_ERR_ARG, "synchronize: null renderer");
+  HIP_CHECK(hipStreamSynchronize(r->stream));
+  int err = 0;
+  HIP_CHECK(hipMemcpy(&err, r->d_err, sizeof(int), hipMemcpyDeviceToHost));
+  if (err) return fail(RFX_ERR_RNG, "RNG pre-pass ran short of accepted triples");
+  return RFX_OK;
+}
+
+extern "C" int rfx_render_frame_host(rfx_renderer *r, const rfx_frame *f, float *rgb, uint32_t *argb_out,
+                                     uint64_t *counters)
+{
+  if (!r || !f || !rgb) return fail(RFX_ERR_ARG, "render_frame_host: bad args");
+  if (f->nranks > 1) return fail(RFX_ERR_ARG, "render_frame_host: whole frames only");
+  int rc;
+  if ((rc = set_dev(r)) != RFX_OK) return rc;
+  const size_t px = (size_t)f->width * f->height;
+  if (px > r->img_cap)
+  {
+    (void)hipFree(r->d_img); (void)hipFree(r->d_argb);
+    r->d_img = nullptr; r->d_argb = nullptr; r->img_cap = 0;
+    HIP_CHECK(hipMalloc(&r->d_img, px * 3 * sizeof(float)));
+    HIP_CHECK(hipMalloc(&r->d_argb, px * sizeof(uint32_t)));
+    r->img_cap = px;
+  }
+  if (!r->d_cnt) HIP_CHECK(hipMalloc(&r->d_cnt, RFX_NCOUNTERS * sizeof(uint64_t)));
+  HIP_CHECK(hipMemcpyAsync(r->d_img, rgb, px * 3 * sizeof(float), hipMemcpyHostToDevice, r->stream));
+  if (counters) HIP_CHECK(hipMemsetAsync(r->d_cnt, 0, RFX_NCOUNTERS * sizeof(uint64_t), r->stream));
+  if ((rc = rfx_render_frame(r, f, r->d_img, argb_out ? r->d_argb : nullptr, counters ? r->d_cnt : nullptr, nullptr)))
+    return rc;
+  HIP_CHECK(hipMemcpyAsync(rgb, r->d_img, px * 3 * sizeof(float), hipMemcpyDeviceToHost, r->stream));
+  if (argb_out) HIP_CHECK(hipMemcpyAsync(argb_out, r->d_argb, px * sizeof(uint32_t), hipMemcpyDeviceToHost, r->stream));
+  if (counters)
+  {
+    uint64_t c[RFX_NCOUNTERS];
+    HIP_CHECK(hipMemcpyAsync(c, r->d_cnt, sizeof(c), hipMemcpyDeviceToHost, r->stream));
+    HIP_CHECK(hipStreamSynchronize(r->stream));
+    for (int k = 0; k < RFX_NCOUNTERS; ++k) counters[k] += c[k];
+  }
+  return rfx_synchronize(r);
+}
+
+extern "C" int rfx_rand_dirs(rfx_renderer *r, uint32_t seed, uint64_t n, float *out3, uint32_t *seed_out)
+{
+  if (!r || !out3 || !n) return fail(RFX_ERR_ARG, "rand_dirs: bad args");
+  int rc;
+  if ((rc = set_dev(r)) != RFX_OK) return rc;
+  uint32_t saved = 0;
+  HIP_CHECK(hipMemcpyAsync(&saved, r->d_seed, sizeof(uint32_t), hipMemcpyDeviceToHost, r->stream));
+  HIP_CHECK(hipStreamSynchronize(r->stream));
+  HIP_CHECK(hipMemcpyAsync(r->d_seed, &seed, sizeof(uint32_t), hipMemcpyHostToDevice, r->stream));
+  if ((rc = enqueue_rng(r, n, r->stream)) != RFX_OK) return rc;
+  std::vector<float> soa(3 * n);
+  for (int k = 0; k < 3; ++k)
+    HIP_CHECK(hipMemcpyAsync(soa.data() + k * n, r->d_rd + k * r->rd_cap, n * sizeof(float), hipMemcpyDeviceToHost, r->stream));
+  uint32_t after = 0;
+  HIP_CHECK(hipMemcpyAsync(&after, r->d_seed, sizeof(uint32_t), hipMemcpyDeviceToHost, r->stream));
+  HIP_CHECK(hipMemcpyAsync(r->d_seed, &saved, sizeof(uint32_t), hipMemcpyHostToDevice, r->stream));
+  if ((rc = rfx_synchronize(r)) != RFX_OK) return rc;
+  for (uint64_t i = 0; i < n; ++i)
+  {
+    out3[i * 3] = soa[i]; out3[i * 3 + 1] = soa[n + i]; out3[i * 3 + 2] = soa[2 * n + i];
+  }
+  if (seed_out) *seed_out = after;
+  return RFX_OK;
+}

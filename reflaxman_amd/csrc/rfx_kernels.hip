@@ -1,0 +1,608 @@
+// gfx950 kernels for ReflaxMan's per-pixel trace loop.
+//
+//   rng_count / rng_scan / rng_emit : the reference's serial LCG stream
+//       (trace_math.h:34-39, Vector3.cpp:176-188) as a parallel pre-pass:
+//       LCG jump-ahead per thread, accept flags, block scan, scatter of the
+//       i-th accepted triple to trace i.
+//   trace_kernel<STATS> : Render::renderNext (Render.cpp:136-215) +
+//       Scene::trace (Scene.cpp:73-236), one lane per trace, 8x8-pixel wave
+//       tiles, the bounce "recursion" as the reference's own iterative loop.
+//       Scene arrays are walked in wave-uniform order (scalar loads);
+//       closest hit keeps only (dist, object, t, u, v) per candidate and
+//       re-derives drop/normal/reflection/texel for the winner with the same
+//       expressions; the shadow any-hit loop exits per lane on the first
+//       occluder and per wave once every lane has (exec-mask early out).
+//
+// Numerics: compiled with -ffp-contract=off, IEEE div/sqrt, f32 denormals on,
+// so every operation rounds exactly as the reference's x86-64 build does.
+#include <hip/hip_runtime.h>
+
+#include "rfx_math.h"
+#include "rfx_powf.h"
+#include "rfx_types.h"
+
+#pragma clang fp contract(off)
+
+namespace rfx {
+
+struct Cnt { uint32_t c[C_COUNT]; };
+
+#define RFX_CNT(k)                   \
+  do {                               \
+    if constexpr (STATS) cnt.c[k]++; \
+  } while (0)
+
+// ------------------------------------------------------------- sampling
+template <bool STATS>
+__device__ __forceinline__ col texel_uv(const DevScene &S, int tex, float u, float v, Cnt &cnt)  // Texture.cpp:231-269
+{
+  if (u < 0.0f || u > 1.0f || v < 0.0f || v > 1.0f) { RFX_CNT(C_TEX_OTHER); return mkc(0.0f, 0.0f, 0.0f); }
+  TexRec t;
+  t.w = 0; t.h = 0; t.offset = 0;
+  if (tex >= 0) t = S.texs[tex];
+  if (t.w == 0)
+  {
+    RFX_CNT(C_TEX_CHECKER);
+    return (((int)(u * 50) % 2) ^ ((int)(v * 50) % 2)) ? mkc(0.5f, 0.5f, 0.5f) : mkc(0.75f, 0.75f, 0.75f);
+  }
+  const float fx = clampf(u, 0.0f, 1.0f - kFltEpsilon) * (float)t.w;
+  const float fy = clampf(v, 0.0f, 1.0f - kFltEpsilon) * (float)t.h;
+  const uint32_t x = (uint32_t)fx, y = (uint32_t)fy;
+  const uint32_t *px = S.texels + t.offset;
+  if (x < t.w - 1 && y < t.h - 1)
+  {
+    RFX_CNT(C_TEX_BILINEAR);
+    const col c00 = from_argb(px[x + t.w * y]), c01 = from_argb(px[x + t.w * (y + 1)]);
+    const col c10 = from_argb(px[x + 1 + t.w * y]), c11 = from_argb(px[x + 1 + t.w * (y + 1)]);
+    const float uf = fx - floorf(fx), vf = fy - floorf(fy);
+    const float uo = 1 - uf, vo = 1 - vf;
+    return cadd(cscale(cadd(cscale(c00, uo), cscale(c10, uf)), vo), cscale(cadd(cscale(c01, uo), cscale(c11, uf)), vf));
+  }
+  RFX_CNT(C_TEX_OTHER);
+  const uint32_t xi = (uint32_t)fx, yi = (uint32_t)fy;                 // Texture.cpp:216-229
+  if (xi >= t.w || yi >= t.h) return mkc(0.0f, 0.0f, 0.0f);
+  return from_argb(px[xi + t.w * yi]);
+}
+
+template <bool STATS>
+__device__ __forceinline__ col skybox_texel(const DevScene &S, v3 ray, Cnt &cnt)       // Skybox.cpp:39-106
+{
+  const float uLeft = 1.0f / 8.0f, vLeft = 3.0f / 6.0f;
+  const float uFront = 3.0f / 8.0f, vFront = 3.0f / 6.0f;
+  const float uRight = 5.0f / 8.0f, vRight = 3.0f / 6.0f;
+  const float uBack = 7.0f / 8.0f, vBack = 3.0f / 6.0f;
+  const float uTop = 3.0f / 8.0f, vTop = 5.0f / 6.0f;
+  const float uBottom = 3.0f / 8.0f, vBottom = 1.0f / 6.0f;
+  const float hw = S.half_tile_w, hh = S.half_tile_h;
+  const v3 n = normalized(ray);
+  const float x = n.x, y = n.y, z = n.z;
+  const float ax = fabsf(x) + kVerySmall, ay = fabsf(y) + kVerySmall, az = fabsf(z) + kVerySmall;
+  float u, v;
+  if (az >= ax && az >= ay)
+  {
+    if (z > 0) { u = uFront + x / az * hw; v = vFront + y / az * hh; }
+    else { u = uBack - x / az * hw; v = vBack + y / az * hh; }
+  }
+  else if (ax >= ay && ax >= az)
+  {
+    if (x > 0) { u = uRight - z / ax * hw; v = vRight + y / ax * hh; }
+    else { u = uLeft + z / ax * hw; v = vLeft + y / ax * hh; }
+  }
+  else
+  {
+    if (y > 0) { u = uTop + x / ay * hw; v = vTop - z / ay * hh; }
+    else { u = uBottom + x / ay * hw; v = vBottom + z / ay * hh; }
+  }
+  return texel_uv<STATS>(S, S.skybox_tex, u, v, cnt);
+}
+
+// ------------------------------------------------------------- shadow any-hit
+// Scene.cpp:129-141: every object but the hit one, in insertion order
+// (spheres precede triangles in every scene the builder emits in that order;
+// the boolean is order-independent either way).
+template <bool STATS>
+__device__ __forceinline__ bool occluded(const DevScene &S, v3 o, v3 ray, int skip_obj, Cnt &cnt)
+{
+  const float a = sqlen(ray);
+  const v3 ray2 = mul(ray, 2.0f);
+  const float a4 = 4.0f * a, a2 = 2.0f * a;
+  const bool a_ok = a > kVerySmall;
+  for (int i = 0; i < S.n_sph; ++i)                                       // Sphere.cpp:44-85, any-hit
+  {
+    if (S.sph_info[2 * i] == skip_obj) continue;
+    RFX_CNT(C_SH_SPH_TESTS);
+    const SphereGeo g = S.sph_geo[i];
+    const v3 vco = sub(o, mk(g.cx, g.cy, g.cz));
+    const float b = dot(ray2, vco);
+    const float c = sqlen(vco) - g.sq_radius;
+    const float d = b * b - a4 * c;
+    if (d >= 0.0f && a_ok)
+    {
+      RFX_CNT(C_SH_SPH_D);
+      const float t = (-b - sqrtf(d)) / a2;
+      if (t > kVerySmall)
+      {
+        RFX_CNT(C_SH_SPH_T);
+        if (len(mul(ray, t)) > kDelta) return true;
+      }
+    }
+  }
+  for (int i = 0; i < S.n_tri; ++i)                                       // Triangle.cpp:53-108, any-hit
+  {
+    if (S.tri_shade[i].obj == skip_obj) continue;
+    RFX_CNT(C_SH_TRI_TESTS);
+    const TriGeo g = S.tri_geo[i];
+    m33 ax;
+    ax.m11 = g.a11; ax.m12 = g.a12; ax.m13 = g.a13;
+    ax.m21 = g.a21; ax.m22 = g.a22; ax.m23 = g.a23;
+    ax.m31 = g.a31; ax.m32 = g.a32; ax.m33 = g.a33;
+    const v3 ao = mmul(ax, sub(o, mk(g.v0x, g.v0y, g.v0z)));
+    const v3 ar = mmul(ax, ray);
+    if (fabsf(ar.z) > kVerySmall)
+    {
+      RFX_CNT(C_SH_TRI_Z);
+      const float t = -ao.z / ar.z;
+      if (t > kVerySmall)
+      {
+        RFX_CNT(C_SH_TRI_T);
+        const float u = ao.x + t * ar.x, v = ao.y + t * ar.y;
+        if (u >= 0.0f && v >= 0.0f && u + v < 1.0f)
+        {
+          RFX_CNT(C_SH_TRI_IN);
+          if (sqlen(mul(ray, t)) > kDelta * kDelta) return true;
+        }
+      }
+    }
+  }
+  return false;
+}
+
+// ------------------------------------------------------------- Scene::trace
+template <bool STATS>
+__device__ col trace(const DevScene &S, v3 origin, v3 ray, int depth, v3 rd, Cnt &cnt)
+{
+  col mulc = mkc(1.0f, 1.0f, 1.0f);
+  col pix = mkc(0.0f, 0.0f, 0.0f);
+  RFX_CNT(C_RAYS);
+  for (int refl = 0; refl < depth; ++refl)
+  {
+    RFX_CNT(C_SEGMENTS);
+    // closest hit (Scene.cpp:86-106): min over (distance, insertion index)
+    float best = kFltMax;
+    int best_obj = -1, best_kind = 0, best_i = 0;
+    float best_t = 0.0f, best_u = 0.0f, best_v = 0.0f;
+    {
+      const float a = sqlen(ray);
+      const v3 ray2 = mul(ray, 2.0f);
+      const float a4 = 4.0f * a, a2 = 2.0f * a;
+      const bool a_ok = a > kVerySmall;
+      for (int i = 0; i < S.n_sph; ++i)
+      {
+        RFX_CNT(C_SPH_TESTS);
+        const SphereGeo g = S.sph_geo[i];
+        const v3 vco = sub(origin, mk(g.cx, g.cy, g.cz));
+        const float b = dot(ray2, vco);
+        const float c = sqlen(vco) - g.sq_radius;
+        const float d = b * b - a4 * c;
+        if (d >= 0.0f && a_ok)
+        {
+          RFX_CNT(C_SPH_D);
+          const float t = (-b - sqrtf(d)) / a2;
+          if (t > kVerySmall)
+          {
+            RFX_CNT(C_SPH_T);
+            const float dist = len(mul(ray, t));
+            if (dist > kDelta)
+            {
+              const int obj = S.sph_info[2 * i];
+              if (dist < best || (dist == best && obj < best_obj))
+              {
+                best = dist; best_obj = obj; best_kind = 0; best_i = i; best_t = t;
+              }
+            }
+          }
+        }
+      }
+    }
+    for (int i = 0; i < S.n_tri; ++i)
+    {
+      RFX_CNT(C_TRI_TESTS);
+      const TriGeo g = S.tri_geo[i];
+      m33 ax;
+      ax.m11 = g.a11; ax.m12 = g.a12; ax.m13 = g.a13;
+      ax.m21 = g.a21; ax.m22 = g.a22; ax.m23 = g.a23;
+      ax.m31 = g.a31; ax.m32 = g.a32; ax.m33 = g.a33;
+      const v3 ao = mmul(ax, sub(origin, mk(g.v0x, g.v0y, g.v0z)));
+      const v3 ar = mmul(ax, ray);
+      if (fabsf(ar.z) > kVerySmall)
+      {
+        RFX_CNT(C_TRI_Z);
+        const float t = -ao.z / ar.z;
+        if (t > kVerySmall)
+        {
+          RFX_CNT(C_TRI_T);
+          const float u = ao.x + t * ar.x, v = ao.y + t * ar.y;
+          if (u >= 0.0f && v >= 0.0f && u + v < 1.0f)
+          {
+            RFX_CNT(C_TRI_IN);
+            const float sq = sqlen(mul(ray, t));
+            if (sq > kDelta * kDelta)
+            {
+              RFX_CNT(C_TRI_D);
+              const float dist = sqrtf(sq);
+              const int obj = S.tri_shade[i].obj;
+              if (dist < best || (dist == best && obj < best_obj))
+              {
+                best = dist; best_obj = obj; best_kind = 1; best_i = i; best_t = t; best_u = u; best_v = v;
+              }
+            }
+          }
+        }
+      }
+    }
+
+    if (best_obj >= 0)
+    {
+      // re-derive the winner's outputs with the reference's expressions
+      const v3 full = mul(ray, best_t);
+      const v3 drop = add(origin, full);
+      v3 norm;
+      MatRec m;
+      int diel;
+      if (best_kind == 0)
+      {
+        RFX_CNT(C_HIT_SPH);
+        const SphereGeo g = S.sph_geo[best_i];
+        norm = sub(drop, mk(g.cx, g.cy, g.cz));                              // Sphere.cpp:69
+        m = S.sph_mat[best_i];
+        diel = S.sph_info[2 * best_i + 1];
+      }
+      else
+      {
+        RFX_CNT(C_HIT_TRI);
+        const TriShade sh = S.tri_shade[best_i];
+        norm = mk(sh.nx, sh.ny, sh.nz);
+        m = S.tri_mat[best_i];
+        diel = sh.dielectric;
+        if (sh.tex >= 0)                                                     // Triangle.cpp:92-99
+        {
+          const float tvx = best_u * sh.t11 + best_v * sh.t12 + 0.0f;
+          const float tvy = best_u * sh.t21 + best_v * sh.t22 + 0.0f;
+          const col c = texel_uv<STATS>(S, sh.tex, sh.tu0 + tvx, sh.tv0 + tvy, cnt);
+          m.r = c.r; m.g = c.g; m.b = c.b;
+        }
+      }
+      const v3 reflv = reflect(full, norm);                                 // trace_math.cpp:14-23
+
+      const float rayLen = len(ray), normLen = len(norm), reflectLen = len(reflv);
+      col sumL = mkc(0.0f, 0.0f, 0.0f), sumS = mkc(0.0f, 0.0f, 0.0f);
+      for (int li = 0; li < S.n_light; ++li)                                 // Scene.cpp:117-181
+      {
+        RFX_CNT(C_L_EVAL);
+        const LightRec L = S.lights[li];
+        const v3 dtl = sub(mk(L.ox, L.oy, L.oz), drop);
+        if (dot(dtl, norm) > kVerySmall)
+        {
+          RFX_CNT(C_L_FACING);
+          const v3 sray = add(dtl, mul(rd, L.radius));
+          if (!occluded<STATS>(S, drop, sray, best_obj, cnt))
+          {
+            RFX_CNT(C_L_LIT);
+            const float dlen = len(dtl);
+            float aa = dlen * normLen;
+            const float cosl = (aa > kVerySmall) ? dot(dtl, norm) / aa : 0.0f;
+            const col lc = mkc(L.r, L.g, L.b);
+            if (L.power > kVerySmall) sumL = cadd(sumL, cscale(cscale(lc, cosl), L.power));
+            aa = sqlen(dtl);
+            const float ang = (aa > kVerySmall) ? 1.0f - L.radius * L.radius / aa : 0.0f;
+            if (ang > 0)
+            {
+              RFX_CNT(C_L_SPEC);
+              const v3 dlr = add(normalized(dtl), mul(rd, 1.0f - m.refl));
+              aa = len(dlr) * reflectLen;
+              float sc = (aa > kVerySmall) ? dot(dlr, reflv) / aa : 0.0f;
+              sc = clampf(sc + (1.0f - sqrtf(ang)), 0.0f, 1.0f);
+              if (sc > kVerySmall && L.radius > kVerySmall)
+              {
+                RFX_CNT(C_L_POW);
+                const float sp = powf_glibc(sc, 1 + 3 * m.refl * dlen / L.radius) * m.refl;
+                sumS = cadd(sumS, cscale(lc, sp));
+              }
+            }
+          }
+        }
+      }
+      sumL = cadd(mkc(S.amb_r, S.amb_g, S.amb_b), sumL);                      // Scene.cpp:186
+      const col color = mkc(m.r, m.g, m.b);
+      col fin;
+      if (diel)                                                                // Scene.cpp:189-201
+      {
+        RFX_CNT(C_DIELECTRIC);
+        const float aa = rayLen * normLen;
+        const float cosA = (aa > kVerySmall) ? clampf(dot(ray, neg(norm)) / aa, 0.0f, 1.0f) : 0.0f;
+        const float r = 0.2f + 0.8f * powf_glibc(1.0f - cosA, 3.0f);
+        fin = cadd(cmul(cscale(color, 1.0f - r), sumL), sumS);
+        fin = cmul(fin, mulc);
+        mulc = cscale(mulc, r);
+      }
+      else                                                                     // Scene.cpp:202-212
+      {
+        RFX_CNT(C_METAL);
+        const float r = 0.8f;
+        fin = cadd(cmul(cscale(color, 1.0f - r), sumL), sumS);
+        fin = cmul(fin, mulc);
+        mulc = cmul(mulc, cscale(color, r));
+      }
+      pix = cclamp(cadd(pix, fin));                                            // Scene.cpp:215-216
+      if (mulc.r < 0.01f && mulc.g < 0.01f && mulc.b < 0.01f) break;          // Scene.cpp:219-220
+      RFX_CNT(C_CONTINUE);
+      origin = drop;                                                           // Scene.cpp:223-224
+      ray = add(normalized(reflv), mul(rd, 1.0f - m.refl));
+    }
+    else                                                                       // Scene.cpp:226-231
+    {
+      RFX_CNT(C_SKY);
+      pix = cclamp(cadd(pix, cmul(cmul(mulc, skybox_texel<STATS>(S, ray, cnt)), mkc(S.env_r, S.env_g, S.env_b))));
+      break;
+    }
+  }
+  return pix;
+}
+
+template <bool STATS>
+__device__ __forceinline__ void flush_counters(const FrameParams &P, Cnt &cnt)
+{
+  if constexpr (STATS)
+  {
+#pragma unroll
+    for (int k = 0; k < C_COUNT; ++k)
+    {
+      unsigned long long v = cnt.c[k];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+      if ((threadIdx.x & 63) == 0 && v) atomicAdd(&P.counters[k], v);
+    }
+  }
+}
+
+__device__ __forceinline__ uint32_t strip_row_to_y(uint32_t r, const FrameParams &P)
+{
+  if (P.nranks <= 1) return r;
+  const uint32_t blk = r / P.row_block, w = r % P.row_block;
+  return (blk * P.nranks + P.rank) * P.row_block + w;
+}
+
+__device__ __forceinline__ v3 load_rd(const FrameParams &P, uint64_t i)
+{
+  return mk(P.rd[i], P.rd[P.n_rd + i], P.rd[2 * P.n_rd + i]);
+}
+
+// one workgroup = 16x16 output pixels, one wave = an 8x8 tile (ray coherence)
+template <bool STATS>
+__global__ __launch_bounds__(256) void trace_kernel(DevScene S, FrameParams P)
+{
+  Cnt cnt;
+  if constexpr (STATS)
+  {
+#pragma unroll
+    for (int k = 0; k < C_COUNT; ++k) cnt.c[k] = 0;
+  }
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint32_t lx = (wave & 1u) * 8u + (lane & 7u), ly = (wave >> 1) * 8u + (lane >> 3);
+  const uint32_t gx = blockIdx.x * 16u + lx, gy = blockIdx.y * 16u + ly;
+  m33 view;
+  view.m11 = P.v11; view.m12 = P.v12; view.m13 = P.v13;
+  view.m21 = P.v21; view.m22 = P.v22; view.m23 = P.v23;
+  view.m31 = P.v31; view.m32 = P.v32; view.m33 = P.v33;
+  const v3 eye = mk(P.eye_x, P.eye_y, P.eye_z);
+
+  if (P.ss < 0)
+  {
+    // block preview (Render.cpp:158-172): only block corners inside the cursor span are traced;
+    // trace order = raster order of corners, so corner (cx, cy) is trace cy * bw + cx.
+    const uint32_t n = (uint32_t)(-P.ss);
+    const uint32_t bw = (P.W + n - 1) / n, bh = (P.H + n - 1) / n;
+    const uint32_t cx = gx, cy = gy + P.row0;
+    if (gy < P.grid_rows && cx < bw && cy < bh)
+    {
+      const uint32_t x = cx * n, y = cy * n;
+      const uint64_t p = (uint64_t)y * P.W + x;
+      if (p >= P.p_begin && p < P.p_end)
+      {
+        const v3 ray = mmul(view, mk((float)x - P.wh, (float)y - P.hh, P.rz));
+        const uint64_t ti = (uint64_t)cy * bw + cx - P.trace_base;
+        const col c = trace<STATS>(S, eye, ray, P.depth, load_rd(P, ti), cnt);
+        const uint32_t ex = min(P.W, x + n), ey = min(P.H, y + n);
+        const uint32_t a = argb(c);
+        for (uint32_t qy = y; qy < ey; ++qy)
+          for (uint32_t qx = x; qx < ex; ++qx)
+          {
+            float *d = P.img + ((size_t)qy * P.W + qx) * 3;
+            d[0] = c.r; d[1] = c.g; d[2] = c.b;
+            if (P.argb) P.argb[(size_t)qy * P.W + qx] = a;
+          }
+      }
+    }
+    flush_counters<STATS>(P, cnt);
+    return;
+  }
+
+  if (gx < P.W && gy < P.grid_rows)
+  {
+    const uint32_t x = gx;
+    const uint32_t y = P.nranks > 1 ? strip_row_to_y(gy, P) : gy + P.row0;
+    const uint32_t orow = P.nranks > 1 ? gy : y;
+    const uint64_t p = (uint64_t)y * P.W + x;
+    if (p >= P.p_begin && p < P.p_end)
+    {
+      const uint64_t pr = p - P.p_begin;
+      const float rx = (float)x - P.wh, ry = (float)y - P.hh;                     // Render.cpp:152-153
+      float rndx = 0.0f, rndy = 0.0f;
+      if (P.additive)                                                              // Render.cpp:177-178
+      {
+        const uint32_t s1 = lcg_jump(P.jitter_seed, 2 * pr + 1);
+        rndx = (float)lcg_out(s1) / (float)0x7FFF;
+        rndy = (float)lcg_out(lcg_step(s1)) / (float)0x7FFF;
+      }
+      const int ss = P.ss;
+      const float ssf = (float)ss;
+      col fin = mkc(0.0f, 0.0f, 0.0f);
+      for (int sx = 0; sx < ss; ++sx)                                              // Render.cpp:181-187
+        for (int sy = 0; sy < ss; ++sy)
+        {
+          v3 ray = mk(rx + (float)sx / ssf + rndx, ry + (float)sy / ssf + rndy, P.rz);
+          ray = mmul(view, ray);
+          const uint64_t ti = pr * (uint64_t)(ss * ss) + (uint64_t)(sx * ss + sy);
+          fin = cadd(fin, trace<STATS>(S, eye, ray, P.depth, load_rd(P, ti), cnt));
+        }
+      const float sq = (float)(ss * ss);                                           // Render.cpp:189
+      if (fabsf(sq) > kVerySmall) fin = mkc(fin.r / sq, fin.g / sq, fin.b / sq);
+      const size_t o = (size_t)orow * P.W + x;
+      float *d = P.img + o * 3;
+      col out = fin;
+      if (P.accumulate) out = mkc(d[0] + fin.r, d[1] + fin.g, d[2] + fin.b);        // Render.cpp:191-194
+      d[0] = out.r; d[1] = out.g; d[2] = out.b;
+      if (P.argb) P.argb[o] = argb(out);                                           // Render::copyImage
+    }
+  }
+  flush_counters<STATS>(P, cnt);
+}
+
+// ------------------------------------------------------------- RNG pre-pass
+constexpr int kTriplesPerThread = 16;
+constexpr int kRngBlock = 256;
+constexpr uint64_t kTriplesPerBlock = (uint64_t)kTriplesPerThread * kRngBlock;
+
+__device__ __forceinline__ bool triple(uint32_t &s, float &x, float &y, float &z)
+{
+  const uint32_t s1 = lcg_step(s), s2 = lcg_step(s1), s3 = lcg_step(s2);
+  s = s3;
+  x = rand_component(lcg_out(s1));
+  y = rand_component(lcg_out(s2));
+  z = rand_component(lcg_out(s3));
+  return !(x * x + y * y + z * z > 1.f);                                        // Vector3.cpp:186
+}
+
+__global__ __launch_bounds__(kRngBlock) void rng_count(const uint32_t *seed, uint32_t *blk_cnt)
+{
+  const uint64_t t = (uint64_t)blockIdx.x * kRngBlock + threadIdx.x;
+  uint32_t s = lcg_jump(*seed, 3ull * kTriplesPerThread * t);
+  uint32_t c = 0;
+  float x, y, z;
+#pragma unroll 4
+  for (int j = 0; j < kTriplesPerThread; ++j) c += triple(s, x, y, z) ? 1u : 0u;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
+  __shared__ uint32_t wsum[kRngBlock / 64];
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0)
+  {
+    uint32_t tot = 0;
+    for (int w = 0; w < kRngBlock / 64; ++w) tot += wsum[w];
+    blk_cnt[blockIdx.x] = tot;
+  }
+}
+
+// single workgroup: exclusive scan of block counts; flags a short stream
+__global__ __launch_bounds__(1024) void rng_scan(const uint32_t *blk_cnt, uint32_t nblk, uint64_t *blk_off,
+                                                 uint64_t need, int *err)
+{
+  __shared__ uint64_t part[1024];
+  const uint32_t per = (nblk + 1023) / 1024;
+  const uint32_t b0 = threadIdx.x * per, b1 = min(nblk, b0 + per);
+  uint64_t sum = 0;
+  for (uint32_t b = b0; b < b1; ++b) sum += blk_cnt[b];
+  part[threadIdx.x] = sum;
+  __syncthreads();
+  for (uint32_t off = 1; off < 1024; off <<= 1)
+  {
+    const uint64_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
+    __syncthreads();
+    part[threadIdx.x] += v;
+    __syncthreads();
+  }
+  uint64_t run = part[threadIdx.x] - sum;
+  for (uint32_t b = b0; b < b1; ++b)
+  {
+    blk_off[b] = run;
+    run += blk_cnt[b];
+  }
+  if (threadIdx.x == 1023 && part[1023] < need) *err = 1;
+}
+
+__global__ __launch_bounds__(kRngBlock) void rng_emit(const uint32_t *seed, const uint64_t *blk_off, uint64_t need,
+                                                      float *rd, uint64_t n_rd, uint32_t *next_seed)
+{
+  const uint64_t t = (uint64_t)blockIdx.x * kRngBlock + threadIdx.x;
+  const uint32_t s0 = lcg_jump(*seed, 3ull * kTriplesPerThread * t);
+  uint32_t s = s0, c = 0;
+  float x, y, z;
+#pragma unroll 4
+  for (int j = 0; j < kTriplesPerThread; ++j) c += triple(s, x, y, z) ? 1u : 0u;
+  // exclusive scan of c across the workgroup
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t inc = c;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1)
+  {
+    const uint32_t v = __shfl_up(inc, off, 64);
+    if (lane >= (uint32_t)off) inc += v;
+  }
+  __shared__ uint32_t wsum[kRngBlock / 64];
+  if (lane == 63) wsum[threadIdx.x >> 6] = inc;
+  __syncthreads();
+  uint32_t wbase = 0;
+  for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) wbase += wsum[w];
+  uint64_t idx = blk_off[blockIdx.x] + wbase + (inc - c);
+  if (idx >= need) return;
+  s = s0;
+  for (int j = 0; j < kTriplesPerThread; ++j)
+  {
+    if (triple(s, x, y, z))
+    {
+      if (idx < need)
+      {
+        rd[idx] = x; rd[n_rd + idx] = y; rd[2 * n_rd + idx] = z;
+        if (idx == need - 1) *next_seed = s;                                    // stream state after trace need-1
+      }
+      ++idx;
+    }
+  }
+}
+
+}  // namespace rfx
+
+// ------------------------------------------------------------- launchers (library-internal)
+namespace rfx {
+
+uint64_t rng_blocks_for(uint64_t traces)
+{
+  // >= 2x the expected 1.91 triples per trace, plus slack; the scan flags a short stream
+  const uint64_t triples = 2 * traces + 65536;
+  return (triples + kTriplesPerBlock - 1) / kTriplesPerBlock;
+}
+
+hipError_t launch_rng(const uint32_t *d_seed, uint32_t *d_next_seed, uint64_t traces, float *d_rd, uint64_t n_rd,
+                      uint32_t *d_blk_cnt, uint64_t *d_blk_off, int *d_err, hipStream_t st)
+{
+  const uint64_t nblk = rng_blocks_for(traces);
+  hipLaunchKernelGGL(rng_count, dim3((uint32_t)nblk), dim3(kRngBlock), 0, st, d_seed, d_blk_cnt);
+  hipLaunchKernelGGL(rng_scan, dim3(1), dim3(1024), 0, st, d_blk_cnt, (uint32_t)nblk, d_blk_off, traces, d_err);
+  hipLaunchKernelGGL(rng_emit, dim3((uint32_t)nblk), dim3(kRngBlock), 0, st, d_seed, d_blk_off, traces, d_rd, n_rd,
+                     d_next_seed);
+  return hipGetLastError();
+}
+
+hipError_t launch_trace(const DevScene &S, const FrameParams &P, bool stats, hipStream_t st)
+{
+  const uint32_t cols = P.ss < 0 ? (P.W + (uint32_t)(-P.ss) - 1) / (uint32_t)(-P.ss) : P.W;
+  const dim3 grid((cols + 15) / 16, (P.grid_rows + 15) / 16);
+  if (stats)
+    hipLaunchKernelGGL(trace_kernel<true>, grid, dim3(256), 0, st, S, P);
+  else
+    hipLaunchKernelGGL(trace_kernel<false>, grid, dim3(256), 0, st, S, P);
+  return hipGetLastError();
+}
+
+}  // namespace rfx

@@ -1,0 +1,153 @@
+// Float math of ReflaxMan's L0 value types, restated operation-for-operation so
+// the device kernels (gfx950) and the host-side scene precompute produce the
+// reference's exact IEEE results.  Compile with -ffp-contract=off and without
+// fast-math: no FMA contraction, correctly rounded '/' and sqrtf, denormals kept.
+//
+// Citations: /root/reference/src/common/<file>:<line>.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define RFX_HD __host__ __device__ __forceinline__
+#else
+#include <math.h>
+#define RFX_HD static inline
+#endif
+
+#pragma clang fp contract(off)
+
+namespace rfx {
+
+// trace_math.h:17-18 (sqrtf(FLT_MIN) == 2^-63 exactly)
+constexpr float kVerySmall = 1.0842021724855044e-19f;
+constexpr float kDelta = 0.0001f;
+constexpr float kFltEpsilon = 1.1920928955078125e-07f;
+constexpr float kFltMax = 3.402823466e+38f;
+
+struct v3 { float x, y, z; };
+struct col { float r, g, b; };
+// Matrix33 element order _11.._33 (Matrix33.h:13-22)
+struct m33 { float m11, m12, m13, m21, m22, m23, m31, m32, m33; };
+
+RFX_HD v3 mk(float x, float y, float z) { v3 v; v.x = x; v.y = y; v.z = z; return v; }
+RFX_HD v3 add(v3 a, v3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }          // Vector3.cpp:106
+RFX_HD v3 sub(v3 a, v3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }          // Vector3.cpp:111
+RFX_HD v3 mul(v3 a, float f) { return mk(a.x * f, a.y * f, a.z * f); }              // Vector3.cpp:116,121
+RFX_HD v3 neg(v3 a) { return mk(-a.x, -a.y, -a.z); }                                 // Vector3.cpp:166
+RFX_HD float dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }          // Vector3.cpp:126
+RFX_HD float sqlen(v3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }              // Vector3.cpp:48
+RFX_HD float len(v3 a) { return sqrtf(a.x * a.x + a.y * a.y + a.z * a.z); }         // Vector3.cpp:43
+RFX_HD v3 cross(v3 a, v3 b)                                                          // Vector3.cpp:138
+{
+  return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+RFX_HD v3 divv(v3 a, float f)                                                        // Vector3.cpp:143-151
+{
+  if (fabsf(f) > kVerySmall) return mk(a.x / f, a.y / f, a.z / f);
+  return a;
+}
+// Vector3::normalized (Vector3.cpp:63-72) == Tracemath::normalize (trace_math.cpp:3-12)
+RFX_HD v3 normalized(v3 a)
+{
+  const float l = len(a);
+  if (l > kVerySmall) return divv(a, l);
+  return a;
+}
+// Tracemath::reflect (trace_math.cpp:14-23): v - (2n) * ((v.n) / (n.n))
+RFX_HD v3 reflect(v3 v, v3 n)
+{
+  const float dn = dot(n, n);
+  if (dn > kVerySmall) return sub(v, mul(mul(n, 2.0f), dot(v, n) / dn));
+  return v;
+}
+RFX_HD float clampf(float v, float lo, float hi) { return v < lo ? lo : v > hi ? hi : v; } // trace_math.h:24
+
+// Matrix33(u, v, n): columns (Matrix33.cpp:10-15)
+RFX_HD m33 from_cols(v3 u, v3 v, v3 n)
+{
+  m33 m;
+  m.m11 = u.x; m.m12 = v.x; m.m13 = n.x;
+  m.m21 = u.y; m.m22 = v.y; m.m23 = n.y;
+  m.m31 = u.z; m.m32 = v.z; m.m33 = n.z;
+  return m;
+}
+// Matrix33 * Vector3 (Matrix33.cpp:230-235)
+RFX_HD v3 mmul(const m33 &m, v3 v)
+{
+  return mk(v.x * m.m11 + v.y * m.m12 + v.z * m.m13,
+            v.x * m.m21 + v.y * m.m22 + v.z * m.m23,
+            v.x * m.m31 + v.y * m.m32 + v.z * m.m33);
+}
+// Matrix33::invert (Matrix33.cpp:50-79)
+RFX_HD m33 inverted(const m33 &a)
+{
+  const float d = a.m11 * (a.m22 * a.m33 - a.m32 * a.m23) +
+                  a.m21 * (a.m32 * a.m13 - a.m12 * a.m33) +
+                  a.m31 * (a.m12 * a.m23 - a.m13 * a.m22);
+  m33 r;
+  if (fabsf(d) > kVerySmall)
+  {
+    r.m11 = (a.m22 * a.m33 - a.m23 * a.m32) / d;
+    r.m12 = (a.m13 * a.m32 - a.m12 * a.m33) / d;
+    r.m13 = (a.m12 * a.m23 - a.m13 * a.m22) / d;
+    r.m21 = (a.m23 * a.m31 - a.m21 * a.m33) / d;
+    r.m22 = (a.m11 * a.m33 - a.m13 * a.m31) / d;
+    r.m23 = (a.m13 * a.m21 - a.m11 * a.m23) / d;
+    r.m31 = (a.m21 * a.m32 - a.m22 * a.m31) / d;
+    r.m32 = (a.m12 * a.m31 - a.m11 * a.m32) / d;
+    r.m33 = (a.m11 * a.m22 - a.m12 * a.m21) / d;
+  }
+  else
+  {
+    r.m11 = 1; r.m12 = 0; r.m13 = 0; r.m21 = 0; r.m22 = 1; r.m23 = 0; r.m31 = 0; r.m32 = 0; r.m33 = 1;
+  }
+  return r;
+}
+
+// Color (Color.cpp)
+RFX_HD col mkc(float r, float g, float b) { col c; c.r = r; c.g = g; c.b = b; return c; }
+RFX_HD col cadd(col a, col b) { return mkc(a.r + b.r, a.g + b.g, a.b + b.b); }      // :78
+RFX_HD col cmul(col a, col b) { return mkc(a.r * b.r, a.g * b.g, a.b * b.b); }      // :108
+RFX_HD col cscale(col a, float f) { return mkc(a.r * f, a.g * f, a.b * f); }        // :88,93
+RFX_HD col cclamp(col a)                                                              // :119-124
+{
+  return mkc(clampf(a.r, 0.0f, 1.0f), clampf(a.g, 0.0f, 1.0f), clampf(a.b, 0.0f, 1.0f));
+}
+RFX_HD col from_argb(uint32_t c)                                                      // :9-14
+{
+  return mkc((float)((c >> 16) & 0xFFu) / 255.0f, (float)((c >> 8) & 0xFFu) / 255.0f, (float)(c & 0xFFu) / 255.0f);
+}
+// Color::argb (Color.cpp:114-117, Color.h:11-15): trunc(c * 255.999f), low byte, alpha 0.
+// Out-of-range sums (additive copyImage) take the low byte of the int32 conversion, as x86-64 g++ does.
+RFX_HD uint32_t q8(float f)
+{
+  const float lim = 2147483648.0f;
+  const int32_t i = (f < lim && f > -lim) ? (int32_t)f : (int32_t)0x80000000;
+  return (uint32_t)(uint8_t)i;
+}
+RFX_HD uint32_t argb(col c)
+{
+  return q8(c.r * 255.999f) << 16 | q8(c.g * 255.999f) << 8 | q8(c.b * 255.999f);
+}
+
+// LCG (trace_math.h:34-39): s = 214013 s + 2531011 (mod 2^32), out (s >> 16) & 0x7FFF
+RFX_HD uint32_t lcg_step(uint32_t s) { return 214013u * s + 2531011u; }
+RFX_HD uint32_t lcg_out(uint32_t s) { return (s >> 16) & 0x7FFFu; }
+// s advanced by n steps: affine map (A, C) composed by binary powering
+RFX_HD uint32_t lcg_jump(uint32_t s, uint64_t n)
+{
+  uint32_t a = 214013u, c = 2531011u, A = 1u, C = 0u;
+  while (n)
+  {
+    if (n & 1u) { A = a * A; C = a * C + c; }
+    c = a * c + c;
+    a = a * a;
+    n >>= 1;
+  }
+  return A * s + C;
+}
+// one component of Vector3::randomInsideSphere (Vector3.cpp:182-184)
+RFX_HD float rand_component(uint32_t k) { return (float)k / ((float)0x7FFF / 2) - 1.f; }
+
+}  // namespace rfx

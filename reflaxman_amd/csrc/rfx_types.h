@@ -1,0 +1,75 @@
+// POD layouts shared by the host C-ABI (rfx_host.cpp) and the gfx950 kernels
+// (rfx_kernels.hip).  All device arrays are structure-of-arrays, 16-B aligned,
+// and walked in wave-uniform order by the trace kernel, so the compiler serves
+// them through the scalar cache (s_load_dwordx4) rather than per-lane loads.
+#pragma once
+#include <stdint.h>
+
+namespace rfx {
+
+// per-frame event counters (same order as oracle/rfx_oracle.h ORC_*)
+enum Counter {
+  C_RAYS = 0, C_SEGMENTS,
+  C_SPH_TESTS, C_SPH_D, C_SPH_T,
+  C_TRI_TESTS, C_TRI_Z, C_TRI_T, C_TRI_IN, C_TRI_D,
+  C_HIT_SPH, C_HIT_TRI,
+  C_SH_SPH_TESTS, C_SH_SPH_D, C_SH_SPH_T,
+  C_SH_TRI_TESTS, C_SH_TRI_Z, C_SH_TRI_T, C_SH_TRI_IN,
+  C_L_EVAL, C_L_FACING, C_L_LIT, C_L_SPEC, C_L_POW,
+  C_DIELECTRIC, C_METAL, C_CONTINUE, C_SKY,
+  C_TEX_BILINEAR, C_TEX_CHECKER, C_TEX_OTHER,
+  C_COUNT
+};
+
+struct alignas(16) SphereGeo { float cx, cy, cz, sq_radius; };      // Sphere.cpp:9-20
+struct alignas(16) MatRec { float r, g, b, refl; };                 // Material.h:9-11 (transparency unused)
+struct alignas(16) TriGeo {                                          // Triangle.cpp:11-21
+  float v0x, v0y, v0z, pad0;
+  float a11, a12, a13, a21, a22, a23, a31, a32, a33, pad1, pad2, pad3;  // axTrans (inverted)
+};
+struct alignas(16) TriShade {                                        // Triangle.cpp:110-120
+  float nx, ny, nz, tu0;
+  float t11, t12, t21, t22;   // tuvTrans _11 _12 _21 _22 (_13 = _23 = 0 by construction)
+  float tv0; int32_t tex; int32_t dielectric; int32_t obj;
+};
+struct alignas(16) LightRec { float ox, oy, oz, radius, r, g, b, power; }; // OmniLight.h
+struct alignas(16) TexRec { uint32_t offset, w, h, pad; };
+
+struct DevScene {
+  const SphereGeo *sph_geo;   // n_sph
+  const MatRec *sph_mat;      // n_sph
+  const int32_t *sph_info;    // n_sph x2: {object index, dielectric}
+  const TriGeo *tri_geo;      // n_tri
+  const TriShade *tri_shade;  // n_tri
+  const MatRec *tri_mat;      // n_tri
+  const LightRec *lights;     // n_light
+  const TexRec *texs;         // n_tex
+  const uint32_t *texels;     // texel pool, ARGB
+  int32_t n_sph, n_tri, n_light, skybox_tex;
+  float amb_r, amb_g, amb_b;  // diffLightColor * diffLightPower (Scene.cpp:186, host-folded)
+  float env_r, env_g, env_b;  // envColor (Scene.cpp:12,55)
+  float half_tile_w, half_tile_h;  // Skybox.cpp:21-37
+};
+
+struct FrameParams {
+  float eye_x, eye_y, eye_z;
+  float v11, v12, v13, v21, v22, v23, v31, v32, v33;  // Render::renderCameraView
+  float rz, wh, hh;             // Render.cpp:148-150
+  uint32_t W, H;
+  int32_t depth, ss;            // reflectNum, sampleNum
+  int32_t accumulate;           // additiveCounter > 1 (Render.cpp:191)
+  int32_t additive;             // jitter on (Render.cpp:177-178)
+  uint32_t jitter_seed;         // Render.cpp stream state at frame start
+  uint32_t row_block, rank, nranks;  // block-cyclic row strips (nranks == 1: whole frame)
+  uint32_t grid_rows;           // rows (ss > 0) or corner rows (ss < 0) covered by the grid
+  uint32_t row0;                // first frame row (ss > 0) / corner row (ss < 0) of the grid (nranks == 1)
+  uint64_t p_begin, p_end;      // raster pixel range of this call (Render::renderNext cursor span)
+  uint64_t trace_base;          // trace index of the first trace in the range (block mode: corner count)
+  float *img;                   // W x H x 3 frame (nranks == 1) or strip_rows x W x 3 (in/out when accumulate)
+  uint32_t *argb;               // same shape, or null
+  const float *rd;              // randDir SoA: rd[i], rd[n_rd + i], rd[2 n_rd + i]
+  uint64_t n_rd;
+  unsigned long long *counters; // C_COUNT u64, stats build only
+};
+
+}  // namespace rfx

@@ -1,0 +1,51 @@
+// Test harness: product powf restatement (reflaxman_amd/csrc/rfx_powf.h) vs the
+// live glibc powf of this host.  Exit 0 iff bit-identical on every sample.
+#include <initializer_list>
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include "rfx_powf.h"
+
+static unsigned long long bad = 0, total = 0;
+static void check(float x, float y)
+{
+  float a = powf(x, y), b = rfx::powf_glibc(x, y);
+  unsigned ua, ub;
+  memcpy(&ua, &a, 4); memcpy(&ub, &b, 4);
+  ++total;
+  if (ua != ub && !(isnan(a) && isnan(b)))
+  {
+    if (bad < 10) fprintf(stderr, "MISMATCH x=%a y=%a libm=%a ours=%a\n", x, y, a, b);
+    ++bad;
+  }
+}
+
+int main(int argc, char **argv)
+{
+  unsigned long long n_random = argc > 1 ? strtoull(argv[1], 0, 10) : 10000000ull;
+  unsigned stride = argc > 2 ? (unsigned)strtoul(argv[2], 0, 10) : 7;
+  // Scene.cpp:196 -- Fresnel: every stride-th float in [0, 1], y = 3
+  for (unsigned u = 0; u <= 0x3f800000u; u += stride) { float x; memcpy(&x, &u, 4); check(x, 3.0f); }
+  check(1.0f, 3.0f); check(0.0f, 3.0f);
+  // Scene.cpp:175 -- specular: x in (2^-63, 1], y = 1 + 3*refl*len/r (1 .. ~200)
+  unsigned s = 12345u;
+  for (unsigned long long i = 0; i < n_random; ++i)
+  {
+    s = s * 1664525u + 1013904223u; unsigned ux = s;
+    s = s * 1664525u + 1013904223u; unsigned uy = s;
+    float x, y;
+    if (i & 1) { unsigned bits = 0x20000000u + ux % (0x3f800001u - 0x20000000u); memcpy(&x, &bits, 4); }
+    else x = (float)((ux >> 8) * (1.0 / 16777216.0));
+    y = 1.0f + (float)((uy >> 8) * (200.0 / 16777216.0));
+    if ((i & 7) == 3) y = 1.0f;
+    check(x, y);
+  }
+  // general special cases outside the renderer's domain
+  const float xs[] = {0.0f, -0.0f, 1.0f, -1.0f, 2.0f, -2.0f, 0.5f, 1e-40f, -1e-40f, 1e30f, INFINITY, -INFINITY, NAN, 3.0f, 1.5f};
+  const float ys[] = {0.0f, -0.0f, 1.0f, -1.0f, 2.0f, 3.0f, 0.5f, -0.5f, 100.0f, -100.0f, 1e10f, INFINITY, -INFINITY, NAN, 7.0f, -3.0f};
+  for (float x : xs) for (float y : ys) check(x, y);
+  for (int e = -149; e < 128; ++e) for (float y : {0.5f, 3.0f, 1.25f, -2.0f}) check(ldexpf(1.3f, e), y);
+  printf("%llu samples, %llu mismatches\n", total, bad);
+  return bad ? 1 : 0;
+}
