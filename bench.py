@@ -1,0 +1,281 @@
+#!/usr/bin/env python3
+"""bench.py -- Mrays/s of ReflaxMan's per-pixel trace loop on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Workload (BASELINE.json metric "Mrays/sec at 3840x2160 depth-8"): config C3 --
+the synth16 scene (16 spheres, ground + back-wall quads = 4 textured
+triangles, the default sun light => shadow rays), 3840x2160, depth 8, 1 spp,
+synthetic 512x512 TGA textures.  A step is one full frame of the hot path
+(Render::renderBegin + renderNext(W*H)): the RNG pre-pass, the trace kernel and
+the ARGB8 epilogue, inputs and outputs resident in HBM.  Every step renders
+the *next* frame of the reference's global random stream, as the reference app
+does.
+
+N > 1 (weak scaling): the frame grows with N at 16:9 (N=4 is C4, 7680x4320);
+rows are dealt to ranks in block-cyclic 8-row strips, each rank traces its
+strips and the ARGB8 strips are gathered to rank 0 over RCCL (xGMI) and
+un-interleaved on device.  value = traces of the whole frame / step time
+(max over ranks).
+
+Also reported: the trace kernel's algorithmic TFLOP/s against the FP32 VALU
+peak (roofline), its HIP-event time, full-frame parity (SHA-256 of the first
+frame vs the reference's, tests/golden/manifest.json), and the reference's own
+CPU path timed on a bounded sample of the same frame on one host core.
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import math
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Mrays/sec at 3840×2160 depth-8; max per-channel |Δ| vs CPU reference"
+SEED = 1350490027
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def frame_size(n: int, w0: int, h0: int):
+    if n == 1:
+        return w0, h0
+    s = math.sqrt(n)
+    return int(round(w0 * s)), int(round(h0 * s))
+
+
+def sha(b: bytes) -> str:
+    return hashlib.sha256(b).hexdigest()
+
+
+def ulp_diff(a: np.ndarray, b: np.ndarray) -> int:
+    ai = a.view(np.int32).astype(np.int64)
+    bi = b.view(np.int32).astype(np.int64)
+    ai = np.where(ai < 0, np.int64(-2 ** 31) - ai, ai)
+    bi = np.where(bi < 0, np.int64(-2 ** 31) - bi, bi)
+    return int(np.abs(ai - bi).max()) if a.size else 0
+
+
+def u8_diff(a: np.ndarray, b: np.ndarray) -> int:
+    ch = lambda x, s: ((x >> s) & 0xFF).astype(np.int32)
+    return int(max(np.abs(ch(a, s) - ch(b, s)).max() for s in (0, 8, 16))) if a.size else 0
+
+
+def cpu_baseline(desc, W, H, depth, gpu_rgb, gpu_argb, stride):
+    """The reference's CPU path (oracle/_ref/refharness, the unmodified sources) on every `stride`-th row of
+    the same frame, one host core; its rows are also compared with the GPU frame's."""
+    harness = os.path.join(ROOT, "oracle", "_ref", "refharness")
+    count = (H + stride - 1) // stride
+    with tempfile.TemporaryDirectory() as tmp:
+        scene_path = desc.write(tmp)
+        out = os.path.join(tmp, "rows")
+        if os.path.exists(harness):
+            kind = "reference"
+            r = subprocess.run([harness, "rows", scene_path, str(W), str(H), str(depth), "0", str(stride), str(count), out],
+                               env={**os.environ, "RFX_SPHERE_SEED": str(SEED)}, capture_output=True, text=True, timeout=600)
+            if r.returncode != 0:
+                raise RuntimeError("refharness failed: " + r.stderr)
+            info = json.loads(r.stdout.strip().splitlines()[-1])
+            rgb = np.fromfile(out + ".f32", np.float32).reshape(count, W, 3)
+            argb = np.fromfile(out + ".argb", np.uint32).reshape(count, W)
+            secs, px = info["trace_seconds"], info["traced_pixels"]
+        else:  # no reference build on this host: the C restatement (bit-exact port), one thread, contiguous band
+            kind = "port"
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import oracle as orc
+            count = min(count, 256)
+            y0 = (H - count) // 2
+            t0 = time.perf_counter()
+            rgb, argb = orc.render_band(desc, W, H, depth, y0, count, SEED, nthreads=1)
+            secs, px = time.perf_counter() - t0, W * count
+            stride, ys = 1, slice(y0, y0 + count)
+    ys = slice(0, count * stride, stride) if kind == "reference" else ys
+    g_rgb, g_argb = gpu_rgb[ys], gpu_argb[ys]
+    sample = (f"rows 0,{stride},..,{(count - 1) * stride} ({count} x {W} px) of the first frame" if kind == "reference"
+              else f"rows {ys.start}..{ys.stop - 1} of the first frame")
+    return {
+        "value": round(px / secs / 1e6, 4), "unit": "Mrays/s", "cores": 1, "kind": kind,
+        "sample": f"{sample}; {secs:.1f} s of single-thread trace time; "
+                  f"{subprocess.run(['nproc'], capture_output=True, text=True).stdout.strip()} host CPUs visible",
+    }, {"max_u8": u8_diff(g_argb, argb), "max_f32_ulp": ulp_diff(g_rgb, rgb), "pixels": int(px)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--scene", default="synth16")
+    ap.add_argument("--width", type=int, default=3840)
+    ap.add_argument("--height", type=int, default=2160)
+    ap.add_argument("--depth", type=int, default=8)
+    ap.add_argument("--row-block", type=int, default=8)
+    ap.add_argument("--cpu-stride", type=int, default=2, help="cpu_baseline samples every n-th row")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+
+    import torch
+    import torch.distributed as dist
+    from reflaxman_amd import _lib, metrics, scenes
+    from reflaxman_amd.render import Renderer, build_scene, make_frame
+
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    L = _lib.load()
+
+    W, H = frame_size(world, args.width, args.height)
+    depth, rb = args.depth, args.row_block
+    desc = scenes.get_scene(args.scene)
+    scene, cam = build_scene(desc)
+    rr = Renderer(device=local, sphere_seed=SEED)
+    rr.set_scene(scene)
+    stream = torch.cuda.current_stream()
+    rr.set_stream(stream.cuda_stream)
+
+    rows = L.rfx_strip_rows(H, rb, rank, world) if world > 1 else H
+    max_rows = max(L.rfx_strip_rows(H, rb, r, world) for r in range(world)) if world > 1 else H
+    img = torch.zeros(rows * W * 3, dtype=torch.float32, device=dev)
+    argb = torch.zeros(max_rows * W, dtype=torch.int32, device=dev)
+    frame = make_frame(cam, W, H, depth, 1, row_block=rb if world > 1 else 0, rank=rank, nranks=world)
+    traces = W * H
+    log(f"rank {rank}/{world}: {args.scene} {W}x{H} d{depth}, strip rows {rows}")
+
+    if world > 1:
+        gather_list = [torch.empty_like(argb) for _ in range(world)] if rank == 0 else None
+        full = torch.empty(H * W, dtype=torch.int32, device=dev) if rank == 0 else None
+        row_idx = []
+        if rank == 0:
+            for r in range(world):
+                n = L.rfx_strip_rows(H, rb, r, world)
+                row_idx.append(torch.tensor([L.rfx_strip_row_to_y(i, rb, r, world) for i in range(n)],
+                                            dtype=torch.int64, device=dev))
+
+    def step():
+        rr.render_frame(frame, img.data_ptr(), argb.data_ptr(), 0, stream.cuda_stream)
+        if world > 1:
+            dist.gather(argb, gather_list, dst=0)
+            if rank == 0:
+                fv = full.view(H, W)
+                for r in range(world):
+                    n = row_idx[r].numel()
+                    fv.index_copy_(0, row_idx[r], gather_list[r][: n * W].view(n, W))
+
+    # ---- frame 0 (from the reference's default seed): parity evidence + event counts
+    step()
+    torch.cuda.synchronize()
+    parity = {}
+    first_rgb = first_argb = None
+    if world == 1:
+        first_rgb = img.view(H, W, 3).cpu().numpy()
+        first_argb = argb[: H * W].view(H, W).cpu().numpy().view(np.uint32)
+        man = json.load(open(os.path.join(ROOT, "tests", "golden", "manifest.json")))["cases"]
+        key = f"hash_{args.scene}_{W}x{H}_d{depth}"
+        if key in man:
+            ok_f = sha(first_rgb.tobytes()) == man[key]["sha_f32"]
+            ok_a = sha(first_argb.tobytes()) == man[key]["sha_argb"]
+            parity["full_frame_vs_reference_sha256"] = {"f32": ok_f, "argb8": ok_a, "case": key}
+    counters = torch.zeros(_lib.RFX_NCOUNTERS, dtype=torch.int64, device=dev)
+    rr.render_frame(frame, img.data_ptr(), argb.data_ptr(), counters.data_ptr(), stream.cuda_stream)
+    torch.cuda.synchronize()
+    cnt = counters.cpu().numpy().astype(np.uint64)
+    if world > 1:
+        c = torch.tensor(cnt.astype(np.int64), device=dev)
+        dist.all_reduce(c)
+        cnt = c.cpu().numpy().astype(np.uint64)
+    work = metrics.summary(cnt)
+    flops_frame = work["flops"]
+
+    # ---- warmup, then K timed steps (barrier + synchronize on both sides)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    rr.get_timing()
+    rr.set_timing(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    pre_ms, trace_ms, nfr = rr.get_timing()
+    rr.set_timing(False)
+    if world > 1:
+        t = torch.tensor([elapsed, trace_ms / max(nfr, 1), pre_ms / max(nfr, 1)], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, trace_avg, pre_avg = t.tolist()
+    else:
+        trace_avg, pre_avg = trace_ms / max(nfr, 1), pre_ms / max(nfr, 1)
+
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+
+    ms_step = elapsed / args.steps * 1e3
+    mrays = traces * args.steps / elapsed / 1e6
+    # the trace kernel of one rank processes its strip: per-launch FLOPs = frame FLOPs / world (balanced strips)
+    flops_launch = flops_frame / world
+    achieved = flops_launch / (trace_avg * 1e-3) / 1e12
+    px_launch = rows * W
+    traffic = None
+    prof = os.path.join(ROOT, "profiles", "pmc_trace_kernel.json")
+    if os.path.exists(prof):
+        p = json.load(open(prof))
+        if p.get("config") == [args.scene, W, H, depth, world]:
+            traffic = p.get("hbm_bytes_per_launch")
+    out = {
+        "metric": METRIC, "value": round(mrays, 2), "unit": "Mrays/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": f"C3 {args.scene}: 16 spheres + 4 textured triangles + sun, {W}x{H}, depth {depth}, 1 spp"
+                               + (" (C4 family, weak-scaled 16:9 frame)" if world > 1 else ""),
+                   "scene": args.scene, "width": W, "height": H, "depth": depth, "spp": 1,
+                   "parallelism": f"row-strips{rb}x{world}" if world > 1 else "single-gpu"},
+        "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": metrics.PEAK_FP32_VALU_TFLOPS,
+                     "unit": "TFLOP/s", "frac": round(achieved / metrics.PEAK_FP32_VALU_TFLOPS, 4),
+                     "traffic": traffic, "kernel": "rfx::trace_kernel<false>",
+                     "flops_per_launch": int(flops_launch), "avg_launch_ms": round(trace_avg, 4),
+                     "frac_vs_nofma_peak": round(achieved / metrics.PEAK_FP32_NOFMA_TFLOPS, 4),
+                     "algo_hbm_bytes_per_launch": px_launch * metrics.ALGO_BYTES_PER_PIXEL,
+                     "algo_hbm_GBps": round(px_launch * metrics.ALGO_BYTES_PER_PIXEL / (trace_avg * 1e-3) / 1e9, 1)},
+        "phases_ms": {"rng_prepass": round(pre_avg, 4), "trace": round(trace_avg, 4)},
+        "work_per_ray": {k: round(v, 3) for k, v in work.items() if k != "flops"},
+        "parity": parity,
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        log("cpu_baseline: reference CPU path on a row sample of the same frame ...")
+        cb, delta = cpu_baseline(desc, W, H, depth, first_rgb, first_argb, args.cpu_stride)
+        out["cpu_baseline"] = cb
+        out["parity"]["sample_vs_cpu_reference"] = delta
+        out["max_abs_delta"] = {"u8": delta["max_u8"], "f32_ulp": delta["max_f32_ulp"]}
+        out["speedup_vs_cpu_1core"] = round(mrays / cb["value"], 1)
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -132,6 +132,12 @@ uint32_t rfx_strip_row_to_y(uint32_t r, uint32_t row_block, uint32_t rank, uint3
 int rfx_render_frame(rfx_renderer *r, const rfx_frame *frame, float *d_rgb, uint32_t *d_argb,
                      uint64_t *d_counters, void *stream);
 
+/* Optional per-phase timing of rfx_render_frame with HIP events recorded on the launch stream:
+ * enable, render, then read the summed device time (ms) of the RNG pre-pass and of the trace kernel
+ * over the frames since the last read (synchronises; resets the sums). */
+int rfx_renderer_set_timing(rfx_renderer *r, int enable);
+int rfx_renderer_get_timing(rfx_renderer *r, double *prepass_ms, double *trace_ms, uint64_t *frames);
+
 /* host-buffer convenience for callers without device memory of their own (PCIe-inclusive):
  * rgb: host W*H*3 (in/out), argb: host W*H or NULL.  Partitioning fields must be rank 0 of 1. */
 int rfx_render_frame_host(rfx_renderer *r, const rfx_frame *frame, float *rgb, uint32_t *argb,

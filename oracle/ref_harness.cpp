@@ -20,6 +20,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <ctime>
 #include <string>
 #include <vector>
 
@@ -195,6 +196,47 @@ int main(int argc, char **argv)
       }
     write_file(std::string(argv[8]) + ".f32", &rgb[0], rgb.size() * 4);
     write_file(std::string(argv[8]) + ".argb", &argb[0], argb.size() * 4);
+    return 0;
+  }
+  if (mode == "rows")
+  {
+    // rows SCENE W H DEPTH Y0 STRIDE COUNT OUT : rows Y0, Y0+STRIDE, ... of an ss=1 frame (bounded,
+    // representative sample for the timed CPU baseline).  The stream is advanced over the skipped rows
+    // outside the timed region; stdout reports the trace time of the sampled rows only.
+    if (argc != 10) die("rows SCENE W H DEPTH Y0 STRIDE COUNT OUT");
+    load_scene(r, argv[2]);
+    unsigned W = atoi(argv[3]), H = atoi(argv[4]);
+    int depth = atoi(argv[5]);
+    unsigned y0 = atoi(argv[6]), stride = atoi(argv[7]), count = atoi(argv[8]);
+    if (!stride || y0 + (size_t)(count - 1) * stride >= H) die("rows out of frame");
+    const float rz = float(W) / 2.0f / tanf(r.camera.fov / 2.0f);
+    const float wh = W / 2.0f, hh = H / 2.0f;
+    std::vector<float> rgb((size_t)W * count * 3);
+    std::vector<ARGB> argb((size_t)W * count);
+    double traced = 0.0;
+    unsigned next = 0;  // next row whose randDirs have not been drawn
+    for (unsigned k = 0; k < count; ++k)
+    {
+      const unsigned y = y0 + k * stride;
+      for (size_t i = (size_t)next * W; i < (size_t)y * W; ++i) Vector3::randomInsideSphere(1.0f);
+      timespec t0, t1;
+      clock_gettime(CLOCK_MONOTONIC, &t0);
+      for (unsigned x = 0; x < W; ++x)
+      {
+        Vector3 ray(float(x) - wh, float(y) - hh, rz);
+        ray = r.camera.view * ray;
+        Color c = r.scene.trace(r.camera.eye, ray, depth);
+        size_t i = (size_t)k * W + x;
+        rgb[i * 3 + 0] = c.r; rgb[i * 3 + 1] = c.g; rgb[i * 3 + 2] = c.b;
+        argb[i] = c.argb();
+      }
+      clock_gettime(CLOCK_MONOTONIC, &t1);
+      traced += (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec);
+      next = y + 1;
+    }
+    write_file(std::string(argv[9]) + ".f32", &rgb[0], rgb.size() * 4);
+    write_file(std::string(argv[9]) + ".argb", &argb[0], argb.size() * 4);
+    printf("{\"traced_pixels\": %llu, \"trace_seconds\": %.6f}\n", (unsigned long long)W * count, traced);
     return 0;
   }
   if (mode == "rand")

@@ -276,12 +276,13 @@ static col texel_xy(const tex_t *t, uint32_t x, uint32_t y)                 /* T
   return from_argb(t->texels[x + t->w * y]);
 }
 
-static col texel_uv(const tex_t *t, float u, float v, uint64_t *cnt)        /* Texture.cpp:231-269 */
+/* *cat receives the ORC_TEX_* category of the sample (for the event counters) */
+static col texel_uv(const tex_t *t, float u, float v, int *cat)             /* Texture.cpp:231-269 */
 {
-  if (u < 0.0f || u > 1.0f || v < 0.0f || v > 1.0f) { if (cnt) cnt[ORC_TEX_OTHER]++; return C(0, 0, 0); }
+  if (u < 0.0f || u > 1.0f || v < 0.0f || v > 1.0f) { *cat = ORC_TEX_OTHER; return C(0, 0, 0); }
   if (!t || !t->texels)
   {
-    if (cnt) cnt[ORC_TEX_CHECKER]++;
+    *cat = ORC_TEX_CHECKER;
     return (((int)(u * 50) % 2) ^ ((int)(v * 50) % 2)) ? C(0.5f, 0.5f, 0.5f) : C(0.75f, 0.75f, 0.75f);
   }
   const float fx = clampf01(u, 0.0f, 1.0f - FLT_EPSILON) * (float)t->w;
@@ -289,14 +290,14 @@ static col texel_uv(const tex_t *t, float u, float v, uint64_t *cnt)        /* T
   const uint32_t x = (uint32_t)fx, y = (uint32_t)fy;
   if (x < t->w - 1 && y < t->h - 1)
   {
-    if (cnt) cnt[ORC_TEX_BILINEAR]++;
+    *cat = ORC_TEX_BILINEAR;
     const col c00 = texel_xy(t, x, y), c01 = texel_xy(t, x, y + 1);
     const col c10 = texel_xy(t, x + 1, y), c11 = texel_xy(t, x + 1, y + 1);
     const float uf = fx - floorf(fx), vf = fy - floorf(fy);
     const float uo = 1 - uf, vo = 1 - vf;
     return cadd(cscale(cadd(cscale(c00, uo), cscale(c10, uf)), vo), cscale(cadd(cscale(c01, uo), cscale(c11, uf)), vf));
   }
-  if (cnt) cnt[ORC_TEX_OTHER]++;
+  *cat = ORC_TEX_OTHER;
   return texel_xy(t, (uint32_t)fx, (uint32_t)fy);
 }
 
@@ -329,11 +330,15 @@ static col skybox_texel(const orc_scene *s, v3 ray, uint64_t *cnt)        /* Sky
     else { u = uBottom + x / ay * hw; v = vBottom + z / ay * hh; }
   }
   const tex_t *t = s->skybox_tex >= 0 ? &s->texs[s->skybox_tex] : NULL;
-  return texel_uv(t, u, v, cnt);
+  int cat;
+  const col c = texel_uv(t, u, v, &cat);
+  if (cnt) cnt[cat]++;
+  return c;
 }
 
 /* ---- primitives ------------------------------------------------------------- */
-typedef struct { v3 drop, norm, refl; float dist; mat_t mat; } hit_t;
+/* tex_cat: ORC_TEX_* category of a textured triangle's sample, -1 if untextured */
+typedef struct { v3 drop, norm, refl; float dist; mat_t mat; int tex_cat; } hit_t;
 
 /* Sphere::trace (Sphere.cpp:44-85); out == NULL -> any-hit query */
 static int sphere_trace(const sphere_t *sp, v3 o, v3 ray, hit_t *out, uint64_t *cnt, int shadow)
@@ -357,6 +362,7 @@ static int sphere_trace(const sphere_t *sp, v3 o, v3 ray, hit_t *out, uint64_t *
       {
         if (out)
         {
+          out->tex_cat = -1;
           out->dist = dist;
           out->drop = vadd(o, full);
           out->norm = vsub(out->drop, sp->center);
@@ -400,10 +406,13 @@ static int tri_trace(const orc_scene *s, const tri_t *tr, v3 o, v3 ray, hit_t *o
             out->refl = tm_reflect(full, tr->norm);
             out->dist = sqrtf(sq);
             out->mat = tr->mat;
+            out->tex_cat = -1;
             if (tr->tex >= 0)
             {
+              /* the reference samples the texel for every candidate hit; only the winner's is used,
+                 so only the winner's sample is counted (scene_trace) -- the GPU samples the winner only */
               const v3 tv = m_mul(&tr->tuv, V(u, v, 0));
-              out->mat.color = texel_uv(&s->texs[tr->tex], tr->tu0 + tv.x, tr->tv0 + tv.y, cnt);
+              out->mat.color = texel_uv(&s->texs[tr->tex], tr->tu0 + tv.x, tr->tv0 + tv.y, &out->tex_cat);
             }
           }
           return 1;
@@ -468,7 +477,11 @@ static col scene_trace(const orc_scene *s, v3 origin, v3 ray, int depth, v3 rand
     }
     if (hitObj >= 0)
     {
-      if (cnt) cnt[s->objs[hitObj].kind == 0 ? ORC_HIT_SPH : ORC_HIT_TRI]++;
+      if (cnt)
+      {
+        cnt[s->objs[hitObj].kind == 0 ? ORC_HIT_SPH : ORC_HIT_TRI]++;
+        if (best.tex_cat >= 0) cnt[best.tex_cat]++;
+      }
       const v3 drop = best.drop, norm = best.norm, reflect = best.refl;
       const mat_t *dm = &best.mat;
       const float rayLen = vlen(ray), normLen = vlen(norm), reflectLen = vlen(reflect);
@@ -837,7 +850,8 @@ void orc_kat_texture(uint32_t tw, uint32_t th, const uint32_t *argb, const float
   tex_t t = {argb ? tw : 0, argb ? th : 0, (uint32_t *)argb};
   for (uint64_t i = 0; i < n; ++i)
   {
-    col c = texel_uv(&t, uv[i * 2], uv[i * 2 + 1], NULL);
+    int cat;
+    col c = texel_uv(&t, uv[i * 2], uv[i * 2 + 1], &cat);
     out[i * 3] = c.r; out[i * 3 + 1] = c.g; out[i * 3 + 2] = c.b;
   }
 }

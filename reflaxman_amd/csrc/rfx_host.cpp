@@ -387,7 +387,53 @@ struct rfx_renderer {
   uint32_t *d_blk_cnt = nullptr; uint64_t *d_blk_off = nullptr; uint64_t blk_cap = 0;
   // host staging for rfx_render_frame_host
   float *d_img = nullptr; uint32_t *d_argb = nullptr; uint64_t *d_cnt = nullptr; size_t img_cap = 0;
+  // per-phase event timing: triples {start, after pre-pass, after trace}
+  bool timing = false;
+  std::vector<hipEvent_t> events;
+  size_t events_used = 0;
 };
+
+static int timing_event(rfx_renderer *r, hipStream_t st)
+{
+  if (!r->timing) return RFX_OK;
+  if (r->events_used == r->events.size())
+  {
+    hipEvent_t e;
+    HIP_CHECK(hipEventCreate(&e));
+    r->events.push_back(e);
+  }
+  HIP_CHECK(hipEventRecord(r->events[r->events_used++], st));
+  return RFX_OK;
+}
+
+extern "C" int rfx_renderer_set_timing(rfx_renderer *r, int enable)
+{
+  if (!r) return fail(RFX_ERR_ARG, "set_timing: null renderer");
+  r->timing = enable != 0;
+  r->events_used = 0;
+  return RFX_OK;
+}
+
+extern "C" int rfx_renderer_get_timing(rfx_renderer *r, double *prepass_ms, double *trace_ms, uint64_t *frames)
+{
+  if (!r) return fail(RFX_ERR_ARG, "get_timing: null renderer");
+  double pre = 0.0, tr = 0.0;
+  const size_t n = r->events_used / 3;
+  if (n) HIP_CHECK(hipEventSynchronize(r->events[3 * n - 1]));
+  for (size_t i = 0; i < n; ++i)
+  {
+    float a = 0.0f, b = 0.0f;
+    HIP_CHECK(hipEventElapsedTime(&a, r->events[3 * i], r->events[3 * i + 1]));
+    HIP_CHECK(hipEventElapsedTime(&b, r->events[3 * i + 1], r->events[3 * i + 2]));
+    pre += a;
+    tr += b;
+  }
+  r->events_used = 0;
+  if (prepass_ms) *prepass_ms = pre;
+  if (trace_ms) *trace_ms = tr;
+  if (frames) *frames = n;
+  return RFX_OK;
+}
 
 static int set_dev(rfx_renderer *r)
 {
@@ -440,6 +486,7 @@ extern "C" void rfx_renderer_destroy(rfx_renderer *r)
   (void)hipFree(r->d_seed); (void)hipFree(r->d_err); (void)hipFree(r->d_rd);
   (void)hipFree(r->d_blk_cnt); (void)hipFree(r->d_blk_off);
   (void)hipFree(r->d_img); (void)hipFree(r->d_argb); (void)hipFree(r->d_cnt);
+  for (hipEvent_t e : r->events) (void)hipEventDestroy(e);
   if (r->own_stream) (void)hipStreamDestroy(r->own_stream);
   delete r;
 }
@@ -635,7 +682,9 @@ extern "C" int rfx_render_frame(rfx_renderer *r, const rfx_frame *f, float *d_rg
   }
   if (traces >= (1ull << 32)) return fail(RFX_ERR_ARG, "render_frame: %llu traces exceed 2^32", (unsigned long long)traces);
   if (traces == 0) return RFX_OK;  // a span with no block corner traces nothing (and draws no randDir)
+  if ((rc = timing_event(r, st)) != RFX_OK) return rc;
   if ((rc = enqueue_rng(r, traces, st)) != RFX_OK) return rc;
+  if ((rc = timing_event(r, st)) != RFX_OK) return rc;
 
   FrameParams P{};
   P.eye_x = f->eye[0]; P.eye_y = f->eye[1]; P.eye_z = f->eye[2];
@@ -666,6 +715,7 @@ extern "C" int rfx_render_frame(rfx_renderer *r, const rfx_frame *f, float *d_rg
   P.counters = (unsigned long long *)d_counters;
   if (grid_rows)
     HIP_CHECK(launch_trace(r->dev, P, d_counters != nullptr, st));
+  if ((rc = timing_event(r, st)) != RFX_OK) return rc;
   if (P.additive)                                                                  // 2 draws per pixel, raster order
     r->jitter_seed = lcg_jump(r->jitter_seed, 2ull * (p1 - p0));
   return RFX_OK;

@@ -1,0 +1,91 @@
+"""Algorithmic work model of the trace loop, priced from the kernel's event counters.
+
+Counting rule: every f32 + - x / sqrt is 1 FLOP, compares,
+abs, clamps, selects and negations are 0, each powf is 1.  The weights are the
+operations the trace loop *needs* per event in our formulation (closest-hit
+candidates stop at their distance; drop/normal/reflection/texel are derived
+once, for the winner) -- read off reflaxman_amd/csrc/rfx_kernels.hip, which
+follows Scene.cpp:73-236 operation for operation.  The event counts come from
+the stats build of the same kernel (``trace_kernel<true>``) and are tested
+equal to the CPU restatement's (tests/test_gpu_parity.py).
+
+Correctly rounded f32 division and sqrt expand to ~10-15 VALU instructions
+on gfx950 (v_div_scale/v_rcp/v_fma.../v_div_fixup; scaled v_sqrt + two fma
+corrections), so VALU instructions per FLOP is well above 1: the FLOP-based
+roofline fraction understates how busy the VALU is.  bench.py reports both.
+"""
+from __future__ import annotations
+
+COUNTER_NAMES = [
+    "rays", "segments",
+    "sph_tests", "sph_d", "sph_t",
+    "tri_tests", "tri_z", "tri_t", "tri_in", "tri_d",
+    "hit_sph", "hit_tri",
+    "sh_sph_tests", "sh_sph_d", "sh_sph_t",
+    "sh_tri_tests", "sh_tri_z", "sh_tri_t", "sh_tri_in",
+    "l_eval", "l_facing", "l_lit", "l_spec", "l_pow",
+    "dielectric", "metal", "continue", "sky",
+    "tex_bilinear", "tex_checker", "tex_other",
+]
+
+# FLOPs per event (see module docstring for the rule)
+FLOP_WEIGHTS = {
+    "rays": 29,         # rx, ry; ss offsets (2 div + 4 add); view * ray (15); pixel sum + /ss^2 (6)
+    "segments": 10,     # |ray|^2 (5), 2*ray (3), 4a, 2a
+    "sph_tests": 17,    # vco (3), b (5), c (6), d (3)                        Sphere.cpp:50-54
+    "sph_d": 3,         # sqrt, -b - sqrt, / 2a                                Sphere.cpp:58
+    "sph_t": 9,         # ray * t (3), |.| (6)                                 Sphere.cpp:62-63
+    "tri_tests": 33,    # o - v0 (3), axTrans * (.) (15), axTrans * ray (15)   Triangle.cpp:55-56
+    "tri_z": 1,         # t = -ao.z / ar.z
+    "tri_t": 5,         # u, v (4), u + v (1)
+    "tri_in": 8,        # ray * t (3), |.|^2 (5)
+    "tri_d": 1,         # sqrt
+    "hit_sph": 47,      # ray*t, drop, norm (9), reflect (20), |ray| |norm| |refl| (18)
+    "hit_tri": 52,      # ray*t, drop (6), reflect (20), lengths (18), tuv * (u,v,0) + (tu0,tv0) (8)
+    "sh_sph_tests": 17, "sh_sph_d": 3, "sh_sph_t": 9,
+    "sh_tri_tests": 33, "sh_tri_z": 1, "sh_tri_t": 5, "sh_tri_in": 8,
+    "l_eval": 8,        # dropToLight (3), . norm (5)                          Scene.cpp:121-124
+    "l_facing": 16,     # shadow ray (6) + any-hit setup (10)                 Scene.cpp:128-129
+    "l_lit": 30,        # |L|, cos, diffuse accumulate, angular radius        Scene.cpp:146-160
+    "l_spec": 32,       # normalized(L) + jitter, |.|*|refl|, cos, clamp     Scene.cpp:162-166
+    "l_pow": 12,        # exponent (4), powf (1), * refl, colour, accumulate Scene.cpp:172-176
+    "dielectric": 33,   # ambient (3), Fresnel (11), finColor (10), mul (6), accumulate (3)
+    "metal": 24,        # ambient (3), finColor (9), mul (6), accumulate (3)
+    "continue": 16,     # normalized(reflect) + randDir * (1 - refl)          Scene.cpp:224
+    "sky": 27,          # normalize (9), |n|+eps (3), u, v (6), accumulate (9)
+    "tex_bilinear": 45, # fx, fy, fractions (6), 4 texels ARGB/255 (12), lerp (27)
+    "tex_checker": 2,   # u*50, v*50
+    "tex_other": 3,
+}
+
+POW_EVENTS = ("l_pow", "dielectric")  # one powf each
+
+# MI355X peaks (MI355X_MICROARCH.md: chip-level parameters)
+PEAK_FP32_VALU_TFLOPS = 157.3   # spec, packed-FMA rate
+PEAK_FP32_NOFMA_TFLOPS = 78.6   # separate v_mul/v_add (parity forbids contraction)
+PEAK_HBM_GBS = 8000.0
+
+# algorithmic HBM bytes per pixel: f32 RGB framebuffer (12) + ARGB8 (4) written once
+ALGO_BYTES_PER_PIXEL = 16
+
+
+def flops(counts) -> int:
+    """Algorithmic FLOPs for a dict/list of event counts."""
+    if not isinstance(counts, dict):
+        counts = dict(zip(COUNTER_NAMES, [int(c) for c in counts]))
+    return int(sum(FLOP_WEIGHTS[k] * int(counts.get(k, 0)) for k in FLOP_WEIGHTS))
+
+
+def summary(counts) -> dict:
+    if not isinstance(counts, dict):
+        counts = dict(zip(COUNTER_NAMES, [int(c) for c in counts]))
+    rays = max(1, counts["rays"])
+    return {
+        "flops": flops(counts),
+        "flops_per_ray": flops(counts) / rays,
+        "segments_per_ray": counts["segments"] / rays,
+        "shadow_rays_per_ray": counts["l_facing"] / rays,
+        "isect_tests_per_ray": (counts["sph_tests"] + counts["tri_tests"]) / rays,
+        "shadow_tests_per_ray": (counts["sh_sph_tests"] + counts["sh_tri_tests"]) / rays,
+        "pow_calls": sum(counts[k] for k in POW_EVENTS),
+    }

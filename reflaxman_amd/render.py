@@ -266,6 +266,15 @@ class Renderer:
     def synchronize(self):
         check(_lib.load().rfx_synchronize(self._h), "rfx_synchronize")
 
+    def set_timing(self, enable: bool):
+        check(_lib.load().rfx_renderer_set_timing(self._h, int(bool(enable))), "set_timing")
+
+    def get_timing(self):
+        """(prepass_ms, trace_ms, frames) summed over the frames since the last call (HIP events)."""
+        a, b, n = C.c_double(), C.c_double(), C.c_uint64()
+        check(_lib.load().rfx_renderer_get_timing(self._h, C.byref(a), C.byref(b), C.byref(n)), "get_timing")
+        return a.value, b.value, n.value
+
     def rand_dirs(self, seed: int, n: int):
         out = np.zeros((n, 3), np.float32)
         after = C.c_uint32()
