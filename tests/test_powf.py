@@ -1,0 +1,24 @@
+"""The device powf restatement (reflaxman_amd/csrc/rfx_powf.h) is bit-identical to this host's
+glibc powf -- the function the reference calls at Scene.cpp:175 and :196."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def checker(tmp_path_factory):
+    exe = str(tmp_path_factory.mktemp("powf") / "powf_check")
+    subprocess.run(["g++", "-std=c++17", "-O2", "-ffp-contract=off", "-Wno-unknown-pragmas",
+                    "-I" + os.path.join(ROOT, "reflaxman_amd", "csrc"),
+                    os.path.join(ROOT, "tests", "native", "powf_check.cpp"), "-o", exe, "-lm"], check=True)
+    return exe
+
+
+def test_powf_bitexact_vs_libm(checker):
+    # Fresnel site: every 7th float in [0, 1] with y = 3; specular site: 2e7 random (x, y); specials
+    r = subprocess.run([checker, "20000000", "7"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert " 0 mismatches" in r.stdout
