@@ -128,7 +128,7 @@ uint32_t rfx_strip_row_to_y(uint32_t r, uint32_t row_block, uint32_t rank, uint3
  *   d_argb : device uint32, strip_rows x W, Color::argb of the stored value (copyImage), or NULL
  *   d_counters : device uint64[RFX_NCOUNTERS] accumulated event counters (stats kernel), or NULL
  */
-#define RFX_NCOUNTERS 31
+#define RFX_NCOUNTERS 35
 int rfx_render_frame(rfx_renderer *r, const rfx_frame *frame, float *d_rgb, uint32_t *d_argb,
                      uint64_t *d_counters, void *stream);
 

@@ -18,11 +18,11 @@ REFHARNESS = os.path.join(HERE, "_ref", "refharness")
 
 COUNTER_NAMES = [
     "rays", "segments",
-    "sph_tests", "sph_d", "sph_t",
-    "tri_tests", "tri_z", "tri_t", "tri_in", "tri_d",
+    "sph_tests", "sph_b", "sph_d", "sph_t",
+    "tri_tests", "tri_z", "tri_s", "tri_t", "tri_in", "tri_d",
     "hit_sph", "hit_tri",
-    "sh_sph_tests", "sh_sph_d", "sh_sph_t",
-    "sh_tri_tests", "sh_tri_z", "sh_tri_t", "sh_tri_in",
+    "sh_sph_tests", "sh_sph_b", "sh_sph_d", "sh_sph_t",
+    "sh_tri_tests", "sh_tri_z", "sh_tri_s", "sh_tri_t", "sh_tri_in",
     "l_eval", "l_facing", "l_lit", "l_spec", "l_pow",
     "dielectric", "metal", "continue", "sky",
     "tex_bilinear", "tex_checker", "tex_other",

@@ -349,9 +349,11 @@ static int sphere_trace(const sphere_t *sp, v3 o, v3 ray, hit_t *out, uint64_t *
   const float b = vdot(vmul(ray, 2.0f), vco);
   const float c = vsqlen(vco) - sp->sq_radius;
   const float d = b * b - 4.0f * a * c;
+  /* counters mirror the events of the GPU formulation: B = the test survives the (exact) b > 0 reject */
+  if (cnt && !(b > 0.0f)) cnt[shadow ? ORC_SH_SPH_B : ORC_SPH_B]++;
   if (d >= 0.0f && a > VSN)
   {
-    if (cnt) cnt[shadow ? ORC_SH_SPH_D : ORC_SPH_D]++;
+    if (cnt && !(b > 0.0f)) cnt[shadow ? ORC_SH_SPH_D : ORC_SPH_D]++;
     const float t = (-b - sqrtf(d)) / (2.0f * a);
     if (t > VSN)
     {
@@ -385,6 +387,8 @@ static int tri_trace(const orc_scene *s, const tri_t *tr, v3 o, v3 ray, hit_t *o
   if (fabsf(ar.z) > VSN)
   {
     if (cnt) cnt[shadow ? ORC_SH_TRI_Z : ORC_TRI_Z]++;
+    /* S = -ao.z and ar.z have equal, non-zero signs (the GPU's exact pre-check before dividing) */
+    if (cnt && ((-ao.z > 0.0f && ar.z > 0.0f) || (-ao.z < 0.0f && ar.z < 0.0f))) cnt[shadow ? ORC_SH_TRI_S : ORC_TRI_S]++;
     const float t = -ao.z / ar.z;
     if (t > VSN)
     {

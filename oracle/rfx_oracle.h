@@ -20,11 +20,11 @@ typedef struct orc_scene orc_scene;
 /* event counters (also produced by the GPU stats kernel; tests compare them) */
 enum {
   ORC_RAYS = 0, ORC_SEGMENTS,
-  ORC_SPH_TESTS, ORC_SPH_D, ORC_SPH_T,
-  ORC_TRI_TESTS, ORC_TRI_Z, ORC_TRI_T, ORC_TRI_IN, ORC_TRI_D,
+  ORC_SPH_TESTS, ORC_SPH_B, ORC_SPH_D, ORC_SPH_T,
+  ORC_TRI_TESTS, ORC_TRI_Z, ORC_TRI_S, ORC_TRI_T, ORC_TRI_IN, ORC_TRI_D,
   ORC_HIT_SPH, ORC_HIT_TRI,
-  ORC_SH_SPH_TESTS, ORC_SH_SPH_D, ORC_SH_SPH_T,
-  ORC_SH_TRI_TESTS, ORC_SH_TRI_Z, ORC_SH_TRI_T, ORC_SH_TRI_IN,
+  ORC_SH_SPH_TESTS, ORC_SH_SPH_B, ORC_SH_SPH_D, ORC_SH_SPH_T,
+  ORC_SH_TRI_TESTS, ORC_SH_TRI_Z, ORC_SH_TRI_S, ORC_SH_TRI_T, ORC_SH_TRI_IN,
   ORC_L_EVAL, ORC_L_FACING, ORC_L_LIT, ORC_L_SPEC, ORC_L_POW,
   ORC_DIELECTRIC, ORC_METAL, ORC_CONTINUE, ORC_SKY,
   ORC_TEX_BILINEAR, ORC_TEX_CHECKER, ORC_TEX_OTHER,

@@ -12,7 +12,7 @@ import os
 from . import _build
 
 RFX_OK = 0
-RFX_NCOUNTERS = 31
+RFX_NCOUNTERS = 35
 METAL, DIELECTRIC = 0, 1
 
 _fp = C.POINTER(C.c_float)

@@ -4,7 +4,7 @@
 //       (trace_math.h:34-39, Vector3.cpp:176-188) as a parallel pre-pass:
 //       LCG jump-ahead per thread, accept flags, block scan, scatter of the
 //       i-th accepted triple to trace i.
-//   trace_kernel<STATS> : Render::renderNext (Render.cpp:136-215) +
+//   trace_kernel<STATS, BLOCK> : Render::renderNext (Render.cpp:136-215) +
 //       Scene::trace (Scene.cpp:73-236), one lane per trace, 8x8-pixel wave
 //       tiles, the bounce "recursion" as the reference's own iterative loop.
 //       Scene arrays are walked in wave-uniform order (scalar loads);
@@ -15,6 +15,8 @@
 //
 // Numerics: compiled with -ffp-contract=off, IEEE div/sqrt, f32 denormals on,
 // so every operation rounds exactly as the reference's x86-64 build does.
+// Work the reference does but whose result cannot matter is skipped only
+// where the skip is provably exact (each site says why).
 #include <hip/hip_runtime.h>
 
 #include "rfx_math.h"
@@ -32,10 +34,17 @@ struct Cnt { uint32_t c[C_COUNT]; };
     if constexpr (STATS) cnt.c[k]++; \
   } while (0)
 
+// Color(ARGB) (Color.cpp:9-14) through a 256-entry LDS table of float(k) / 255.0f:
+// the table holds exactly the quotients the reference computes per channel.
+__device__ __forceinline__ col from_argb_lut(uint32_t c, const float *lut)
+{
+  return mkc(lut[(c >> 16) & 0xFFu], lut[(c >> 8) & 0xFFu], lut[c & 0xFFu]);
+}
+
 // ------------------------------------------------------------- sampling
 template <bool STATS>
-__device__ __forceinline__ col texel_uv(const DevScene &S, int tex, float u, float v, Cnt &cnt)  // Texture.cpp:231-269
-{
+__device__ __forceinline__ col texel_uv(const DevScene &S, int tex, float u, float v, const float *lut, Cnt &cnt)
+{                                                                         // Texture.cpp:231-269
   if (u < 0.0f || u > 1.0f || v < 0.0f || v > 1.0f) { RFX_CNT(C_TEX_OTHER); return mkc(0.0f, 0.0f, 0.0f); }
   TexRec t;
   t.w = 0; t.h = 0; t.offset = 0;
@@ -52,8 +61,8 @@ __device__ __forceinline__ col texel_uv(const DevScene &S, int tex, float u, flo
   if (x < t.w - 1 && y < t.h - 1)
   {
     RFX_CNT(C_TEX_BILINEAR);
-    const col c00 = from_argb(px[x + t.w * y]), c01 = from_argb(px[x + t.w * (y + 1)]);
-    const col c10 = from_argb(px[x + 1 + t.w * y]), c11 = from_argb(px[x + 1 + t.w * (y + 1)]);
+    const col c00 = from_argb_lut(px[x + t.w * y], lut), c01 = from_argb_lut(px[x + t.w * (y + 1)], lut);
+    const col c10 = from_argb_lut(px[x + 1 + t.w * y], lut), c11 = from_argb_lut(px[x + 1 + t.w * (y + 1)], lut);
     const float uf = fx - floorf(fx), vf = fy - floorf(fy);
     const float uo = 1 - uf, vo = 1 - vf;
     return cadd(cscale(cadd(cscale(c00, uo), cscale(c10, uf)), vo), cscale(cadd(cscale(c01, uo), cscale(c11, uf)), vf));
@@ -61,11 +70,11 @@ __device__ __forceinline__ col texel_uv(const DevScene &S, int tex, float u, flo
   RFX_CNT(C_TEX_OTHER);
   const uint32_t xi = (uint32_t)fx, yi = (uint32_t)fy;                 // Texture.cpp:216-229
   if (xi >= t.w || yi >= t.h) return mkc(0.0f, 0.0f, 0.0f);
-  return from_argb(px[xi + t.w * yi]);
+  return from_argb_lut(px[xi + t.w * yi], lut);
 }
 
 template <bool STATS>
-__device__ __forceinline__ col skybox_texel(const DevScene &S, v3 ray, Cnt &cnt)       // Skybox.cpp:39-106
+__device__ __forceinline__ col skybox_texel(const DevScene &S, v3 ray, const float *lut, Cnt &cnt)  // Skybox.cpp:39-106
 {
   const float uLeft = 1.0f / 8.0f, vLeft = 3.0f / 6.0f;
   const float uFront = 3.0f / 8.0f, vFront = 3.0f / 6.0f;
@@ -93,73 +102,110 @@ __device__ __forceinline__ col skybox_texel(const DevScene &S, v3 ray, Cnt &cnt)
     if (y > 0) { u = uTop + x / ay * hw; v = vTop - z / ay * hh; }
     else { u = uBottom + x / ay * hw; v = vBottom + z / ay * hh; }
   }
-  return texel_uv<STATS>(S, S.skybox_tex, u, v, cnt);
+  return texel_uv<STATS>(S, S.skybox_tex, u, v, lut, cnt);
+}
+
+// ------------------------------------------------------------- primitives
+// Per-ray constants of Sphere::trace (Sphere.cpp:50-52,58), hoisted out of the object loop.
+struct RayConst {
+  v3 ray2;      // 2.0f * ray
+  float a4, a2; // 4.0f * a, 2.0f * a  with a = |ray|^2
+  bool a_ok;    // a > VERY_SMALL_NUMBER
+};
+__device__ __forceinline__ RayConst ray_const(v3 ray)
+{
+  RayConst k;
+  const float a = sqlen(ray);
+  k.ray2 = mul(ray, 2.0f);
+  k.a4 = 4.0f * a;
+  k.a2 = 2.0f * a;
+  k.a_ok = a > kVerySmall;
+  return k;
+}
+
+// Sphere::trace (Sphere.cpp:44-85) up to its hit decision; on a hit returns t and |ray t|.
+template <bool STATS, bool SHADOW>
+__device__ __forceinline__ bool sphere_hit(const SphereGeo &g, v3 o, v3 ray, const RayConst &k, float &t_out,
+                                           float &dist_out, Cnt &cnt)
+{
+  RFX_CNT(SHADOW ? C_SH_SPH_TESTS : C_SPH_TESTS);
+  const v3 vco = sub(o, mk(g.cx, g.cy, g.cz));
+  const float b = dot(k.ray2, vco);
+  // b > 0  =>  -b - sqrtf(d) < 0  =>  t < 0 (or -0): the reference's `t > VERY_SMALL_NUMBER` fails.  Exact.
+  if (b > 0.0f) return false;
+  RFX_CNT(SHADOW ? C_SH_SPH_B : C_SPH_B);
+  const float c = sqlen(vco) - g.sq_radius;
+  const float d = b * b - k.a4 * c;
+  if (!(d >= 0.0f && k.a_ok)) return false;
+  RFX_CNT(SHADOW ? C_SH_SPH_D : C_SPH_D);
+  const float t = (-b - sqrtf(d)) / k.a2;
+  if (!(t > kVerySmall)) return false;
+  RFX_CNT(SHADOW ? C_SH_SPH_T : C_SPH_T);
+  const float dist = len(mul(ray, t));
+  if (!(dist > kDelta)) return false;
+  t_out = t;
+  dist_out = dist;
+  return true;
+}
+
+// Triangle::trace (Triangle.cpp:53-108) up to its hit decision; on a hit returns t, u, v, |ray t|^2.
+// axTrans * (o - v0) and axTrans * ray are evaluated row by row, z first (same expressions).
+template <bool STATS, bool SHADOW>
+__device__ __forceinline__ bool tri_hit(const TriGeo &g, v3 o, v3 ray, float &t_out, float &u_out, float &v_out,
+                                        float &sq_out, Cnt &cnt)
+{
+  RFX_CNT(SHADOW ? C_SH_TRI_TESTS : C_TRI_TESTS);
+  const v3 dv = sub(o, mk(g.v0x, g.v0y, g.v0z));
+  const float aoz = dv.x * g.a31 + dv.y * g.a32 + dv.z * g.a33;
+  const float arz = ray.x * g.a31 + ray.y * g.a32 + ray.z * g.a33;
+  if (!(fabsf(arz) > kVerySmall)) return false;
+  RFX_CNT(SHADOW ? C_SH_TRI_Z : C_TRI_Z);
+  // t = -aoz / arz > VERY_SMALL_NUMBER needs -aoz and arz non-zero with equal signs; otherwise the
+  // quotient is <= 0 or NaN and the reference rejects it.  Exact.
+  const float nz = -aoz;
+  if (!((nz > 0.0f && arz > 0.0f) || (nz < 0.0f && arz < 0.0f))) return false;
+  RFX_CNT(SHADOW ? C_SH_TRI_S : C_TRI_S);
+  const float t = nz / arz;
+  if (!(t > kVerySmall)) return false;
+  RFX_CNT(SHADOW ? C_SH_TRI_T : C_TRI_T);
+  const float aox = dv.x * g.a11 + dv.y * g.a12 + dv.z * g.a13;
+  const float aoy = dv.x * g.a21 + dv.y * g.a22 + dv.z * g.a23;
+  const float arx = ray.x * g.a11 + ray.y * g.a12 + ray.z * g.a13;
+  const float ary = ray.x * g.a21 + ray.y * g.a22 + ray.z * g.a23;
+  const float u = aox + t * arx, v = aoy + t * ary;
+  if (!(u >= 0.0f && v >= 0.0f && u + v < 1.0f)) return false;
+  RFX_CNT(SHADOW ? C_SH_TRI_IN : C_TRI_IN);
+  const float sq = sqlen(mul(ray, t));
+  if (!(sq > kDelta * kDelta)) return false;
+  t_out = t; u_out = u; v_out = v; sq_out = sq;
+  return true;
 }
 
 // ------------------------------------------------------------- shadow any-hit
-// Scene.cpp:129-141: every object but the hit one, in insertion order
-// (spheres precede triangles in every scene the builder emits in that order;
-// the boolean is order-independent either way).
+// Scene.cpp:129-141: every object but the hit one; the boolean does not depend on the order.
+// (Spheres precede triangles, which is the reference's order for every scene whose objects are
+// added spheres-first -- then even the event counters match it.)
 template <bool STATS>
 __device__ __forceinline__ bool occluded(const DevScene &S, v3 o, v3 ray, int skip_obj, Cnt &cnt)
 {
-  const float a = sqlen(ray);
-  const v3 ray2 = mul(ray, 2.0f);
-  const float a4 = 4.0f * a, a2 = 2.0f * a;
-  const bool a_ok = a > kVerySmall;
-  for (int i = 0; i < S.n_sph; ++i)                                       // Sphere.cpp:44-85, any-hit
+  const RayConst k = ray_const(ray);
+  float t, dist, u, v;
+  for (int i = 0; i < S.n_sph; ++i)
   {
     if (S.sph_info[2 * i] == skip_obj) continue;
-    RFX_CNT(C_SH_SPH_TESTS);
-    const SphereGeo g = S.sph_geo[i];
-    const v3 vco = sub(o, mk(g.cx, g.cy, g.cz));
-    const float b = dot(ray2, vco);
-    const float c = sqlen(vco) - g.sq_radius;
-    const float d = b * b - a4 * c;
-    if (d >= 0.0f && a_ok)
-    {
-      RFX_CNT(C_SH_SPH_D);
-      const float t = (-b - sqrtf(d)) / a2;
-      if (t > kVerySmall)
-      {
-        RFX_CNT(C_SH_SPH_T);
-        if (len(mul(ray, t)) > kDelta) return true;
-      }
-    }
+    if (sphere_hit<STATS, true>(S.sph_geo[i], o, ray, k, t, dist, cnt)) return true;
   }
-  for (int i = 0; i < S.n_tri; ++i)                                       // Triangle.cpp:53-108, any-hit
+  for (int i = 0; i < S.n_tri; ++i)
   {
     if (S.tri_shade[i].obj == skip_obj) continue;
-    RFX_CNT(C_SH_TRI_TESTS);
-    const TriGeo g = S.tri_geo[i];
-    m33 ax;
-    ax.m11 = g.a11; ax.m12 = g.a12; ax.m13 = g.a13;
-    ax.m21 = g.a21; ax.m22 = g.a22; ax.m23 = g.a23;
-    ax.m31 = g.a31; ax.m32 = g.a32; ax.m33 = g.a33;
-    const v3 ao = mmul(ax, sub(o, mk(g.v0x, g.v0y, g.v0z)));
-    const v3 ar = mmul(ax, ray);
-    if (fabsf(ar.z) > kVerySmall)
-    {
-      RFX_CNT(C_SH_TRI_Z);
-      const float t = -ao.z / ar.z;
-      if (t > kVerySmall)
-      {
-        RFX_CNT(C_SH_TRI_T);
-        const float u = ao.x + t * ar.x, v = ao.y + t * ar.y;
-        if (u >= 0.0f && v >= 0.0f && u + v < 1.0f)
-        {
-          RFX_CNT(C_SH_TRI_IN);
-          if (sqlen(mul(ray, t)) > kDelta * kDelta) return true;
-        }
-      }
-    }
+    if (tri_hit<STATS, true>(S.tri_geo[i], o, ray, t, u, v, dist, cnt)) return true;
   }
   return false;
 }
 
 // ------------------------------------------------------------- Scene::trace
 template <bool STATS>
-__device__ col trace(const DevScene &S, v3 origin, v3 ray, int depth, v3 rd, Cnt &cnt)
+__device__ col trace(const DevScene &S, v3 origin, v3 ray, int depth, v3 rd, const float *lut, Cnt &cnt)
 {
   col mulc = mkc(1.0f, 1.0f, 1.0f);
   col pix = mkc(0.0f, 0.0f, 0.0f);
@@ -167,76 +213,37 @@ __device__ col trace(const DevScene &S, v3 origin, v3 ray, int depth, v3 rd, Cnt
   for (int refl = 0; refl < depth; ++refl)
   {
     RFX_CNT(C_SEGMENTS);
-    // closest hit (Scene.cpp:86-106): min over (distance, insertion index)
+    // closest hit (Scene.cpp:86-106): the reference keeps the first object with the minimal distance,
+    // i.e. the lexicographic minimum of (distance, insertion index) -- any visiting order gives it.
     float best = kFltMax;
     int best_obj = -1, best_kind = 0, best_i = 0;
     float best_t = 0.0f, best_u = 0.0f, best_v = 0.0f;
     {
-      const float a = sqlen(ray);
-      const v3 ray2 = mul(ray, 2.0f);
-      const float a4 = 4.0f * a, a2 = 2.0f * a;
-      const bool a_ok = a > kVerySmall;
+      const RayConst k = ray_const(ray);
       for (int i = 0; i < S.n_sph; ++i)
       {
-        RFX_CNT(C_SPH_TESTS);
-        const SphereGeo g = S.sph_geo[i];
-        const v3 vco = sub(origin, mk(g.cx, g.cy, g.cz));
-        const float b = dot(ray2, vco);
-        const float c = sqlen(vco) - g.sq_radius;
-        const float d = b * b - a4 * c;
-        if (d >= 0.0f && a_ok)
+        float t, dist;
+        if (sphere_hit<STATS, false>(S.sph_geo[i], origin, ray, k, t, dist, cnt))
         {
-          RFX_CNT(C_SPH_D);
-          const float t = (-b - sqrtf(d)) / a2;
-          if (t > kVerySmall)
+          const int obj = S.sph_info[2 * i];
+          if (dist < best || (dist == best && obj < best_obj))
           {
-            RFX_CNT(C_SPH_T);
-            const float dist = len(mul(ray, t));
-            if (dist > kDelta)
-            {
-              const int obj = S.sph_info[2 * i];
-              if (dist < best || (dist == best && obj < best_obj))
-              {
-                best = dist; best_obj = obj; best_kind = 0; best_i = i; best_t = t;
-              }
-            }
+            best = dist; best_obj = obj; best_kind = 0; best_i = i; best_t = t;
           }
         }
       }
     }
     for (int i = 0; i < S.n_tri; ++i)
     {
-      RFX_CNT(C_TRI_TESTS);
-      const TriGeo g = S.tri_geo[i];
-      m33 ax;
-      ax.m11 = g.a11; ax.m12 = g.a12; ax.m13 = g.a13;
-      ax.m21 = g.a21; ax.m22 = g.a22; ax.m23 = g.a23;
-      ax.m31 = g.a31; ax.m32 = g.a32; ax.m33 = g.a33;
-      const v3 ao = mmul(ax, sub(origin, mk(g.v0x, g.v0y, g.v0z)));
-      const v3 ar = mmul(ax, ray);
-      if (fabsf(ar.z) > kVerySmall)
+      float t, u, v, sq;
+      if (tri_hit<STATS, false>(S.tri_geo[i], origin, ray, t, u, v, sq, cnt))
       {
-        RFX_CNT(C_TRI_Z);
-        const float t = -ao.z / ar.z;
-        if (t > kVerySmall)
+        RFX_CNT(C_TRI_D);
+        const float dist = sqrtf(sq);
+        const int obj = S.tri_shade[i].obj;
+        if (dist < best || (dist == best && obj < best_obj))
         {
-          RFX_CNT(C_TRI_T);
-          const float u = ao.x + t * ar.x, v = ao.y + t * ar.y;
-          if (u >= 0.0f && v >= 0.0f && u + v < 1.0f)
-          {
-            RFX_CNT(C_TRI_IN);
-            const float sq = sqlen(mul(ray, t));
-            if (sq > kDelta * kDelta)
-            {
-              RFX_CNT(C_TRI_D);
-              const float dist = sqrtf(sq);
-              const int obj = S.tri_shade[i].obj;
-              if (dist < best || (dist == best && obj < best_obj))
-              {
-                best = dist; best_obj = obj; best_kind = 1; best_i = i; best_t = t; best_u = u; best_v = v;
-              }
-            }
-          }
+          best = dist; best_obj = obj; best_kind = 1; best_i = i; best_t = t; best_u = u; best_v = v;
         }
       }
     }
@@ -268,7 +275,7 @@ __device__ col trace(const DevScene &S, v3 origin, v3 ray, int depth, v3 rd, Cnt
         {
           const float tvx = best_u * sh.t11 + best_v * sh.t12 + 0.0f;
           const float tvy = best_u * sh.t21 + best_v * sh.t22 + 0.0f;
-          const col c = texel_uv<STATS>(S, sh.tex, sh.tu0 + tvx, sh.tv0 + tvy, cnt);
+          const col c = texel_uv<STATS>(S, sh.tex, sh.tu0 + tvx, sh.tv0 + tvy, lut, cnt);
           m.r = c.r; m.g = c.g; m.b = c.b;
         }
       }
@@ -342,7 +349,7 @@ __device__ col trace(const DevScene &S, v3 origin, v3 ray, int depth, v3 rd, Cnt
     else                                                                       // Scene.cpp:226-231
     {
       RFX_CNT(C_SKY);
-      pix = cclamp(cadd(pix, cmul(cmul(mulc, skybox_texel<STATS>(S, ray, cnt)), mkc(S.env_r, S.env_g, S.env_b))));
+      pix = cclamp(cadd(pix, cmul(cmul(mulc, skybox_texel<STATS>(S, ray, lut, cnt)), mkc(S.env_r, S.env_g, S.env_b))));
       break;
     }
   }
@@ -377,10 +384,13 @@ __device__ __forceinline__ v3 load_rd(const FrameParams &P, uint64_t i)
   return mk(P.rd[i], P.rd[P.n_rd + i], P.rd[2 * P.n_rd + i]);
 }
 
-// one workgroup = 16x16 output pixels, one wave = an 8x8 tile (ray coherence)
-template <bool STATS>
+// one workgroup = 16x16 output pixels (BLOCK: block corners), one wave = an 8x8 tile (ray coherence)
+template <bool STATS, bool BLOCK>
 __global__ __launch_bounds__(256) void trace_kernel(DevScene S, FrameParams P)
 {
+  __shared__ float lut[256];
+  lut[threadIdx.x] = (float)threadIdx.x / 255.0f;                               // Color.cpp:11-13
+  __syncthreads();
   Cnt cnt;
   if constexpr (STATS)
   {
@@ -396,7 +406,7 @@ __global__ __launch_bounds__(256) void trace_kernel(DevScene S, FrameParams P)
   view.m31 = P.v31; view.m32 = P.v32; view.m33 = P.v33;
   const v3 eye = mk(P.eye_x, P.eye_y, P.eye_z);
 
-  if (P.ss < 0)
+  if constexpr (BLOCK)
   {
     // block preview (Render.cpp:158-172): only block corners inside the cursor span are traced;
     // trace order = raster order of corners, so corner (cx, cy) is trace cy * bw + cx.
@@ -411,7 +421,7 @@ __global__ __launch_bounds__(256) void trace_kernel(DevScene S, FrameParams P)
       {
         const v3 ray = mmul(view, mk((float)x - P.wh, (float)y - P.hh, P.rz));
         const uint64_t ti = (uint64_t)cy * bw + cx - P.trace_base;
-        const col c = trace<STATS>(S, eye, ray, P.depth, load_rd(P, ti), cnt);
+        const col c = trace<STATS>(S, eye, ray, P.depth, load_rd(P, ti), lut, cnt);
         const uint32_t ex = min(P.W, x + n), ey = min(P.H, y + n);
         const uint32_t a = argb(c);
         for (uint32_t qy = y; qy < ey; ++qy)
@@ -423,11 +433,8 @@ __global__ __launch_bounds__(256) void trace_kernel(DevScene S, FrameParams P)
           }
       }
     }
-    flush_counters<STATS>(P, cnt);
-    return;
   }
-
-  if (gx < P.W && gy < P.grid_rows)
+  else if (gx < P.W && gy < P.grid_rows)
   {
     const uint32_t x = gx;
     const uint32_t y = P.nranks > 1 ? strip_row_to_y(gy, P) : gy + P.row0;
@@ -450,13 +457,18 @@ __global__ __launch_bounds__(256) void trace_kernel(DevScene S, FrameParams P)
       for (int sx = 0; sx < ss; ++sx)                                              // Render.cpp:181-187
         for (int sy = 0; sy < ss; ++sy)
         {
-          v3 ray = mk(rx + (float)sx / ssf + rndx, ry + (float)sy / ssf + rndy, P.rz);
+          // float(0) / ss == +0 exactly, so the first sample's offsets need no division
+          const float ox = sx ? (float)sx / ssf : 0.0f, oy = sy ? (float)sy / ssf : 0.0f;
+          v3 ray = mk(rx + ox + rndx, ry + oy + rndy, P.rz);
           ray = mmul(view, ray);
           const uint64_t ti = pr * (uint64_t)(ss * ss) + (uint64_t)(sx * ss + sy);
-          fin = cadd(fin, trace<STATS>(S, eye, ray, P.depth, load_rd(P, ti), cnt));
+          fin = cadd(fin, trace<STATS>(S, eye, ray, P.depth, load_rd(P, ti), lut, cnt));
         }
-      const float sq = (float)(ss * ss);                                           // Render.cpp:189
-      if (fabsf(sq) > kVerySmall) fin = mkc(fin.r / sq, fin.g / sq, fin.b / sq);
+      if (ss != 1)                                                                 // Render.cpp:189 (x / 1.0f == x)
+      {
+        const float sq = (float)(ss * ss);
+        if (fabsf(sq) > kVerySmall) fin = mkc(fin.r / sq, fin.g / sq, fin.b / sq);
+      }
       const size_t o = (size_t)orow * P.W + x;
       float *d = P.img + o * 3;
       col out = fin;
@@ -598,10 +610,16 @@ hipError_t launch_trace(const DevScene &S, const FrameParams &P, bool stats, hip
 {
   const uint32_t cols = P.ss < 0 ? (P.W + (uint32_t)(-P.ss) - 1) / (uint32_t)(-P.ss) : P.W;
   const dim3 grid((cols + 15) / 16, (P.grid_rows + 15) / 16);
-  if (stats)
-    hipLaunchKernelGGL(trace_kernel<true>, grid, dim3(256), 0, st, S, P);
+  if (P.ss < 0)
+  {
+    if (stats) hipLaunchKernelGGL((trace_kernel<true, true>), grid, dim3(256), 0, st, S, P);
+    else hipLaunchKernelGGL((trace_kernel<false, true>), grid, dim3(256), 0, st, S, P);
+  }
   else
-    hipLaunchKernelGGL(trace_kernel<false>, grid, dim3(256), 0, st, S, P);
+  {
+    if (stats) hipLaunchKernelGGL((trace_kernel<true, false>), grid, dim3(256), 0, st, S, P);
+    else hipLaunchKernelGGL((trace_kernel<false, false>), grid, dim3(256), 0, st, S, P);
+  }
   return hipGetLastError();
 }
 

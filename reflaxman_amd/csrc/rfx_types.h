@@ -10,11 +10,11 @@ namespace rfx {
 // per-frame event counters (same order as oracle/rfx_oracle.h ORC_*)
 enum Counter {
   C_RAYS = 0, C_SEGMENTS,
-  C_SPH_TESTS, C_SPH_D, C_SPH_T,
-  C_TRI_TESTS, C_TRI_Z, C_TRI_T, C_TRI_IN, C_TRI_D,
+  C_SPH_TESTS, C_SPH_B, C_SPH_D, C_SPH_T,
+  C_TRI_TESTS, C_TRI_Z, C_TRI_S, C_TRI_T, C_TRI_IN, C_TRI_D,
   C_HIT_SPH, C_HIT_TRI,
-  C_SH_SPH_TESTS, C_SH_SPH_D, C_SH_SPH_T,
-  C_SH_TRI_TESTS, C_SH_TRI_Z, C_SH_TRI_T, C_SH_TRI_IN,
+  C_SH_SPH_TESTS, C_SH_SPH_B, C_SH_SPH_D, C_SH_SPH_T,
+  C_SH_TRI_TESTS, C_SH_TRI_Z, C_SH_TRI_S, C_SH_TRI_T, C_SH_TRI_IN,
   C_L_EVAL, C_L_FACING, C_L_LIT, C_L_SPEC, C_L_POW,
   C_DIELECTRIC, C_METAL, C_CONTINUE, C_SKY,
   C_TEX_BILINEAR, C_TEX_CHECKER, C_TEX_OTHER,

@@ -18,11 +18,11 @@ from __future__ import annotations
 
 COUNTER_NAMES = [
     "rays", "segments",
-    "sph_tests", "sph_d", "sph_t",
-    "tri_tests", "tri_z", "tri_t", "tri_in", "tri_d",
+    "sph_tests", "sph_b", "sph_d", "sph_t",
+    "tri_tests", "tri_z", "tri_s", "tri_t", "tri_in", "tri_d",
     "hit_sph", "hit_tri",
-    "sh_sph_tests", "sh_sph_d", "sh_sph_t",
-    "sh_tri_tests", "sh_tri_z", "sh_tri_t", "sh_tri_in",
+    "sh_sph_tests", "sh_sph_b", "sh_sph_d", "sh_sph_t",
+    "sh_tri_tests", "sh_tri_z", "sh_tri_s", "sh_tri_t", "sh_tri_in",
     "l_eval", "l_facing", "l_lit", "l_spec", "l_pow",
     "dielectric", "metal", "continue", "sky",
     "tex_bilinear", "tex_checker", "tex_other",
@@ -30,20 +30,22 @@ COUNTER_NAMES = [
 
 # FLOPs per event (see module docstring for the rule)
 FLOP_WEIGHTS = {
-    "rays": 29,         # rx, ry; ss offsets (2 div + 4 add); view * ray (15); pixel sum + /ss^2 (6)
+    "rays": 24,         # rx, ry (2); + ss offset + jitter (4); view * ray (15); pixel sum (3)  [ss = 1]
     "segments": 10,     # |ray|^2 (5), 2*ray (3), 4a, 2a
-    "sph_tests": 17,    # vco (3), b (5), c (6), d (3)                        Sphere.cpp:50-54
+    "sph_tests": 8,     # vco (3), b (5)                                       Sphere.cpp:50-52
+    "sph_b": 9,         # c (6), d (3)  -- only when b <= 0 (b > 0 is an exact reject)
     "sph_d": 3,         # sqrt, -b - sqrt, / 2a                                Sphere.cpp:58
     "sph_t": 9,         # ray * t (3), |.| (6)                                 Sphere.cpp:62-63
-    "tri_tests": 33,    # o - v0 (3), axTrans * (.) (15), axTrans * ray (15)   Triangle.cpp:55-56
-    "tri_z": 1,         # t = -ao.z / ar.z
-    "tri_t": 5,         # u, v (4), u + v (1)
+    "tri_tests": 13,    # o - v0 (3), z rows of axTrans * (o - v0) and axTrans * ray (10)  Triangle.cpp:55-56
+    "tri_z": 0,         # sign pre-check (compares only)
+    "tri_s": 1,         # t = -ao.z / ar.z
+    "tri_t": 25,        # x, y rows of both products (20), u, v (4), u + v (1)
     "tri_in": 8,        # ray * t (3), |.|^2 (5)
     "tri_d": 1,         # sqrt
     "hit_sph": 47,      # ray*t, drop, norm (9), reflect (20), |ray| |norm| |refl| (18)
     "hit_tri": 52,      # ray*t, drop (6), reflect (20), lengths (18), tuv * (u,v,0) + (tu0,tv0) (8)
-    "sh_sph_tests": 17, "sh_sph_d": 3, "sh_sph_t": 9,
-    "sh_tri_tests": 33, "sh_tri_z": 1, "sh_tri_t": 5, "sh_tri_in": 8,
+    "sh_sph_tests": 8, "sh_sph_b": 9, "sh_sph_d": 3, "sh_sph_t": 9,
+    "sh_tri_tests": 13, "sh_tri_z": 0, "sh_tri_s": 1, "sh_tri_t": 25, "sh_tri_in": 8,
     "l_eval": 8,        # dropToLight (3), . norm (5)                          Scene.cpp:121-124
     "l_facing": 16,     # shadow ray (6) + any-hit setup (10)                 Scene.cpp:128-129
     "l_lit": 30,        # |L|, cos, diffuse accumulate, angular radius        Scene.cpp:146-160

@@ -163,13 +163,13 @@ def test_event_counters_match_oracle():
         desc = scene(name)
         o = orc.OracleRender(desc, 4242, 0)
         o.set_image_size(W, H)
-        oc = np.zeros(31, np.uint64)
+        oc = np.zeros(len(orc.COUNTER_NAMES), np.uint64)
         o.render(depth, 1, counters=oc)
         s, cam = build_scene(desc)
         rr = Renderer(sphere_seed=4242)
         rr.set_scene(s)
         img = np.zeros((H, W, 3), np.float32)
-        gc = np.zeros(31, np.uint64)
+        gc = np.zeros(len(orc.COUNTER_NAMES), np.uint64)
         f = make_frame(cam, W, H, depth, 1)
         L = _lib.load()
         _lib.check(L.rfx_render_frame_host(rr._h, C.byref(f), _lib.fptr(img), None, _lib.u64ptr(gc)))
