@@ -44,6 +44,17 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
+def build_variant(name: str, defines, verbose: bool = False) -> str:
+    """Compile a variant librfx_<name>.so with extra -D flags (A/B timing builds, tools/ab.py)."""
+    out = os.path.join(LIBDIR, "variants", f"librfx_{name}.so")
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    cmd = [hipcc(), *FLAGS, *[f"-D{d}" for d in defines], *[os.path.join(CSRC, s) for s in SOURCES], "-o", out]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"variant {name} build failed:\n" + r.stdout + r.stderr)
+    return out
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
     """Compile librfx.so if missing or older than its sources; return its path."""
     if not force and not _stale():

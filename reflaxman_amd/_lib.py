@@ -85,6 +85,16 @@ def lib_path() -> str:
     return _build.LIB
 
 
+def bind(path: str):
+    """Load and bind any build of librfx.so (e.g. a variant build for A/B timing)."""
+    L = C.CDLL(os.path.abspath(path))
+    for name, res, args in SIGNATURES:
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    return L
+
+
 def load(build_if_missing: bool = True):
     """Load librfx.so (building it in-tree first if it is missing/stale and hipcc exists)."""
     global _lib

@@ -38,7 +38,56 @@ struct Cnt { uint32_t c[C_COUNT]; };
 // the table holds exactly the quotients the reference computes per channel.
 __device__ __forceinline__ col from_argb_lut(uint32_t c, const float *lut)
 {
+#ifdef RFX_NO_LUT
+  (void)lut;
+  return from_argb(c);
+#else
   return mkc(lut[(c >> 16) & 0xFFu], lut[(c >> 8) & 0xFFu], lut[c & 0xFFu]);
+#endif
+}
+
+// ------------------------------------------------------------- scene geometry access
+// The object loops read every primitive in wave-uniform order.  Scenes up to kLdsSph spheres and
+// kLdsTri triangles are staged once per workgroup into LDS (one broadcast ds_read per primitive,
+// in-order returns so reads pipeline); larger scenes read through the scalar cache.
+constexpr int kLdsSph = 256;
+constexpr int kLdsTri = 64;
+__shared__ SphereGeo g_lds_sph[kLdsSph];
+__shared__ int32_t g_lds_sph_obj[kLdsSph];
+__shared__ TriGeo g_lds_tri[kLdsTri];
+__shared__ int32_t g_lds_tri_obj[kLdsTri];
+
+template <bool LDS>
+struct Geo;
+template <>
+struct Geo<false> {
+  const DevScene &S;
+  __device__ __forceinline__ SphereGeo sph(int i) const { return S.sph_geo[i]; }
+  __device__ __forceinline__ int sph_obj(int i) const { return S.sph_info[2 * i]; }
+  __device__ __forceinline__ TriGeo tri(int i) const { return S.tri_geo[i]; }
+  __device__ __forceinline__ int tri_obj(int i) const { return S.tri_shade[i].obj; }
+};
+template <>
+struct Geo<true> {
+  const DevScene &S;
+  __device__ __forceinline__ SphereGeo sph(int i) const { return g_lds_sph[i]; }
+  __device__ __forceinline__ int sph_obj(int i) const { return g_lds_sph_obj[i]; }
+  __device__ __forceinline__ TriGeo tri(int i) const { return g_lds_tri[i]; }
+  __device__ __forceinline__ int tri_obj(int i) const { return g_lds_tri_obj[i]; }
+};
+
+__device__ __forceinline__ void stage_scene_lds(const DevScene &S)
+{
+  for (int i = threadIdx.x; i < S.n_sph; i += blockDim.x)
+  {
+    g_lds_sph[i] = S.sph_geo[i];
+    g_lds_sph_obj[i] = S.sph_info[2 * i];
+  }
+  for (int i = threadIdx.x; i < S.n_tri; i += blockDim.x)
+  {
+    g_lds_tri[i] = S.tri_geo[i];
+    g_lds_tri_obj[i] = S.tri_shade[i].obj;
+  }
 }
 
 // ------------------------------------------------------------- sampling
@@ -131,13 +180,33 @@ __device__ __forceinline__ bool sphere_hit(const SphereGeo &g, v3 o, v3 ray, con
   RFX_CNT(SHADOW ? C_SH_SPH_TESTS : C_SPH_TESTS);
   const v3 vco = sub(o, mk(g.cx, g.cy, g.cz));
   const float b = dot(k.ray2, vco);
-  // b > 0  =>  -b - sqrtf(d) < 0  =>  t < 0 (or -0): the reference's `t > VERY_SMALL_NUMBER` fails.  Exact.
+#ifdef RFX_BREJECT
+  // b > 0  =>  -b - sqrtf(d) < 0  =>  t < 0 (or -0): the reference's `t > VERY_SMALL_NUMBER` fails.  Exact,
+  // but measured slower than evaluating the discriminant (an extra divergent branch per sphere).
   if (b > 0.0f) return false;
-  RFX_CNT(SHADOW ? C_SH_SPH_B : C_SPH_B);
+#endif
+  if constexpr (STATS)
+    if (!(b > 0.0f)) RFX_CNT(SHADOW ? C_SH_SPH_B : C_SPH_B);
   const float c = sqlen(vco) - g.sq_radius;
   const float d = b * b - k.a4 * c;
+#ifdef RFX_FLAT_SPHERE
+  // predicated: every lane evaluates t and |ray t| (sqrtf of a negative d is a NaN that fails every compare)
+  const bool ok1 = d >= 0.0f && k.a_ok;
+  const float t = (-b - sqrtf(d)) / k.a2;
+  const bool ok2 = ok1 && t > kVerySmall;
+  const float dist = len(mul(ray, t));
+  if constexpr (STATS)
+  {
+    if (ok1 && !(b > 0.0f)) RFX_CNT(SHADOW ? C_SH_SPH_D : C_SPH_D);
+    if (ok2) RFX_CNT(SHADOW ? C_SH_SPH_T : C_SPH_T);
+  }
+  t_out = t;
+  dist_out = dist;
+  return ok2 && dist > kDelta;
+#else
   if (!(d >= 0.0f && k.a_ok)) return false;
-  RFX_CNT(SHADOW ? C_SH_SPH_D : C_SPH_D);
+  if constexpr (STATS)
+    if (!(b > 0.0f)) RFX_CNT(SHADOW ? C_SH_SPH_D : C_SPH_D);
   const float t = (-b - sqrtf(d)) / k.a2;
   if (!(t > kVerySmall)) return false;
   RFX_CNT(SHADOW ? C_SH_SPH_T : C_SPH_T);
@@ -146,6 +215,7 @@ __device__ __forceinline__ bool sphere_hit(const SphereGeo &g, v3 o, v3 ray, con
   t_out = t;
   dist_out = dist;
   return true;
+#endif
 }
 
 // Triangle::trace (Triangle.cpp:53-108) up to its hit decision; on a hit returns t, u, v, |ray t|^2.
@@ -163,8 +233,12 @@ __device__ __forceinline__ bool tri_hit(const TriGeo &g, v3 o, v3 ray, float &t_
   // t = -aoz / arz > VERY_SMALL_NUMBER needs -aoz and arz non-zero with equal signs; otherwise the
   // quotient is <= 0 or NaN and the reference rejects it.  Exact.
   const float nz = -aoz;
-  if (!((nz > 0.0f && arz > 0.0f) || (nz < 0.0f && arz < 0.0f))) return false;
-  RFX_CNT(SHADOW ? C_SH_TRI_S : C_TRI_S);
+  const bool same_sign = (nz > 0.0f && arz > 0.0f) || (nz < 0.0f && arz < 0.0f);
+#ifdef RFX_TRISIGN
+  if (!same_sign) return false;
+#endif
+  if constexpr (STATS)
+    if (same_sign) RFX_CNT(SHADOW ? C_SH_TRI_S : C_TRI_S);
   const float t = nz / arz;
   if (!(t > kVerySmall)) return false;
   RFX_CNT(SHADOW ? C_SH_TRI_T : C_TRI_T);
@@ -185,32 +259,56 @@ __device__ __forceinline__ bool tri_hit(const TriGeo &g, v3 o, v3 ray, float &t_
 // Scene.cpp:129-141: every object but the hit one; the boolean does not depend on the order.
 // (Spheres precede triangles, which is the reference's order for every scene whose objects are
 // added spheres-first -- then even the event counters match it.)
-template <bool STATS>
+template <bool STATS, bool LDS>
 __device__ __forceinline__ bool occluded(const DevScene &S, v3 o, v3 ray, int skip_obj, Cnt &cnt)
 {
+  const Geo<LDS> G{S};
   const RayConst k = ray_const(ray);
   float t, dist, u, v;
   for (int i = 0; i < S.n_sph; ++i)
   {
-    if (S.sph_info[2 * i] == skip_obj) continue;
-    if (sphere_hit<STATS, true>(S.sph_geo[i], o, ray, k, t, dist, cnt)) return true;
+    if (G.sph_obj(i) == skip_obj) continue;
+    if (sphere_hit<STATS, true>(G.sph(i), o, ray, k, t, dist, cnt)) return true;
   }
   for (int i = 0; i < S.n_tri; ++i)
   {
-    if (S.tri_shade[i].obj == skip_obj) continue;
-    if (tri_hit<STATS, true>(S.tri_geo[i], o, ray, t, u, v, dist, cnt)) return true;
+    if (G.tri_obj(i) == skip_obj) continue;
+    if (tri_hit<STATS, true>(G.tri(i), o, ray, t, u, v, dist, cnt)) return true;
   }
   return false;
 }
 
 // ------------------------------------------------------------- Scene::trace
+// State of one trace between bounce segments (Scene.cpp:75-80 locals).
+struct Path {
+  v3 origin, ray, rd;  // rd: this trace's randomInsideSphere draw (Scene.cpp:75)
+  col mulc, pix;
+  int refl;
+};
+
 template <bool STATS>
-__device__ col trace(const DevScene &S, v3 origin, v3 ray, int depth, v3 rd, const float *lut, Cnt &cnt)
+__device__ __forceinline__ void path_begin(Path &p, v3 origin, v3 ray, v3 rd, Cnt &cnt)
 {
-  col mulc = mkc(1.0f, 1.0f, 1.0f);
-  col pix = mkc(0.0f, 0.0f, 0.0f);
   RFX_CNT(C_RAYS);
-  for (int refl = 0; refl < depth; ++refl)
+  p.origin = origin;
+  p.ray = ray;
+  p.rd = rd;
+  p.mulc = mkc(1.0f, 1.0f, 1.0f);
+  p.pix = mkc(0.0f, 0.0f, 0.0f);
+  p.refl = 0;
+}
+
+// One iteration of the bounce loop (Scene.cpp:78-233).  Returns true once the trace is finished:
+// sky hit, mulColor early-out, or reflNumber segments done.
+template <bool STATS, bool LDS>
+__device__ __forceinline__ bool segment(const DevScene &S, Path &p, int depth, const float *lut, Cnt &cnt)
+{
+  const Geo<LDS> G{S};
+  v3 &origin = p.origin;
+  v3 &ray = p.ray;
+  col &mulc = p.mulc;
+  col &pix = p.pix;
+  const v3 rd = p.rd;
   {
     RFX_CNT(C_SEGMENTS);
     // closest hit (Scene.cpp:86-106): the reference keeps the first object with the minimal distance,
@@ -223,9 +321,9 @@ __device__ col trace(const DevScene &S, v3 origin, v3 ray, int depth, v3 rd, con
       for (int i = 0; i < S.n_sph; ++i)
       {
         float t, dist;
-        if (sphere_hit<STATS, false>(S.sph_geo[i], origin, ray, k, t, dist, cnt))
+        if (sphere_hit<STATS, false>(G.sph(i), origin, ray, k, t, dist, cnt))
         {
-          const int obj = S.sph_info[2 * i];
+          const int obj = G.sph_obj(i);
           if (dist < best || (dist == best && obj < best_obj))
           {
             best = dist; best_obj = obj; best_kind = 0; best_i = i; best_t = t;
@@ -236,11 +334,11 @@ __device__ col trace(const DevScene &S, v3 origin, v3 ray, int depth, v3 rd, con
     for (int i = 0; i < S.n_tri; ++i)
     {
       float t, u, v, sq;
-      if (tri_hit<STATS, false>(S.tri_geo[i], origin, ray, t, u, v, sq, cnt))
+      if (tri_hit<STATS, false>(G.tri(i), origin, ray, t, u, v, sq, cnt))
       {
         RFX_CNT(C_TRI_D);
         const float dist = sqrtf(sq);
-        const int obj = S.tri_shade[i].obj;
+        const int obj = G.tri_obj(i);
         if (dist < best || (dist == best && obj < best_obj))
         {
           best = dist; best_obj = obj; best_kind = 1; best_i = i; best_t = t; best_u = u; best_v = v;
@@ -292,7 +390,7 @@ __device__ col trace(const DevScene &S, v3 origin, v3 ray, int depth, v3 rd, con
         {
           RFX_CNT(C_L_FACING);
           const v3 sray = add(dtl, mul(rd, L.radius));
-          if (!occluded<STATS>(S, drop, sray, best_obj, cnt))
+          if (!occluded<STATS, LDS>(S, drop, sray, best_obj, cnt))
           {
             RFX_CNT(C_L_LIT);
             const float dlen = len(dtl);
@@ -341,19 +439,30 @@ __device__ col trace(const DevScene &S, v3 origin, v3 ray, int depth, v3 rd, con
         mulc = cmul(mulc, cscale(color, r));
       }
       pix = cclamp(cadd(pix, fin));                                            // Scene.cpp:215-216
-      if (mulc.r < 0.01f && mulc.g < 0.01f && mulc.b < 0.01f) break;          // Scene.cpp:219-220
+      if (mulc.r < 0.01f && mulc.g < 0.01f && mulc.b < 0.01f) return true;    // Scene.cpp:219-220
       RFX_CNT(C_CONTINUE);
       origin = drop;                                                           // Scene.cpp:223-224
       ray = add(normalized(reflv), mul(rd, 1.0f - m.refl));
+      return ++p.refl >= depth;                                                // Scene.cpp:78
     }
     else                                                                       // Scene.cpp:226-231
     {
       RFX_CNT(C_SKY);
       pix = cclamp(cadd(pix, cmul(cmul(mulc, skybox_texel<STATS>(S, ray, lut, cnt)), mkc(S.env_r, S.env_g, S.env_b))));
-      break;
+      return true;
     }
   }
-  return pix;
+}
+
+// Scene::trace (Scene.cpp:73-236) as a whole: the reference's bounce loop over segment().
+template <bool STATS, bool LDS>
+__device__ __forceinline__ col trace(const DevScene &S, v3 origin, v3 ray, int depth, v3 rd, const float *lut, Cnt &cnt)
+{
+  Path p;
+  path_begin<STATS>(p, origin, ray, rd, cnt);
+  if (depth > 0)
+    while (!segment<STATS, LDS>(S, p, depth, lut, cnt)) {}
+  return p.pix;
 }
 
 template <bool STATS>
@@ -384,12 +493,19 @@ __device__ __forceinline__ v3 load_rd(const FrameParams &P, uint64_t i)
   return mk(P.rd[i], P.rd[P.n_rd + i], P.rd[2 * P.n_rd + i]);
 }
 
+// 5 waves per SIMD (<= 96 VGPRs): measured +8% over the unconstrained 4 waves (tools/ab.py, r01)
+#ifndef RFX_WAVES_PER_EU
+#define RFX_WAVES_PER_EU 5
+#endif
+#define RFX_TRACE_BOUNDS __launch_bounds__(256, RFX_WAVES_PER_EU)
+
 // one workgroup = 16x16 output pixels (BLOCK: block corners), one wave = an 8x8 tile (ray coherence)
-template <bool STATS, bool BLOCK>
-__global__ __launch_bounds__(256) void trace_kernel(DevScene S, FrameParams P)
+template <bool STATS, bool BLOCK, bool LDS>
+__global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
 {
   __shared__ float lut[256];
   lut[threadIdx.x] = (float)threadIdx.x / 255.0f;                               // Color.cpp:11-13
+  if constexpr (LDS) stage_scene_lds(S);
   __syncthreads();
   Cnt cnt;
   if constexpr (STATS)
@@ -421,7 +537,7 @@ __global__ __launch_bounds__(256) void trace_kernel(DevScene S, FrameParams P)
       {
         const v3 ray = mmul(view, mk((float)x - P.wh, (float)y - P.hh, P.rz));
         const uint64_t ti = (uint64_t)cy * bw + cx - P.trace_base;
-        const col c = trace<STATS>(S, eye, ray, P.depth, load_rd(P, ti), lut, cnt);
+        const col c = trace<STATS, LDS>(S, eye, ray, P.depth, load_rd(P, ti), lut, cnt);
         const uint32_t ex = min(P.W, x + n), ey = min(P.H, y + n);
         const uint32_t a = argb(c);
         for (uint32_t qy = y; qy < ey; ++qy)
@@ -462,7 +578,7 @@ __global__ __launch_bounds__(256) void trace_kernel(DevScene S, FrameParams P)
           v3 ray = mk(rx + ox + rndx, ry + oy + rndy, P.rz);
           ray = mmul(view, ray);
           const uint64_t ti = pr * (uint64_t)(ss * ss) + (uint64_t)(sx * ss + sy);
-          fin = cadd(fin, trace<STATS>(S, eye, ray, P.depth, load_rd(P, ti), lut, cnt));
+          fin = cadd(fin, trace<STATS, LDS>(S, eye, ray, P.depth, load_rd(P, ti), lut, cnt));
         }
       if (ss != 1)                                                                 // Render.cpp:189 (x / 1.0f == x)
       {
@@ -475,6 +591,128 @@ __global__ __launch_bounds__(256) void trace_kernel(DevScene S, FrameParams P)
       if (P.accumulate) out = mkc(d[0] + fin.r, d[1] + fin.g, d[2] + fin.b);        // Render.cpp:191-194
       d[0] = out.r; d[1] = out.g; d[2] = out.b;
       if (P.argb) P.argb[o] = argb(out);                                           // Render::copyImage
+    }
+  }
+  flush_counters<STATS>(P, cnt);
+}
+
+// ------------------------------------------------------------- persistent-lane variant
+// Path regeneration: a wave owns a 16x16-pixel chunk (four 8x8 tiles, visited tile by tile) and
+// runs one bounce segment per iteration for all its lanes; a lane whose trace finishes writes its
+// pixel (or starts its pixel's next SSAA sample, keeping the reference's summation order) and takes
+// the chunk's next pixel, so lanes stop idling behind the wave's longest path.  Every lane computes
+// exactly the reference's per-trace arithmetic; only the schedule differs.
+constexpr uint32_t kRegenChunk = 256;  // pixels per wave
+
+template <bool STATS, bool LDS>
+__global__ RFX_TRACE_BOUNDS void trace_regen_kernel(DevScene S, FrameParams P)
+{
+  __shared__ float lut[256];
+  lut[threadIdx.x] = (float)threadIdx.x / 255.0f;                               // Color.cpp:11-13
+  if constexpr (LDS) stage_scene_lds(S);
+  __syncthreads();
+  Cnt cnt;
+  if constexpr (STATS)
+  {
+#pragma unroll
+    for (int k = 0; k < C_COUNT; ++k) cnt.c[k] = 0;
+  }
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint64_t lt_mask = (1ull << lane) - 1ull;
+  const uint32_t cx0 = blockIdx.x * 32u + (wave & 1u) * 16u, cy0 = blockIdx.y * 32u + (wave >> 1) * 16u;
+  m33 view;
+  view.m11 = P.v11; view.m12 = P.v12; view.m13 = P.v13;
+  view.m21 = P.v21; view.m22 = P.v22; view.m23 = P.v23;
+  view.m31 = P.v31; view.m32 = P.v32; view.m33 = P.v33;
+  const v3 eye = mk(P.eye_x, P.eye_y, P.eye_z);
+  const int ss = P.ss;
+  const float ssf = (float)ss;
+
+  Path path;
+  col fin = mkc(0.0f, 0.0f, 0.0f);
+  uint32_t x = 0, orow = 0;
+  uint64_t pr = 0;
+  float rx = 0.0f, ry = 0.0f, rndx = 0.0f, rndy = 0.0f;
+  int sample = 0;
+  bool active = false, need = true;
+  uint32_t next = 0;  // wave-uniform: next chunk index to hand out
+
+  auto start_sample = [&]() {
+    const int sx = sample / ss, sy = sample % ss;
+    const float ox = sx ? (float)sx / ssf : 0.0f, oy = sy ? (float)sy / ssf : 0.0f;
+    v3 ray = mk(rx + ox + rndx, ry + oy + rndy, P.rz);                           // Render.cpp:183-184
+    ray = mmul(view, ray);
+    path_begin<STATS>(path, eye, ray, load_rd(P, pr * (uint64_t)(ss * ss) + (uint64_t)sample), cnt);
+  };
+
+  for (;;)
+  {
+    // hand out chunk pixels to lanes that need one (skipping pixels outside the frame / span)
+    for (;;)
+    {
+      const uint64_t m = __ballot(need);
+      if (!m || next >= kRegenChunk) break;
+      if (need)
+      {
+        const uint32_t ci = next + (uint32_t)__popcll(m & lt_mask);
+        if (ci < kRegenChunk)
+        {
+          const uint32_t tile = ci >> 6, t = ci & 63u;
+          const uint32_t gx = cx0 + (tile & 1u) * 8u + (t & 7u), gy = cy0 + (tile >> 1) * 8u + (t >> 3);
+          if (gx < P.W && gy < P.grid_rows)
+          {
+            const uint32_t y = P.nranks > 1 ? strip_row_to_y(gy, P) : gy + P.row0;
+            const uint64_t p = (uint64_t)y * P.W + gx;
+            if (p >= P.p_begin && p < P.p_end)
+            {
+              x = gx;
+              orow = P.nranks > 1 ? gy : y;
+              pr = p - P.p_begin;
+              rx = (float)x - P.wh;                                              // Render.cpp:152-153
+              ry = (float)y - P.hh;
+              rndx = 0.0f;
+              rndy = 0.0f;
+              if (P.additive)                                                    // Render.cpp:177-178
+              {
+                const uint32_t s1 = lcg_jump(P.jitter_seed, 2 * pr + 1);
+                rndx = (float)lcg_out(s1) / (float)0x7FFF;
+                rndy = (float)lcg_out(lcg_step(s1)) / (float)0x7FFF;
+              }
+              fin = mkc(0.0f, 0.0f, 0.0f);
+              sample = 0;
+              start_sample();
+              active = true;
+              need = false;
+            }
+          }
+        }
+      }
+      next += (uint32_t)__popcll(m);
+    }
+    if (next >= kRegenChunk) need = false;  // queue drained: idle lanes stay idle
+    if (!__any(active)) break;
+
+    if (active && segment<STATS, LDS>(S, path, P.depth, lut, cnt))
+    {
+      fin = cadd(fin, path.pix);                                                 // Render.cpp:185
+      if (++sample < ss * ss)
+        start_sample();
+      else
+      {
+        if (ss != 1)                                                             // Render.cpp:189
+        {
+          const float sq = (float)(ss * ss);
+          if (fabsf(sq) > kVerySmall) fin = mkc(fin.r / sq, fin.g / sq, fin.b / sq);
+        }
+        const size_t o = (size_t)orow * P.W + x;
+        float *d = P.img + o * 3;
+        col out = fin;
+        if (P.accumulate) out = mkc(d[0] + fin.r, d[1] + fin.g, d[2] + fin.b);   // Render.cpp:191-194
+        d[0] = out.r; d[1] = out.g; d[2] = out.b;
+        if (P.argb) P.argb[o] = argb(out);
+        active = false;
+        need = true;
+      }
     }
   }
   flush_counters<STATS>(P, cnt);
@@ -610,15 +848,36 @@ hipError_t launch_trace(const DevScene &S, const FrameParams &P, bool stats, hip
 {
   const uint32_t cols = P.ss < 0 ? (P.W + (uint32_t)(-P.ss) - 1) / (uint32_t)(-P.ss) : P.W;
   const dim3 grid((cols + 15) / 16, (P.grid_rows + 15) / 16);
-  if (P.ss < 0)
+  const bool block = P.ss < 0;
+#ifdef RFX_REGEN
+  if (!block)
   {
-    if (stats) hipLaunchKernelGGL((trace_kernel<true, true>), grid, dim3(256), 0, st, S, P);
-    else hipLaunchKernelGGL((trace_kernel<false, true>), grid, dim3(256), 0, st, S, P);
+    const dim3 g32((P.W + 31) / 32, (P.grid_rows + 31) / 32);
+    const bool lds32 = S.n_sph <= kLdsSph && S.n_tri <= kLdsTri;
+    if (stats) hipLaunchKernelGGL((trace_regen_kernel<true, false>), g32, dim3(256), 0, st, S, P);
+    else if (lds32) hipLaunchKernelGGL((trace_regen_kernel<false, true>), g32, dim3(256), 0, st, S, P);
+    else hipLaunchKernelGGL((trace_regen_kernel<false, false>), g32, dim3(256), 0, st, S, P);
+    return hipGetLastError();
+  }
+#endif
+#ifndef RFX_NO_LDS_SCENE
+  const bool lds = S.n_sph <= kLdsSph && S.n_tri <= kLdsTri;
+  if (!stats && lds)
+  {
+    if (block) hipLaunchKernelGGL((trace_kernel<false, true, true>), grid, dim3(256), 0, st, S, P);
+    else hipLaunchKernelGGL((trace_kernel<false, false, true>), grid, dim3(256), 0, st, S, P);
+    return hipGetLastError();
+  }
+#endif
+  if (block)
+  {
+    if (stats) hipLaunchKernelGGL((trace_kernel<true, true, false>), grid, dim3(256), 0, st, S, P);
+    else hipLaunchKernelGGL((trace_kernel<false, true, false>), grid, dim3(256), 0, st, S, P);
   }
   else
   {
-    if (stats) hipLaunchKernelGGL((trace_kernel<true, false>), grid, dim3(256), 0, st, S, P);
-    else hipLaunchKernelGGL((trace_kernel<false, false>), grid, dim3(256), 0, st, S, P);
+    if (stats) hipLaunchKernelGGL((trace_kernel<true, false, false>), grid, dim3(256), 0, st, S, P);
+    else hipLaunchKernelGGL((trace_kernel<false, false, false>), grid, dim3(256), 0, st, S, P);
   }
   return hipGetLastError();
 }

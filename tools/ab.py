@@ -1,0 +1,177 @@
+#!/usr/bin/env python3
+"""A/B timing of librfx.so variant builds, interleaved in ONE process on ONE GPU.
+
+    python tools/ab.py build                 # (CPU) compile reflaxman_amd/lib/variants/librfx_<name>.so
+    python tools/ab.py run [--rounds R] ...  # (GPU) parity-check + interleaved timing of every built variant
+
+Cross-run / cross-device timings differ by up to ~12% (DVFS, device spread), so
+kernel changes are judged only by interleaved rounds in one process
+(cdna_hip_programming.md §5.4 rule 24).  Every variant's first frame must
+hash to the reference's full-frame SHA-256 before its timing counts.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import glob
+import hashlib
+import json
+import os
+import statistics
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from reflaxman_amd import _build, _lib, scenes  # noqa: E402
+
+VARIANTS = {
+    "base": [],
+    "wpe6": ["RFX_WAVES_PER_EU=6"],
+    "regen": ["RFX_REGEN"],
+    "regen6": ["RFX_REGEN", "RFX_WAVES_PER_EU=6"],
+    "regen4": ["RFX_REGEN", "RFX_WAVES_PER_EU=4"],
+}
+
+
+def build_scene_with(L, desc):
+    fa = _lib.farr
+    s = C.c_void_p(L.rfx_scene_create(*desc.diffuse))
+    keep = []
+    if desc.skybox is not None and desc.skybox.argb is not None:
+        a = np.ascontiguousarray(desc.skybox.argb, np.uint32)
+        keep.append(a)
+        L.rfx_scene_set_skybox_argb(s, a.shape[1], a.shape[0], _lib.u32ptr(a))
+    for (o, r, c, p) in desc.lights:
+        L.rfx_scene_add_light(s, fa(o), r, fa(c), p)
+    tex = []
+    for t in desc.textures:
+        if t.argb is None:
+            tex.append(L.rfx_scene_add_texture_argb(s, 0, 0, None))
+        else:
+            a = np.ascontiguousarray(t.argb, np.uint32)
+            keep.append(a)
+            tex.append(L.rfx_scene_add_texture_argb(s, a.shape[1], a.shape[0], _lib.u32ptr(a)))
+    for ob in desc.objects:
+        mt, rgb, refl, tr = ob[-1]
+        if ob[0] == "sphere":
+            L.rfx_scene_add_sphere(s, fa(ob[1]), ob[2], mt, fa(rgb), refl, tr)
+        else:
+            L.rfx_scene_add_triangle(s, fa(ob[1]), fa(ob[2]), fa(ob[3]), mt, fa(rgb), refl, tr)
+    for (oi, ti, uv) in desc.settex:
+        L.rfx_triangle_set_texture(s, oi, tex[ti], fa(uv))
+    eye, at, fov = desc.camera
+    view = (C.c_float * 9)()
+    L.rfx_camera_view(fa(eye), fa(at), view)
+    return s, list(eye), list(view), fov
+
+
+class Runner:
+    def __init__(self, name, path, desc, W, H, depth, seed):
+        self.name = name
+        L = self.L = _lib.bind(path)
+        self.scene, eye, view, fov = build_scene_with(L, desc)
+        self.r = C.c_void_p()
+        _lib.check(L.rfx_renderer_create(C.byref(self.r), 0)) if False else None
+        rc = L.rfx_renderer_create(C.byref(self.r), 0)
+        assert rc == 0, L.rfx_last_error()
+        assert L.rfx_renderer_set_scene(self.r, self.scene) == 0, L.rfx_last_error()
+        assert L.rfx_renderer_set_rng(self.r, seed, 0) == 0
+        self.W, self.H = W, H
+        self.img, self.argb = C.c_void_p(), C.c_void_p()
+        assert L.rfx_device_alloc(self.r, W * H * 12, C.byref(self.img)) == 0
+        assert L.rfx_device_alloc(self.r, W * H * 4, C.byref(self.argb)) == 0
+        f = _lib.Frame()
+        f.eye[:] = eye
+        f.view[:] = view
+        f.fov = fov
+        f.width, f.height, f.reflect_num, f.sample_num, f.nranks = W, H, depth, 1, 1
+        self.frame = f
+
+    def render(self, n=1):
+        for _ in range(n):
+            rc = self.L.rfx_render_frame(self.r, C.byref(self.frame), self.img, self.argb, None, None)
+            assert rc == 0, self.L.rfx_last_error()
+
+    def first_frame_hashes(self):
+        self.render(1)
+        assert self.L.rfx_synchronize(self.r) == 0
+        rgb = np.empty(self.W * self.H * 3, np.float32)
+        argb = np.empty(self.W * self.H, np.uint32)
+        self.L.rfx_memcpy_d2h(self.r, rgb.ctypes.data_as(C.c_void_p), self.img, rgb.nbytes)
+        self.L.rfx_memcpy_d2h(self.r, argb.ctypes.data_as(C.c_void_p), self.argb, argb.nbytes)
+        return hashlib.sha256(rgb.tobytes()).hexdigest(), hashlib.sha256(argb.tobytes()).hexdigest()
+
+    def timed(self, frames):
+        self.L.rfx_renderer_set_timing(self.r, 1)
+        self.render(frames)
+        pre, tr, n = C.c_double(), C.c_double(), C.c_uint64()
+        self.L.rfx_renderer_get_timing(self.r, C.byref(pre), C.byref(tr), C.byref(n))
+        self.L.rfx_renderer_set_timing(self.r, 0)
+        return pre.value / n.value, tr.value / n.value
+
+
+def cmd_build(names):
+    for n in names:
+        p = _build.build_variant(n, VARIANTS[n])
+        print("built", p)
+
+
+def cmd_run(args):
+    man = json.load(open(os.path.join(ROOT, "tests", "golden", "manifest.json")))["cases"]
+    key = f"hash_{args.scene}_{args.width}x{args.height}_d{args.depth}"
+    desc = scenes.get_scene(args.scene)
+    paths = sorted(glob.glob(os.path.join(_build.LIBDIR, "variants", "librfx_*.so")))
+    names = [os.path.basename(p)[len("librfx_"):-3] for p in paths]
+    if args.only:
+        keep = set(args.only.split(","))
+        paths, names = zip(*[(p, n) for p, n in zip(paths, names) if n in keep])
+    runners = [Runner(n, p, desc, args.width, args.height, args.depth, 1350490027) for n, p in zip(names, paths)]
+    parity = {}
+    for r in runners:
+        hf, ha = r.first_frame_hashes()
+        parity[r.name] = (key in man and hf == man[key]["sha_f32"] and ha == man[key]["sha_argb"]) if key in man else None
+        r.render(args.warmup)
+    times = {r.name: [] for r in runners}
+    pre = {r.name: [] for r in runners}
+    for _ in range(args.rounds):
+        for r in runners:
+            p, t = r.timed(args.frames)
+            times[r.name].append(t)
+            pre[r.name].append(p)
+    base = statistics.median(times[runners[0].name])
+    out = []
+    for r in runners:
+        med = statistics.median(times[r.name])
+        out.append({"variant": r.name, "defines": VARIANTS.get(r.name), "parity_sha_ok": parity[r.name],
+                    "trace_ms_median": round(med, 4), "trace_ms_min": round(min(times[r.name]), 4),
+                    "prepass_ms_median": round(statistics.median(pre[r.name]), 4),
+                    "vs_first": round(med / base, 4),
+                    "mrays_trace_only": round(args.width * args.height / (med * 1e-3) / 1e6, 1)})
+    for o in out:
+        print(json.dumps(o))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("cmd", choices=["build", "run"])
+    ap.add_argument("--variants", default=",".join(VARIANTS))
+    ap.add_argument("--only", default="")
+    ap.add_argument("--scene", default="synth16")
+    ap.add_argument("--width", type=int, default=3840)
+    ap.add_argument("--height", type=int, default=2160)
+    ap.add_argument("--depth", type=int, default=8)
+    ap.add_argument("--rounds", type=int, default=12)
+    ap.add_argument("--frames", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=2)
+    args = ap.parse_args()
+    if args.cmd == "build":
+        cmd_build(args.variants.split(","))
+    else:
+        cmd_run(args)
+
+
+if __name__ == "__main__":
+    main()
