@@ -132,6 +132,21 @@ uint32_t rfx_strip_row_to_y(uint32_t r, uint32_t row_block, uint32_t rank, uint3
 int rfx_render_frame(rfx_renderer *r, const rfx_frame *frame, float *d_rgb, uint32_t *d_argb,
                      uint64_t *d_counters, void *stream);
 
+/*
+ * Multi-GPU form of the RNG pre-pass, around ONE exchange step.  The trace-ordered
+ * random stream is cut into nslices equal slices of LCG blocks; rank r counts the accepted triples of
+ * slice r only (rfx_frame_rng_count), the per-block counts are all-gathered (RCCL: nslices *
+ * blocks_per_slice uint32 on the device), and rfx_render_frame_counted scans them and emits only the
+ * randDirs of this rank's strips before tracing them.  Every rank also carries the stream state past
+ * the frame's last trace, so the next frame starts where the reference's would.  rfx_render_frame is
+ * the same with nslices = 1 and every block counted locally.
+ */
+int rfx_frame_rng_blocks(rfx_renderer *r, const rfx_frame *frame, uint32_t nslices, uint64_t *blocks_per_slice);
+int rfx_frame_rng_count(rfx_renderer *r, const rfx_frame *frame, uint32_t slice, uint32_t nslices,
+                        uint32_t *d_blk_counts, void *stream);
+int rfx_render_frame_counted(rfx_renderer *r, const rfx_frame *frame, uint32_t nslices, const uint32_t *d_blk_counts,
+                             float *d_rgb, uint32_t *d_argb, uint64_t *d_counters, void *stream);
+
 /* Optional per-phase timing of rfx_render_frame with HIP events recorded on the launch stream:
  * enable, render, then read the summed device time (ms) of the RNG pre-pass and of the trace kernel
  * over the frames since the last read (synchronises; resets the sums). */

@@ -68,6 +68,10 @@ SIGNATURES = [
     ("rfx_strip_row_to_y", C.c_uint32, [C.c_uint32] * 4),
     ("rfx_render_frame", C.c_int, [C.c_void_p, C.POINTER(Frame), C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     ("rfx_render_frame_host", C.c_int, [C.c_void_p, C.POINTER(Frame), _fp, _u32p, _u64p]),
+    ("rfx_frame_rng_blocks", C.c_int, [C.c_void_p, C.POINTER(Frame), C.c_uint32, _u64p]),
+    ("rfx_frame_rng_count", C.c_int, [C.c_void_p, C.POINTER(Frame), C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p]),
+    ("rfx_render_frame_counted", C.c_int, [C.c_void_p, C.POINTER(Frame), C.c_uint32, C.c_void_p, C.c_void_p,
+                                           C.c_void_p, C.c_void_p, C.c_void_p]),
     ("rfx_renderer_set_timing", C.c_int, [C.c_void_p, C.c_int]),
     ("rfx_renderer_get_timing", C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double), _u64p]),
     ("rfx_device_alloc", C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p)]),

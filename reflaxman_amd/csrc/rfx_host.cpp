@@ -24,8 +24,12 @@
 
 namespace rfx {
 uint64_t rng_blocks_for(uint64_t traces);
-hipError_t launch_rng(const uint32_t *d_seed, uint32_t *d_next_seed, uint64_t traces, float *d_rd, uint64_t n_rd,
-                      uint32_t *d_blk_cnt, uint64_t *d_blk_off, int *d_err, hipStream_t st);
+hipError_t launch_rng_count(const uint32_t *d_seed, uint32_t *d_blk_cnt, uint64_t blk0, uint64_t nblk_slice,
+                            hipStream_t st);
+hipError_t launch_rng_finish(const uint32_t *d_seed, uint32_t *d_next_seed, const uint32_t *d_blk_cnt, uint64_t nblk,
+                             uint64_t traces, float *d_rd, uint64_t n_rd, uint64_t *d_blk_off, int *d_err,
+                             uint64_t ss2, uint64_t W, uint32_t row_block, uint32_t rank, uint32_t nranks,
+                             hipStream_t st);
 hipError_t launch_trace(const DevScene &S, const FrameParams &P, bool stats, hipStream_t st);
 }  // namespace rfx
 
@@ -602,7 +606,16 @@ extern "C" int rfx_renderer_get_rng(rfx_renderer *r, uint32_t *sphere_seed, uint
   return RFX_OK;
 }
 
-static int ensure_rng_workspace(rfx_renderer *r, uint64_t traces)
+// RNG blocks of a frame's traces, split into nslices equal slices (one per rank in the multi-GPU pre-pass)
+static uint64_t rng_layout(uint64_t traces, uint32_t nslices, uint64_t *per_slice)
+{
+  if (!nslices) nslices = 1;
+  const uint64_t bps = (rng_blocks_for(traces) + nslices - 1) / nslices;
+  if (per_slice) *per_slice = bps;
+  return bps * nslices;
+}
+
+static int ensure_rng_workspace(rfx_renderer *r, uint64_t traces, uint64_t nblk)
 {
   if (traces > r->rd_cap)
   {
@@ -612,7 +625,6 @@ static int ensure_rng_workspace(rfx_renderer *r, uint64_t traces)
     HIP_CHECK(hipMalloc(&r->d_rd, traces * 3 * sizeof(float)));
     r->rd_cap = traces;
   }
-  const uint64_t nblk = rng_blocks_for(traces);
   if (nblk > r->blk_cap)
   {
     (void)hipFree(r->d_blk_cnt); (void)hipFree(r->d_blk_off);
@@ -624,20 +636,109 @@ static int ensure_rng_workspace(rfx_renderer *r, uint64_t traces)
   return RFX_OK;
 }
 
-// sphere stream: d_seed[0] -> pre-pass -> d_seed[1] -> copy back to d_seed[0]
+// Whole pre-pass on one device: every block counted here (the 1-GPU path, and the redundant form of the
+// multi-GPU one).  Sphere stream: d_seed[0] -> pre-pass -> d_seed[1] -> copied back to d_seed[0].
 static int enqueue_rng(rfx_renderer *r, uint64_t traces, hipStream_t st)
 {
   int rc;
-  if ((rc = ensure_rng_workspace(r, traces)) != RFX_OK) return rc;
-  HIP_CHECK(launch_rng(r->d_seed, r->d_seed + 1, traces, r->d_rd, r->rd_cap, r->d_blk_cnt, r->d_blk_off, r->d_err, st));
+  const uint64_t nblk = rng_layout(traces, 1, nullptr);
+  if ((rc = ensure_rng_workspace(r, traces, nblk)) != RFX_OK) return rc;
+  HIP_CHECK(launch_rng_count(r->d_seed, r->d_blk_cnt, 0, nblk, st));
+  HIP_CHECK(launch_rng_finish(r->d_seed, r->d_seed + 1, r->d_blk_cnt, nblk, traces, r->d_rd, r->rd_cap, r->d_blk_off,
+                              r->d_err, 1, 1, 1, 0, 1, st));
   HIP_CHECK(hipMemcpyAsync(r->d_seed, r->d_seed + 1, sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
   return RFX_OK;
+}
+
+// Validate a frame and build its kernel parameters (everything but the output pointers).
+struct FramePlan {
+  FrameParams P;
+  uint64_t traces = 0;
+  hipStream_t st = nullptr;
+};
+
+static int plan_frame(rfx_renderer *r, const rfx_frame *f, void *stream, FramePlan &plan);
+
+extern "C" int rfx_frame_rng_blocks(rfx_renderer *r, const rfx_frame *f, uint32_t nslices, uint64_t *per_slice)
+{
+  FramePlan pl;
+  int rc;
+  if ((rc = plan_frame(r, f, nullptr, pl)) != RFX_OK) return rc;
+  if (!nslices || !per_slice) return fail(RFX_ERR_ARG, "frame_rng_blocks: nslices > 0 and an output required");
+  rng_layout(pl.traces, nslices, per_slice);
+  return RFX_OK;
+}
+
+extern "C" int rfx_frame_rng_count(rfx_renderer *r, const rfx_frame *f, uint32_t slice, uint32_t nslices,
+                                   uint32_t *d_blk_counts, void *stream)
+{
+  FramePlan pl;
+  int rc;
+  if ((rc = plan_frame(r, f, stream, pl)) != RFX_OK) return rc;
+  if (!d_blk_counts || !nslices || slice >= nslices) return fail(RFX_ERR_ARG, "frame_rng_count: bad slice");
+  uint64_t bps = 0;
+  const uint64_t nblk = rng_layout(pl.traces, nslices, &bps);
+  if ((rc = ensure_rng_workspace(r, pl.traces, nblk)) != RFX_OK) return rc;
+  HIP_CHECK(launch_rng_count(r->d_seed, d_blk_counts, (uint64_t)slice * bps, bps, pl.st));
+  return RFX_OK;
+}
+
+static int finish_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *d_counts, uint64_t nblk, float *d_rgb,
+                        uint32_t *d_argb, uint64_t *d_counters)
+{
+  int rc;
+  FrameParams &P = pl.P;
+  const hipStream_t st = pl.st;
+  const uint64_t ss2 = P.ss > 0 ? (uint64_t)(P.ss * P.ss) : 1;
+  HIP_CHECK(launch_rng_finish(r->d_seed, r->d_seed + 1, d_counts, nblk, pl.traces, r->d_rd, r->rd_cap, r->d_blk_off,
+                              r->d_err, ss2, P.W, P.row_block, P.rank, P.nranks, st));
+  HIP_CHECK(hipMemcpyAsync(r->d_seed, r->d_seed + 1, sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+  if ((rc = timing_event(r, st)) != RFX_OK) return rc;
+  P.img = d_rgb;
+  P.argb = d_argb;
+  P.rd = r->d_rd;
+  P.n_rd = r->rd_cap;
+  P.counters = (unsigned long long *)d_counters;
+  if (P.grid_rows) HIP_CHECK(launch_trace(r->dev, P, d_counters != nullptr, st));
+  if ((rc = timing_event(r, st)) != RFX_OK) return rc;
+  if (P.additive)                                                                  // 2 draws per pixel, raster order
+    r->jitter_seed = lcg_jump(r->jitter_seed, 2ull * (P.p_end - P.p_begin));
+  return RFX_OK;
+}
+
+extern "C" int rfx_render_frame_counted(rfx_renderer *r, const rfx_frame *f, uint32_t nslices,
+                                        const uint32_t *d_blk_counts, float *d_rgb, uint32_t *d_argb,
+                                        uint64_t *d_counters, void *stream)
+{
+  FramePlan pl;
+  int rc;
+  if ((rc = plan_frame(r, f, stream, pl)) != RFX_OK) return rc;
+  if (!d_rgb || !d_blk_counts || !nslices) return fail(RFX_ERR_ARG, "render_frame_counted: bad args");
+  if (pl.traces == 0) return RFX_OK;
+  const uint64_t nblk = rng_layout(pl.traces, nslices, nullptr);
+  if ((rc = ensure_rng_workspace(r, pl.traces, nblk)) != RFX_OK) return rc;
+  if ((rc = timing_event(r, pl.st)) != RFX_OK) return rc;
+  return finish_frame(r, pl, d_blk_counts, nblk, d_rgb, d_argb, d_counters);
 }
 
 extern "C" int rfx_render_frame(rfx_renderer *r, const rfx_frame *f, float *d_rgb, uint32_t *d_argb,
                                 uint64_t *d_counters, void *stream)
 {
-  if (!r || !f || !d_rgb) return fail(RFX_ERR_ARG, "render_frame: bad args");
+  FramePlan pl;
+  int rc;
+  if (!d_rgb) return fail(RFX_ERR_ARG, "render_frame: null framebuffer");
+  if ((rc = plan_frame(r, f, stream, pl)) != RFX_OK) return rc;
+  if (pl.traces == 0) return RFX_OK;  // a span with no block corner traces nothing (and draws no randDir)
+  const uint64_t nblk = rng_layout(pl.traces, 1, nullptr);
+  if ((rc = ensure_rng_workspace(r, pl.traces, nblk)) != RFX_OK) return rc;
+  if ((rc = timing_event(r, pl.st)) != RFX_OK) return rc;
+  HIP_CHECK(launch_rng_count(r->d_seed, r->d_blk_cnt, 0, nblk, pl.st));
+  return finish_frame(r, pl, r->d_blk_cnt, nblk, d_rgb, d_argb, d_counters);
+}
+
+static int plan_frame(rfx_renderer *r, const rfx_frame *f, void *stream, FramePlan &plan)
+{
+  if (!r || !f) return fail(RFX_ERR_ARG, "render_frame: bad args");
   if (!r->has_scene) return fail(RFX_ERR_STATE, "render_frame: no scene uploaded");
   if (!f->width || !f->height || f->reflect_num <= 0 || f->sample_num == 0)
     return fail(RFX_ERR_ARG, "render_frame: W=%u H=%u reflect_num=%d sample_num=%d", f->width, f->height,
@@ -681,12 +782,10 @@ extern "C" int rfx_render_frame(rfx_renderer *r, const rfx_frame *f, float *d_rg
     grid_rows = nranks > 1 ? rfx_strip_rows(H, f->row_block, f->rank, nranks) : y1 - y0 + 1;
   }
   if (traces >= (1ull << 32)) return fail(RFX_ERR_ARG, "render_frame: %llu traces exceed 2^32", (unsigned long long)traces);
-  if (traces == 0) return RFX_OK;  // a span with no block corner traces nothing (and draws no randDir)
-  if ((rc = timing_event(r, st)) != RFX_OK) return rc;
-  if ((rc = enqueue_rng(r, traces, st)) != RFX_OK) return rc;
-  if ((rc = timing_event(r, st)) != RFX_OK) return rc;
-
-  FrameParams P{};
+  plan.traces = traces;
+  plan.st = st;
+  FrameParams &P = plan.P;
+  P = FrameParams{};
   P.eye_x = f->eye[0]; P.eye_y = f->eye[1]; P.eye_z = f->eye[2];
   P.v11 = f->view[0]; P.v12 = f->view[1]; P.v13 = f->view[2];
   P.v21 = f->view[3]; P.v22 = f->view[4]; P.v23 = f->view[5];
@@ -708,16 +807,6 @@ extern "C" int rfx_render_frame(rfx_renderer *r, const rfx_frame *f, float *d_rg
   P.p_begin = p0;
   P.p_end = p1;
   P.trace_base = trace_base;
-  P.img = d_rgb;
-  P.argb = d_argb;
-  P.rd = r->d_rd;
-  P.n_rd = r->rd_cap;
-  P.counters = (unsigned long long *)d_counters;
-  if (grid_rows)
-    HIP_CHECK(launch_trace(r->dev, P, d_counters != nullptr, st));
-  if ((rc = timing_event(r, st)) != RFX_OK) return rc;
-  if (P.additive)                                                                  // 2 draws per pixel, raster order
-    r->jitter_seed = lcg_jump(r->jitter_seed, 2ull * (p1 - p0));
   return RFX_OK;
 }
 

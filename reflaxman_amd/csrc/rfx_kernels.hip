@@ -733,9 +733,11 @@ __device__ __forceinline__ bool triple(uint32_t &s, float &x, float &y, float &z
   return !(x * x + y * y + z * z > 1.f);                                        // Vector3.cpp:186
 }
 
-__global__ __launch_bounds__(kRngBlock) void rng_count(const uint32_t *seed, uint32_t *blk_cnt)
+// accepted-triple count of blocks [blk0, blk0 + gridDim.x): one slice of the stream (multi-GPU: one per rank)
+__global__ __launch_bounds__(kRngBlock) void rng_count(const uint32_t *seed, uint32_t *blk_cnt, uint64_t blk0)
 {
-  const uint64_t t = (uint64_t)blockIdx.x * kRngBlock + threadIdx.x;
+  const uint64_t b = blk0 + blockIdx.x;
+  const uint64_t t = b * kRngBlock + threadIdx.x;
   uint32_t s = lcg_jump(*seed, 3ull * kTriplesPerThread * t);
   uint32_t c = 0;
   float x, y, z;
@@ -750,7 +752,7 @@ __global__ __launch_bounds__(kRngBlock) void rng_count(const uint32_t *seed, uin
   {
     uint32_t tot = 0;
     for (int w = 0; w < kRngBlock / 64; ++w) tot += wsum[w];
-    blk_cnt[blockIdx.x] = tot;
+    blk_cnt[b] = tot;
   }
 }
 
@@ -781,9 +783,35 @@ __global__ __launch_bounds__(1024) void rng_scan(const uint32_t *blk_cnt, uint32
   if (threadIdx.x == 1023 && part[1023] < need) *err = 1;
 }
 
-__global__ __launch_bounds__(kRngBlock) void rng_emit(const uint32_t *seed, const uint64_t *blk_off, uint64_t need,
-                                                      float *rd, uint64_t n_rd, uint32_t *next_seed)
+// Which traces a rank needs randDirs for: trace i -> pixel i / ss2 -> row -> strip (row / row_block)
+// -> owner strip % nranks (rfx_strip_row_to_y).  nranks <= 1: every trace.
+struct EmitFilter {
+  uint64_t ss2;       // traces per pixel (ss^2), 1 in block mode
+  uint64_t W;         // pixels per row of the trace index space
+  uint32_t row_block, rank, nranks;
+};
+
+__device__ __forceinline__ bool owned(uint64_t idx, const EmitFilter &f)
 {
+  return ((idx / f.ss2 / f.W / f.row_block) % f.nranks) == f.rank;
+}
+
+__global__ __launch_bounds__(kRngBlock) void rng_emit(const uint32_t *seed, const uint64_t *blk_off,
+                                                      const uint32_t *blk_cnt, uint64_t need, float *rd, uint64_t n_rd,
+                                                      uint32_t *next_seed, EmitFilter flt)
+{
+  // block-uniform skip: a block whose accepted indices all belong to other ranks' strips (and do not
+  // include the frame's last trace, whose stream state every rank carries forward) writes nothing
+  const uint64_t off = blk_off[blockIdx.x];
+  if (off >= need) return;
+  const uint64_t last = min(off + (uint64_t)blk_cnt[blockIdx.x], need) - 1;
+  if (flt.nranks > 1 && last != need - 1)
+  {
+    const uint64_t s_lo = off / flt.ss2 / flt.W / flt.row_block, s_hi = last / flt.ss2 / flt.W / flt.row_block;
+    bool any = false;
+    for (uint64_t s = s_lo; s <= s_hi && !any; ++s) any = (s % flt.nranks) == flt.rank;
+    if (!any) return;
+  }
   const uint64_t t = (uint64_t)blockIdx.x * kRngBlock + threadIdx.x;
   const uint32_t s0 = lcg_jump(*seed, 3ull * kTriplesPerThread * t);
   uint32_t s = s0, c = 0;
@@ -811,11 +839,9 @@ __global__ __launch_bounds__(kRngBlock) void rng_emit(const uint32_t *seed, cons
   {
     if (triple(s, x, y, z))
     {
-      if (idx < need)
-      {
-        rd[idx] = x; rd[n_rd + idx] = y; rd[2 * n_rd + idx] = z;
-        if (idx == need - 1) *next_seed = s;                                    // stream state after trace need-1
-      }
+      if (idx < need && (flt.nranks <= 1 || owned(idx, flt)))
+        { rd[idx] = x; rd[n_rd + idx] = y; rd[2 * n_rd + idx] = z; }
+      if (idx == need - 1) *next_seed = s;                                      // stream state after trace need-1
       ++idx;
     }
   }
@@ -833,14 +859,25 @@ uint64_t rng_blocks_for(uint64_t traces)
   return (triples + kTriplesPerBlock - 1) / kTriplesPerBlock;
 }
 
-hipError_t launch_rng(const uint32_t *d_seed, uint32_t *d_next_seed, uint64_t traces, float *d_rd, uint64_t n_rd,
-                      uint32_t *d_blk_cnt, uint64_t *d_blk_off, int *d_err, hipStream_t st)
+// first half of the pre-pass: accept counts of blocks [blk0, blk0 + nblk_slice)
+hipError_t launch_rng_count(const uint32_t *d_seed, uint32_t *d_blk_cnt, uint64_t blk0, uint64_t nblk_slice,
+                            hipStream_t st)
 {
-  const uint64_t nblk = rng_blocks_for(traces);
-  hipLaunchKernelGGL(rng_count, dim3((uint32_t)nblk), dim3(kRngBlock), 0, st, d_seed, d_blk_cnt);
+  if (nblk_slice)
+    hipLaunchKernelGGL(rng_count, dim3((uint32_t)nblk_slice), dim3(kRngBlock), 0, st, d_seed, d_blk_cnt, blk0);
+  return hipGetLastError();
+}
+
+// second half: scan all nblk counts, scatter the randDirs this rank needs, carry the stream state
+hipError_t launch_rng_finish(const uint32_t *d_seed, uint32_t *d_next_seed, const uint32_t *d_blk_cnt, uint64_t nblk,
+                             uint64_t traces, float *d_rd, uint64_t n_rd, uint64_t *d_blk_off, int *d_err,
+                             uint64_t ss2, uint64_t W, uint32_t row_block, uint32_t rank, uint32_t nranks,
+                             hipStream_t st)
+{
   hipLaunchKernelGGL(rng_scan, dim3(1), dim3(1024), 0, st, d_blk_cnt, (uint32_t)nblk, d_blk_off, traces, d_err);
-  hipLaunchKernelGGL(rng_emit, dim3((uint32_t)nblk), dim3(kRngBlock), 0, st, d_seed, d_blk_off, traces, d_rd, n_rd,
-                     d_next_seed);
+  const EmitFilter flt{ss2 ? ss2 : 1, W ? W : 1, row_block ? row_block : 1, rank, nranks ? nranks : 1};
+  hipLaunchKernelGGL(rng_emit, dim3((uint32_t)nblk), dim3(kRngBlock), 0, st, d_seed, d_blk_off, d_blk_cnt, traces,
+                     d_rd, n_rd, d_next_seed, flt);
   return hipGetLastError();
 }
 

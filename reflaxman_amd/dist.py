@@ -1,0 +1,121 @@
+"""Multi-GPU frames: block-cyclic row strips, one RCCL exchange in the RNG pre-pass, strip gather.
+
+One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI).  Per
+frame, rank r:
+
+1. counts the accepted LCG triples of its 1/N slice of the random stream
+   (``rfx_frame_rng_count``) into its slice of a device array;
+2. all-gathers that array -- the only exchange the path needs, N x ~1K uint32;
+3. scans it, emits the randDirs of *its* strips and traces them
+   (``rfx_render_frame_counted``) -- pre-pass and trace work are both 1/N;
+4. gathers its ARGB8 strip to rank 0, which un-interleaves the strips into
+   the frame with one device ``index_copy_`` (rfx_strip_row_to_y).
+
+The assembled frame equals the 1-GPU frame bit-exactly (tests/test_gpu_parity.py
+emulates the ranks in one process; tests/test_dist_gloo.py runs this module's
+collectives with world_size 2 over gloo on CPU).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+from . import _lib
+
+
+class RfxStripOps:
+    """The renderer side of a rank's strip frame (librfx.so C-ABI)."""
+
+    def __init__(self, renderer, frame: _lib.Frame, stream_ptr: int = 0):
+        self.r = renderer
+        self.frame = frame
+        self.stream = stream_ptr
+        self.L = _lib.load()
+
+    def blocks_per_slice(self, nslices: int) -> int:
+        bps = C.c_uint64()
+        _lib.check(self.L.rfx_frame_rng_blocks(self.r._h, C.byref(self.frame), nslices, C.byref(bps)), "rng_blocks")
+        return bps.value
+
+    def rng_count(self, slice_: int, nslices: int, d_counts: int):
+        _lib.check(self.L.rfx_frame_rng_count(self.r._h, C.byref(self.frame), slice_, nslices, C.c_void_p(d_counts),
+                                              C.c_void_p(self.stream or None)), "rng_count")
+
+    def render_counted(self, nslices: int, d_counts: int, d_img: int, d_argb: int, d_counters: int = 0):
+        _lib.check(self.L.rfx_render_frame_counted(self.r._h, C.byref(self.frame), nslices, C.c_void_p(d_counts),
+                                                   C.c_void_p(d_img), C.c_void_p(d_argb or None),
+                                                   C.c_void_p(d_counters or None), C.c_void_p(self.stream or None)),
+                   "render_frame_counted")
+
+
+def strip_rows(H: int, row_block: int, rank: int, world: int) -> int:
+    """Rows of rank `rank` under block-cyclic strips (== rfx_strip_rows)."""
+    if world <= 1:
+        return H
+    full, rem = divmod(H, row_block)
+    rows = (full // world) * row_block + (row_block if rank < full % world else 0)
+    if rem and full % world == rank:
+        rows += rem
+    return rows
+
+
+def strip_row_to_y(i: int, row_block: int, rank: int, world: int) -> int:
+    """Frame row of strip row i (== rfx_strip_row_to_y)."""
+    if world <= 1:
+        return i
+    return (i // row_block * world + rank) * row_block + i % row_block
+
+
+class StripFrame:
+    """Rank `rank`'s part of a W x H frame rendered by `world` ranks; rank 0 ends with the ARGB8 frame."""
+
+    def __init__(self, ops, W: int, H: int, row_block: int, rank: int, world: int, device: torch.device,
+                 gather_to_root: bool = True):
+        self.ops, self.W, self.H, self.rb = ops, W, H, row_block
+        self.rank, self.world, self.device = rank, world, device
+        self.gather_to_root = gather_to_root
+        self.rows = strip_rows(H, row_block, rank, world)
+        self.max_rows = max(strip_rows(H, row_block, r, world) for r in range(world))
+        self.bps = ops.blocks_per_slice(world)
+        self.counts = torch.zeros(world * self.bps, dtype=torch.int32, device=device)
+        self.img = torch.zeros(max(self.rows, 1) * W * 3, dtype=torch.float32, device=device)
+        self.argb = torch.zeros(self.max_rows * W, dtype=torch.int32, device=device)
+        self.full: Optional[torch.Tensor] = None
+        self.gather_list: Optional[List[torch.Tensor]] = None
+        self.row_index: List[torch.Tensor] = []
+        if gather_to_root and rank == 0:
+            self.full = torch.zeros(H * W, dtype=torch.int32, device=device)
+            self.gather_list = [torch.empty_like(self.argb) for _ in range(world)]
+            for r in range(world):
+                n = strip_rows(H, row_block, r, world)
+                self.row_index.append(torch.tensor([strip_row_to_y(i, row_block, r, world) for i in range(n)],
+                                                   dtype=torch.int64, device=device))
+
+    def _all_gather_counts(self):
+        mine = self.counts[self.rank * self.bps:(self.rank + 1) * self.bps]
+        if dist.get_backend() == "nccl":
+            dist.all_gather_into_tensor(self.counts, mine.clone())
+        else:
+            dist.all_gather(list(self.counts.split(self.bps)), mine.clone())
+
+    def step(self, d_counters: int = 0) -> Optional[torch.Tensor]:
+        """Render this rank's strips of one frame; rank 0 returns the assembled (H, W) int32 ARGB frame."""
+        self.ops.rng_count(self.rank, self.world, self.counts.data_ptr())
+        if self.world > 1:
+            self._all_gather_counts()
+        self.ops.render_counted(self.world, self.counts.data_ptr(), self.img.data_ptr(), self.argb.data_ptr(),
+                                d_counters)
+        if self.world == 1 or not self.gather_to_root:
+            return self.argb[: self.rows * self.W].view(self.rows, self.W) if self.world == 1 else None
+        dist.gather(self.argb, self.gather_list if self.rank == 0 else None, dst=0)
+        if self.rank != 0:
+            return None
+        fv = self.full.view(self.H, self.W)
+        for r in range(self.world):
+            n = self.row_index[r].numel()
+            if n:
+                fv.index_copy_(0, self.row_index[r], self.gather_list[r][: n * self.W].view(n, self.W))
+        return fv

@@ -153,6 +153,62 @@ def test_strip_partition_assembles_to_whole_frame(nranks, row_block):
     assert np.array_equal(argb, whole_argb)
 
 
+@pytest.mark.parametrize("nranks,row_block,ss", [(2, 8, 1), (3, 5, 1), (4, 16, 2), (8, 8, 1)])
+def test_sliced_rng_prepass_multi_rank(nranks, row_block, ss):
+    """The multi-GPU pre-pass (slice counts -> all-gather -> filtered emit), emulated rank by rank in one
+    process: the assembled strips equal the 1-GPU frame and every rank carries the same stream state."""
+    import ctypes as C
+    from reflaxman_amd import _lib
+    from reflaxman_amd.render import Renderer, build_scene, make_frame
+    desc = scene("synth16")
+    W, H, depth = 160, 101, 8
+    s, cam = build_scene(desc)
+    L = _lib.load()
+
+    def fetch(rr, d, n, dtype):
+        a = np.empty(n, dtype)
+        _lib.check(L.rfx_memcpy_d2h(rr._h, a.ctypes.data_as(C.c_void_p), d, a.nbytes))
+        return a
+
+    whole = Renderer(sphere_seed=97531)
+    whole.set_scene(s)
+    d_img, d_argb = C.c_void_p(), C.c_void_p()
+    _lib.check(L.rfx_device_alloc(whole._h, W * H * 12, C.byref(d_img)))
+    _lib.check(L.rfx_device_alloc(whole._h, W * H * 4, C.byref(d_argb)))
+    whole.render_frame(make_frame(cam, W, H, depth, ss), d_img.value, d_argb.value)
+    ref = fetch(whole, d_img, W * H * 3, np.float32).reshape(H, W, 3)
+    ref_argb = fetch(whole, d_argb, W * H, np.uint32).reshape(H, W)
+    ref_seed = whole.get_rng()[0]
+
+    img = np.zeros_like(ref)
+    argb = np.zeros_like(ref_argb)
+    for rank in range(nranks):
+        rr = Renderer(sphere_seed=97531)
+        rr.set_scene(s)
+        f = make_frame(cam, W, H, depth, ss, row_block=row_block, rank=rank, nranks=nranks)
+        bps = C.c_uint64()
+        _lib.check(L.rfx_frame_rng_blocks(rr._h, C.byref(f), nranks, C.byref(bps)))
+        d_cnt = C.c_void_p()
+        _lib.check(L.rfx_device_alloc(rr._h, nranks * bps.value * 4, C.byref(d_cnt)))
+        for sl in range(nranks):  # what the all-gather assembles from every rank's slice
+            _lib.check(L.rfx_frame_rng_count(rr._h, C.byref(f), sl, nranks, d_cnt, None))
+        rows = L.rfx_strip_rows(H, row_block, rank, nranks)
+        p_img, p_argb = C.c_void_p(), C.c_void_p()
+        _lib.check(L.rfx_device_alloc(rr._h, max(rows, 1) * W * 12, C.byref(p_img)))
+        _lib.check(L.rfx_device_alloc(rr._h, max(rows, 1) * W * 4, C.byref(p_argb)))
+        _lib.check(L.rfx_render_frame_counted(rr._h, C.byref(f), nranks, d_cnt, p_img, p_argb, None, None))
+        part = fetch(rr, p_img, rows * W * 3, np.float32).reshape(rows, W, 3)
+        part_argb = fetch(rr, p_argb, rows * W, np.uint32).reshape(rows, W)
+        ys = [L.rfx_strip_row_to_y(i, row_block, rank, nranks) for i in range(rows)]
+        img[ys] = part
+        argb[ys] = part_argb
+        assert rr.get_rng()[0] == ref_seed, rank
+        rr.close()
+    assert img.tobytes() == ref.tobytes()
+    assert np.array_equal(argb, ref_argb)
+    whole.close()
+
+
 def test_event_counters_match_oracle():
     """The stats kernel's event counts equal the CPU restatement's (same algorithm, same branches)."""
     import ctypes as C
