@@ -533,6 +533,17 @@ extern "C" int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *s)
     si.push_back(sp.obj);
     si.push_back(sp.mat.dielectric);
   }
+  std::vector<SpherePair> sp((sg.size() + 1) / 2);
+  for (size_t i = 0; i < 2 * sp.size(); ++i)
+  {
+    SpherePair &p = sp[i / 2];
+    const int l = (int)(i & 1);
+    const bool real = i < sg.size();
+    p.cx[l] = real ? sg[i].cx : 0.0f;
+    p.cy[l] = real ? sg[i].cy : 0.0f;
+    p.cz[l] = real ? sg[i].cz : 0.0f;
+    p.r2[l] = real ? sg[i].sq_radius : -INFINITY;
+  }
   std::vector<TriGeo> tg;
   std::vector<TriShade> ts;
   for (const HostTri &t : s->tris)
@@ -561,7 +572,8 @@ extern "C" int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *s)
     pool.insert(pool.end(), t.texels.begin(), t.texels.end());
   }
   DevScene d{};
-  if ((rc = upload(r, sg, &d.sph_geo)) || (rc = upload(r, sm, &d.sph_mat)) || (rc = upload(r, si, &d.sph_info)) ||
+  if ((rc = upload(r, sg, &d.sph_geo)) || (rc = upload(r, sp, &d.sph_pair)) || (rc = upload(r, sm, &d.sph_mat)) ||
+      (rc = upload(r, si, &d.sph_info)) ||
       (rc = upload(r, tg, &d.tri_geo)) || (rc = upload(r, ts, &d.tri_shade)) || (rc = upload(r, tm, &d.tri_mat)) ||
       (rc = upload(r, lr, &d.lights)) || (rc = upload(r, tr, &d.texs)) || (rc = upload(r, pool, &d.texels)))
     return rc;

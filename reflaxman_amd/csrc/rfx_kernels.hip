@@ -34,6 +34,27 @@ struct Cnt { uint32_t c[C_COUNT]; };
     if constexpr (STATS) cnt.c[k]++; \
   } while (0)
 
+// Diagnostic build only (RFX_DEBUG_PROF, tools/regionprof.py): wave clock cycles spent per region of
+// the bounce segment, summed by each region's first active lane into a device-global table.
+#ifdef RFX_DEBUG_PROF
+enum ProfRegion { P_SPH = 0, P_TRI, P_WIN, P_LIGHT, P_SHADOW, P_MAT, P_SKY, P_SEG, P_COUNT };
+__device__ unsigned long long g_prof[P_COUNT];
+#define RFX_PROF_BEGIN(k) const uint64_t prof_t0_##k = __builtin_amdgcn_s_memtime()
+#define RFX_PROF_END(k)                                                                   \
+  do {                                                                                    \
+    const uint64_t dt_ = __builtin_amdgcn_s_memtime() - prof_t0_##k;                     \
+    if ((threadIdx.x & 63u) == (uint32_t)(__ffsll((long long)__ballot(1)) - 1))           \
+      atomicAdd(&g_prof[k], (unsigned long long)dt_);                                     \
+  } while (0)
+#else
+#define RFX_PROF_BEGIN(k) \
+  do {                    \
+  } while (0)
+#define RFX_PROF_END(k) \
+  do {                  \
+  } while (0)
+#endif
+
 // Color(ARGB) (Color.cpp:9-14) through a 256-entry LDS table of float(k) / 255.0f:
 // the table holds exactly the quotients the reference computes per channel.
 __device__ __forceinline__ col from_argb_lut(uint32_t c, const float *lut)
@@ -52,8 +73,7 @@ __device__ __forceinline__ col from_argb_lut(uint32_t c, const float *lut)
 // in-order returns so reads pipeline); larger scenes read through the scalar cache.
 constexpr int kLdsSph = 256;
 constexpr int kLdsTri = 64;
-__shared__ SphereGeo g_lds_sph[kLdsSph];
-__shared__ int32_t g_lds_sph_obj[kLdsSph];
+__shared__ SpherePair g_lds_pair[kLdsSph / 2];
 __shared__ TriGeo g_lds_tri[kLdsTri];
 __shared__ int32_t g_lds_tri_obj[kLdsTri];
 
@@ -62,27 +82,23 @@ struct Geo;
 template <>
 struct Geo<false> {
   const DevScene &S;
-  __device__ __forceinline__ SphereGeo sph(int i) const { return S.sph_geo[i]; }
-  __device__ __forceinline__ int sph_obj(int i) const { return S.sph_info[2 * i]; }
+  __device__ __forceinline__ SpherePair pair(int j) const { return S.sph_pair[j]; }
   __device__ __forceinline__ TriGeo tri(int i) const { return S.tri_geo[i]; }
   __device__ __forceinline__ int tri_obj(int i) const { return S.tri_shade[i].obj; }
 };
 template <>
 struct Geo<true> {
   const DevScene &S;
-  __device__ __forceinline__ SphereGeo sph(int i) const { return g_lds_sph[i]; }
-  __device__ __forceinline__ int sph_obj(int i) const { return g_lds_sph_obj[i]; }
+  __device__ __forceinline__ SpherePair pair(int j) const { return g_lds_pair[j]; }
   __device__ __forceinline__ TriGeo tri(int i) const { return g_lds_tri[i]; }
   __device__ __forceinline__ int tri_obj(int i) const { return g_lds_tri_obj[i]; }
 };
 
+__device__ __forceinline__ int n_pairs(const DevScene &S) { return (S.n_sph + 1) >> 1; }
+
 __device__ __forceinline__ void stage_scene_lds(const DevScene &S)
 {
-  for (int i = threadIdx.x; i < S.n_sph; i += blockDim.x)
-  {
-    g_lds_sph[i] = S.sph_geo[i];
-    g_lds_sph_obj[i] = S.sph_info[2 * i];
-  }
+  for (int j = threadIdx.x; j < n_pairs(S); j += blockDim.x) g_lds_pair[j] = S.sph_pair[j];
   for (int i = threadIdx.x; i < S.n_tri; i += blockDim.x)
   {
     g_lds_tri[i] = S.tri_geo[i];
@@ -172,38 +188,29 @@ __device__ __forceinline__ RayConst ray_const(v3 ray)
   return k;
 }
 
-// Sphere::trace (Sphere.cpp:44-85) up to its hit decision; on a hit returns t and |ray t|.
+// Sphere::trace (Sphere.cpp:44-85) for spheres 2j and 2j+1 at once, up to the discriminant: each half
+// of an f2 runs the reference's scalar expressions in the reference's order (vco = o - c,
+// b = 2ray . vco, c = |vco|^2 - r^2, d = b*b - 4a*c), so v_pk_* results round exactly as scalar ones.
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ void pair_bd(const SpherePair &g, v3 o, const RayConst &k, f2 &b, f2 &d)
+{
+  const f2 vx = o.x - f2{g.cx[0], g.cx[1]};
+  const f2 vy = o.y - f2{g.cy[0], g.cy[1]};
+  const f2 vz = o.z - f2{g.cz[0], g.cz[1]};
+  b = k.ray2.x * vx + k.ray2.y * vy + k.ray2.z * vz;
+  const f2 c = vx * vx + vy * vy + vz * vz - f2{g.r2[0], g.r2[1]};
+  d = b * b - k.a4 * c;
+}
+
+// The rest of Sphere::trace for one sphere given its b and d: on a hit returns t and |ray t|.
 template <bool STATS, bool SHADOW>
-__device__ __forceinline__ bool sphere_hit(const SphereGeo &g, v3 o, v3 ray, const RayConst &k, float &t_out,
-                                           float &dist_out, Cnt &cnt)
+__device__ __forceinline__ bool sphere_tail(float b, float d, v3 ray, const RayConst &k, float &t_out,
+                                            float &dist_out, Cnt &cnt)
 {
   RFX_CNT(SHADOW ? C_SH_SPH_TESTS : C_SPH_TESTS);
-  const v3 vco = sub(o, mk(g.cx, g.cy, g.cz));
-  const float b = dot(k.ray2, vco);
-#ifdef RFX_BREJECT
-  // b > 0  =>  -b - sqrtf(d) < 0  =>  t < 0 (or -0): the reference's `t > VERY_SMALL_NUMBER` fails.  Exact,
-  // but measured slower than evaluating the discriminant (an extra divergent branch per sphere).
-  if (b > 0.0f) return false;
-#endif
   if constexpr (STATS)
     if (!(b > 0.0f)) RFX_CNT(SHADOW ? C_SH_SPH_B : C_SPH_B);
-  const float c = sqlen(vco) - g.sq_radius;
-  const float d = b * b - k.a4 * c;
-#ifdef RFX_FLAT_SPHERE
-  // predicated: every lane evaluates t and |ray t| (sqrtf of a negative d is a NaN that fails every compare)
-  const bool ok1 = d >= 0.0f && k.a_ok;
-  const float t = (-b - sqrtf(d)) / k.a2;
-  const bool ok2 = ok1 && t > kVerySmall;
-  const float dist = len(mul(ray, t));
-  if constexpr (STATS)
-  {
-    if (ok1 && !(b > 0.0f)) RFX_CNT(SHADOW ? C_SH_SPH_D : C_SPH_D);
-    if (ok2) RFX_CNT(SHADOW ? C_SH_SPH_T : C_SPH_T);
-  }
-  t_out = t;
-  dist_out = dist;
-  return ok2 && dist > kDelta;
-#else
   if (!(d >= 0.0f && k.a_ok)) return false;
   if constexpr (STATS)
     if (!(b > 0.0f)) RFX_CNT(SHADOW ? C_SH_SPH_D : C_SPH_D);
@@ -215,7 +222,6 @@ __device__ __forceinline__ bool sphere_hit(const SphereGeo &g, v3 o, v3 ray, con
   t_out = t;
   dist_out = dist;
   return true;
-#endif
 }
 
 // Triangle::trace (Triangle.cpp:53-108) up to its hit decision; on a hit returns t, u, v, |ray t|^2.
@@ -256,23 +262,29 @@ __device__ __forceinline__ bool tri_hit(const TriGeo &g, v3 o, v3 ray, float &t_
 }
 
 // ------------------------------------------------------------- shadow any-hit
-// Scene.cpp:129-141: every object but the hit one; the boolean does not depend on the order.
-// (Spheres precede triangles, which is the reference's order for every scene whose objects are
-// added spheres-first -- then even the event counters match it.)
+// Scene.cpp:129-141: every object but the hit one (skip_sph / skip_tri: its sphere or triangle index,
+// -1 for the other kind); the boolean does not depend on the order.  (Spheres precede triangles, the
+// reference's order for every scene whose objects are added spheres-first -- then even the event
+// counters match it: the second sphere of a pair is counted only when the first did not occlude.)
 template <bool STATS, bool LDS>
-__device__ __forceinline__ bool occluded(const DevScene &S, v3 o, v3 ray, int skip_obj, Cnt &cnt)
+__device__ __forceinline__ bool occluded(const DevScene &S, v3 o, v3 ray, int skip_sph, int skip_tri, Cnt &cnt)
 {
   const Geo<LDS> G{S};
   const RayConst k = ray_const(ray);
   float t, dist, u, v;
-  for (int i = 0; i < S.n_sph; ++i)
+  const int np = n_pairs(S);
+  for (int j = 0; j < np; ++j)
   {
-    if (G.sph_obj(i) == skip_obj) continue;
-    if (sphere_hit<STATS, true>(G.sph(i), o, ray, k, t, dist, cnt)) return true;
+    f2 b, d;
+    pair_bd(G.pair(j), o, k, b, d);
+    if (2 * j != skip_sph && sphere_tail<STATS, true>(b.x, d.x, ray, k, t, dist, cnt)) return true;
+    if (2 * j + 1 != skip_sph && (!STATS || 2 * j + 1 < S.n_sph) &&
+        sphere_tail<STATS, true>(b.y, d.y, ray, k, t, dist, cnt))
+      return true;
   }
   for (int i = 0; i < S.n_tri; ++i)
   {
-    if (G.tri_obj(i) == skip_obj) continue;
+    if (i == skip_tri) continue;
     if (tri_hit<STATS, true>(G.tri(i), o, ray, t, u, v, dist, cnt)) return true;
   }
   return false;
@@ -316,21 +328,36 @@ __device__ __forceinline__ bool segment(const DevScene &S, Path &p, int depth, c
     float best = kFltMax;
     int best_obj = -1, best_kind = 0, best_i = 0;
     float best_t = 0.0f, best_u = 0.0f, best_v = 0.0f;
+    RFX_PROF_BEGIN(P_SPH);
     {
+      // spheres in index order carry increasing object indices, so among spheres a strict `<` already
+      // keeps the first of equal distances
       const RayConst k = ray_const(ray);
-      for (int i = 0; i < S.n_sph; ++i)
+      const int np = n_pairs(S);
+      int best_sph = -1;
+      for (int j = 0; j < np; ++j)
       {
+        f2 b, d;
+        pair_bd(G.pair(j), origin, k, b, d);
         float t, dist;
-        if (sphere_hit<STATS, false>(G.sph(i), origin, ray, k, t, dist, cnt))
+        if (sphere_tail<STATS, false>(b.x, d.x, ray, k, t, dist, cnt) && dist < best)
         {
-          const int obj = G.sph_obj(i);
-          if (dist < best || (dist == best && obj < best_obj))
-          {
-            best = dist; best_obj = obj; best_kind = 0; best_i = i; best_t = t;
-          }
+          best = dist; best_sph = 2 * j; best_t = t;
+        }
+        if ((!STATS || 2 * j + 1 < S.n_sph) && sphere_tail<STATS, false>(b.y, d.y, ray, k, t, dist, cnt) &&
+            dist < best)
+        {
+          best = dist; best_sph = 2 * j + 1; best_t = t;
         }
       }
+      if (best_sph >= 0)
+      {
+        best_i = best_sph;
+        best_obj = S.sph_info[2 * best_sph];
+      }
     }
+    RFX_PROF_END(P_SPH);
+    RFX_PROF_BEGIN(P_TRI);
     for (int i = 0; i < S.n_tri; ++i)
     {
       float t, u, v, sq;
@@ -346,8 +373,10 @@ __device__ __forceinline__ bool segment(const DevScene &S, Path &p, int depth, c
       }
     }
 
+    RFX_PROF_END(P_TRI);
     if (best_obj >= 0)
     {
+      RFX_PROF_BEGIN(P_WIN);
       // re-derive the winner's outputs with the reference's expressions
       const v3 full = mul(ray, best_t);
       const v3 drop = add(origin, full);
@@ -381,6 +410,8 @@ __device__ __forceinline__ bool segment(const DevScene &S, Path &p, int depth, c
 
       const float rayLen = len(ray), normLen = len(norm), reflectLen = len(reflv);
       col sumL = mkc(0.0f, 0.0f, 0.0f), sumS = mkc(0.0f, 0.0f, 0.0f);
+      RFX_PROF_END(P_WIN);
+      RFX_PROF_BEGIN(P_LIGHT);
       for (int li = 0; li < S.n_light; ++li)                                 // Scene.cpp:117-181
       {
         RFX_CNT(C_L_EVAL);
@@ -390,7 +421,10 @@ __device__ __forceinline__ bool segment(const DevScene &S, Path &p, int depth, c
         {
           RFX_CNT(C_L_FACING);
           const v3 sray = add(dtl, mul(rd, L.radius));
-          if (!occluded<STATS, LDS>(S, drop, sray, best_obj, cnt))
+          RFX_PROF_BEGIN(P_SHADOW);
+          const bool occ = occluded<STATS, LDS>(S, drop, sray, best_kind == 0 ? best_i : -1, best_kind == 1 ? best_i : -1, cnt);
+          RFX_PROF_END(P_SHADOW);
+          if (!occ)
           {
             RFX_CNT(C_L_LIT);
             const float dlen = len(dtl);
@@ -417,6 +451,8 @@ __device__ __forceinline__ bool segment(const DevScene &S, Path &p, int depth, c
           }
         }
       }
+      RFX_PROF_END(P_LIGHT);
+      RFX_PROF_BEGIN(P_MAT);
       sumL = cadd(mkc(S.amb_r, S.amb_g, S.amb_b), sumL);                      // Scene.cpp:186
       const col color = mkc(m.r, m.g, m.b);
       col fin;
@@ -439,6 +475,7 @@ __device__ __forceinline__ bool segment(const DevScene &S, Path &p, int depth, c
         mulc = cmul(mulc, cscale(color, r));
       }
       pix = cclamp(cadd(pix, fin));                                            // Scene.cpp:215-216
+      RFX_PROF_END(P_MAT);
       if (mulc.r < 0.01f && mulc.g < 0.01f && mulc.b < 0.01f) return true;    // Scene.cpp:219-220
       RFX_CNT(C_CONTINUE);
       origin = drop;                                                           // Scene.cpp:223-224
@@ -448,7 +485,9 @@ __device__ __forceinline__ bool segment(const DevScene &S, Path &p, int depth, c
     else                                                                       // Scene.cpp:226-231
     {
       RFX_CNT(C_SKY);
+      RFX_PROF_BEGIN(P_SKY);
       pix = cclamp(cadd(pix, cmul(cmul(mulc, skybox_texel<STATS>(S, ray, lut, cnt)), mkc(S.env_r, S.env_g, S.env_b))));
+      RFX_PROF_END(P_SKY);
       return true;
     }
   }
@@ -460,9 +499,19 @@ __device__ __forceinline__ col trace(const DevScene &S, v3 origin, v3 ray, int d
 {
   Path p;
   path_begin<STATS>(p, origin, ray, rd, cnt);
+#ifdef RFX_DEBUG_SEGS
+  // diagnostic build only (tools/segstats.py): the trace's segment count replaces its color
+  int nseg = 0;
+  if (depth > 0)
+    while (++nseg, !segment<STATS, LDS>(S, p, depth, lut, cnt)) {}
+  return mkc((float)nseg, 0.0f, 0.0f);
+#else
+  RFX_PROF_BEGIN(P_SEG);
   if (depth > 0)
     while (!segment<STATS, LDS>(S, p, depth, lut, cnt)) {}
+  RFX_PROF_END(P_SEG);
   return p.pix;
+#endif
 }
 
 template <bool STATS>
@@ -591,128 +640,6 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
       if (P.accumulate) out = mkc(d[0] + fin.r, d[1] + fin.g, d[2] + fin.b);        // Render.cpp:191-194
       d[0] = out.r; d[1] = out.g; d[2] = out.b;
       if (P.argb) P.argb[o] = argb(out);                                           // Render::copyImage
-    }
-  }
-  flush_counters<STATS>(P, cnt);
-}
-
-// ------------------------------------------------------------- persistent-lane variant
-// Path regeneration: a wave owns a 16x16-pixel chunk (four 8x8 tiles, visited tile by tile) and
-// runs one bounce segment per iteration for all its lanes; a lane whose trace finishes writes its
-// pixel (or starts its pixel's next SSAA sample, keeping the reference's summation order) and takes
-// the chunk's next pixel, so lanes stop idling behind the wave's longest path.  Every lane computes
-// exactly the reference's per-trace arithmetic; only the schedule differs.
-constexpr uint32_t kRegenChunk = 256;  // pixels per wave
-
-template <bool STATS, bool LDS>
-__global__ RFX_TRACE_BOUNDS void trace_regen_kernel(DevScene S, FrameParams P)
-{
-  __shared__ float lut[256];
-  lut[threadIdx.x] = (float)threadIdx.x / 255.0f;                               // Color.cpp:11-13
-  if constexpr (LDS) stage_scene_lds(S);
-  __syncthreads();
-  Cnt cnt;
-  if constexpr (STATS)
-  {
-#pragma unroll
-    for (int k = 0; k < C_COUNT; ++k) cnt.c[k] = 0;
-  }
-  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-  const uint64_t lt_mask = (1ull << lane) - 1ull;
-  const uint32_t cx0 = blockIdx.x * 32u + (wave & 1u) * 16u, cy0 = blockIdx.y * 32u + (wave >> 1) * 16u;
-  m33 view;
-  view.m11 = P.v11; view.m12 = P.v12; view.m13 = P.v13;
-  view.m21 = P.v21; view.m22 = P.v22; view.m23 = P.v23;
-  view.m31 = P.v31; view.m32 = P.v32; view.m33 = P.v33;
-  const v3 eye = mk(P.eye_x, P.eye_y, P.eye_z);
-  const int ss = P.ss;
-  const float ssf = (float)ss;
-
-  Path path;
-  col fin = mkc(0.0f, 0.0f, 0.0f);
-  uint32_t x = 0, orow = 0;
-  uint64_t pr = 0;
-  float rx = 0.0f, ry = 0.0f, rndx = 0.0f, rndy = 0.0f;
-  int sample = 0;
-  bool active = false, need = true;
-  uint32_t next = 0;  // wave-uniform: next chunk index to hand out
-
-  auto start_sample = [&]() {
-    const int sx = sample / ss, sy = sample % ss;
-    const float ox = sx ? (float)sx / ssf : 0.0f, oy = sy ? (float)sy / ssf : 0.0f;
-    v3 ray = mk(rx + ox + rndx, ry + oy + rndy, P.rz);                           // Render.cpp:183-184
-    ray = mmul(view, ray);
-    path_begin<STATS>(path, eye, ray, load_rd(P, pr * (uint64_t)(ss * ss) + (uint64_t)sample), cnt);
-  };
-
-  for (;;)
-  {
-    // hand out chunk pixels to lanes that need one (skipping pixels outside the frame / span)
-    for (;;)
-    {
-      const uint64_t m = __ballot(need);
-      if (!m || next >= kRegenChunk) break;
-      if (need)
-      {
-        const uint32_t ci = next + (uint32_t)__popcll(m & lt_mask);
-        if (ci < kRegenChunk)
-        {
-          const uint32_t tile = ci >> 6, t = ci & 63u;
-          const uint32_t gx = cx0 + (tile & 1u) * 8u + (t & 7u), gy = cy0 + (tile >> 1) * 8u + (t >> 3);
-          if (gx < P.W && gy < P.grid_rows)
-          {
-            const uint32_t y = P.nranks > 1 ? strip_row_to_y(gy, P) : gy + P.row0;
-            const uint64_t p = (uint64_t)y * P.W + gx;
-            if (p >= P.p_begin && p < P.p_end)
-            {
-              x = gx;
-              orow = P.nranks > 1 ? gy : y;
-              pr = p - P.p_begin;
-              rx = (float)x - P.wh;                                              // Render.cpp:152-153
-              ry = (float)y - P.hh;
-              rndx = 0.0f;
-              rndy = 0.0f;
-              if (P.additive)                                                    // Render.cpp:177-178
-              {
-                const uint32_t s1 = lcg_jump(P.jitter_seed, 2 * pr + 1);
-                rndx = (float)lcg_out(s1) / (float)0x7FFF;
-                rndy = (float)lcg_out(lcg_step(s1)) / (float)0x7FFF;
-              }
-              fin = mkc(0.0f, 0.0f, 0.0f);
-              sample = 0;
-              start_sample();
-              active = true;
-              need = false;
-            }
-          }
-        }
-      }
-      next += (uint32_t)__popcll(m);
-    }
-    if (next >= kRegenChunk) need = false;  // queue drained: idle lanes stay idle
-    if (!__any(active)) break;
-
-    if (active && segment<STATS, LDS>(S, path, P.depth, lut, cnt))
-    {
-      fin = cadd(fin, path.pix);                                                 // Render.cpp:185
-      if (++sample < ss * ss)
-        start_sample();
-      else
-      {
-        if (ss != 1)                                                             // Render.cpp:189
-        {
-          const float sq = (float)(ss * ss);
-          if (fabsf(sq) > kVerySmall) fin = mkc(fin.r / sq, fin.g / sq, fin.b / sq);
-        }
-        const size_t o = (size_t)orow * P.W + x;
-        float *d = P.img + o * 3;
-        col out = fin;
-        if (P.accumulate) out = mkc(d[0] + fin.r, d[1] + fin.g, d[2] + fin.b);   // Render.cpp:191-194
-        d[0] = out.r; d[1] = out.g; d[2] = out.b;
-        if (P.argb) P.argb[o] = argb(out);
-        active = false;
-        need = true;
-      }
     }
   }
   flush_counters<STATS>(P, cnt);
@@ -849,6 +776,19 @@ __global__ __launch_bounds__(kRngBlock) void rng_emit(const uint32_t *seed, cons
 
 }  // namespace rfx
 
+#ifdef RFX_DEBUG_PROF
+extern "C" int rfx_debug_prof_read(unsigned long long *out, int reset)
+{
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rfx::g_prof), sizeof(rfx::g_prof)) != hipSuccess) return -1;
+  if (reset)
+  {
+    static const unsigned long long zero[rfx::P_COUNT] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(rfx::g_prof), zero, sizeof(zero)) != hipSuccess) return -1;
+  }
+  return rfx::P_COUNT;
+}
+#endif
+
 // ------------------------------------------------------------- launchers (library-internal)
 namespace rfx {
 
@@ -886,17 +826,6 @@ hipError_t launch_trace(const DevScene &S, const FrameParams &P, bool stats, hip
   const uint32_t cols = P.ss < 0 ? (P.W + (uint32_t)(-P.ss) - 1) / (uint32_t)(-P.ss) : P.W;
   const dim3 grid((cols + 15) / 16, (P.grid_rows + 15) / 16);
   const bool block = P.ss < 0;
-#ifdef RFX_REGEN
-  if (!block)
-  {
-    const dim3 g32((P.W + 31) / 32, (P.grid_rows + 31) / 32);
-    const bool lds32 = S.n_sph <= kLdsSph && S.n_tri <= kLdsTri;
-    if (stats) hipLaunchKernelGGL((trace_regen_kernel<true, false>), g32, dim3(256), 0, st, S, P);
-    else if (lds32) hipLaunchKernelGGL((trace_regen_kernel<false, true>), g32, dim3(256), 0, st, S, P);
-    else hipLaunchKernelGGL((trace_regen_kernel<false, false>), g32, dim3(256), 0, st, S, P);
-    return hipGetLastError();
-  }
-#endif
 #ifndef RFX_NO_LDS_SCENE
   const bool lds = S.n_sph <= kLdsSph && S.n_tri <= kLdsTri;
   if (!stats && lds)

@@ -22,6 +22,9 @@ enum Counter {
 };
 
 struct alignas(16) SphereGeo { float cx, cy, cz, sq_radius; };      // Sphere.cpp:9-20
+// Spheres 2j and 2j+1 side by side, so one packed-f32 (v_pk_*) instruction runs the same step of both
+// miss tests.  An odd count is padded with sq_radius = -inf: c = +inf, d = -inf or NaN, never a hit.
+struct alignas(32) SpherePair { float cx[2], cy[2], cz[2], r2[2]; };
 struct alignas(16) MatRec { float r, g, b, refl; };                 // Material.h:9-11 (transparency unused)
 struct alignas(16) TriGeo {                                          // Triangle.cpp:11-21
   float v0x, v0y, v0z, pad0;
@@ -37,6 +40,7 @@ struct alignas(16) TexRec { uint32_t offset, w, h, pad; };
 
 struct DevScene {
   const SphereGeo *sph_geo;   // n_sph
+  const SpherePair *sph_pair; // (n_sph + 1) / 2
   const MatRec *sph_mat;      // n_sph
   const int32_t *sph_info;    // n_sph x2: {object index, dielectric}
   const TriGeo *tri_geo;      // n_tri

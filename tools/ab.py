@@ -30,9 +30,8 @@ from reflaxman_amd import _build, _lib, scenes  # noqa: E402
 VARIANTS = {
     "base": [],
     "wpe6": ["RFX_WAVES_PER_EU=6"],
-    "regen": ["RFX_REGEN"],
-    "regen6": ["RFX_REGEN", "RFX_WAVES_PER_EU=6"],
-    "regen4": ["RFX_REGEN", "RFX_WAVES_PER_EU=4"],
+    "nolds": ["RFX_NO_LDS_SCENE"],
+    "nolds6": ["RFX_NO_LDS_SCENE", "RFX_WAVES_PER_EU=6"],
 }
 
 

@@ -1,0 +1,39 @@
+"""Where the trace kernel's wave time goes (diagnostic; needs a GPU).
+
+Renders C3 with a RFX_DEBUG_PROF build, which sums s_memtime deltas per region of the bounce segment
+(sphere loop, triangle loop, winner re-derivation, light loop, its shadow any-hit, material, sky) and
+of the whole trace, and prints each region's share of the trace total.
+"""
+import ctypes as C
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+from reflaxman_amd import _build, scenes  # noqa: E402
+import ab  # noqa: E402
+
+REGIONS = ["sphere_loop", "triangle_loop", "winner", "light_loop", "shadow_anyhit", "material", "sky", "trace"]
+
+
+def main():
+    path = os.path.join(_build.LIBDIR, "diag", "librfx_prof.so")
+    scene = sys.argv[1] if len(sys.argv) > 1 else "synth16"
+    r = ab.Runner("prof", path, scenes.get_scene(scene), 3840, 2160, 8, 1350490027)
+    r.render(2)
+    assert r.L.rfx_synchronize(r.r) == 0
+    buf = (C.c_ulonglong * 8)()
+    assert r.L.rfx_debug_prof_read(buf, 1) == 8
+    r.render(1)
+    assert r.L.rfx_synchronize(r.r) == 0
+    assert r.L.rfx_debug_prof_read(buf, 1) == 8
+    tot = buf[7]
+    print(json.dumps({"scene": scene, "cycles": {k: int(v) for k, v in zip(REGIONS, buf)},
+                      "share_of_trace": {k: round(v / tot, 4) for k, v in zip(REGIONS, buf)}}))
+
+
+if __name__ == "__main__":
+    main()
