@@ -25,6 +25,7 @@ FLAGS = [
     "-O3", "-std=c++17", f"--offload-arch={ARCH}",
     "-ffp-contract=off", "-fno-fast-math",
     "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-gpu-flush-denormals-to-zero",
+    "-fno-slp-vectorize",  # auto-packing v3 code costs more v_mov than it saves (tools/ab.py: -7% trace time)
     "-fPIC", "-shared", "-Wall", "-Wno-unknown-pragmas",
 ]
 
@@ -45,10 +46,11 @@ def _stale() -> bool:
 
 
 def build_variant(name: str, defines, verbose: bool = False) -> str:
-    """Compile a variant librfx_<name>.so with extra -D flags (A/B timing builds, tools/ab.py)."""
+    """Compile a variant librfx_<name>.so with extra -D defines / compiler flags (A/B timing builds, tools/ab.py)."""
     out = os.path.join(LIBDIR, "variants", f"librfx_{name}.so")
     os.makedirs(os.path.dirname(out), exist_ok=True)
-    cmd = [hipcc(), *FLAGS, *[f"-D{d}" for d in defines], *[os.path.join(CSRC, s) for s in SOURCES], "-o", out]
+    extra = [d if d.startswith("-") else f"-D{d}" for d in defines]  # "-..." entries are compiler flags
+    cmd = [hipcc(), *FLAGS, *extra, *[os.path.join(CSRC, s) for s in SOURCES], "-o", out]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"variant {name} build failed:\n" + r.stdout + r.stderr)

@@ -38,15 +38,34 @@ struct Cnt { uint32_t c[C_COUNT]; };
 // the bounce segment, summed by each region's first active lane into a device-global table.
 #ifdef RFX_DEBUG_PROF
 enum ProfRegion { P_SPH = 0, P_TRI, P_WIN, P_LIGHT, P_SHADOW, P_MAT, P_SKY, P_SEG, P_COUNT };
-__device__ unsigned long long g_prof[P_COUNT];
+__device__ unsigned long long g_prof[2 * P_COUNT];  // cycles, then wave executions
+__shared__ unsigned long long s_prof[2 * P_COUNT];  // per workgroup, flushed to g_prof at kernel end
 #define RFX_PROF_BEGIN(k) const uint64_t prof_t0_##k = __builtin_amdgcn_s_memtime()
 #define RFX_PROF_END(k)                                                                   \
   do {                                                                                    \
     const uint64_t dt_ = __builtin_amdgcn_s_memtime() - prof_t0_##k;                     \
     if ((threadIdx.x & 63u) == (uint32_t)(__ffsll((long long)__ballot(1)) - 1))           \
-      atomicAdd(&g_prof[k], (unsigned long long)dt_);                                     \
+    {                                                                                     \
+      atomicAdd(&s_prof[k], (unsigned long long)dt_);                                     \
+      atomicAdd(&s_prof[P_COUNT + k], 1ull);                                              \
+    }                                                                                     \
+  } while (0)
+#define RFX_PROF_INIT()                                          \
+  do {                                                           \
+    if (threadIdx.x < 2 * P_COUNT) s_prof[threadIdx.x] = 0ull;   \
+  } while (0)
+#define RFX_PROF_FLUSH()                                                            \
+  do {                                                                              \
+    __syncthreads();                                                                \
+    if (threadIdx.x < 2 * P_COUNT) atomicAdd(&g_prof[threadIdx.x], s_prof[threadIdx.x]); \
   } while (0)
 #else
+#define RFX_PROF_INIT() \
+  do {                  \
+  } while (0)
+#define RFX_PROF_FLUSH() \
+  do {                   \
+  } while (0)
 #define RFX_PROF_BEGIN(k) \
   do {                    \
   } while (0)
@@ -68,14 +87,14 @@ __device__ __forceinline__ col from_argb_lut(uint32_t c, const float *lut)
 }
 
 // ------------------------------------------------------------- scene geometry access
-// The object loops read every primitive in wave-uniform order.  Scenes up to kLdsSph spheres and
-// kLdsTri triangles are staged once per workgroup into LDS (one broadcast ds_read per primitive,
-// in-order returns so reads pipeline); larger scenes read through the scalar cache.
+// The object loops read every primitive in wave-uniform order, so the default build serves them through
+// the scalar cache (s_load_dwordx8 of a sphere pair straight into SGPR operands of the v_pk_* ops).
+// RFX_LDS_SCENE instead stages scenes up to kLdsSph spheres / kLdsTri triangles into LDS per workgroup
+// (broadcast ds_reads); it costs VGPRs and measured slower (tools/ab.py).
 constexpr int kLdsSph = 256;
 constexpr int kLdsTri = 64;
 __shared__ SpherePair g_lds_pair[kLdsSph / 2];
-__shared__ TriGeo g_lds_tri[kLdsTri];
-__shared__ int32_t g_lds_tri_obj[kLdsTri];
+__shared__ TriPair g_lds_tpair[kLdsTri / 2];
 
 template <bool LDS>
 struct Geo;
@@ -83,27 +102,22 @@ template <>
 struct Geo<false> {
   const DevScene &S;
   __device__ __forceinline__ SpherePair pair(int j) const { return S.sph_pair[j]; }
-  __device__ __forceinline__ TriGeo tri(int i) const { return S.tri_geo[i]; }
-  __device__ __forceinline__ int tri_obj(int i) const { return S.tri_shade[i].obj; }
+  __device__ __forceinline__ TriPair tpair(int j) const { return S.tri_pair[j]; }
 };
 template <>
 struct Geo<true> {
   const DevScene &S;
   __device__ __forceinline__ SpherePair pair(int j) const { return g_lds_pair[j]; }
-  __device__ __forceinline__ TriGeo tri(int i) const { return g_lds_tri[i]; }
-  __device__ __forceinline__ int tri_obj(int i) const { return g_lds_tri_obj[i]; }
+  __device__ __forceinline__ TriPair tpair(int j) const { return g_lds_tpair[j]; }
 };
 
 __device__ __forceinline__ int n_pairs(const DevScene &S) { return (S.n_sph + 1) >> 1; }
+__device__ __forceinline__ int n_tpairs(const DevScene &S) { return (S.n_tri + 1) >> 1; }
 
 __device__ __forceinline__ void stage_scene_lds(const DevScene &S)
 {
   for (int j = threadIdx.x; j < n_pairs(S); j += blockDim.x) g_lds_pair[j] = S.sph_pair[j];
-  for (int i = threadIdx.x; i < S.n_tri; i += blockDim.x)
-  {
-    g_lds_tri[i] = S.tri_geo[i];
-    g_lds_tri_obj[i] = S.tri_shade[i].obj;
-  }
+  for (int j = threadIdx.x; j < n_tpairs(S); j += blockDim.x) g_lds_tpair[j] = S.tri_pair[j];
 }
 
 // ------------------------------------------------------------- sampling
@@ -224,35 +238,39 @@ __device__ __forceinline__ bool sphere_tail(float b, float d, v3 ray, const RayC
   return true;
 }
 
-// Triangle::trace (Triangle.cpp:53-108) up to its hit decision; on a hit returns t, u, v, |ray t|^2.
-// axTrans * (o - v0) and axTrans * ray are evaluated row by row, z first (same expressions).
+// Triangle::trace (Triangle.cpp:53-108) for triangles 2j and 2j+1, the part every test runs:
+// dv = o - v0 and the z rows of axTrans * dv and axTrans * ray (same expressions, packed in pairs).
+__device__ __forceinline__ void tri_pair_z(const TriPair &g, v3 o, v3 ray, f2 &dx, f2 &dy, f2 &dz, f2 &aoz, f2 &arz)
+{
+  const f2 a31{g.a31[0], g.a31[1]}, a32{g.a32[0], g.a32[1]}, a33{g.a33[0], g.a33[1]};
+  dx = o.x - f2{g.v0x[0], g.v0x[1]};
+  dy = o.y - f2{g.v0y[0], g.v0y[1]};
+  dz = o.z - f2{g.v0z[0], g.v0z[1]};
+  aoz = dx * a31 + dy * a32 + dz * a33;
+  arz = ray.x * a31 + ray.y * a32 + ray.z * a33;
+}
+
+// The rest of Triangle::trace for one triangle: t = -aoz / arz, then its x and y rows as one packed
+// chain ((aox, aoy), (arx, ary), (u, v)); on a hit returns t, u, v, |ray t|^2.
 template <bool STATS, bool SHADOW>
-__device__ __forceinline__ bool tri_hit(const TriGeo &g, v3 o, v3 ray, float &t_out, float &u_out, float &v_out,
-                                        float &sq_out, Cnt &cnt)
+__device__ __forceinline__ bool tri_tail(const float *xy, float dx, float dy, float dz, float aoz, float arz, v3 ray,
+                                         float &t_out, float &u_out, float &v_out, float &sq_out, Cnt &cnt)
 {
   RFX_CNT(SHADOW ? C_SH_TRI_TESTS : C_TRI_TESTS);
-  const v3 dv = sub(o, mk(g.v0x, g.v0y, g.v0z));
-  const float aoz = dv.x * g.a31 + dv.y * g.a32 + dv.z * g.a33;
-  const float arz = ray.x * g.a31 + ray.y * g.a32 + ray.z * g.a33;
   if (!(fabsf(arz) > kVerySmall)) return false;
   RFX_CNT(SHADOW ? C_SH_TRI_Z : C_TRI_Z);
-  // t = -aoz / arz > VERY_SMALL_NUMBER needs -aoz and arz non-zero with equal signs; otherwise the
-  // quotient is <= 0 or NaN and the reference rejects it.  Exact.
+  // t = -aoz / arz > VERY_SMALL_NUMBER needs -aoz and arz non-zero with equal signs (event counter only)
   const float nz = -aoz;
-  const bool same_sign = (nz > 0.0f && arz > 0.0f) || (nz < 0.0f && arz < 0.0f);
-#ifdef RFX_TRISIGN
-  if (!same_sign) return false;
-#endif
   if constexpr (STATS)
-    if (same_sign) RFX_CNT(SHADOW ? C_SH_TRI_S : C_TRI_S);
+    if ((nz > 0.0f && arz > 0.0f) || (nz < 0.0f && arz < 0.0f)) RFX_CNT(SHADOW ? C_SH_TRI_S : C_TRI_S);
   const float t = nz / arz;
   if (!(t > kVerySmall)) return false;
   RFX_CNT(SHADOW ? C_SH_TRI_T : C_TRI_T);
-  const float aox = dv.x * g.a11 + dv.y * g.a12 + dv.z * g.a13;
-  const float aoy = dv.x * g.a21 + dv.y * g.a22 + dv.z * g.a23;
-  const float arx = ray.x * g.a11 + ray.y * g.a12 + ray.z * g.a13;
-  const float ary = ray.x * g.a21 + ray.y * g.a22 + ray.z * g.a23;
-  const float u = aox + t * arx, v = aoy + t * ary;
+  const f2 c1{xy[0], xy[1]}, c2{xy[2], xy[3]}, c3{xy[4], xy[5]};
+  const f2 ao = dx * c1 + dy * c2 + dz * c3;                  // (aox, aoy)
+  const f2 ar = ray.x * c1 + ray.y * c2 + ray.z * c3;         // (arx, ary)
+  const f2 uv = ao + t * ar;                                  // (u, v)
+  const float u = uv.x, v = uv.y;
   if (!(u >= 0.0f && v >= 0.0f && u + v < 1.0f)) return false;
   RFX_CNT(SHADOW ? C_SH_TRI_IN : C_TRI_IN);
   const float sq = sqlen(mul(ray, t));
@@ -277,15 +295,43 @@ __device__ __forceinline__ bool occluded(const DevScene &S, v3 o, v3 ray, int sk
   {
     f2 b, d;
     pair_bd(G.pair(j), o, k, b, d);
-    if (2 * j != skip_sph && sphere_tail<STATS, true>(b.x, d.x, ray, k, t, dist, cnt)) return true;
-    if (2 * j + 1 != skip_sph && (!STATS || 2 * j + 1 < S.n_sph) &&
-        sphere_tail<STATS, true>(b.y, d.y, ray, k, t, dist, cnt))
-      return true;
+    if constexpr (STATS)
+    {
+      if (2 * j != skip_sph && sphere_tail<STATS, true>(b.x, d.x, ray, k, t, dist, cnt)) return true;
+      if (2 * j + 1 != skip_sph && 2 * j + 1 < S.n_sph && sphere_tail<STATS, true>(b.y, d.y, ray, k, t, dist, cnt))
+        return true;
+    }
+    else
+    {
+      // a miss on both spheres (the common case) costs one branch; the hit object is filtered out
+      // after its test, which does not change the boolean
+      if (!(d.x >= 0.0f || d.y >= 0.0f)) continue;
+      if (sphere_tail<STATS, true>(b.x, d.x, ray, k, t, dist, cnt) && 2 * j != skip_sph) return true;
+      if (sphere_tail<STATS, true>(b.y, d.y, ray, k, t, dist, cnt) && 2 * j + 1 != skip_sph) return true;
+    }
   }
-  for (int i = 0; i < S.n_tri; ++i)
+  const int ntp = n_tpairs(S);
+  for (int j = 0; j < ntp; ++j)
   {
-    if (i == skip_tri) continue;
-    if (tri_hit<STATS, true>(G.tri(i), o, ray, t, u, v, dist, cnt)) return true;
+    const TriPair g = G.tpair(j);
+    f2 dx, dy, dz, aoz, arz;
+    tri_pair_z(g, o, ray, dx, dy, dz, aoz, arz);
+    if constexpr (STATS)
+    {
+      if (2 * j != skip_tri && tri_tail<STATS, true>(g.xy[0], dx.x, dy.x, dz.x, aoz.x, arz.x, ray, t, u, v, dist, cnt))
+        return true;
+      if (2 * j + 1 != skip_tri && 2 * j + 1 < S.n_tri &&
+          tri_tail<STATS, true>(g.xy[1], dx.y, dy.y, dz.y, aoz.y, arz.y, ray, t, u, v, dist, cnt))
+        return true;
+    }
+    else
+    {
+      if (tri_tail<STATS, true>(g.xy[0], dx.x, dy.x, dz.x, aoz.x, arz.x, ray, t, u, v, dist, cnt) && 2 * j != skip_tri)
+        return true;
+      if (tri_tail<STATS, true>(g.xy[1], dx.y, dy.y, dz.y, aoz.y, arz.y, ray, t, u, v, dist, cnt) &&
+          2 * j + 1 != skip_tri)
+        return true;
+    }
   }
   return false;
 }
@@ -339,6 +385,8 @@ __device__ __forceinline__ bool segment(const DevScene &S, Path &p, int depth, c
       {
         f2 b, d;
         pair_bd(G.pair(j), origin, k, b, d);
+        if constexpr (!STATS)
+          if (!(d.x >= 0.0f || d.y >= 0.0f)) continue;  // both miss: one branch
         float t, dist;
         if (sphere_tail<STATS, false>(b.x, d.x, ray, k, t, dist, cnt) && dist < best)
         {
@@ -358,17 +406,27 @@ __device__ __forceinline__ bool segment(const DevScene &S, Path &p, int depth, c
     }
     RFX_PROF_END(P_SPH);
     RFX_PROF_BEGIN(P_TRI);
-    for (int i = 0; i < S.n_tri; ++i)
+    const int ntp = n_tpairs(S);
+    for (int j = 0; j < ntp; ++j)
     {
-      float t, u, v, sq;
-      if (tri_hit<STATS, false>(G.tri(i), origin, ray, t, u, v, sq, cnt))
+      const TriPair g = G.tpair(j);
+      f2 dx, dy, dz, aoz, arz;
+      tri_pair_z(g, origin, ray, dx, dy, dz, aoz, arz);
+#pragma unroll
+      for (int l = 0; l < 2; ++l)
       {
-        RFX_CNT(C_TRI_D);
-        const float dist = sqrtf(sq);
-        const int obj = G.tri_obj(i);
-        if (dist < best || (dist == best && obj < best_obj))
+        const int i = 2 * j + l;
+        if (STATS && i >= S.n_tri) break;
+        float t, u, v, sq;
+        if (tri_tail<STATS, false>(g.xy[l], dx[l], dy[l], dz[l], aoz[l], arz[l], ray, t, u, v, sq, cnt))
         {
-          best = dist; best_obj = obj; best_kind = 1; best_i = i; best_t = t; best_u = u; best_v = v;
+          RFX_CNT(C_TRI_D);
+          const float dist = sqrtf(sq);
+          const int obj = S.tri_shade[i].obj;
+          if (dist < best || (dist == best && obj < best_obj))
+          {
+            best = dist; best_obj = obj; best_kind = 1; best_i = i; best_t = t; best_u = u; best_v = v;
+          }
         }
       }
     }
@@ -542,9 +600,10 @@ __device__ __forceinline__ v3 load_rd(const FrameParams &P, uint64_t i)
   return mk(P.rd[i], P.rd[P.n_rd + i], P.rd[2 * P.n_rd + i]);
 }
 
-// 5 waves per SIMD (<= 96 VGPRs): measured +8% over the unconstrained 4 waves (tools/ab.py, r01)
+// 6 waves per SIMD (<= 80 VGPRs): the kernel is VALU-issue bound (~90% busy, PMC); more waves hide
+// the scene-load and texel latencies better than the spills cost (tools/ab.py: 4 -> 5 -> 6 each won)
 #ifndef RFX_WAVES_PER_EU
-#define RFX_WAVES_PER_EU 5
+#define RFX_WAVES_PER_EU 6
 #endif
 #define RFX_TRACE_BOUNDS __launch_bounds__(256, RFX_WAVES_PER_EU)
 
@@ -555,6 +614,7 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
   __shared__ float lut[256];
   lut[threadIdx.x] = (float)threadIdx.x / 255.0f;                               // Color.cpp:11-13
   if constexpr (LDS) stage_scene_lds(S);
+  RFX_PROF_INIT();
   __syncthreads();
   Cnt cnt;
   if constexpr (STATS)
@@ -643,6 +703,7 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
     }
   }
   flush_counters<STATS>(P, cnt);
+  RFX_PROF_FLUSH();
 }
 
 // ------------------------------------------------------------- RNG pre-pass
@@ -782,10 +843,10 @@ extern "C" int rfx_debug_prof_read(unsigned long long *out, int reset)
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rfx::g_prof), sizeof(rfx::g_prof)) != hipSuccess) return -1;
   if (reset)
   {
-    static const unsigned long long zero[rfx::P_COUNT] = {};
+    static const unsigned long long zero[2 * rfx::P_COUNT] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(rfx::g_prof), zero, sizeof(zero)) != hipSuccess) return -1;
   }
-  return rfx::P_COUNT;
+  return 2 * rfx::P_COUNT;
 }
 #endif
 
@@ -826,7 +887,7 @@ hipError_t launch_trace(const DevScene &S, const FrameParams &P, bool stats, hip
   const uint32_t cols = P.ss < 0 ? (P.W + (uint32_t)(-P.ss) - 1) / (uint32_t)(-P.ss) : P.W;
   const dim3 grid((cols + 15) / 16, (P.grid_rows + 15) / 16);
   const bool block = P.ss < 0;
-#ifndef RFX_NO_LDS_SCENE
+#ifdef RFX_LDS_SCENE  // staged scene: measured slower than scalar loads since sphere pairs (tools/ab.py)
   const bool lds = S.n_sph <= kLdsSph && S.n_tri <= kLdsTri;
   if (!stats && lds)
   {

@@ -29,9 +29,8 @@ from reflaxman_amd import _build, _lib, scenes  # noqa: E402
 
 VARIANTS = {
     "base": [],
-    "wpe6": ["RFX_WAVES_PER_EU=6"],
-    "nolds": ["RFX_NO_LDS_SCENE"],
-    "nolds6": ["RFX_NO_LDS_SCENE", "RFX_WAVES_PER_EU=6"],
+    "wpe5": ["RFX_WAVES_PER_EU=5"],
+    "lds": ["RFX_LDS_SCENE"],
 }
 
 

@@ -25,14 +25,15 @@ def main():
     r = ab.Runner("prof", path, scenes.get_scene(scene), 3840, 2160, 8, 1350490027)
     r.render(2)
     assert r.L.rfx_synchronize(r.r) == 0
-    buf = (C.c_ulonglong * 8)()
-    assert r.L.rfx_debug_prof_read(buf, 1) == 8
+    buf = (C.c_ulonglong * 16)()
+    assert r.L.rfx_debug_prof_read(buf, 1) == 16
     r.render(1)
     assert r.L.rfx_synchronize(r.r) == 0
-    assert r.L.rfx_debug_prof_read(buf, 1) == 8
+    assert r.L.rfx_debug_prof_read(buf, 1) == 16
     tot = buf[7]
-    print(json.dumps({"scene": scene, "cycles": {k: int(v) for k, v in zip(REGIONS, buf)},
-                      "share_of_trace": {k: round(v / tot, 4) for k, v in zip(REGIONS, buf)}}))
+    print(json.dumps({"scene": scene, "cycles": {k: int(v) for k, v in zip(REGIONS, buf[:8])},
+                      "wave_executions": {k: int(v) for k, v in zip(REGIONS, buf[8:])},
+                      "share_of_trace": {k: round(v / tot, 4) for k, v in zip(REGIONS, buf[:8])}}))
 
 
 if __name__ == "__main__":
