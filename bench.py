@@ -15,8 +15,9 @@ does.
 
 N > 1 (weak scaling): the frame grows with N at 16:9 (N=4 is C4, 7680x4320);
 rows are dealt to ranks in block-cyclic 8-row strips, each rank traces its
-strips and the ARGB8 strips are gathered to rank 0 over RCCL (xGMI) and
-un-interleaved on device.  value = traces of the whole frame / step time
+strips; the RNG pre-pass is sliced too (each rank counts 1/N of the random
+stream, one all-gather of ~1K block counts over RCCL), and the ARGB8 strips
+are gathered to rank 0 over RCCL (xGMI) and un-interleaved on device.  value = traces of the whole frame / step time
 (max over ranks).
 
 Also reported: the trace kernel's algorithmic TFLOP/s against the FP32 VALU
@@ -124,11 +125,13 @@ def main():
     ap.add_argument("--row-block", type=int, default=8)
     ap.add_argument("--cpu-stride", type=int, default=2, help="cpu_baseline samples every n-th row")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend (gloo: multi-rank rehearsal)")
+    ap.add_argument("--one-device", action="store_true", help="all ranks on cuda:0 (rehearsal on a 1-GPU box)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    local = 0 if args.one_device else int(os.environ.get("LOCAL_RANK", str(rank)))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
 
@@ -140,7 +143,10 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.backend)
     L = _lib.load()
 
     W, H = frame_size(world, args.width, args.height)
@@ -149,41 +155,52 @@ def main():
     scene, cam = build_scene(desc)
     rr = Renderer(device=local, sphere_seed=SEED)
     rr.set_scene(scene)
-    stream = torch.cuda.current_stream()
+    # one non-default stream, current for torch (collectives, copies) and passed to librfx (a NULL stream
+    # would select the renderer's own non-blocking stream, unordered with torch's work)
+    stream = torch.cuda.Stream(device=dev)
+    torch.cuda.set_stream(stream)
     rr.set_stream(stream.cuda_stream)
 
-    rows = L.rfx_strip_rows(H, rb, rank, world) if world > 1 else H
-    max_rows = max(L.rfx_strip_rows(H, rb, r, world) for r in range(world)) if world > 1 else H
-    img = torch.zeros(rows * W * 3, dtype=torch.float32, device=dev)
-    argb = torch.zeros(max_rows * W, dtype=torch.int32, device=dev)
     frame = make_frame(cam, W, H, depth, 1, row_block=rb if world > 1 else 0, rank=rank, nranks=world)
     traces = W * H
+    if world > 1:
+        # sliced RNG pre-pass (count own slice -> all-gather block counts -> emit own strips), trace of
+        # the own strips, ARGB8 strip gather to rank 0 + device un-interleave (reflaxman_amd/dist.py)
+        from reflaxman_amd.dist import RfxStripOps, StripFrame
+        sf = StripFrame(RfxStripOps(rr, frame, stream.cuda_stream), W, H, rb, rank, world, dev)
+        rows, img, argb = sf.rows, sf.img, sf.argb
+    else:
+        rows = H
+        img = torch.zeros(H * W * 3, dtype=torch.float32, device=dev)
+        argb = torch.zeros(H * W, dtype=torch.int32, device=dev)
     log(f"rank {rank}/{world}: {args.scene} {W}x{H} d{depth}, strip rows {rows}")
 
-    if world > 1:
-        gather_list = [torch.empty_like(argb) for _ in range(world)] if rank == 0 else None
-        full = torch.empty(H * W, dtype=torch.int32, device=dev) if rank == 0 else None
-        row_idx = []
-        if rank == 0:
-            for r in range(world):
-                n = L.rfx_strip_rows(H, rb, r, world)
-                row_idx.append(torch.tensor([L.rfx_strip_row_to_y(i, rb, r, world) for i in range(n)],
-                                            dtype=torch.int64, device=dev))
-
     def step():
-        rr.render_frame(frame, img.data_ptr(), argb.data_ptr(), 0, stream.cuda_stream)
         if world > 1:
-            dist.gather(argb, gather_list, dst=0)
-            if rank == 0:
-                fv = full.view(H, W)
-                for r in range(world):
-                    n = row_idx[r].numel()
-                    fv.index_copy_(0, row_idx[r], gather_list[r][: n * W].view(n, W))
+            return sf.step()
+        rr.render_frame(frame, img.data_ptr(), argb.data_ptr(), 0, stream.cuda_stream)
+        return None
 
     # ---- frame 0 (from the reference's default seed): parity evidence + event counts
-    step()
+    full0 = step()
     torch.cuda.synchronize()
     parity = {}
+    if world > 1 and rank == 0:
+        # the assembled multi-rank frame must equal a single-GPU render of the same frame (untimed)
+        r1 = Renderer(device=local, sphere_seed=SEED)
+        r1.set_scene(scene)
+        r1.set_stream(stream.cuda_stream)
+        f1 = make_frame(cam, W, H, depth, 1)
+        img1 = torch.zeros(H * W * 3, dtype=torch.float32, device=dev)
+        argb1 = torch.zeros(H * W, dtype=torch.int32, device=dev)
+        r1.render_frame(f1, img1.data_ptr(), argb1.data_ptr(), 0, stream.cuda_stream)
+        torch.cuda.synchronize()
+        parity["multi_rank_frame_equals_single_gpu"] = bool(torch.equal(full0.reshape(-1), argb1))
+        if os.environ.get("RFX_BENCH_DUMP"):
+            np.save(os.path.join(os.environ["RFX_BENCH_DUMP"], "multi.npy"), full0.cpu().numpy())
+            np.save(os.path.join(os.environ["RFX_BENCH_DUMP"], "single.npy"), argb1.view(H, W).cpu().numpy())
+        r1.close()
+        del img1, argb1
     first_rgb = first_argb = None
     if world == 1:
         first_rgb = img.view(H, W, 3).cpu().numpy()

@@ -92,7 +92,8 @@ void rfx_argb_from_rgb(const float *rgb, size_t pixels, uint32_t *argb);
 int rfx_renderer_create(rfx_renderer **out, int device);
 void rfx_renderer_destroy(rfx_renderer *r);
 int rfx_renderer_device(const rfx_renderer *r);
-/* launches go to this stream (hipStream_t); NULL = a stream the renderer owns */
+/* launches go to this stream (hipStream_t); NULL = a non-blocking stream the renderer owns (so work on the
+ * legacy default stream is NOT ordered with it: callers that mix in their own work pass their stream) */
 int rfx_renderer_set_stream(rfx_renderer *r, void *hip_stream);
 /* upload the scene (host precompute already done by the builder calls) */
 int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *scene);

@@ -562,18 +562,6 @@ extern "C" int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *s)
     ts.push_back(h);
     tm.push_back({t.mat.r, t.mat.g, t.mat.b, t.mat.refl});
   }
-  std::vector<TriPair> tp((tg.size() + 1) / 2);
-  memset(tp.data(), 0, tp.size() * sizeof(TriPair));
-  for (size_t i = 0; i < tg.size(); ++i)
-  {
-    TriPair &p = tp[i / 2];
-    const int l = (int)(i & 1);
-    const TriGeo &g = tg[i];
-    p.v0x[l] = g.v0x; p.v0y[l] = g.v0y; p.v0z[l] = g.v0z;
-    p.a31[l] = g.a31; p.a32[l] = g.a32; p.a33[l] = g.a33;
-    const float xy[6] = {g.a11, g.a21, g.a12, g.a22, g.a13, g.a23};
-    memcpy(p.xy[l], xy, sizeof(xy));
-  }
   std::vector<LightRec> lr;
   for (const HostLight &l : s->lights) lr.push_back({l.origin.x, l.origin.y, l.origin.z, l.radius, l.r, l.g, l.b, l.power});
   std::vector<TexRec> tr;
@@ -586,7 +574,7 @@ extern "C" int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *s)
   DevScene d{};
   if ((rc = upload(r, sg, &d.sph_geo)) || (rc = upload(r, sp, &d.sph_pair)) || (rc = upload(r, sm, &d.sph_mat)) ||
       (rc = upload(r, si, &d.sph_info)) ||
-      (rc = upload(r, tg, &d.tri_geo)) || (rc = upload(r, tp, &d.tri_pair)) || (rc = upload(r, ts, &d.tri_shade)) || (rc = upload(r, tm, &d.tri_mat)) ||
+      (rc = upload(r, tg, &d.tri_geo)) || (rc = upload(r, ts, &d.tri_shade)) || (rc = upload(r, tm, &d.tri_mat)) ||
       (rc = upload(r, lr, &d.lights)) || (rc = upload(r, tr, &d.texs)) || (rc = upload(r, pool, &d.texels)))
     return rc;
   d.n_sph = (int32_t)sg.size();

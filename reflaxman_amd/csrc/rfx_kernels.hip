@@ -94,7 +94,7 @@ __device__ __forceinline__ col from_argb_lut(uint32_t c, const float *lut)
 constexpr int kLdsSph = 256;
 constexpr int kLdsTri = 64;
 __shared__ SpherePair g_lds_pair[kLdsSph / 2];
-__shared__ TriPair g_lds_tpair[kLdsTri / 2];
+__shared__ TriGeo g_lds_tri[kLdsTri];
 
 template <bool LDS>
 struct Geo;
@@ -102,22 +102,21 @@ template <>
 struct Geo<false> {
   const DevScene &S;
   __device__ __forceinline__ SpherePair pair(int j) const { return S.sph_pair[j]; }
-  __device__ __forceinline__ TriPair tpair(int j) const { return S.tri_pair[j]; }
+  __device__ __forceinline__ TriGeo tri(int i) const { return S.tri_geo[i]; }
 };
 template <>
 struct Geo<true> {
   const DevScene &S;
   __device__ __forceinline__ SpherePair pair(int j) const { return g_lds_pair[j]; }
-  __device__ __forceinline__ TriPair tpair(int j) const { return g_lds_tpair[j]; }
+  __device__ __forceinline__ TriGeo tri(int i) const { return g_lds_tri[i]; }
 };
 
 __device__ __forceinline__ int n_pairs(const DevScene &S) { return (S.n_sph + 1) >> 1; }
-__device__ __forceinline__ int n_tpairs(const DevScene &S) { return (S.n_tri + 1) >> 1; }
 
 __device__ __forceinline__ void stage_scene_lds(const DevScene &S)
 {
   for (int j = threadIdx.x; j < n_pairs(S); j += blockDim.x) g_lds_pair[j] = S.sph_pair[j];
-  for (int j = threadIdx.x; j < n_tpairs(S); j += blockDim.x) g_lds_tpair[j] = S.tri_pair[j];
+  for (int i = threadIdx.x; i < S.n_tri; i += blockDim.x) g_lds_tri[i] = S.tri_geo[i];
 }
 
 // ------------------------------------------------------------- sampling
@@ -238,25 +237,18 @@ __device__ __forceinline__ bool sphere_tail(float b, float d, v3 ray, const RayC
   return true;
 }
 
-// Triangle::trace (Triangle.cpp:53-108) for triangles 2j and 2j+1, the part every test runs:
-// dv = o - v0 and the z rows of axTrans * dv and axTrans * ray (same expressions, packed in pairs).
-__device__ __forceinline__ void tri_pair_z(const TriPair &g, v3 o, v3 ray, f2 &dx, f2 &dy, f2 &dz, f2 &aoz, f2 &arz)
-{
-  const f2 a31{g.a31[0], g.a31[1]}, a32{g.a32[0], g.a32[1]}, a33{g.a33[0], g.a33[1]};
-  dx = o.x - f2{g.v0x[0], g.v0x[1]};
-  dy = o.y - f2{g.v0y[0], g.v0y[1]};
-  dz = o.z - f2{g.v0z[0], g.v0z[1]};
-  aoz = dx * a31 + dy * a32 + dz * a33;
-  arz = ray.x * a31 + ray.y * a32 + ray.z * a33;
-}
-
-// The rest of Triangle::trace for one triangle: t = -aoz / arz, then its x and y rows as one packed
-// chain ((aox, aoy), (arx, ary), (u, v)); on a hit returns t, u, v, |ray t|^2.
+// Triangle::trace (Triangle.cpp:53-108) up to its hit decision; on a hit returns t, u, v, |ray t|^2.
+// axTrans * (o - v0) and axTrans * ray are evaluated row by row with the reference's expressions: the
+// z row first, then -- only for t > VERY_SMALL_NUMBER -- the x and y rows as one packed chain
+// ((aox, aoy), (arx, ary), (u, v)), each half rounding exactly as the scalar expression.
 template <bool STATS, bool SHADOW>
-__device__ __forceinline__ bool tri_tail(const float *xy, float dx, float dy, float dz, float aoz, float arz, v3 ray,
-                                         float &t_out, float &u_out, float &v_out, float &sq_out, Cnt &cnt)
+__device__ __forceinline__ bool tri_hit(const TriGeo &g, v3 o, v3 ray, float &t_out, float &u_out, float &v_out,
+                                        float &sq_out, Cnt &cnt)
 {
   RFX_CNT(SHADOW ? C_SH_TRI_TESTS : C_TRI_TESTS);
+  const float dx = o.x - g.v0x, dy = o.y - g.v0y, dz = o.z - g.v0z;
+  const float aoz = dx * g.a31 + dy * g.a32 + dz * g.a33;
+  const float arz = ray.x * g.a31 + ray.y * g.a32 + ray.z * g.a33;
   if (!(fabsf(arz) > kVerySmall)) return false;
   RFX_CNT(SHADOW ? C_SH_TRI_Z : C_TRI_Z);
   // t = -aoz / arz > VERY_SMALL_NUMBER needs -aoz and arz non-zero with equal signs (event counter only)
@@ -266,7 +258,7 @@ __device__ __forceinline__ bool tri_tail(const float *xy, float dx, float dy, fl
   const float t = nz / arz;
   if (!(t > kVerySmall)) return false;
   RFX_CNT(SHADOW ? C_SH_TRI_T : C_TRI_T);
-  const f2 c1{xy[0], xy[1]}, c2{xy[2], xy[3]}, c3{xy[4], xy[5]};
+  const f2 c1{g.a11, g.a21}, c2{g.a12, g.a22}, c3{g.a13, g.a23};
   const f2 ao = dx * c1 + dy * c2 + dz * c3;                  // (aox, aoy)
   const f2 ar = ray.x * c1 + ray.y * c2 + ray.z * c3;         // (arx, ary)
   const f2 uv = ao + t * ar;                                  // (u, v)
@@ -310,28 +302,14 @@ __device__ __forceinline__ bool occluded(const DevScene &S, v3 o, v3 ray, int sk
       if (sphere_tail<STATS, true>(b.y, d.y, ray, k, t, dist, cnt) && 2 * j + 1 != skip_sph) return true;
     }
   }
-  const int ntp = n_tpairs(S);
-  for (int j = 0; j < ntp; ++j)
+  for (int i = 0; i < S.n_tri; ++i)
   {
-    const TriPair g = G.tpair(j);
-    f2 dx, dy, dz, aoz, arz;
-    tri_pair_z(g, o, ray, dx, dy, dz, aoz, arz);
     if constexpr (STATS)
     {
-      if (2 * j != skip_tri && tri_tail<STATS, true>(g.xy[0], dx.x, dy.x, dz.x, aoz.x, arz.x, ray, t, u, v, dist, cnt))
-        return true;
-      if (2 * j + 1 != skip_tri && 2 * j + 1 < S.n_tri &&
-          tri_tail<STATS, true>(g.xy[1], dx.y, dy.y, dz.y, aoz.y, arz.y, ray, t, u, v, dist, cnt))
-        return true;
+      if (i != skip_tri && tri_hit<STATS, true>(G.tri(i), o, ray, t, u, v, dist, cnt)) return true;
     }
-    else
-    {
-      if (tri_tail<STATS, true>(g.xy[0], dx.x, dy.x, dz.x, aoz.x, arz.x, ray, t, u, v, dist, cnt) && 2 * j != skip_tri)
-        return true;
-      if (tri_tail<STATS, true>(g.xy[1], dx.y, dy.y, dz.y, aoz.y, arz.y, ray, t, u, v, dist, cnt) &&
-          2 * j + 1 != skip_tri)
-        return true;
-    }
+    else if (tri_hit<STATS, true>(G.tri(i), o, ray, t, u, v, dist, cnt) && i != skip_tri)
+      return true;
   }
   return false;
 }
@@ -406,27 +384,17 @@ __device__ __forceinline__ bool segment(const DevScene &S, Path &p, int depth, c
     }
     RFX_PROF_END(P_SPH);
     RFX_PROF_BEGIN(P_TRI);
-    const int ntp = n_tpairs(S);
-    for (int j = 0; j < ntp; ++j)
+    for (int i = 0; i < S.n_tri; ++i)
     {
-      const TriPair g = G.tpair(j);
-      f2 dx, dy, dz, aoz, arz;
-      tri_pair_z(g, origin, ray, dx, dy, dz, aoz, arz);
-#pragma unroll
-      for (int l = 0; l < 2; ++l)
+      float t, u, v, sq;
+      if (tri_hit<STATS, false>(G.tri(i), origin, ray, t, u, v, sq, cnt))
       {
-        const int i = 2 * j + l;
-        if (STATS && i >= S.n_tri) break;
-        float t, u, v, sq;
-        if (tri_tail<STATS, false>(g.xy[l], dx[l], dy[l], dz[l], aoz[l], arz[l], ray, t, u, v, sq, cnt))
+        RFX_CNT(C_TRI_D);
+        const float dist = sqrtf(sq);
+        const int obj = S.tri_shade[i].obj;
+        if (dist < best || (dist == best && obj < best_obj))
         {
-          RFX_CNT(C_TRI_D);
-          const float dist = sqrtf(sq);
-          const int obj = S.tri_shade[i].obj;
-          if (dist < best || (dist == best && obj < best_obj))
-          {
-            best = dist; best_obj = obj; best_kind = 1; best_i = i; best_t = t; best_u = u; best_v = v;
-          }
+          best = dist; best_obj = obj; best_kind = 1; best_i = i; best_t = t; best_u = u; best_v = v;
         }
       }
     }

@@ -26,16 +26,12 @@ struct alignas(16) SphereGeo { float cx, cy, cz, sq_radius; };      // Sphere.cp
 // miss tests.  An odd count is padded with sq_radius = -inf: c = +inf, d = -inf or NaN, never a hit.
 struct alignas(32) SpherePair { float cx[2], cy[2], cz[2], r2[2]; };
 struct alignas(16) MatRec { float r, g, b, refl; };                 // Material.h:9-11 (transparency unused)
-struct alignas(16) TriGeo {                                          // Triangle.cpp:11-21
-  float v0x, v0y, v0z, pad0;
-  float a11, a12, a13, a21, a22, a23, a31, a32, a33, pad1, pad2, pad3;  // axTrans (inverted)
-};
-// Triangles 2j and 2j+1 for packed tests: the z rows (t test) of both side by side, then per triangle
-// its x and y rows interleaved -- (a11,a21), (a12,a22), (a13,a23) -- so (u, v) come out of one v_pk
-// chain.  An odd count is padded with zeros: arz = 0 fails |arz| > VERY_SMALL_NUMBER, never a hit.
-struct alignas(32) TriPair {
-  float v0x[2], v0y[2], v0z[2], a31[2], a32[2], a33[2];
-  float xy[2][6];  // triangle l: a11, a21, a12, a22, a13, a23
+// Triangle.cpp:11-21: v0 and axTrans (inverted) -- z row first (every test needs it), then the x and
+// y rows interleaved, (a11,a21), (a12,a22), (a13,a23), so (u, v) come out of one v_pk_* chain.
+struct alignas(16) TriGeo {
+  float v0x, v0y, v0z, a31, a32, a33;
+  float a11, a21, a12, a22, a13, a23;
+  float pad[4];
 };
 struct alignas(16) TriShade {                                        // Triangle.cpp:110-120
   float nx, ny, nz, tu0;
@@ -51,7 +47,6 @@ struct DevScene {
   const MatRec *sph_mat;      // n_sph
   const int32_t *sph_info;    // n_sph x2: {object index, dielectric}
   const TriGeo *tri_geo;      // n_tri
-  const TriPair *tri_pair;    // (n_tri + 1) / 2
   const TriShade *tri_shade;  // n_tri
   const MatRec *tri_mat;      // n_tri
   const LightRec *lights;     // n_light

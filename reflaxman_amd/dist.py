@@ -29,7 +29,10 @@ from . import _lib
 class RfxStripOps:
     """The renderer side of a rank's strip frame (librfx.so C-ABI)."""
 
-    def __init__(self, renderer, frame: _lib.Frame, stream_ptr: int = 0):
+    def __init__(self, renderer, frame: _lib.Frame, stream_ptr: int):
+        if not stream_ptr:
+            # NULL would select the renderer's own non-blocking stream, unordered with the collectives
+            raise ValueError("RfxStripOps needs the (non-default) torch stream the collectives run on")
         self.r = renderer
         self.frame = frame
         self.stream = stream_ptr
@@ -94,12 +97,30 @@ class StripFrame:
                 self.row_index.append(torch.tensor([strip_row_to_y(i, row_block, r, world) for i in range(n)],
                                                    dtype=torch.int64, device=device))
 
+    def _host_staged(self) -> bool:
+        # gloo on device tensors (a multi-rank rehearsal on one GPU): stage the collectives through host memory
+        return self.device.type == "cuda" and dist.get_backend() != "nccl"
+
     def _all_gather_counts(self):
         mine = self.counts[self.rank * self.bps:(self.rank + 1) * self.bps]
         if dist.get_backend() == "nccl":
             dist.all_gather_into_tensor(self.counts, mine.clone())
+        elif self._host_staged():
+            h = self.counts.cpu()
+            dist.all_gather(list(h.split(self.bps)), h[self.rank * self.bps:(self.rank + 1) * self.bps].clone())
+            self.counts.copy_(h)
         else:
             dist.all_gather(list(self.counts.split(self.bps)), mine.clone())
+
+    def _gather_strips(self):
+        if not self._host_staged():
+            dist.gather(self.argb, self.gather_list if self.rank == 0 else None, dst=0)
+            return
+        lst = [torch.empty(self.argb.shape, dtype=self.argb.dtype) for _ in range(self.world)] if self.rank == 0 else None
+        dist.gather(self.argb.cpu(), lst, dst=0)
+        if self.rank == 0:
+            for d, h in zip(self.gather_list, lst):
+                d.copy_(h)
 
     def step(self, d_counters: int = 0) -> Optional[torch.Tensor]:
         """Render this rank's strips of one frame; rank 0 returns the assembled (H, W) int32 ARGB frame."""
@@ -110,7 +131,7 @@ class StripFrame:
                                 d_counters)
         if self.world == 1 or not self.gather_to_root:
             return self.argb[: self.rows * self.W].view(self.rows, self.W) if self.world == 1 else None
-        dist.gather(self.argb, self.gather_list if self.rank == 0 else None, dst=0)
+        self._gather_strips()
         if self.rank != 0:
             return None
         fv = self.full.view(self.H, self.W)
