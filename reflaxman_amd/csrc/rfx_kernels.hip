@@ -216,6 +216,17 @@ __device__ __forceinline__ void pair_bd(const SpherePair &g, v3 o, const RayCons
   d = b * b - k.a4 * c;
 }
 
+// Can either sphere of a pair hit?  d < 0 misses; so does b >= 0 (or NaN), since then -b - sqrt(d) <= 0
+// gives t <= 0, which `t > VERY_SMALL_NUMBER` rejects (Sphere.cpp:58-60) -- both are exact rejects.
+__device__ __forceinline__ bool pair_may_hit(f2 b, f2 d)
+{
+#ifdef RFX_NO_SPH_B
+  return d.x >= 0.0f || d.y >= 0.0f;
+#else
+  return (d.x >= 0.0f && b.x < 0.0f) || (d.y >= 0.0f && b.y < 0.0f);
+#endif
+}
+
 // The rest of Sphere::trace for one sphere given its b and d: on a hit returns t and |ray t|.
 template <bool STATS, bool SHADOW>
 __device__ __forceinline__ bool sphere_tail(float b, float d, v3 ray, const RayConst &k, float &t_out,
@@ -225,6 +236,11 @@ __device__ __forceinline__ bool sphere_tail(float b, float d, v3 ray, const RayC
   if constexpr (STATS)
     if (!(b > 0.0f)) RFX_CNT(SHADOW ? C_SH_SPH_B : C_SPH_B);
   if (!(d >= 0.0f && k.a_ok)) return false;
+#ifndef RFX_NO_SPH_B
+  // b >= 0 (or NaN): -b - sqrt(d) <= 0, so t <= 0 and `t > VERY_SMALL_NUMBER` rejects -- exact early out
+  if constexpr (!STATS)
+    if (!(b < 0.0f)) return false;
+#endif
   if constexpr (STATS)
     if (!(b > 0.0f)) RFX_CNT(SHADOW ? C_SH_SPH_D : C_SPH_D);
   const float t = (-b - sqrtf(d)) / k.a2;
@@ -253,8 +269,14 @@ __device__ __forceinline__ bool tri_hit(const TriGeo &g, v3 o, v3 ray, float &t_
   RFX_CNT(SHADOW ? C_SH_TRI_Z : C_TRI_Z);
   // t = -aoz / arz > VERY_SMALL_NUMBER needs -aoz and arz non-zero with equal signs (event counter only)
   const float nz = -aoz;
+  const bool same_sign = (nz > 0.0f && arz > 0.0f) || (nz < 0.0f && arz < 0.0f);
   if constexpr (STATS)
-    if ((nz > 0.0f && arz > 0.0f) || (nz < 0.0f && arz < 0.0f)) RFX_CNT(SHADOW ? C_SH_TRI_S : C_TRI_S);
+    if (same_sign) RFX_CNT(SHADOW ? C_SH_TRI_S : C_TRI_S);
+#ifndef RFX_NO_TRI_SIGN
+  // exact reject before the division: with opposite signs or a zero (or NaN) numerator, t <= 0 or NaN,
+  // which `t > VERY_SMALL_NUMBER` rejects anyway; the divide is skipped when no lane of the wave needs it
+  if (!same_sign) return false;
+#endif
   const float t = nz / arz;
   if (!(t > kVerySmall)) return false;
   RFX_CNT(SHADOW ? C_SH_TRI_T : C_TRI_T);
@@ -297,7 +319,7 @@ __device__ __forceinline__ bool occluded(const DevScene &S, v3 o, v3 ray, int sk
     {
       // a miss on both spheres (the common case) costs one branch; the hit object is filtered out
       // after its test, which does not change the boolean
-      if (!(d.x >= 0.0f || d.y >= 0.0f)) continue;
+      if (!pair_may_hit(b, d)) continue;
       if (sphere_tail<STATS, true>(b.x, d.x, ray, k, t, dist, cnt) && 2 * j != skip_sph) return true;
       if (sphere_tail<STATS, true>(b.y, d.y, ray, k, t, dist, cnt) && 2 * j + 1 != skip_sph) return true;
     }
@@ -312,6 +334,29 @@ __device__ __forceinline__ bool occluded(const DevScene &S, v3 o, v3 ray, int sk
       return true;
   }
   return false;
+}
+
+// Scene.cpp:117-141 for lights [base, base + 32): bit k set when light base + k faces the hit point
+// (dot(dropToLight, norm) > VERY_SMALL_NUMBER) and its jittered shadow ray reaches it unoccluded.
+template <bool STATS, bool LDS>
+__device__ __forceinline__ uint32_t lights_visible(const DevScene &S, v3 drop, v3 norm, v3 rd, int base, int skip_sph,
+                                                   int skip_tri, Cnt &cnt)
+{
+  uint32_t lit = 0;
+  const int nl = min(32, S.n_light - base);
+  for (int k = 0; k < nl; ++k)
+  {
+    RFX_CNT(C_L_EVAL);
+    const LightRec L = S.lights[base + k];
+    const v3 dtl = sub(mk(L.ox, L.oy, L.oz), drop);
+    if (dot(dtl, norm) > kVerySmall)
+    {
+      RFX_CNT(C_L_FACING);
+      const v3 sray = add(dtl, mul(rd, L.radius));                          // Scene.cpp:129
+      if (!occluded<STATS, LDS>(S, drop, sray, skip_sph, skip_tri, cnt)) lit |= 1u << k;
+    }
+  }
+  return lit;
 }
 
 // ------------------------------------------------------------- Scene::trace
@@ -336,9 +381,14 @@ __device__ __forceinline__ void path_begin(Path &p, v3 origin, v3 ray, v3 rd, Cn
 
 // One iteration of the bounce loop (Scene.cpp:78-233).  Returns true once the trace is finished:
 // sky hit, mulColor early-out, or reflNumber segments done.
-template <bool STATS, bool LDS>
+// CFG bits: kCfgLds -- scene staged in LDS; kCfgManyLights -- more than 32 lights (shadow masks in blocks)
+constexpr int kCfgLds = 1, kCfgManyLights = 2;
+
+template <bool STATS, int CFG>
 __device__ __forceinline__ bool segment(const DevScene &S, Path &p, int depth, const float *lut, Cnt &cnt)
 {
+  constexpr bool LDS = (CFG & kCfgLds) != 0;
+  constexpr bool MANYL = (CFG & kCfgManyLights) != 0;
   const Geo<LDS> G{S};
   v3 &origin = p.origin;
   v3 &ray = p.ray;
@@ -364,7 +414,7 @@ __device__ __forceinline__ bool segment(const DevScene &S, Path &p, int depth, c
         f2 b, d;
         pair_bd(G.pair(j), origin, k, b, d);
         if constexpr (!STATS)
-          if (!(d.x >= 0.0f || d.y >= 0.0f)) continue;  // both miss: one branch
+          if (!pair_may_hit(b, d)) continue;  // both miss: one branch
         float t, dist;
         if (sphere_tail<STATS, false>(b.x, d.x, ray, k, t, dist, cnt) && dist < best)
         {
@@ -404,80 +454,91 @@ __device__ __forceinline__ bool segment(const DevScene &S, Path &p, int depth, c
     {
       RFX_PROF_BEGIN(P_WIN);
       // re-derive the winner's outputs with the reference's expressions
-      const v3 full = mul(ray, best_t);
-      const v3 drop = add(origin, full);
+      const v3 drop = add(origin, mul(ray, best_t));
       v3 norm;
-      MatRec m;
-      int diel;
       if (best_kind == 0)
       {
         RFX_CNT(C_HIT_SPH);
         const SphereGeo g = S.sph_geo[best_i];
         norm = sub(drop, mk(g.cx, g.cy, g.cz));                              // Sphere.cpp:69
-        m = S.sph_mat[best_i];
-        diel = S.sph_info[2 * best_i + 1];
       }
       else
       {
         RFX_CNT(C_HIT_TRI);
-        const TriShade sh = S.tri_shade[best_i];
-        norm = mk(sh.nx, sh.ny, sh.nz);
-        m = S.tri_mat[best_i];
-        diel = sh.dielectric;
-        if (sh.tex >= 0)                                                     // Triangle.cpp:92-99
-        {
-          const float tvx = best_u * sh.t11 + best_v * sh.t12 + 0.0f;
-          const float tvy = best_u * sh.t21 + best_v * sh.t22 + 0.0f;
-          const col c = texel_uv<STATS>(S, sh.tex, sh.tu0 + tvx, sh.tv0 + tvy, lut, cnt);
-          m.r = c.r; m.g = c.g; m.b = c.b;
-        }
+        norm = mk(S.tri_shade[best_i].nx, S.tri_shade[best_i].ny, S.tri_shade[best_i].nz);
       }
-      const v3 reflv = reflect(full, norm);                                 // trace_math.cpp:14-23
-
-      const float rayLen = len(ray), normLen = len(norm), reflectLen = len(reflv);
-      col sumL = mkc(0.0f, 0.0f, 0.0f), sumS = mkc(0.0f, 0.0f, 0.0f);
       RFX_PROF_END(P_WIN);
-      RFX_PROF_BEGIN(P_LIGHT);
-      for (int li = 0; li < S.n_light; ++li)                                 // Scene.cpp:117-181
+      // Scene.cpp:117-141 first, for up to 32 lights: which of them reach the hit point.  The occlusion
+      // tests depend on nothing the shading computes, so running them before it (with only the hit point,
+      // its normal and the jitter live) changes no result and keeps the any-hit loop's registers free.
+      const int skip_sph = best_kind == 0 ? best_i : -1, skip_tri = best_kind == 1 ? best_i : -1;
+      MatRec m{0.0f, 0.0f, 0.0f, 0.0f};
+      int diel = 0;
+      v3 reflv = mk(0.0f, 0.0f, 0.0f);
+      float rayLen = 0.0f, normLen = 0.0f, reflectLen = 0.0f;
+      col sumL = mkc(0.0f, 0.0f, 0.0f), sumS = mkc(0.0f, 0.0f, 0.0f);
+      for (int base = 0;; base += 32)                                        // Scene.cpp:117-181
       {
-        RFX_CNT(C_L_EVAL);
-        const LightRec L = S.lights[li];
-        const v3 dtl = sub(mk(L.ox, L.oy, L.oz), drop);
-        if (dot(dtl, norm) > kVerySmall)
+        RFX_PROF_BEGIN(P_SHADOW);
+        const uint32_t lit = lights_visible<STATS, LDS>(S, drop, norm, rd, base, skip_sph, skip_tri, cnt);
+        RFX_PROF_END(P_SHADOW);
+        RFX_PROF_BEGIN(P_LIGHT);
+        if (!MANYL || base == 0)
         {
-          RFX_CNT(C_L_FACING);
-          const v3 sray = add(dtl, mul(rd, L.radius));
-          RFX_PROF_BEGIN(P_SHADOW);
-          const bool occ = occluded<STATS, LDS>(S, drop, sray, best_kind == 0 ? best_i : -1, best_kind == 1 ? best_i : -1, cnt);
-          RFX_PROF_END(P_SHADOW);
-          if (!occ)
+          // the hit object's material, texel, reflection and lengths (Sphere.cpp:66-80, Triangle.cpp:86-105)
+          if (best_kind == 0)
           {
-            RFX_CNT(C_L_LIT);
-            const float dlen = len(dtl);
-            float aa = dlen * normLen;
-            const float cosl = (aa > kVerySmall) ? dot(dtl, norm) / aa : 0.0f;
-            const col lc = mkc(L.r, L.g, L.b);
-            if (L.power > kVerySmall) sumL = cadd(sumL, cscale(cscale(lc, cosl), L.power));
-            aa = sqlen(dtl);
-            const float ang = (aa > kVerySmall) ? 1.0f - L.radius * L.radius / aa : 0.0f;
-            if (ang > 0)
+            m = S.sph_mat[best_i];
+            diel = S.sph_info[2 * best_i + 1];
+          }
+          else
+          {
+            const TriShade sh = S.tri_shade[best_i];
+            m = S.tri_mat[best_i];
+            diel = sh.dielectric;
+            if (sh.tex >= 0)                                                 // Triangle.cpp:92-99
             {
-              RFX_CNT(C_L_SPEC);
-              const v3 dlr = add(normalized(dtl), mul(rd, 1.0f - m.refl));
-              aa = len(dlr) * reflectLen;
-              float sc = (aa > kVerySmall) ? dot(dlr, reflv) / aa : 0.0f;
-              sc = clampf(sc + (1.0f - sqrtf(ang)), 0.0f, 1.0f);
-              if (sc > kVerySmall && L.radius > kVerySmall)
-              {
-                RFX_CNT(C_L_POW);
-                const float sp = powf_glibc(sc, 1 + 3 * m.refl * dlen / L.radius) * m.refl;
-                sumS = cadd(sumS, cscale(lc, sp));
-              }
+              const float tvx = best_u * sh.t11 + best_v * sh.t12 + 0.0f;
+              const float tvy = best_u * sh.t21 + best_v * sh.t22 + 0.0f;
+              const col c = texel_uv<STATS>(S, sh.tex, sh.tu0 + tvx, sh.tv0 + tvy, lut, cnt);
+              m.r = c.r; m.g = c.g; m.b = c.b;
+            }
+          }
+          reflv = reflect(mul(ray, best_t), norm);                           // trace_math.cpp:14-23
+          rayLen = len(ray); normLen = len(norm); reflectLen = len(reflv);
+        }
+        const int nl = min(32, S.n_light - base);
+        for (int k = 0; k < nl; ++k)
+        {
+          if (!((lit >> k) & 1u)) continue;
+          RFX_CNT(C_L_LIT);
+          const LightRec L = S.lights[base + k];
+          const v3 dtl = sub(mk(L.ox, L.oy, L.oz), drop);
+          const float dlen = len(dtl);
+          float aa = dlen * normLen;
+          const float cosl = (aa > kVerySmall) ? dot(dtl, norm) / aa : 0.0f;
+          const col lc = mkc(L.r, L.g, L.b);
+          if (L.power > kVerySmall) sumL = cadd(sumL, cscale(cscale(lc, cosl), L.power));
+          aa = sqlen(dtl);
+          const float ang = (aa > kVerySmall) ? 1.0f - L.radius * L.radius / aa : 0.0f;
+          if (ang > 0)
+          {
+            RFX_CNT(C_L_SPEC);
+            const v3 dlr = add(normalized(dtl), mul(rd, 1.0f - m.refl));
+            aa = len(dlr) * reflectLen;
+            float sc = (aa > kVerySmall) ? dot(dlr, reflv) / aa : 0.0f;
+            sc = clampf(sc + (1.0f - sqrtf(ang)), 0.0f, 1.0f);
+            if (sc > kVerySmall && L.radius > kVerySmall)
+            {
+              RFX_CNT(C_L_POW);
+              const float sp = powf_glibc(sc, 1 + 3 * m.refl * dlen / L.radius) * m.refl;
+              sumS = cadd(sumS, cscale(lc, sp));
             }
           }
         }
+        RFX_PROF_END(P_LIGHT);
+        if (!MANYL || base + 32 >= S.n_light) break;
       }
-      RFX_PROF_END(P_LIGHT);
       RFX_PROF_BEGIN(P_MAT);
       sumL = cadd(mkc(S.amb_r, S.amb_g, S.amb_b), sumL);                      // Scene.cpp:186
       const col color = mkc(m.r, m.g, m.b);
@@ -520,7 +581,7 @@ __device__ __forceinline__ bool segment(const DevScene &S, Path &p, int depth, c
 }
 
 // Scene::trace (Scene.cpp:73-236) as a whole: the reference's bounce loop over segment().
-template <bool STATS, bool LDS>
+template <bool STATS, int CFG>
 __device__ __forceinline__ col trace(const DevScene &S, v3 origin, v3 ray, int depth, v3 rd, const float *lut, Cnt &cnt)
 {
   Path p;
@@ -529,12 +590,12 @@ __device__ __forceinline__ col trace(const DevScene &S, v3 origin, v3 ray, int d
   // diagnostic build only (tools/segstats.py): the trace's segment count replaces its color
   int nseg = 0;
   if (depth > 0)
-    while (++nseg, !segment<STATS, LDS>(S, p, depth, lut, cnt)) {}
+    while (++nseg, !segment<STATS, CFG>(S, p, depth, lut, cnt)) {}
   return mkc((float)nseg, 0.0f, 0.0f);
 #else
   RFX_PROF_BEGIN(P_SEG);
   if (depth > 0)
-    while (!segment<STATS, LDS>(S, p, depth, lut, cnt)) {}
+    while (!segment<STATS, CFG>(S, p, depth, lut, cnt)) {}
   RFX_PROF_END(P_SEG);
   return p.pix;
 #endif
@@ -575,10 +636,17 @@ __device__ __forceinline__ v3 load_rd(const FrameParams &P, uint64_t i)
 #endif
 #define RFX_TRACE_BOUNDS __launch_bounds__(256, RFX_WAVES_PER_EU)
 
-// one workgroup = 16x16 output pixels (BLOCK: block corners), one wave = an 8x8 tile (ray coherence)
-template <bool STATS, bool BLOCK, bool LDS>
+// Pixel loop variants of Render::renderNext: block preview (sampleNum < 0), one plain trace per pixel
+// (sampleNum == 1, no jitter, no accumulation -- the benchmark frame), and the general SSAA / additive
+// loop.  The plain variant drops the sample loops and their live state (no spills before the bounce loop).
+enum TraceMode { kModeSsaa = 0, kModeBlock = 1, kModePlain = 2 };
+
+// one workgroup = 16x16 output pixels (block mode: block corners), one wave = an 8x8 tile (ray coherence)
+template <bool STATS, int MODE, int CFG>
 __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
 {
+  constexpr bool BLOCK = MODE == kModeBlock;
+  constexpr bool LDS = (CFG & kCfgLds) != 0;
   __shared__ float lut[256];
   lut[threadIdx.x] = (float)threadIdx.x / 255.0f;                               // Color.cpp:11-13
   if constexpr (LDS) stage_scene_lds(S);
@@ -614,7 +682,7 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
       {
         const v3 ray = mmul(view, mk((float)x - P.wh, (float)y - P.hh, P.rz));
         const uint64_t ti = (uint64_t)cy * bw + cx - P.trace_base;
-        const col c = trace<STATS, LDS>(S, eye, ray, P.depth, load_rd(P, ti), lut, cnt);
+        const col c = trace<STATS, CFG>(S, eye, ray, P.depth, load_rd(P, ti), lut, cnt);
         const uint32_t ex = min(P.W, x + n), ey = min(P.H, y + n);
         const uint32_t a = argb(c);
         for (uint32_t qy = y; qy < ey; ++qy)
@@ -624,6 +692,28 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
             d[0] = c.r; d[1] = c.g; d[2] = c.b;
             if (P.argb) P.argb[(size_t)qy * P.W + qx] = a;
           }
+      }
+    }
+  }
+  else if constexpr (MODE == kModePlain)
+  {
+    if (gx < P.W && gy < P.grid_rows)
+    {
+      const uint32_t x = gx;
+      const uint32_t y = P.nranks > 1 ? strip_row_to_y(gy, P) : gy + P.row0;
+      const uint32_t orow = P.nranks > 1 ? gy : y;
+      const uint64_t p = (uint64_t)y * P.W + x;
+      if (p >= P.p_begin && p < P.p_end)
+      {
+        const float rx = (float)x - P.wh, ry = (float)y - P.hh;                   // Render.cpp:152-153
+        // Render.cpp:183 with ssx = ssy = 0, sampleNum = 1, no jitter: float(0) / 1 == +0, rnd == 0
+        const v3 ray = mmul(view, mk(rx + 0.0f + 0.0f, ry + 0.0f + 0.0f, P.rz));
+        const col c = trace<STATS, CFG>(S, eye, ray, P.depth, load_rd(P, p - P.p_begin), lut, cnt);
+        const col out = cadd(mkc(0.0f, 0.0f, 0.0f), c);                            // Render.cpp:185 (/ 1.0f exact)
+        const size_t o = (size_t)orow * P.W + x;
+        float *d = P.img + o * 3;
+        d[0] = out.r; d[1] = out.g; d[2] = out.b;
+        if (P.argb) P.argb[o] = argb(out);                                         // Render::copyImage
       }
     }
   }
@@ -655,7 +745,7 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
           v3 ray = mk(rx + ox + rndx, ry + oy + rndy, P.rz);
           ray = mmul(view, ray);
           const uint64_t ti = pr * (uint64_t)(ss * ss) + (uint64_t)(sx * ss + sy);
-          fin = cadd(fin, trace<STATS, LDS>(S, eye, ray, P.depth, load_rd(P, ti), lut, cnt));
+          fin = cadd(fin, trace<STATS, CFG>(S, eye, ray, P.depth, load_rd(P, ti), lut, cnt));
         }
       if (ss != 1)                                                                 // Render.cpp:189 (x / 1.0f == x)
       {
@@ -850,30 +940,49 @@ hipError_t launch_rng_finish(const uint32_t *d_seed, uint32_t *d_next_seed, cons
   return hipGetLastError();
 }
 
+template <bool STATS, int MODE>
+static void launch_cfg(int cfg, dim3 grid, const DevScene &S, const FrameParams &P, hipStream_t st)
+{
+  switch (cfg)
+  {
+    case 0: hipLaunchKernelGGL((trace_kernel<STATS, MODE, 0>), grid, dim3(256), 0, st, S, P); break;
+    case kCfgManyLights: hipLaunchKernelGGL((trace_kernel<STATS, MODE, kCfgManyLights>), grid, dim3(256), 0, st, S, P); break;
+#ifdef RFX_LDS_SCENE
+    case kCfgLds: hipLaunchKernelGGL((trace_kernel<STATS, MODE, kCfgLds>), grid, dim3(256), 0, st, S, P); break;
+    case kCfgLds | kCfgManyLights:
+      hipLaunchKernelGGL((trace_kernel<STATS, MODE, kCfgLds | kCfgManyLights>), grid, dim3(256), 0, st, S, P);
+      break;
+#endif
+  }
+}
+
+static void launch_mode_cfg(bool stats, int mode, int cfg, dim3 grid, const DevScene &S, const FrameParams &P,
+                            hipStream_t st)
+{
+  if (stats)
+  {
+    if (mode == kModeBlock) launch_cfg<true, kModeBlock>(cfg, grid, S, P, st);
+    else if (mode == kModePlain) launch_cfg<true, kModePlain>(cfg, grid, S, P, st);
+    else launch_cfg<true, kModeSsaa>(cfg, grid, S, P, st);
+  }
+  else
+  {
+    if (mode == kModeBlock) launch_cfg<false, kModeBlock>(cfg, grid, S, P, st);
+    else if (mode == kModePlain) launch_cfg<false, kModePlain>(cfg, grid, S, P, st);
+    else launch_cfg<false, kModeSsaa>(cfg, grid, S, P, st);
+  }
+}
+
 hipError_t launch_trace(const DevScene &S, const FrameParams &P, bool stats, hipStream_t st)
 {
   const uint32_t cols = P.ss < 0 ? (P.W + (uint32_t)(-P.ss) - 1) / (uint32_t)(-P.ss) : P.W;
   const dim3 grid((cols + 15) / 16, (P.grid_rows + 15) / 16);
-  const bool block = P.ss < 0;
+  const int mode = P.ss < 0 ? kModeBlock : (P.ss == 1 && !P.additive && !P.accumulate) ? kModePlain : kModeSsaa;
+  int cfg = S.n_light > 32 ? kCfgManyLights : 0;
 #ifdef RFX_LDS_SCENE  // staged scene: measured slower than scalar loads since sphere pairs (tools/ab.py)
-  const bool lds = S.n_sph <= kLdsSph && S.n_tri <= kLdsTri;
-  if (!stats && lds)
-  {
-    if (block) hipLaunchKernelGGL((trace_kernel<false, true, true>), grid, dim3(256), 0, st, S, P);
-    else hipLaunchKernelGGL((trace_kernel<false, false, true>), grid, dim3(256), 0, st, S, P);
-    return hipGetLastError();
-  }
+  if (!stats && S.n_sph <= kLdsSph && S.n_tri <= kLdsTri) cfg |= kCfgLds;
 #endif
-  if (block)
-  {
-    if (stats) hipLaunchKernelGGL((trace_kernel<true, true, false>), grid, dim3(256), 0, st, S, P);
-    else hipLaunchKernelGGL((trace_kernel<false, true, false>), grid, dim3(256), 0, st, S, P);
-  }
-  else
-  {
-    if (stats) hipLaunchKernelGGL((trace_kernel<true, false, false>), grid, dim3(256), 0, st, S, P);
-    else hipLaunchKernelGGL((trace_kernel<false, false, false>), grid, dim3(256), 0, st, S, P);
-  }
+  launch_mode_cfg(stats, mode, cfg, grid, S, P, st);
   return hipGetLastError();
 }
 

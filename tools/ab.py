@@ -31,6 +31,9 @@ VARIANTS = {
     "base": [],
     "wpe5": ["RFX_WAVES_PER_EU=5"],
     "lds": ["RFX_LDS_SCENE"],
+    "old": ["RFX_NO_TRI_SIGN", "RFX_NO_SPH_B"],
+    "notrisign": ["RFX_NO_TRI_SIGN"],
+    "nosphb": ["RFX_NO_SPH_B"],
 }
 
 
