@@ -24,12 +24,13 @@
 
 namespace rfx {
 uint64_t rng_blocks_for(uint64_t traces);
-hipError_t launch_rng_count(const uint32_t *d_seed, uint32_t *d_blk_cnt, uint64_t blk0, uint64_t nblk_slice,
-                            hipStream_t st);
-hipError_t launch_rng_finish(const uint32_t *d_seed, uint32_t *d_next_seed, const uint32_t *d_blk_cnt, uint64_t nblk,
-                             uint64_t traces, float *d_rd, uint64_t n_rd, uint64_t *d_blk_off, int *d_err,
-                             uint64_t ss2, uint64_t W, uint32_t row_block, uint32_t rank, uint32_t nranks,
-                             hipStream_t st);
+void rng_jump_table(uint64_t nblk, uint32_t *out);
+hipError_t launch_rng_count(const uint32_t *d_seed, const uint32_t *d_jump, uint32_t *d_blk_cnt, uint64_t blk0,
+                            uint64_t nblk_slice, hipStream_t st);
+hipError_t launch_rng_finish(const uint32_t *d_seed, const uint32_t *d_jump, uint32_t *d_next_seed,
+                             const uint32_t *d_blk_cnt, uint64_t nblk, uint64_t traces, float *d_rd, uint64_t n_rd,
+                             uint64_t *d_blk_off, int *d_err, uint64_t ss2, uint64_t W, uint32_t row_block,
+                             uint32_t rank, uint32_t nranks, hipStream_t st);
 hipError_t launch_trace(const DevScene &S, const FrameParams &P, bool stats, hipStream_t st);
 }  // namespace rfx
 
@@ -389,6 +390,7 @@ struct rfx_renderer {
   // workspaces
   float *d_rd = nullptr; uint64_t rd_cap = 0;
   uint32_t *d_blk_cnt = nullptr; uint64_t *d_blk_off = nullptr; uint64_t blk_cap = 0;
+  uint32_t *d_jump = nullptr;  // LCG jump table for blk_cap blocks (rng_jump_table)
   // host staging for rfx_render_frame_host
   float *d_img = nullptr; uint32_t *d_argb = nullptr; uint64_t *d_cnt = nullptr; size_t img_cap = 0;
   // per-phase event timing: triples {start, after pre-pass, after trace}
@@ -488,7 +490,7 @@ extern "C" void rfx_renderer_destroy(rfx_renderer *r)
   (void)hipStreamSynchronize(r->stream);
   free_scene(r);
   (void)hipFree(r->d_seed); (void)hipFree(r->d_err); (void)hipFree(r->d_rd);
-  (void)hipFree(r->d_blk_cnt); (void)hipFree(r->d_blk_off);
+  (void)hipFree(r->d_blk_cnt); (void)hipFree(r->d_blk_off); (void)hipFree(r->d_jump);
   (void)hipFree(r->d_img); (void)hipFree(r->d_argb); (void)hipFree(r->d_cnt);
   for (hipEvent_t e : r->events) (void)hipEventDestroy(e);
   if (r->own_stream) (void)hipStreamDestroy(r->own_stream);
@@ -639,10 +641,14 @@ static int ensure_rng_workspace(rfx_renderer *r, uint64_t traces, uint64_t nblk)
   }
   if (nblk > r->blk_cap)
   {
-    (void)hipFree(r->d_blk_cnt); (void)hipFree(r->d_blk_off);
-    r->d_blk_cnt = nullptr; r->d_blk_off = nullptr; r->blk_cap = 0;
+    (void)hipFree(r->d_blk_cnt); (void)hipFree(r->d_blk_off); (void)hipFree(r->d_jump);
+    r->d_blk_cnt = nullptr; r->d_blk_off = nullptr; r->d_jump = nullptr; r->blk_cap = 0;
     HIP_CHECK(hipMalloc(&r->d_blk_cnt, nblk * sizeof(uint32_t)));
     HIP_CHECK(hipMalloc(&r->d_blk_off, nblk * sizeof(uint64_t)));
+    std::vector<uint32_t> jump(2 * (256 + nblk));
+    rng_jump_table(nblk, jump.data());
+    HIP_CHECK(hipMalloc(&r->d_jump, jump.size() * sizeof(uint32_t)));
+    HIP_CHECK(hipMemcpy(r->d_jump, jump.data(), jump.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     r->blk_cap = nblk;
   }
   return RFX_OK;
@@ -655,9 +661,9 @@ static int enqueue_rng(rfx_renderer *r, uint64_t traces, hipStream_t st)
   int rc;
   const uint64_t nblk = rng_layout(traces, 1, nullptr);
   if ((rc = ensure_rng_workspace(r, traces, nblk)) != RFX_OK) return rc;
-  HIP_CHECK(launch_rng_count(r->d_seed, r->d_blk_cnt, 0, nblk, st));
-  HIP_CHECK(launch_rng_finish(r->d_seed, r->d_seed + 1, r->d_blk_cnt, nblk, traces, r->d_rd, r->rd_cap, r->d_blk_off,
-                              r->d_err, 1, 1, 1, 0, 1, st));
+  HIP_CHECK(launch_rng_count(r->d_seed, r->d_jump, r->d_blk_cnt, 0, nblk, st));
+  HIP_CHECK(launch_rng_finish(r->d_seed, r->d_jump, r->d_seed + 1, r->d_blk_cnt, nblk, traces, r->d_rd, r->rd_cap,
+                              r->d_blk_off, r->d_err, 1, 1, 1, 0, 1, st));
   HIP_CHECK(hipMemcpyAsync(r->d_seed, r->d_seed + 1, sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
   return RFX_OK;
 }
@@ -691,7 +697,7 @@ extern "C" int rfx_frame_rng_count(rfx_renderer *r, const rfx_frame *f, uint32_t
   uint64_t bps = 0;
   const uint64_t nblk = rng_layout(pl.traces, nslices, &bps);
   if ((rc = ensure_rng_workspace(r, pl.traces, nblk)) != RFX_OK) return rc;
-  HIP_CHECK(launch_rng_count(r->d_seed, d_blk_counts, (uint64_t)slice * bps, bps, pl.st));
+  HIP_CHECK(launch_rng_count(r->d_seed, r->d_jump, d_blk_counts, (uint64_t)slice * bps, bps, pl.st));
   return RFX_OK;
 }
 
@@ -702,8 +708,8 @@ static int finish_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *d_counts
   FrameParams &P = pl.P;
   const hipStream_t st = pl.st;
   const uint64_t ss2 = P.ss > 0 ? (uint64_t)(P.ss * P.ss) : 1;
-  HIP_CHECK(launch_rng_finish(r->d_seed, r->d_seed + 1, d_counts, nblk, pl.traces, r->d_rd, r->rd_cap, r->d_blk_off,
-                              r->d_err, ss2, P.W, P.row_block, P.rank, P.nranks, st));
+  HIP_CHECK(launch_rng_finish(r->d_seed, r->d_jump, r->d_seed + 1, d_counts, nblk, pl.traces, r->d_rd, r->rd_cap,
+                              r->d_blk_off, r->d_err, ss2, P.W, P.row_block, P.rank, P.nranks, st));
   HIP_CHECK(hipMemcpyAsync(r->d_seed, r->d_seed + 1, sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
   if ((rc = timing_event(r, st)) != RFX_OK) return rc;
   P.img = d_rgb;
@@ -744,7 +750,7 @@ extern "C" int rfx_render_frame(rfx_renderer *r, const rfx_frame *f, float *d_rg
   const uint64_t nblk = rng_layout(pl.traces, 1, nullptr);
   if ((rc = ensure_rng_workspace(r, pl.traces, nblk)) != RFX_OK) return rc;
   if ((rc = timing_event(r, pl.st)) != RFX_OK) return rc;
-  HIP_CHECK(launch_rng_count(r->d_seed, r->d_blk_cnt, 0, nblk, pl.st));
+  HIP_CHECK(launch_rng_count(r->d_seed, r->d_jump, r->d_blk_cnt, 0, nblk, pl.st));
   return finish_frame(r, pl, r->d_blk_cnt, nblk, d_rgb, d_argb, d_counters);
 }
 

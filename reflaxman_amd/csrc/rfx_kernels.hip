@@ -765,26 +765,36 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
 }
 
 // ------------------------------------------------------------- RNG pre-pass
+// Triple j of the stream (0-based) is LCG draws 3j+1..3j+3 after the frame's starting state.  Thread t
+// of the pre-pass owns triples [16t, 16t + 16); its starting state is the frame state jumped 48t draws,
+// composed from two host-made tables of affine LCG maps (A, C): 48*256*b draws for its block b and
+// 48*tid draws for its place in the block -- two multiply-adds instead of a 27-step binary power.
 constexpr int kTriplesPerThread = 16;
 constexpr int kRngBlock = 256;
 constexpr uint64_t kTriplesPerBlock = (uint64_t)kTriplesPerThread * kRngBlock;
+
+__device__ __forceinline__ uint32_t thread_state(uint32_t s, const uint32_t *jump, uint64_t b, uint32_t tid)
+{
+  const uint32_t *bj = jump + 2 * (kRngBlock + b), *tj = jump + 2 * tid;
+  return tj[0] * (bj[0] * s + bj[1]) + tj[1];
+}
 
 __device__ __forceinline__ bool triple(uint32_t &s, float &x, float &y, float &z)
 {
   const uint32_t s1 = lcg_step(s), s2 = lcg_step(s1), s3 = lcg_step(s2);
   s = s3;
-  x = rand_component(lcg_out(s1));
-  y = rand_component(lcg_out(s2));
-  z = rand_component(lcg_out(s3));
-  return !(x * x + y * y + z * z > 1.f);                                        // Vector3.cpp:186
+  x = rand_component_dev(lcg_out(s1));
+  y = rand_component_dev(lcg_out(s2));
+  z = rand_component_dev(lcg_out(s3));
+  return !(x * x + y * y + z * z > 1.f);                                        // Vector3.cpp:185
 }
 
 // accepted-triple count of blocks [blk0, blk0 + gridDim.x): one slice of the stream (multi-GPU: one per rank)
-__global__ __launch_bounds__(kRngBlock) void rng_count(const uint32_t *seed, uint32_t *blk_cnt, uint64_t blk0)
+__global__ __launch_bounds__(kRngBlock) void rng_count(const uint32_t *seed, const uint32_t *jump, uint32_t *blk_cnt,
+                                                       uint64_t blk0)
 {
   const uint64_t b = blk0 + blockIdx.x;
-  const uint64_t t = b * kRngBlock + threadIdx.x;
-  uint32_t s = lcg_jump(*seed, 3ull * kTriplesPerThread * t);
+  uint32_t s = thread_state(*seed, jump, b, threadIdx.x);
   uint32_t c = 0;
   float x, y, z;
 #pragma unroll 4
@@ -842,53 +852,79 @@ __device__ __forceinline__ bool owned(uint64_t idx, const EmitFilter &f)
   return ((idx / f.ss2 / f.W / f.row_block) % f.nranks) == f.rank;
 }
 
-__global__ __launch_bounds__(kRngBlock) void rng_emit(const uint32_t *seed, const uint64_t *blk_off,
+// Scatter of the accepted triples: a block's accepted triples are the contiguous trace range
+// [blk_off[b], blk_off[b] + blk_cnt[b]); each thread regenerates its 16 triples into registers, the block
+// scans the accept counts, places its accepted triples in LDS at their block-local rank, and then writes
+// the range out with coalesced stores (randDir SoA, one plane per component).
+__global__ __launch_bounds__(kRngBlock) void rng_emit(const uint32_t *seed, const uint32_t *jump, const uint64_t *blk_off,
                                                       const uint32_t *blk_cnt, uint64_t need, float *rd, uint64_t n_rd,
                                                       uint32_t *next_seed, EmitFilter flt)
 {
-  // block-uniform skip: a block whose accepted indices all belong to other ranks' strips (and do not
-  // include the frame's last trace, whose stream state every rank carries forward) writes nothing
+  __shared__ float sx[kTriplesPerBlock], sy[kTriplesPerBlock], sz[kTriplesPerBlock];
+  __shared__ uint32_t wsum[kRngBlock / 64];
   const uint64_t off = blk_off[blockIdx.x];
   if (off >= need) return;
-  const uint64_t last = min(off + (uint64_t)blk_cnt[blockIdx.x], need) - 1;
+  const uint32_t cnt = (uint32_t)min((uint64_t)blk_cnt[blockIdx.x], need - off);  // triples this block emits
+  const uint64_t last = off + cnt - 1;
+  // block-uniform skip: a block whose accepted indices all belong to other ranks' strips (and do not
+  // include the frame's last trace, whose stream state every rank carries forward) writes nothing
   if (flt.nranks > 1 && last != need - 1)
   {
     const uint64_t s_lo = off / flt.ss2 / flt.W / flt.row_block, s_hi = last / flt.ss2 / flt.W / flt.row_block;
     bool any = false;
-    for (uint64_t s = s_lo; s <= s_hi && !any; ++s) any = (s % flt.nranks) == flt.rank;
+    for (uint64_t st = s_lo; st <= s_hi && !any; ++st) any = (st % flt.nranks) == flt.rank;
     if (!any) return;
   }
-  const uint64_t t = (uint64_t)blockIdx.x * kRngBlock + threadIdx.x;
-  const uint32_t s0 = lcg_jump(*seed, 3ull * kTriplesPerThread * t);
-  uint32_t s = s0, c = 0;
-  float x, y, z;
-#pragma unroll 4
-  for (int j = 0; j < kTriplesPerThread; ++j) c += triple(s, x, y, z) ? 1u : 0u;
+  uint32_t s = thread_state(*seed, jump, blockIdx.x, threadIdx.x);
+  float x[kTriplesPerThread], y[kTriplesPerThread], z[kTriplesPerThread];
+  uint32_t acc = 0, c = 0;
+#pragma unroll
+  for (int j = 0; j < kTriplesPerThread; ++j)
+  {
+    const bool a = triple(s, x[j], y[j], z[j]);
+    acc |= (a ? 1u : 0u) << j;
+    c += a ? 1u : 0u;
+  }
   // exclusive scan of c across the workgroup
   const uint32_t lane = threadIdx.x & 63;
   uint32_t inc = c;
 #pragma unroll
-  for (int off = 1; off < 64; off <<= 1)
+  for (int o = 1; o < 64; o <<= 1)
   {
-    const uint32_t v = __shfl_up(inc, off, 64);
-    if (lane >= (uint32_t)off) inc += v;
+    const uint32_t v = __shfl_up(inc, o, 64);
+    if (lane >= (uint32_t)o) inc += v;
   }
-  __shared__ uint32_t wsum[kRngBlock / 64];
   if (lane == 63) wsum[threadIdx.x >> 6] = inc;
   __syncthreads();
   uint32_t wbase = 0;
   for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) wbase += wsum[w];
-  uint64_t idx = blk_off[blockIdx.x] + wbase + (inc - c);
-  if (idx >= need) return;
-  s = s0;
-  for (int j = 0; j < kTriplesPerThread; ++j)
+  uint32_t li = wbase + (inc - c);                                               // block-local rank
+  if (li < cnt && li + c >= cnt && off + cnt == need)
   {
-    if (triple(s, x, y, z))
+    // this thread holds trace need-1: the stream state after it is the next frame's state
+    uint32_t st = thread_state(*seed, jump, blockIdx.x, threadIdx.x);
+    uint32_t k = li;
+    for (int j = 0; j < kTriplesPerThread; ++j)
     {
-      if (idx < need && (flt.nranks <= 1 || owned(idx, flt)))
-        { rd[idx] = x; rd[n_rd + idx] = y; rd[2 * n_rd + idx] = z; }
-      if (idx == need - 1) *next_seed = s;                                      // stream state after trace need-1
-      ++idx;
+      st = lcg_step(lcg_step(lcg_step(st)));
+      if ((acc >> j) & 1u)
+        if (k++ == cnt - 1) { *next_seed = st; break; }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < kTriplesPerThread; ++j)
+    if ((acc >> j) & 1u)
+    {
+      sx[li] = x[j]; sy[li] = y[j]; sz[li] = z[j];
+      ++li;
+    }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < cnt; i += kRngBlock)
+  {
+    const uint64_t idx = off + i;
+    if (flt.nranks <= 1 || owned(idx, flt))
+    {
+      rd[idx] = sx[i]; rd[n_rd + idx] = sy[i]; rd[2 * n_rd + idx] = sz[i];
     }
   }
 }
@@ -918,25 +954,46 @@ uint64_t rng_blocks_for(uint64_t traces)
   return (triples + kTriplesPerBlock - 1) / kTriplesPerBlock;
 }
 
+// the jump table rng_count / rng_emit expect: (A, C) of 3*16*tid draws for tid < 256, then of
+// 3*16*256*b draws for b < nblk (affine LCG maps s -> A s + C, trace_math.h:36)
+void rng_jump_table(uint64_t nblk, uint32_t *out)
+{
+  uint32_t a1 = 1u, c1 = 0u;  // one thread's 48 draws
+  for (int i = 0; i < 3 * kTriplesPerThread; ++i) { c1 = 214013u * c1 + 2531011u; a1 = 214013u * a1; }
+  uint32_t A = 1u, C = 0u;
+  for (int t = 0; t < kRngBlock; ++t)
+  {
+    out[2 * t] = A; out[2 * t + 1] = C;
+    C = a1 * C + c1; A = a1 * A;            // compose one more thread stride
+  }
+  const uint32_t ab = A, cb = C;            // one block's 48 * 256 draws
+  A = 1u; C = 0u;
+  for (uint64_t b = 0; b < nblk; ++b)
+  {
+    out[2 * (kRngBlock + b)] = A; out[2 * (kRngBlock + b) + 1] = C;
+    C = ab * C + cb; A = ab * A;
+  }
+}
+
 // first half of the pre-pass: accept counts of blocks [blk0, blk0 + nblk_slice)
-hipError_t launch_rng_count(const uint32_t *d_seed, uint32_t *d_blk_cnt, uint64_t blk0, uint64_t nblk_slice,
-                            hipStream_t st)
+hipError_t launch_rng_count(const uint32_t *d_seed, const uint32_t *d_jump, uint32_t *d_blk_cnt, uint64_t blk0,
+                            uint64_t nblk_slice, hipStream_t st)
 {
   if (nblk_slice)
-    hipLaunchKernelGGL(rng_count, dim3((uint32_t)nblk_slice), dim3(kRngBlock), 0, st, d_seed, d_blk_cnt, blk0);
+    hipLaunchKernelGGL(rng_count, dim3((uint32_t)nblk_slice), dim3(kRngBlock), 0, st, d_seed, d_jump, d_blk_cnt, blk0);
   return hipGetLastError();
 }
 
 // second half: scan all nblk counts, scatter the randDirs this rank needs, carry the stream state
-hipError_t launch_rng_finish(const uint32_t *d_seed, uint32_t *d_next_seed, const uint32_t *d_blk_cnt, uint64_t nblk,
-                             uint64_t traces, float *d_rd, uint64_t n_rd, uint64_t *d_blk_off, int *d_err,
-                             uint64_t ss2, uint64_t W, uint32_t row_block, uint32_t rank, uint32_t nranks,
-                             hipStream_t st)
+hipError_t launch_rng_finish(const uint32_t *d_seed, const uint32_t *d_jump, uint32_t *d_next_seed,
+                             const uint32_t *d_blk_cnt, uint64_t nblk, uint64_t traces, float *d_rd, uint64_t n_rd,
+                             uint64_t *d_blk_off, int *d_err, uint64_t ss2, uint64_t W, uint32_t row_block,
+                             uint32_t rank, uint32_t nranks, hipStream_t st)
 {
   hipLaunchKernelGGL(rng_scan, dim3(1), dim3(1024), 0, st, d_blk_cnt, (uint32_t)nblk, d_blk_off, traces, d_err);
   const EmitFilter flt{ss2 ? ss2 : 1, W ? W : 1, row_block ? row_block : 1, rank, nranks ? nranks : 1};
-  hipLaunchKernelGGL(rng_emit, dim3((uint32_t)nblk), dim3(kRngBlock), 0, st, d_seed, d_blk_off, d_blk_cnt, traces,
-                     d_rd, n_rd, d_next_seed, flt);
+  hipLaunchKernelGGL(rng_emit, dim3((uint32_t)nblk), dim3(kRngBlock), 0, st, d_seed, d_jump, d_blk_off, d_blk_cnt,
+                     traces, d_rd, n_rd, d_next_seed, flt);
   return hipGetLastError();
 }
 

@@ -149,5 +149,9 @@ RFX_HD uint32_t lcg_jump(uint32_t s, uint64_t n)
 }
 // one component of Vector3::randomInsideSphere (Vector3.cpp:182-184)
 RFX_HD float rand_component(uint32_t k) { return (float)k / ((float)0x7FFF / 2) - 1.f; }
+// The same value without the f32 divide (the RNG pre-pass kernels): for every k in [0, 0x7FFF],
+// (float)k / 16383.5f == (float)((double)k * (1.0 / 16383.5)) -- checked exhaustively by
+// tests/test_rng_exact.py -- and the subtraction of 1 is the reference's own.
+RFX_HD float rand_component_dev(uint32_t k) { return (float)((double)k * (1.0 / 16383.5)) - 1.f; }
 
 }  // namespace rfx
