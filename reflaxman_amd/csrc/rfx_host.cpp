@@ -63,7 +63,8 @@ struct HostTexture { uint32_t w = 0, h = 0; std::vector<uint32_t> texels; };
 struct HostMat { int dielectric; float r, g, b, refl, transp; };
 struct HostSphere { v3 center; float radius, sq_radius; HostMat mat; int obj; };
 struct HostTri {
-  v3 v0, norm;
+  v3 v0, v1, v2, norm;
+  double cond = INFINITY;  // ||M||_F ||M^-1||_F of the basis M = [v2-v0 | v1-v0 | -norm] (cull bound)
   m33 ax, tuv;
   float tu0 = 0, tv0 = 0;
   int tex = -1;
@@ -139,7 +140,19 @@ extern "C" int rfx_scene_add_triangle(rfx_scene *s, const float a[3], const floa
   t.v0 = v0;
   t.mat = make_mat(type, rgb, refl, transp);
   t.norm = normalized(cross(sub(v1, v0), sub(v2, v0)));
-  t.ax = inverted(from_cols(sub(v2, v0), sub(v1, v0), neg(t.norm)));
+  const m33 basis = from_cols(sub(v2, v0), sub(v1, v0), neg(t.norm));
+  t.ax = inverted(basis);
+  t.v1 = v1;
+  t.v2 = v2;
+  {
+    const float *a = &basis.m11, *b = &t.ax.m11;
+    double na = 0.0, nb = 0.0;
+    for (int k = 0; k < 9; ++k) { na += (double)a[k] * a[k]; nb += (double)b[k] * b[k]; }
+    const float det = basis.m11 * (basis.m22 * basis.m33 - basis.m32 * basis.m23) +
+                      basis.m21 * (basis.m32 * basis.m13 - basis.m12 * basis.m33) +
+                      basis.m31 * (basis.m12 * basis.m23 - basis.m13 * basis.m22);
+    t.cond = fabsf(det) > kVerySmall ? sqrt(na * nb) : INFINITY;
+  }
   memset(&t.tuv, 0, sizeof(t.tuv));
   t.obj = (int)s->obj_kind.size();
   s->obj_kind.push_back(1);
@@ -564,6 +577,24 @@ extern "C" int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *s)
     ts.push_back(h);
     tm.push_back({t.mat.r, t.mat.g, t.mat.b, t.mat.refl});
   }
+  // bounding spheres for the wave-bundle cull: a sphere's own (radius grown by a relative 1e-5), a
+  // triangle's centroid and farthest vertex; a triangle whose axTrans is ill-conditioned (the reference
+  // falls back to the identity for a singular basis, Matrix33.cpp:58-79) may report hits far from its
+  // vertices, so it gets r = +inf and is never culled
+  std::vector<Bound> bd;
+  for (const HostSphere &sp : s->spheres)
+    bd.push_back({sp.center.x, sp.center.y, sp.center.z, sp.radius * 1.00001f});
+  for (const HostTri &t : s->tris)
+  {
+    const double cx = ((double)t.v0.x + t.v1.x + t.v2.x) / 3.0, cy = ((double)t.v0.y + t.v1.y + t.v2.y) / 3.0,
+                 cz = ((double)t.v0.z + t.v1.z + t.v2.z) / 3.0;
+    double r2 = 0.0;
+    for (const v3 &q : {t.v0, t.v1, t.v2})
+      r2 = fmax(r2, (q.x - cx) * (q.x - cx) + (q.y - cy) * (q.y - cy) + (q.z - cz) * (q.z - cz));
+    float r = (float)(sqrt(r2) * 1.0001 + 1e-6);
+    if (!(t.cond < 1000.0)) r = INFINITY;
+    bd.push_back({(float)cx, (float)cy, (float)cz, r});
+  }
   std::vector<LightRec> lr;
   for (const HostLight &l : s->lights) lr.push_back({l.origin.x, l.origin.y, l.origin.z, l.radius, l.r, l.g, l.b, l.power});
   std::vector<TexRec> tr;
@@ -577,7 +608,8 @@ extern "C" int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *s)
   if ((rc = upload(r, sg, &d.sph_geo)) || (rc = upload(r, sp, &d.sph_pair)) || (rc = upload(r, sm, &d.sph_mat)) ||
       (rc = upload(r, si, &d.sph_info)) ||
       (rc = upload(r, tg, &d.tri_geo)) || (rc = upload(r, ts, &d.tri_shade)) || (rc = upload(r, tm, &d.tri_mat)) ||
-      (rc = upload(r, lr, &d.lights)) || (rc = upload(r, tr, &d.texs)) || (rc = upload(r, pool, &d.texels)))
+      (rc = upload(r, lr, &d.lights)) || (rc = upload(r, tr, &d.texs)) || (rc = upload(r, pool, &d.texels)) ||
+      (rc = upload(r, bd, &d.bound)))
     return rc;
   d.n_sph = (int32_t)sg.size();
   d.n_tri = (int32_t)tg.size();

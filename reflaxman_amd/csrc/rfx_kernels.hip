@@ -86,39 +86,6 @@ __device__ __forceinline__ col from_argb_lut(uint32_t c, const float *lut)
 #endif
 }
 
-// ------------------------------------------------------------- scene geometry access
-// The object loops read every primitive in wave-uniform order, so the default build serves them through
-// the scalar cache (s_load_dwordx8 of a sphere pair straight into SGPR operands of the v_pk_* ops).
-// RFX_LDS_SCENE instead stages scenes up to kLdsSph spheres / kLdsTri triangles into LDS per workgroup
-// (broadcast ds_reads); it costs VGPRs and measured slower (tools/ab.py).
-constexpr int kLdsSph = 256;
-constexpr int kLdsTri = 64;
-__shared__ SpherePair g_lds_pair[kLdsSph / 2];
-__shared__ TriGeo g_lds_tri[kLdsTri];
-
-template <bool LDS>
-struct Geo;
-template <>
-struct Geo<false> {
-  const DevScene &S;
-  __device__ __forceinline__ SpherePair pair(int j) const { return S.sph_pair[j]; }
-  __device__ __forceinline__ TriGeo tri(int i) const { return S.tri_geo[i]; }
-};
-template <>
-struct Geo<true> {
-  const DevScene &S;
-  __device__ __forceinline__ SpherePair pair(int j) const { return g_lds_pair[j]; }
-  __device__ __forceinline__ TriGeo tri(int i) const { return g_lds_tri[i]; }
-};
-
-__device__ __forceinline__ int n_pairs(const DevScene &S) { return (S.n_sph + 1) >> 1; }
-
-__device__ __forceinline__ void stage_scene_lds(const DevScene &S)
-{
-  for (int j = threadIdx.x; j < n_pairs(S); j += blockDim.x) g_lds_pair[j] = S.sph_pair[j];
-  for (int i = threadIdx.x; i < S.n_tri; i += blockDim.x) g_lds_tri[i] = S.tri_geo[i];
-}
-
 // ------------------------------------------------------------- sampling
 template <bool STATS>
 __device__ __forceinline__ col texel_uv(const DevScene &S, int tex, float u, float v, const float *lut, Cnt &cnt)
@@ -220,36 +187,32 @@ __device__ __forceinline__ void pair_bd(const SpherePair &g, v3 o, const RayCons
 // gives t <= 0, which `t > VERY_SMALL_NUMBER` rejects (Sphere.cpp:58-60) -- both are exact rejects.
 __device__ __forceinline__ bool pair_may_hit(f2 b, f2 d)
 {
-#ifdef RFX_NO_SPH_B
-  return d.x >= 0.0f || d.y >= 0.0f;
-#else
   return (d.x >= 0.0f && b.x < 0.0f) || (d.y >= 0.0f && b.y < 0.0f);
-#endif
 }
 
-// The rest of Sphere::trace for one sphere given its b and d: on a hit returns t and |ray t|.
+// The rest of Sphere::trace for one sphere given its b and d: on a hit returns t and |ray t|^2.
+// `(ray * t).length() > DELTA` (Sphere.cpp:61-64) is tested as |ray t|^2 >= kSqDeltaSphere: the same
+// decision without the square root (rfx_math.h).
 template <bool STATS, bool SHADOW>
 __device__ __forceinline__ bool sphere_tail(float b, float d, v3 ray, const RayConst &k, float &t_out,
-                                            float &dist_out, Cnt &cnt)
+                                            float &sq_out, Cnt &cnt)
 {
   RFX_CNT(SHADOW ? C_SH_SPH_TESTS : C_SPH_TESTS);
   if constexpr (STATS)
     if (!(b > 0.0f)) RFX_CNT(SHADOW ? C_SH_SPH_B : C_SPH_B);
   if (!(d >= 0.0f && k.a_ok)) return false;
-#ifndef RFX_NO_SPH_B
   // b >= 0 (or NaN): -b - sqrt(d) <= 0, so t <= 0 and `t > VERY_SMALL_NUMBER` rejects -- exact early out
   if constexpr (!STATS)
     if (!(b < 0.0f)) return false;
-#endif
   if constexpr (STATS)
     if (!(b > 0.0f)) RFX_CNT(SHADOW ? C_SH_SPH_D : C_SPH_D);
-  const float t = (-b - sqrtf(d)) / k.a2;
+  const float t = (-b - sqrt_rn(d)) / k.a2;
   if (!(t > kVerySmall)) return false;
   RFX_CNT(SHADOW ? C_SH_SPH_T : C_SPH_T);
-  const float dist = len(mul(ray, t));
-  if (!(dist > kDelta)) return false;
+  const float sq = sqlen(mul(ray, t));
+  if (!(sq >= kSqDeltaSphere)) return false;
   t_out = t;
-  dist_out = dist;
+  sq_out = sq;
   return true;
 }
 
@@ -272,11 +235,9 @@ __device__ __forceinline__ bool tri_hit(const TriGeo &g, v3 o, v3 ray, float &t_
   const bool same_sign = (nz > 0.0f && arz > 0.0f) || (nz < 0.0f && arz < 0.0f);
   if constexpr (STATS)
     if (same_sign) RFX_CNT(SHADOW ? C_SH_TRI_S : C_TRI_S);
-#ifndef RFX_NO_TRI_SIGN
   // exact reject before the division: with opposite signs or a zero (or NaN) numerator, t <= 0 or NaN,
   // which `t > VERY_SMALL_NUMBER` rejects anyway; the divide is skipped when no lane of the wave needs it
   if (!same_sign) return false;
-#endif
   const float t = nz / arz;
   if (!(t > kVerySmall)) return false;
   RFX_CNT(SHADOW ? C_SH_TRI_T : C_TRI_T);
@@ -293,226 +254,546 @@ __device__ __forceinline__ bool tri_hit(const TriGeo &g, v3 o, v3 ray, float &t_
   return true;
 }
 
-// ------------------------------------------------------------- shadow any-hit
-// Scene.cpp:129-141: every object but the hit one (skip_sph / skip_tri: its sphere or triangle index,
-// -1 for the other kind); the boolean does not depend on the order.  (Spheres precede triangles, the
-// reference's order for every scene whose objects are added spheres-first -- then even the event
-// counters match it: the second sphere of a pair is counted only when the first did not occlude.)
-template <bool STATS, bool LDS>
-__device__ __forceinline__ bool occluded(const DevScene &S, v3 o, v3 ray, int skip_sph, int skip_tri, Cnt &cnt)
+// ------------------------------------------------------------- wave ray bundles (exact culling)
+// The live rays of a wave form a bundle: origins within rw of (cx, cy, cz) -- the first live lane's
+// origin -- and directions within the half-angle acos(cosa) of that lane's direction (ax, ay, az).
+// A ray the reference's float test reports as hitting a sphere passes within r + 8.1e-4 |o - c| of the
+// centre (rounding of d = b^2 - 4ac, DESIGN.md "Exact culling"); kCullRel = 4e-3 covers that five times,
+// so an object whose bounding sphere, grown by rw and kCullRel (L + rw), lies outside the bundle's cone
+// is missed by every lane of the wave and its exact test is skipped for the whole wave.  Skipping a test
+// that misses changes no result: the closest hit and the any-hit only ever take hits.  Every cull
+// decision is a conjunction of comparisons, so a NaN anywhere keeps the object.
+constexpr float kCullRel = 4e-3f;
+
+struct Bundle {
+  float cx, cy, cz, rw;
+  float ax, ay, az, cosa, sina;
+  bool ok;  // wave-uniform: the bound is finite and the cone narrower than ~84 degrees
+};
+
+__device__ __forceinline__ float lane_bcast(float v, int lane)
 {
-  const Geo<LDS> G{S};
-  const RayConst k = ray_const(ray);
-  float t, dist, u, v;
-  const int np = n_pairs(S);
-  for (int j = 0; j < np; ++j)
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+
+// max over the wave of a value >= 0 (every lane active): the bit patterns of non-negative floats order
+// like the floats, and a NaN pattern (above +inf) wins, which makes the bound unusable below.
+// DPP inclusive max-scan within each 16-lane row (row_shr 1, 2, 4, 8), then across rows (row_bcast 15,
+// row_bcast 31): lane 63 ends with the wave's maximum.  Lanes a shift leaves without a source keep 0.
+__device__ __forceinline__ float wave_max_nonneg(float v)
+{
+  uint32_t u = __float_as_uint(v);
+#ifdef RFX_BPERM_REDUCE
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) u = max(u, (uint32_t)__shfl_xor((int)u, off, 64));
+  return __uint_as_float(u);
+#else
+  u = max(u, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x111, 0xf, 0xf, false));  // row_shr:1
+  u = max(u, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x112, 0xf, 0xf, false));  // row_shr:2
+  u = max(u, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x114, 0xf, 0xf, false));  // row_shr:4
+  u = max(u, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x118, 0xf, 0xf, false));  // row_shr:8
+  u = max(u, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x142, 0xa, 0xf, false));  // row_bcast:15
+  u = max(u, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x143, 0xc, 0xf, false));  // row_bcast:31
+  return __int_as_float(__builtin_amdgcn_readlane((int)u, 63));
+#endif
+}
+
+// Bundle of the rays (o, d) of the `live` lanes.  Call with every lane of the wave active and at least
+// one live lane.  Approximate square roots are fine here: every bound is widened well past their error.
+__device__ __forceinline__ Bundle make_bundle(v3 o, v3 d, bool live)
+{
+  Bundle B;
+  const int ref = __ffsll((long long)__ballot(live)) - 1;
+  B.cx = lane_bcast(o.x, ref); B.cy = lane_bcast(o.y, ref); B.cz = lane_bcast(o.z, ref);
+  const float dx = lane_bcast(d.x, ref), dy = lane_bcast(d.y, ref), dz = lane_bcast(d.z, ref);
+  const float inv = __builtin_amdgcn_rsqf(dx * dx + dy * dy + dz * dz);
+  B.ax = dx * inv; B.ay = dy * inv; B.az = dz * inv;
+  const float ex = o.x - B.cx, ey = o.y - B.cy, ez = o.z - B.cz;
+  const float e2 = ex * ex + ey * ey + ez * ez;
+  const float cosl = (d.x * B.ax + d.y * B.ay + d.z * B.az) * __builtin_amdgcn_rsqf(d.x * d.x + d.y * d.y + d.z * d.z);
+  const float dev = 1.0f - cosl;
+  // a live lane with a non-finite or degenerate ray disables the bound for the whole wave
+  const bool bad = live && !(e2 <= 1.0e30f && dev >= -0.5f && dev <= 2.5f);
+  const float e2m = wave_max_nonneg(live ? e2 : 0.0f);
+  const float devm = wave_max_nonneg(live ? fmaxf(dev, 0.0f) : 0.0f);
+  B.rw = __builtin_amdgcn_sqrtf(e2m) * 1.0001f;
+  B.cosa = 1.0f - devm - 4e-6f;                                                // approximate cosines: widen
+  B.sina = __builtin_amdgcn_sqrtf(fmaxf(1.0f - B.cosa * B.cosa, 0.0f) + 1e-7f) * 1.001f;
+  B.ok = __ballot(bad) == 0 && B.cosa > 0.1f && B.rw <= 1.0e15f;
+  return B;
+}
+
+// Bit l: object first + l (l < n <= 64) of the bounding-sphere array may be hit by a ray of the bundle.
+// Call with every lane of the wave active.  Cone test: the ray set meets the grown sphere (centre at
+// distance L, radius rp) only if the angle between (centre - c) and the axis is at most
+// acos(cosa) + asin(rp / L), i.e. va >= cosa sqrt(L^2 - rp^2) - sina rp.
+__device__ __forceinline__ uint64_t cull_chunk(const Bound *bound, int first, int n, const Bundle &B)
+{
+  const int l = (int)(threadIdx.x & 63u);
+  bool keep = false;
+  if (l < n)
   {
+    const Bound g = bound[first + l];
+    const float vx = g.x - B.cx, vy = g.y - B.cy, vz = g.z - B.cz;
+    const float L2 = vx * vx + vy * vy + vz * vz;
+    const float L = __builtin_amdgcn_sqrtf(L2);
+    const float rp = g.r + B.rw + kCullRel * (L + B.rw);
+    const float va = vx * B.ax + vy * B.ay + vz * B.az;
+    const float lim = B.cosa * __builtin_amdgcn_sqrtf(fmaxf(L2 - rp * rp, 0.0f)) - B.sina * rp;
+    keep = !(L > rp && va < lim);
+  }
+  return __ballot(keep);
+}
+
+#ifdef RFX_ONE_CHUNK  // A/B only: scenes of at most 64 spheres and 64 triangles
+constexpr int kChunkLimit = 64;
+#else
+constexpr int kChunkLimit = 0x7fffffff;
+#endif
+
+__device__ __forceinline__ uint64_t all_bits(int n) { return n >= 64 ? ~0ull : ((1ull << n) - 1ull); }
+
+// sphere bits (2q, 2q+1) -> pair bit q
+__device__ __forceinline__ uint32_t pair_bits(uint64_t m)
+{
+  uint64_t x = (m | (m >> 1)) & 0x5555555555555555ull;
+  x = (x | (x >> 1)) & 0x3333333333333333ull;
+  x = (x | (x >> 2)) & 0x0F0F0F0F0F0F0F0Full;
+  x = (x | (x >> 4)) & 0x00FF00FF00FF00FFull;
+  x = (x | (x >> 8)) & 0x0000FFFF0000FFFFull;
+  x = (x | (x >> 16)) & 0x00000000FFFFFFFFull;
+  return (uint32_t)x;
+}
+
+// ------------------------------------------------------------- closest hit
+// Scene.cpp:86-106: the reference keeps the first object with the minimal distance, i.e. the
+// lexicographic minimum of (distance, insertion index); any visiting order gives it.  Distances are
+// compared through their squares (dist = sqrt_rn(sq) for both kinds, Sphere.cpp:61-62,
+// Triangle.cpp:70-85): for sq < best_sq, dist < best unless both round to the same float, i.e. unless
+// sq >= sq_lower_bound(best); for sq >= best_sq, dist >= best (tests/test_sqrt_bounds.py).
+struct Hit {
+  int obj, kind, i;  // object index (-1: none), 0 sphere / 1 triangle, index within its kind
+  float t, u, v, sq;
+};
+
+__device__ __forceinline__ bool strictly_closer(float sq, float best_sq)
+{
+  return sq < best_sq && (best_sq == INFINITY || sq < sq_lower_bound(sqrt_rn(best_sq)));
+}
+
+// the comparison key of a candidate and the two decisions on it (Hit::sq holds the winner's key)
+#ifdef RFX_DIST_CMP  // A/B reference: compare the rounded distances themselves
+constexpr float kNoHitKey = kFltMax;
+__device__ __forceinline__ float hit_key(float sq) { return sqrt_rn(sq); }
+__device__ __forceinline__ bool sph_takes(float key, float best) { return key < best; }
+__device__ __forceinline__ bool tri_takes(float key, float best, int obj, int best_obj)
+{
+  return key < best || (key == best && obj < best_obj);
+}
+#else
+constexpr float kNoHitKey = INFINITY;
+__device__ __forceinline__ float hit_key(float sq) { return sq; }
+__device__ __forceinline__ bool sph_takes(float sq, float best_sq) { return strictly_closer(sq, best_sq); }
+// dist < best || (dist == best && obj < best_obj)
+__device__ __forceinline__ bool tri_takes(float sq, float best_sq, int obj, int best_obj)
+{
+  return sq < best_sq ? (obj < best_obj || strictly_closer(sq, best_sq))
+                      : (obj < best_obj && sqrt_rn(sq) == sqrt_rn(best_sq));
+}
+#endif
+
+// Call with every lane of the wave active; `live` lanes trace (origin, ray).  B: the bundle, or null.
+template <bool STATS>
+__device__ __forceinline__ void closest_hit(const DevScene &S, v3 origin, v3 ray, bool live, const Bundle *B, Hit &h,
+                                            Cnt &cnt)
+{
+  if (live) RFX_CNT(C_SEGMENTS);
+  h.obj = -1; h.kind = 0; h.i = 0; h.t = 0.0f; h.u = 0.0f; h.v = 0.0f; h.sq = kNoHitKey;
+  const RayConst k = ray_const(ray);
+  RFX_PROF_BEGIN(P_SPH);
+  // spheres in index order carry increasing object indices, so among spheres `strictly_closer` already
+  // keeps the first of equal distances
+  for (int first = 0; first < S.n_sph && first < kChunkLimit; first += 64)
+  {
+    const int n = min(64, S.n_sph - first);
+    const uint64_t m = (B && B->ok) ? cull_chunk(S.bound, first, n, *B) : all_bits(n);
+    uint32_t pm = pair_bits(m);
+    while (pm)
+    {
+      const int j = (first >> 1) + __builtin_ctz(pm);
+      pm &= pm - 1u;
+      f2 b, d;
+      pair_bd(S.sph_pair[j], origin, k, b, d);
+      if (!live) continue;
+      if constexpr (!STATS)
+        if (!pair_may_hit(b, d)) continue;  // both miss: one branch
+      float t, sq;
+      if (sphere_tail<STATS, false>(b.x, d.x, ray, k, t, sq, cnt))
+      {
+        const float key = hit_key(sq);
+        if (sph_takes(key, h.sq)) { h.sq = key; h.obj = 2 * j; h.t = t; }
+      }
+      if ((!STATS || 2 * j + 1 < S.n_sph) && sphere_tail<STATS, false>(b.y, d.y, ray, k, t, sq, cnt))
+      {
+        const float key = hit_key(sq);
+        if (sph_takes(key, h.sq)) { h.sq = key; h.obj = 2 * j + 1; h.t = t; }
+      }
+    }
+  }
+  if (h.obj >= 0)
+  {
+    h.i = h.obj;
+    h.obj = S.sph_info[2 * h.i];
+  }
+  RFX_PROF_END(P_SPH);
+  RFX_PROF_BEGIN(P_TRI);
+  for (int first = 0; first < S.n_tri && first < kChunkLimit; first += 64)
+  {
+    const int n = min(64, S.n_tri - first);
+    uint64_t m = (B && B->ok) ? cull_chunk(S.bound, S.n_sph + first, n, *B) : all_bits(n);
+    while (m)
+    {
+      const int i = first + __builtin_ctzll(m);
+      m &= m - 1ull;
+      if (!live) continue;
+      float t, u, v, sq;
+      if (tri_hit<STATS, false>(S.tri_geo[i], origin, ray, t, u, v, sq, cnt))
+      {
+        RFX_CNT(C_TRI_D);
+        const int obj = S.tri_shade[i].obj;
+        const float key = hit_key(sq);
+        if (tri_takes(key, h.sq, obj, h.obj))
+        {
+          h.sq = key; h.obj = obj; h.kind = 1; h.i = i; h.t = t; h.u = u; h.v = v;
+        }
+      }
+    }
+  }
+  RFX_PROF_END(P_TRI);
+}
+
+// ------------------------------------------------------------- small scenes (<= 64 objects)
+// One cull mask covers the whole scene (bit l: object l of the bound array, spheres then triangles), so
+// the object loops need no wave-wide step and run only in the lanes that trace -- a lane leaves the
+// any-hit loop at its first occluder.
+__device__ __forceinline__ uint64_t tri_bits(uint64_t om, int n_sph) { return n_sph >= 64 ? 0ull : om >> n_sph; }
+
+template <bool STATS>
+__device__ __forceinline__ void closest_hit_small(const DevScene &S, v3 origin, v3 ray, uint64_t om, Hit &h, Cnt &cnt)
+{
+  RFX_CNT(C_SEGMENTS);
+  h.obj = -1; h.kind = 0; h.i = 0; h.t = 0.0f; h.u = 0.0f; h.v = 0.0f; h.sq = kNoHitKey;
+  const RayConst k = ray_const(ray);
+  RFX_PROF_BEGIN(P_SPH);
+  // spheres in index order carry increasing object indices, so among spheres a strict `<` already keeps
+  // the first of equal distances
+  uint32_t pm = pair_bits(om & all_bits(S.n_sph));
+  while (pm)
+  {
+    const int j = __builtin_ctz(pm);
+    pm &= pm - 1u;
     f2 b, d;
-    pair_bd(G.pair(j), o, k, b, d);
+    pair_bd(S.sph_pair[j], origin, k, b, d);
+    if constexpr (!STATS)
+      if (!pair_may_hit(b, d)) continue;  // both miss: one branch
+    float t, sq;
+    if (sphere_tail<STATS, false>(b.x, d.x, ray, k, t, sq, cnt))
+    {
+      const float key = hit_key(sq);
+      if (sph_takes(key, h.sq)) { h.sq = key; h.obj = 2 * j; h.t = t; }
+    }
+    if ((!STATS || 2 * j + 1 < S.n_sph) && sphere_tail<STATS, false>(b.y, d.y, ray, k, t, sq, cnt))
+    {
+      const float key = hit_key(sq);
+      if (sph_takes(key, h.sq)) { h.sq = key; h.obj = 2 * j + 1; h.t = t; }
+    }
+  }
+  if (h.obj >= 0)
+  {
+    h.i = h.obj;
+    h.obj = S.sph_info[2 * h.i];
+  }
+  RFX_PROF_END(P_SPH);
+  RFX_PROF_BEGIN(P_TRI);
+  uint64_t tm = tri_bits(om, S.n_sph);
+  while (tm)
+  {
+    const int i = __builtin_ctzll(tm);
+    tm &= tm - 1ull;
+    float t, u, v, sq;
+    if (tri_hit<STATS, false>(S.tri_geo[i], origin, ray, t, u, v, sq, cnt))
+    {
+      RFX_CNT(C_TRI_D);
+      const int obj = S.tri_shade[i].obj;
+      const float key = hit_key(sq);
+      if (tri_takes(key, h.sq, obj, h.obj))
+      {
+        h.sq = key; h.obj = obj; h.kind = 1; h.i = i; h.t = t; h.u = u; h.v = v;
+      }
+    }
+  }
+  RFX_PROF_END(P_TRI);
+}
+
+// Scene.cpp:129-141 for a small scene (see occluded below for the order and counter notes)
+template <bool STATS>
+__device__ __forceinline__ bool occluded_small(const DevScene &S, v3 o, v3 ray, int skip_sph, int skip_tri, uint64_t om,
+                                               Cnt &cnt)
+{
+  const RayConst k = ray_const(ray);
+  float t, sq, u, v;
+  uint32_t pm = pair_bits(om & all_bits(S.n_sph));
+  while (pm)
+  {
+    const int j = __builtin_ctz(pm);
+    pm &= pm - 1u;
+    f2 b, d;
+    pair_bd(S.sph_pair[j], o, k, b, d);
     if constexpr (STATS)
     {
-      if (2 * j != skip_sph && sphere_tail<STATS, true>(b.x, d.x, ray, k, t, dist, cnt)) return true;
-      if (2 * j + 1 != skip_sph && 2 * j + 1 < S.n_sph && sphere_tail<STATS, true>(b.y, d.y, ray, k, t, dist, cnt))
+      if (2 * j != skip_sph && sphere_tail<STATS, true>(b.x, d.x, ray, k, t, sq, cnt)) return true;
+      if (2 * j + 1 != skip_sph && 2 * j + 1 < S.n_sph && sphere_tail<STATS, true>(b.y, d.y, ray, k, t, sq, cnt))
         return true;
     }
     else
     {
-      // a miss on both spheres (the common case) costs one branch; the hit object is filtered out
-      // after its test, which does not change the boolean
+      // a miss on both spheres (the common case) costs one branch; the hit object is filtered out after
+      // its test, which does not change the boolean
       if (!pair_may_hit(b, d)) continue;
-      if (sphere_tail<STATS, true>(b.x, d.x, ray, k, t, dist, cnt) && 2 * j != skip_sph) return true;
-      if (sphere_tail<STATS, true>(b.y, d.y, ray, k, t, dist, cnt) && 2 * j + 1 != skip_sph) return true;
+      if (sphere_tail<STATS, true>(b.x, d.x, ray, k, t, sq, cnt) && 2 * j != skip_sph) return true;
+      if (sphere_tail<STATS, true>(b.y, d.y, ray, k, t, sq, cnt) && 2 * j + 1 != skip_sph) return true;
     }
   }
-  for (int i = 0; i < S.n_tri; ++i)
+  uint64_t tm = tri_bits(om, S.n_sph);
+  while (tm)
   {
+    const int i = __builtin_ctzll(tm);
+    tm &= tm - 1ull;
     if constexpr (STATS)
     {
-      if (i != skip_tri && tri_hit<STATS, true>(G.tri(i), o, ray, t, u, v, dist, cnt)) return true;
+      if (i != skip_tri && tri_hit<STATS, true>(S.tri_geo[i], o, ray, t, u, v, sq, cnt)) return true;
     }
-    else if (tri_hit<STATS, true>(G.tri(i), o, ray, t, u, v, dist, cnt) && i != skip_tri)
+    else if (tri_hit<STATS, true>(S.tri_geo[i], o, ray, t, u, v, sq, cnt) && i != skip_tri)
       return true;
   }
   return false;
 }
 
-// Scene.cpp:117-141 for lights [base, base + 32): bit k set when light base + k faces the hit point
-// (dot(dropToLight, norm) > VERY_SMALL_NUMBER) and its jittered shadow ray reaches it unoccluded.
-template <bool STATS, bool LDS>
-__device__ __forceinline__ uint32_t lights_visible(const DevScene &S, v3 drop, v3 norm, v3 rd, int base, int skip_sph,
-                                                   int skip_tri, Cnt &cnt)
+// ------------------------------------------------------------- shadow any-hit
+// Scene.cpp:129-141: every object but the hit one (skip_sph / skip_tri: its sphere or triangle index,
+// -1 for the other kind); the boolean does not depend on the order.  Call with every lane of the wave
+// active; `live` lanes test (o, ray).  A lane stops at its first occluder and the wave once every live
+// lane has one.  (Spheres precede triangles, the reference's order for scenes whose objects are added
+// spheres-first -- then even the event counters match it: the second sphere of a pair is counted only
+// when the first did not occlude.)
+template <bool STATS>
+__device__ __forceinline__ bool occluded(const DevScene &S, v3 o, v3 ray, bool live, int skip_sph, int skip_tri,
+                                         const Bundle *B, Cnt &cnt)
 {
-  uint32_t lit = 0;
-  const int nl = min(32, S.n_light - base);
-  for (int k = 0; k < nl; ++k)
+  const RayConst k = ray_const(ray);
+  bool occ = false;
+  float t, sq, u, v;
+  for (int first = 0; first < S.n_sph && first < kChunkLimit; first += 64)
   {
-    RFX_CNT(C_L_EVAL);
-    const LightRec L = S.lights[base + k];
-    const v3 dtl = sub(mk(L.ox, L.oy, L.oz), drop);
-    if (dot(dtl, norm) > kVerySmall)
+    if (__ballot(live && !occ) == 0) return occ;
+    const int n = min(64, S.n_sph - first);
+    const uint64_t m = (B && B->ok) ? cull_chunk(S.bound, first, n, *B) : all_bits(n);
+    uint32_t pm = pair_bits(m);
+    while (pm)
     {
-      RFX_CNT(C_L_FACING);
-      const v3 sray = add(dtl, mul(rd, L.radius));                          // Scene.cpp:129
-      if (!occluded<STATS, LDS>(S, drop, sray, skip_sph, skip_tri, cnt)) lit |= 1u << k;
+      const int j = (first >> 1) + __builtin_ctz(pm);
+      pm &= pm - 1u;
+      f2 b, d;
+      pair_bd(S.sph_pair[j], o, k, b, d);
+      if (live && !occ)
+      {
+        if constexpr (STATS)
+        {
+          if (2 * j != skip_sph && sphere_tail<STATS, true>(b.x, d.x, ray, k, t, sq, cnt)) occ = true;
+          else if (2 * j + 1 != skip_sph && 2 * j + 1 < S.n_sph &&
+                   sphere_tail<STATS, true>(b.y, d.y, ray, k, t, sq, cnt))
+            occ = true;
+        }
+        else if (pair_may_hit(b, d))
+        {
+          // the hit object is filtered out after its test, which does not change the boolean
+          if (sphere_tail<STATS, true>(b.x, d.x, ray, k, t, sq, cnt) && 2 * j != skip_sph) occ = true;
+          else if (sphere_tail<STATS, true>(b.y, d.y, ray, k, t, sq, cnt) && 2 * j + 1 != skip_sph) occ = true;
+        }
+      }
+      if (__ballot(live && !occ) == 0) return occ;
     }
   }
-  return lit;
+  for (int first = 0; first < S.n_tri && first < kChunkLimit; first += 64)
+  {
+    if (__ballot(live && !occ) == 0) return occ;
+    const int n = min(64, S.n_tri - first);
+    uint64_t m = (B && B->ok) ? cull_chunk(S.bound, S.n_sph + first, n, *B) : all_bits(n);
+    while (m)
+    {
+      const int i = first + __builtin_ctzll(m);
+      m &= m - 1ull;
+      if (live && !occ)
+      {
+        if constexpr (STATS)
+        {
+          if (i != skip_tri && tri_hit<STATS, true>(S.tri_geo[i], o, ray, t, u, v, sq, cnt)) occ = true;
+        }
+        else if (tri_hit<STATS, true>(S.tri_geo[i], o, ray, t, u, v, sq, cnt) && i != skip_tri)
+          occ = true;
+      }
+      if (__ballot(live && !occ) == 0) return occ;
+    }
+  }
+  return occ;
 }
 
 // ------------------------------------------------------------- Scene::trace
-// State of one trace between bounce segments (Scene.cpp:75-80 locals).
-struct Path {
-  v3 origin, ray, rd;  // rd: this trace's randomInsideSphere draw (Scene.cpp:75)
-  col mulc, pix;
-  int refl;
-};
-
-template <bool STATS>
-__device__ __forceinline__ void path_begin(Path &p, v3 origin, v3 ray, v3 rd, Cnt &cnt)
+// Scene::trace (Scene.cpp:73-236) for one trace per lane, the bounce loop run wave-wide: every
+// iteration is one segment of every live lane -- closest hit, then per light the facing test and the
+// shadow any-hit (Scene.cpp:117-141; the occlusion tests depend on nothing the shading computes, so
+// they run first, with few registers live), then material, shading and the next ray or the sky.
+// CULL: wave bundles skip objects no live lane can hit (closest hit and shadow rays); MANYL: more than
+// 32 lights (shadow masks and shading in blocks of 32).  Call with every lane of the wave active;
+// `valid` lanes trace.  Returns the trace's colour (zero for invalid lanes).
+template <bool STATS, bool CULL, bool MANYL, bool SMALL>
+__device__ __forceinline__ col trace(const DevScene &S, v3 origin, v3 ray, int depth, v3 rd, const float *lut,
+                                     Cnt &cnt, bool valid)
 {
-  RFX_CNT(C_RAYS);
-  p.origin = origin;
-  p.ray = ray;
-  p.rd = rd;
-  p.mulc = mkc(1.0f, 1.0f, 1.0f);
-  p.pix = mkc(0.0f, 0.0f, 0.0f);
-  p.refl = 0;
-}
-
-// One iteration of the bounce loop (Scene.cpp:78-233).  Returns true once the trace is finished:
-// sky hit, mulColor early-out, or reflNumber segments done.
-// CFG bits: kCfgLds -- scene staged in LDS; kCfgManyLights -- more than 32 lights (shadow masks in blocks)
-constexpr int kCfgLds = 1, kCfgManyLights = 2;
-
-template <bool STATS, int CFG>
-__device__ __forceinline__ bool segment(const DevScene &S, Path &p, int depth, const float *lut, Cnt &cnt)
-{
-  constexpr bool LDS = (CFG & kCfgLds) != 0;
-  constexpr bool MANYL = (CFG & kCfgManyLights) != 0;
-  const Geo<LDS> G{S};
-  v3 &origin = p.origin;
-  v3 &ray = p.ray;
-  col &mulc = p.mulc;
-  col &pix = p.pix;
-  const v3 rd = p.rd;
+  if (valid) RFX_CNT(C_RAYS);
+  col mulc = mkc(1.0f, 1.0f, 1.0f), pix = mkc(0.0f, 0.0f, 0.0f);
+  int refl = 0;
+  bool alive = valid && depth > 0;
+#ifdef RFX_DEBUG_SEGS
+  int nseg = 0;  // diagnostic build only (tools/segstats.py): the trace's segment count replaces its colour
+#endif
+  RFX_PROF_BEGIN(P_SEG);
+  while (__ballot(alive))
   {
-    RFX_CNT(C_SEGMENTS);
-    // closest hit (Scene.cpp:86-106): the reference keeps the first object with the minimal distance,
-    // i.e. the lexicographic minimum of (distance, insertion index) -- any visiting order gives it.
-    float best = kFltMax;
-    int best_obj = -1, best_kind = 0, best_i = 0;
-    float best_t = 0.0f, best_u = 0.0f, best_v = 0.0f;
-    RFX_PROF_BEGIN(P_SPH);
+#ifdef RFX_DEBUG_SEGS
+    if (alive) ++nseg;
+#endif
+    Hit h;
+    if constexpr (SMALL)
     {
-      // spheres in index order carry increasing object indices, so among spheres a strict `<` already
-      // keeps the first of equal distances
-      const RayConst k = ray_const(ray);
-      const int np = n_pairs(S);
-      int best_sph = -1;
-      for (int j = 0; j < np; ++j)
+      const int n_obj = S.n_sph + S.n_tri;
+      uint64_t om = all_bits(n_obj);
+      if constexpr (CULL)
       {
-        f2 b, d;
-        pair_bd(G.pair(j), origin, k, b, d);
-        if constexpr (!STATS)
-          if (!pair_may_hit(b, d)) continue;  // both miss: one branch
-        float t, dist;
-        if (sphere_tail<STATS, false>(b.x, d.x, ray, k, t, dist, cnt) && dist < best)
-        {
-          best = dist; best_sph = 2 * j; best_t = t;
-        }
-        if ((!STATS || 2 * j + 1 < S.n_sph) && sphere_tail<STATS, false>(b.y, d.y, ray, k, t, dist, cnt) &&
-            dist < best)
-        {
-          best = dist; best_sph = 2 * j + 1; best_t = t;
-        }
+        const Bundle B = make_bundle(origin, ray, alive);
+        if (B.ok) om = cull_chunk(S.bound, 0, n_obj, B);
       }
-      if (best_sph >= 0)
-      {
-        best_i = best_sph;
-        best_obj = S.sph_info[2 * best_sph];
-      }
+      if (alive) closest_hit_small<STATS>(S, origin, ray, om, h, cnt);
+      else h.obj = -1;
     }
-    RFX_PROF_END(P_SPH);
-    RFX_PROF_BEGIN(P_TRI);
-    for (int i = 0; i < S.n_tri; ++i)
+    else
     {
-      float t, u, v, sq;
-      if (tri_hit<STATS, false>(G.tri(i), origin, ray, t, u, v, sq, cnt))
-      {
-        RFX_CNT(C_TRI_D);
-        const float dist = sqrtf(sq);
-        const int obj = S.tri_shade[i].obj;
-        if (dist < best || (dist == best && obj < best_obj))
-        {
-          best = dist; best_obj = obj; best_kind = 1; best_i = i; best_t = t; best_u = u; best_v = v;
-        }
-      }
+      Bundle B;
+      if constexpr (CULL) B = make_bundle(origin, ray, alive);
+      closest_hit<STATS>(S, origin, ray, alive, CULL ? &B : nullptr, h, cnt);
     }
-
-    RFX_PROF_END(P_TRI);
-    if (best_obj >= 0)
+    const bool hit = alive && h.obj >= 0;
+    // re-derive the winner's outputs with the reference's expressions
+    v3 drop = origin, norm = mk(0.0f, 0.0f, 0.0f);
+    RFX_PROF_BEGIN(P_WIN);
+    if (hit)
     {
-      RFX_PROF_BEGIN(P_WIN);
-      // re-derive the winner's outputs with the reference's expressions
-      const v3 drop = add(origin, mul(ray, best_t));
-      v3 norm;
-      if (best_kind == 0)
+      drop = add(origin, mul(ray, h.t));
+      if (h.kind == 0)
       {
         RFX_CNT(C_HIT_SPH);
-        const SphereGeo g = S.sph_geo[best_i];
-        norm = sub(drop, mk(g.cx, g.cy, g.cz));                              // Sphere.cpp:69
+        const SphereGeo g = S.sph_geo[h.i];
+        norm = sub(drop, mk(g.cx, g.cy, g.cz));                                // Sphere.cpp:67
       }
       else
       {
         RFX_CNT(C_HIT_TRI);
-        norm = mk(S.tri_shade[best_i].nx, S.tri_shade[best_i].ny, S.tri_shade[best_i].nz);
+        norm = mk(S.tri_shade[h.i].nx, S.tri_shade[h.i].ny, S.tri_shade[h.i].nz);
       }
-      RFX_PROF_END(P_WIN);
-      // Scene.cpp:117-141 first, for up to 32 lights: which of them reach the hit point.  The occlusion
-      // tests depend on nothing the shading computes, so running them before it (with only the hit point,
-      // its normal and the jitter live) changes no result and keeps the any-hit loop's registers free.
-      const int skip_sph = best_kind == 0 ? best_i : -1, skip_tri = best_kind == 1 ? best_i : -1;
-      MatRec m{0.0f, 0.0f, 0.0f, 0.0f};
-      int diel = 0;
-      v3 reflv = mk(0.0f, 0.0f, 0.0f);
-      float rayLen = 0.0f, normLen = 0.0f, reflectLen = 0.0f;
-      col sumL = mkc(0.0f, 0.0f, 0.0f), sumS = mkc(0.0f, 0.0f, 0.0f);
-      for (int base = 0;; base += 32)                                        // Scene.cpp:117-181
+    }
+    RFX_PROF_END(P_WIN);
+    const int skip_sph = h.kind == 0 ? h.i : -1, skip_tri = h.kind == 1 ? h.i : -1;
+    MatRec m{0.0f, 0.0f, 0.0f, 0.0f};
+    int diel = 0;
+    v3 reflv = mk(0.0f, 0.0f, 0.0f);
+    float rayLen = 0.0f, normLen = 0.0f, reflectLen = 0.0f;
+    col sumL = mkc(0.0f, 0.0f, 0.0f), sumS = mkc(0.0f, 0.0f, 0.0f);
+    for (int base = 0;; base += 32)                                            // Scene.cpp:117-181
+    {
+      RFX_PROF_BEGIN(P_SHADOW);
+      uint32_t lit = 0;
+      const int nl = min(32, S.n_light - base);
+      for (int q = 0; q < nl; ++q)
       {
-        RFX_PROF_BEGIN(P_SHADOW);
-        const uint32_t lit = lights_visible<STATS, LDS>(S, drop, norm, rd, base, skip_sph, skip_tri, cnt);
-        RFX_PROF_END(P_SHADOW);
-        RFX_PROF_BEGIN(P_LIGHT);
-        if (!MANYL || base == 0)
+        const LightRec L = S.lights[base + q];
+        bool facing = false;
+        v3 sray = mk(0.0f, 0.0f, 0.0f);
+        if (hit)
         {
-          // the hit object's material, texel, reflection and lengths (Sphere.cpp:66-80, Triangle.cpp:86-105)
-          if (best_kind == 0)
+          RFX_CNT(C_L_EVAL);
+          const v3 dtl = sub(mk(L.ox, L.oy, L.oz), drop);
+          if (dot(dtl, norm) > kVerySmall)
           {
-            m = S.sph_mat[best_i];
-            diel = S.sph_info[2 * best_i + 1];
+            RFX_CNT(C_L_FACING);
+            facing = true;
+            sray = add(dtl, mul(rd, L.radius));                                  // Scene.cpp:129
+          }
+        }
+        if (__ballot(facing))
+        {
+          if constexpr (SMALL)
+          {
+            const int n_obj = S.n_sph + S.n_tri;
+            uint64_t om = all_bits(n_obj);
+            if constexpr (CULL)
+            {
+              const Bundle SB = make_bundle(drop, sray, facing);
+              if (SB.ok) om = cull_chunk(S.bound, 0, n_obj, SB);
+            }
+            if (facing && !occluded_small<STATS>(S, drop, sray, skip_sph, skip_tri, om, cnt)) lit |= 1u << q;
           }
           else
           {
-            const TriShade sh = S.tri_shade[best_i];
-            m = S.tri_mat[best_i];
+            Bundle SB;
+            if constexpr (CULL) SB = make_bundle(drop, sray, facing);
+            const bool occ = occluded<STATS>(S, drop, sray, facing, skip_sph, skip_tri, CULL ? &SB : nullptr, cnt);
+            if (facing && !occ) lit |= 1u << q;
+          }
+        }
+      }
+      RFX_PROF_END(P_SHADOW);
+      RFX_PROF_BEGIN(P_LIGHT);
+      if (hit)
+      {
+        if (!MANYL || base == 0)
+        {
+          // the hit object's material, texel, reflection and lengths (Sphere.cpp:66-80, Triangle.cpp:86-105)
+          if (h.kind == 0)
+          {
+            m = S.sph_mat[h.i];
+            diel = S.sph_info[2 * h.i + 1];
+          }
+          else
+          {
+            const TriShade sh = S.tri_shade[h.i];
+            m = S.tri_mat[h.i];
             diel = sh.dielectric;
-            if (sh.tex >= 0)                                                 // Triangle.cpp:92-99
+            if (sh.tex >= 0)                                                   // Triangle.cpp:89-96
             {
-              const float tvx = best_u * sh.t11 + best_v * sh.t12 + 0.0f;
-              const float tvy = best_u * sh.t21 + best_v * sh.t22 + 0.0f;
+              const float tvx = h.u * sh.t11 + h.v * sh.t12 + 0.0f;
+              const float tvy = h.u * sh.t21 + h.v * sh.t22 + 0.0f;
               const col c = texel_uv<STATS>(S, sh.tex, sh.tu0 + tvx, sh.tv0 + tvy, lut, cnt);
               m.r = c.r; m.g = c.g; m.b = c.b;
             }
           }
-          reflv = reflect(mul(ray, best_t), norm);                           // trace_math.cpp:14-23
+          reflv = reflect(mul(ray, h.t), norm);                                // trace_math.cpp:14-23
           rayLen = len(ray); normLen = len(norm); reflectLen = len(reflv);
         }
-        const int nl = min(32, S.n_light - base);
-        for (int k = 0; k < nl; ++k)
+        for (int q = 0; q < nl; ++q)
         {
-          if (!((lit >> k) & 1u)) continue;
+          if (!((lit >> q) & 1u)) continue;
           RFX_CNT(C_L_LIT);
-          const LightRec L = S.lights[base + k];
+          const LightRec L = S.lights[base + q];
           const v3 dtl = sub(mk(L.ox, L.oy, L.oz), drop);
           const float dlen = len(dtl);
           float aa = dlen * normLen;
@@ -527,7 +808,7 @@ __device__ __forceinline__ bool segment(const DevScene &S, Path &p, int depth, c
             const v3 dlr = add(normalized(dtl), mul(rd, 1.0f - m.refl));
             aa = len(dlr) * reflectLen;
             float sc = (aa > kVerySmall) ? dot(dlr, reflv) / aa : 0.0f;
-            sc = clampf(sc + (1.0f - sqrtf(ang)), 0.0f, 1.0f);
+            sc = clampf(sc + (1.0f - sqrt_rn(ang)), 0.0f, 1.0f);
             if (sc > kVerySmall && L.radius > kVerySmall)
             {
               RFX_CNT(C_L_POW);
@@ -536,14 +817,17 @@ __device__ __forceinline__ bool segment(const DevScene &S, Path &p, int depth, c
             }
           }
         }
-        RFX_PROF_END(P_LIGHT);
-        if (!MANYL || base + 32 >= S.n_light) break;
       }
+      RFX_PROF_END(P_LIGHT);
+      if (!MANYL || base + 32 >= S.n_light) break;
+    }
+    if (hit)
+    {
       RFX_PROF_BEGIN(P_MAT);
-      sumL = cadd(mkc(S.amb_r, S.amb_g, S.amb_b), sumL);                      // Scene.cpp:186
+      sumL = cadd(mkc(S.amb_r, S.amb_g, S.amb_b), sumL);                        // Scene.cpp:186
       const col color = mkc(m.r, m.g, m.b);
       col fin;
-      if (diel)                                                                // Scene.cpp:189-201
+      if (diel)                                                                  // Scene.cpp:189-201
       {
         RFX_CNT(C_DIELECTRIC);
         const float aa = rayLen * normLen;
@@ -553,7 +837,7 @@ __device__ __forceinline__ bool segment(const DevScene &S, Path &p, int depth, c
         fin = cmul(fin, mulc);
         mulc = cscale(mulc, r);
       }
-      else                                                                     // Scene.cpp:202-212
+      else                                                                       // Scene.cpp:202-212
       {
         RFX_CNT(C_METAL);
         const float r = 0.8f;
@@ -561,43 +845,32 @@ __device__ __forceinline__ bool segment(const DevScene &S, Path &p, int depth, c
         fin = cmul(fin, mulc);
         mulc = cmul(mulc, cscale(color, r));
       }
-      pix = cclamp(cadd(pix, fin));                                            // Scene.cpp:215-216
+      pix = cclamp(cadd(pix, fin));                                              // Scene.cpp:215-216
       RFX_PROF_END(P_MAT);
-      if (mulc.r < 0.01f && mulc.g < 0.01f && mulc.b < 0.01f) return true;    // Scene.cpp:219-220
-      RFX_CNT(C_CONTINUE);
-      origin = drop;                                                           // Scene.cpp:223-224
-      ray = add(normalized(reflv), mul(rd, 1.0f - m.refl));
-      return ++p.refl >= depth;                                                // Scene.cpp:78
+      if (mulc.r < 0.01f && mulc.g < 0.01f && mulc.b < 0.01f)                    // Scene.cpp:219-220
+        alive = false;
+      else
+      {
+        RFX_CNT(C_CONTINUE);
+        origin = drop;                                                           // Scene.cpp:223-224
+        ray = add(normalized(reflv), mul(rd, 1.0f - m.refl));
+        if (++refl >= depth) alive = false;                                      // Scene.cpp:78
+      }
     }
-    else                                                                       // Scene.cpp:226-231
+    else if (alive)                                                              // Scene.cpp:226-231
     {
       RFX_CNT(C_SKY);
       RFX_PROF_BEGIN(P_SKY);
       pix = cclamp(cadd(pix, cmul(cmul(mulc, skybox_texel<STATS>(S, ray, lut, cnt)), mkc(S.env_r, S.env_g, S.env_b))));
       RFX_PROF_END(P_SKY);
-      return true;
+      alive = false;
     }
   }
-}
-
-// Scene::trace (Scene.cpp:73-236) as a whole: the reference's bounce loop over segment().
-template <bool STATS, int CFG>
-__device__ __forceinline__ col trace(const DevScene &S, v3 origin, v3 ray, int depth, v3 rd, const float *lut, Cnt &cnt)
-{
-  Path p;
-  path_begin<STATS>(p, origin, ray, rd, cnt);
+  RFX_PROF_END(P_SEG);
 #ifdef RFX_DEBUG_SEGS
-  // diagnostic build only (tools/segstats.py): the trace's segment count replaces its color
-  int nseg = 0;
-  if (depth > 0)
-    while (++nseg, !segment<STATS, CFG>(S, p, depth, lut, cnt)) {}
   return mkc((float)nseg, 0.0f, 0.0f);
 #else
-  RFX_PROF_BEGIN(P_SEG);
-  if (depth > 0)
-    while (!segment<STATS, CFG>(S, p, depth, lut, cnt)) {}
-  RFX_PROF_END(P_SEG);
-  return p.pix;
+  return pix;
 #endif
 }
 
@@ -629,8 +902,8 @@ __device__ __forceinline__ v3 load_rd(const FrameParams &P, uint64_t i)
   return mk(P.rd[i], P.rd[P.n_rd + i], P.rd[2 * P.n_rd + i]);
 }
 
-// 6 waves per SIMD (<= 80 VGPRs): the kernel is VALU-issue bound (~90% busy, PMC); more waves hide
-// the scene-load and texel latencies better than the spills cost (tools/ab.py: 4 -> 5 -> 6 each won)
+// 6 waves per SIMD (<= 80 VGPRs): the kernel is VALU-issue bound; more waves hide the scene-load and
+// texel latencies better than spills cost (tools/ab.py: 4 -> 5 -> 6 each won)
 #ifndef RFX_WAVES_PER_EU
 #define RFX_WAVES_PER_EU 6
 #endif
@@ -640,16 +913,19 @@ __device__ __forceinline__ v3 load_rd(const FrameParams &P, uint64_t i)
 // (sampleNum == 1, no jitter, no accumulation -- the benchmark frame), and the general SSAA / additive
 // loop.  The plain variant drops the sample loops and their live state (no spills before the bounce loop).
 enum TraceMode { kModeSsaa = 0, kModeBlock = 1, kModePlain = 2 };
+// CFG bits: kCfgCull -- wave-bundle culling (every non-stats launch); kCfgManyLights -- more than 32 lights;
+// kCfgSmall -- at most 64 objects (one cull mask for the whole scene)
+constexpr int kCfgCull = 1, kCfgManyLights = 2, kCfgSmall = 4;
 
-// one workgroup = 16x16 output pixels (block mode: block corners), one wave = an 8x8 tile (ray coherence)
+// one workgroup = 16x16 output pixels (block mode: block corners), one wave = an 8x8 tile (ray coherence).
+// Every lane of a wave reaches trace() -- lanes outside the frame or the cursor span as invalid -- so the
+// bounce loop can use wave-wide bundles.
 template <bool STATS, int MODE, int CFG>
 __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
 {
-  constexpr bool BLOCK = MODE == kModeBlock;
-  constexpr bool LDS = (CFG & kCfgLds) != 0;
+  constexpr bool CULL = (CFG & kCfgCull) != 0, MANYL = (CFG & kCfgManyLights) != 0, SMALL = (CFG & kCfgSmall) != 0;
   __shared__ float lut[256];
   lut[threadIdx.x] = (float)threadIdx.x / 255.0f;                               // Color.cpp:11-13
-  if constexpr (LDS) stage_scene_lds(S);
   RFX_PROF_INIT();
   __syncthreads();
   Cnt cnt;
@@ -667,68 +943,56 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
   view.m31 = P.v31; view.m32 = P.v32; view.m33 = P.v33;
   const v3 eye = mk(P.eye_x, P.eye_y, P.eye_z);
 
-  if constexpr (BLOCK)
+  if constexpr (MODE == kModeBlock)
   {
     // block preview (Render.cpp:158-172): only block corners inside the cursor span are traced;
     // trace order = raster order of corners, so corner (cx, cy) is trace cy * bw + cx.
     const uint32_t n = (uint32_t)(-P.ss);
     const uint32_t bw = (P.W + n - 1) / n, bh = (P.H + n - 1) / n;
     const uint32_t cx = gx, cy = gy + P.row0;
-    if (gy < P.grid_rows && cx < bw && cy < bh)
+    const uint32_t x = cx * n, y = cy * n;
+    const uint64_t p = (uint64_t)y * P.W + x;
+    const bool valid = gy < P.grid_rows && cx < bw && cy < bh && p >= P.p_begin && p < P.p_end;
+    const v3 ray = mmul(view, mk((float)x - P.wh, (float)y - P.hh, P.rz));
+    v3 rd = mk(0.0f, 0.0f, 0.0f);
+    if (valid) rd = load_rd(P, (uint64_t)cy * bw + cx - P.trace_base);
+    const col c = trace<STATS, CULL, MANYL, SMALL>(S, eye, ray, P.depth, rd, lut, cnt, valid);
+    if (valid)
     {
-      const uint32_t x = cx * n, y = cy * n;
-      const uint64_t p = (uint64_t)y * P.W + x;
-      if (p >= P.p_begin && p < P.p_end)
-      {
-        const v3 ray = mmul(view, mk((float)x - P.wh, (float)y - P.hh, P.rz));
-        const uint64_t ti = (uint64_t)cy * bw + cx - P.trace_base;
-        const col c = trace<STATS, CFG>(S, eye, ray, P.depth, load_rd(P, ti), lut, cnt);
-        const uint32_t ex = min(P.W, x + n), ey = min(P.H, y + n);
-        const uint32_t a = argb(c);
-        for (uint32_t qy = y; qy < ey; ++qy)
-          for (uint32_t qx = x; qx < ex; ++qx)
-          {
-            float *d = P.img + ((size_t)qy * P.W + qx) * 3;
-            d[0] = c.r; d[1] = c.g; d[2] = c.b;
-            if (P.argb) P.argb[(size_t)qy * P.W + qx] = a;
-          }
-      }
+      const uint32_t ex = min(P.W, x + n), ey = min(P.H, y + n);
+      const uint32_t a = argb(c);
+      for (uint32_t qy = y; qy < ey; ++qy)
+        for (uint32_t qx = x; qx < ex; ++qx)
+        {
+          float *d = P.img + ((size_t)qy * P.W + qx) * 3;
+          d[0] = c.r; d[1] = c.g; d[2] = c.b;
+          if (P.argb) P.argb[(size_t)qy * P.W + qx] = a;
+        }
     }
   }
-  else if constexpr (MODE == kModePlain)
-  {
-    if (gx < P.W && gy < P.grid_rows)
-    {
-      const uint32_t x = gx;
-      const uint32_t y = P.nranks > 1 ? strip_row_to_y(gy, P) : gy + P.row0;
-      const uint32_t orow = P.nranks > 1 ? gy : y;
-      const uint64_t p = (uint64_t)y * P.W + x;
-      if (p >= P.p_begin && p < P.p_end)
-      {
-        const float rx = (float)x - P.wh, ry = (float)y - P.hh;                   // Render.cpp:152-153
-        // Render.cpp:183 with ssx = ssy = 0, sampleNum = 1, no jitter: float(0) / 1 == +0, rnd == 0
-        const v3 ray = mmul(view, mk(rx + 0.0f + 0.0f, ry + 0.0f + 0.0f, P.rz));
-        const col c = trace<STATS, CFG>(S, eye, ray, P.depth, load_rd(P, p - P.p_begin), lut, cnt);
-        const col out = cadd(mkc(0.0f, 0.0f, 0.0f), c);                            // Render.cpp:185 (/ 1.0f exact)
-        const size_t o = (size_t)orow * P.W + x;
-        float *d = P.img + o * 3;
-        d[0] = out.r; d[1] = out.g; d[2] = out.b;
-        if (P.argb) P.argb[o] = argb(out);                                         // Render::copyImage
-      }
-    }
-  }
-  else if (gx < P.W && gy < P.grid_rows)
+  else
   {
     const uint32_t x = gx;
     const uint32_t y = P.nranks > 1 ? strip_row_to_y(gy, P) : gy + P.row0;
     const uint32_t orow = P.nranks > 1 ? gy : y;
     const uint64_t p = (uint64_t)y * P.W + x;
-    if (p >= P.p_begin && p < P.p_end)
+    const bool valid = gx < P.W && gy < P.grid_rows && p >= P.p_begin && p < P.p_end;
+    const uint64_t pr = p - P.p_begin;
+    const float rx = (float)x - P.wh, ry = (float)y - P.hh;                       // Render.cpp:152-153
+    col out;
+    if constexpr (MODE == kModePlain)
     {
-      const uint64_t pr = p - P.p_begin;
-      const float rx = (float)x - P.wh, ry = (float)y - P.hh;                     // Render.cpp:152-153
+      // Render.cpp:183 with ssx = ssy = 0, sampleNum = 1, no jitter: float(0) / 1 == +0, rnd == 0
+      const v3 ray = mmul(view, mk(rx + 0.0f + 0.0f, ry + 0.0f + 0.0f, P.rz));
+      v3 rd = mk(0.0f, 0.0f, 0.0f);
+      if (valid) rd = load_rd(P, pr);
+      const col c = trace<STATS, CULL, MANYL, SMALL>(S, eye, ray, P.depth, rd, lut, cnt, valid);
+      out = cadd(mkc(0.0f, 0.0f, 0.0f), c);                                      // Render.cpp:185 (/ 1.0f exact)
+    }
+    else
+    {
       float rndx = 0.0f, rndy = 0.0f;
-      if (P.additive)                                                              // Render.cpp:177-178
+      if (P.additive && valid)                                                     // Render.cpp:177-178
       {
         const uint32_t s1 = lcg_jump(P.jitter_seed, 2 * pr + 1);
         rndx = (float)lcg_out(s1) / (float)0x7FFF;
@@ -744,18 +1008,22 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
           const float ox = sx ? (float)sx / ssf : 0.0f, oy = sy ? (float)sy / ssf : 0.0f;
           v3 ray = mk(rx + ox + rndx, ry + oy + rndy, P.rz);
           ray = mmul(view, ray);
-          const uint64_t ti = pr * (uint64_t)(ss * ss) + (uint64_t)(sx * ss + sy);
-          fin = cadd(fin, trace<STATS, CFG>(S, eye, ray, P.depth, load_rd(P, ti), lut, cnt));
+          v3 rd = mk(0.0f, 0.0f, 0.0f);
+          if (valid) rd = load_rd(P, pr * (uint64_t)(ss * ss) + (uint64_t)(sx * ss + sy));
+          fin = cadd(fin, trace<STATS, CULL, MANYL, SMALL>(S, eye, ray, P.depth, rd, lut, cnt, valid));
         }
       if (ss != 1)                                                                 // Render.cpp:189 (x / 1.0f == x)
       {
         const float sq = (float)(ss * ss);
         if (fabsf(sq) > kVerySmall) fin = mkc(fin.r / sq, fin.g / sq, fin.b / sq);
       }
+      out = fin;
+    }
+    if (valid)
+    {
       const size_t o = (size_t)orow * P.W + x;
       float *d = P.img + o * 3;
-      col out = fin;
-      if (P.accumulate) out = mkc(d[0] + fin.r, d[1] + fin.g, d[2] + fin.b);        // Render.cpp:191-194
+      if (MODE == kModeSsaa && P.accumulate) out = mkc(d[0] + out.r, d[1] + out.g, d[2] + out.b);  // Render.cpp:191-194
       d[0] = out.r; d[1] = out.g; d[2] = out.b;
       if (P.argb) P.argb[o] = argb(out);                                           // Render::copyImage
     }
@@ -997,19 +1265,26 @@ hipError_t launch_rng_finish(const uint32_t *d_seed, const uint32_t *d_jump, uin
   return hipGetLastError();
 }
 
+template <bool STATS, int MODE, int CFG>
+static void launch_one(dim3 grid, const DevScene &S, const FrameParams &P, hipStream_t st)
+{
+  if constexpr (!STATS || !(CFG & kCfgCull))  // the stats build never culls
+    hipLaunchKernelGGL((trace_kernel<STATS, MODE, CFG>), grid, dim3(256), 0, st, S, P);
+}
+
 template <bool STATS, int MODE>
 static void launch_cfg(int cfg, dim3 grid, const DevScene &S, const FrameParams &P, hipStream_t st)
 {
   switch (cfg)
   {
-    case 0: hipLaunchKernelGGL((trace_kernel<STATS, MODE, 0>), grid, dim3(256), 0, st, S, P); break;
-    case kCfgManyLights: hipLaunchKernelGGL((trace_kernel<STATS, MODE, kCfgManyLights>), grid, dim3(256), 0, st, S, P); break;
-#ifdef RFX_LDS_SCENE
-    case kCfgLds: hipLaunchKernelGGL((trace_kernel<STATS, MODE, kCfgLds>), grid, dim3(256), 0, st, S, P); break;
-    case kCfgLds | kCfgManyLights:
-      hipLaunchKernelGGL((trace_kernel<STATS, MODE, kCfgLds | kCfgManyLights>), grid, dim3(256), 0, st, S, P);
-      break;
-#endif
+    case 0: launch_one<STATS, MODE, 0>(grid, S, P, st); break;
+    case 1: launch_one<STATS, MODE, 1>(grid, S, P, st); break;
+    case 2: launch_one<STATS, MODE, 2>(grid, S, P, st); break;
+    case 3: launch_one<STATS, MODE, 3>(grid, S, P, st); break;
+    case 4: launch_one<STATS, MODE, 4>(grid, S, P, st); break;
+    case 5: launch_one<STATS, MODE, 5>(grid, S, P, st); break;
+    case 6: launch_one<STATS, MODE, 6>(grid, S, P, st); break;
+    case 7: launch_one<STATS, MODE, 7>(grid, S, P, st); break;
   }
 }
 
@@ -1035,9 +1310,11 @@ hipError_t launch_trace(const DevScene &S, const FrameParams &P, bool stats, hip
   const uint32_t cols = P.ss < 0 ? (P.W + (uint32_t)(-P.ss) - 1) / (uint32_t)(-P.ss) : P.W;
   const dim3 grid((cols + 15) / 16, (P.grid_rows + 15) / 16);
   const int mode = P.ss < 0 ? kModeBlock : (P.ss == 1 && !P.additive && !P.accumulate) ? kModePlain : kModeSsaa;
-  int cfg = S.n_light > 32 ? kCfgManyLights : 0;
-#ifdef RFX_LDS_SCENE  // staged scene: measured slower than scalar loads since sphere pairs (tools/ab.py)
-  if (!stats && S.n_sph <= kLdsSph && S.n_tri <= kLdsTri) cfg |= kCfgLds;
+  // the stats build counts the reference's every test, so it never culls
+  int cfg = (S.n_light > 32 ? kCfgManyLights : 0) | (stats ? 0 : kCfgCull) |
+            (S.n_sph + S.n_tri <= 64 ? kCfgSmall : 0);
+#ifdef RFX_NO_CULL
+  cfg &= ~kCfgCull;
 #endif
   launch_mode_cfg(stats, mode, cfg, grid, S, P, st);
   return hipGetLastError();

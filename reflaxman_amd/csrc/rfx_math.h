@@ -6,6 +6,7 @@
 // Citations: /root/reference/src/common/<file>:<line>.
 #pragma once
 #include <stdint.h>
+#include <string.h>
 
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
@@ -25,6 +26,26 @@ constexpr float kDelta = 0.0001f;
 constexpr float kFltEpsilon = 1.1920928955078125e-07f;
 constexpr float kFltMax = 3.402823466e+38f;
 
+// Correctly rounded f32 square root.  On gfx950 the IEEE lowering of sqrtf is: scale inputs below
+// 2^-96 by 2^32, v_sqrt_f32, fix the result by +-1 ulp from the signs of two fma residuals, unscale,
+// and pass +-0 / +inf through.  For x >= 2^-96 (and +inf) the scaling and the special-value select are
+// identities, so the device path runs the remaining instructions -- the same ones, in the same order,
+// hence the same bits -- and keeps the full sequence for the other inputs.
+RFX_HD float sqrt_rn(float x)
+{
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(RFX_PLAIN_SQRT)
+  if (x >= 0x1p-96f)
+  {
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float s_dn = __uint_as_float(__float_as_uint(s) - 1u), s_up = __uint_as_float(__float_as_uint(s) + 1u);
+    const float r_dn = __builtin_fmaf(-s_dn, s, x), r_up = __builtin_fmaf(-s_up, s, x);
+    const float t = r_dn <= 0.0f ? s_dn : s;
+    return r_up > 0.0f ? s_up : t;
+  }
+#endif
+  return sqrtf(x);
+}
+
 struct v3 { float x, y, z; };
 struct col { float r, g, b; };
 // Matrix33 element order _11.._33 (Matrix33.h:13-22)
@@ -37,7 +58,7 @@ RFX_HD v3 mul(v3 a, float f) { return mk(a.x * f, a.y * f, a.z * f); }          
 RFX_HD v3 neg(v3 a) { return mk(-a.x, -a.y, -a.z); }                                 // Vector3.cpp:166
 RFX_HD float dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }          // Vector3.cpp:126
 RFX_HD float sqlen(v3 a) { return a.x * a.x + a.y * a.y + a.z * a.z; }              // Vector3.cpp:48
-RFX_HD float len(v3 a) { return sqrtf(a.x * a.x + a.y * a.y + a.z * a.z); }         // Vector3.cpp:43
+RFX_HD float len(v3 a) { return sqrt_rn(a.x * a.x + a.y * a.y + a.z * a.z); }       // Vector3.cpp:43
 RFX_HD v3 cross(v3 a, v3 b)                                                          // Vector3.cpp:138
 {
   return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
@@ -62,6 +83,26 @@ RFX_HD v3 reflect(v3 v, v3 n)
   return v;
 }
 RFX_HD float clampf(float v, float lo, float hi) { return v < lo ? lo : v > hi ? hi : v; } // trace_math.h:24
+
+// Distances compared through their squares.  sqrt_rn is monotone, so for dist = sqrt_rn(sq):
+//   dist >= y  <=>  sq >= sq_lower_bound(y)     (y > 0 finite)
+// where sq_lower_bound(y) is the smallest float whose rounded square root is >= y.  sqrt_rn(x) >= y iff
+// sqrt(x) lies above the midpoint m between y and its predecessor; sqrt(x) is never exactly such a
+// midpoint (an odd 25-bit significand squared has no 24-bit form), so the bound is the first float above
+// m^2, which double arithmetic gets exactly (m has 25 significant bits, m^2 at most 50).
+RFX_HD uint32_t f2u(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+RFX_HD float u2f(uint32_t u) { float f; memcpy(&f, &u, 4); return f; }
+RFX_HD float sq_lower_bound(float y)
+{
+  const double m = ((double)u2f(f2u(y) - 1u) + (double)y) * 0.5;
+  const double m2 = m * m;
+  float f = (float)m2;
+  if ((double)f <= m2) f = u2f(f2u(f) + 1u);
+  return f;
+}
+// Sphere.cpp:62-64 `(ray * t).length() > DELTA` as a test on the squared length:
+// sqrt_rn(sq) > 1e-4f  <=>  sq >= sq_lower_bound(succ(1e-4f)) (tests/test_sqrt_bounds.py)
+constexpr float kSqDeltaSphere = 0x1.5798fp-27f;
 
 // Matrix33(u, v, n): columns (Matrix33.cpp:10-15)
 RFX_HD m33 from_cols(v3 u, v3 v, v3 n)

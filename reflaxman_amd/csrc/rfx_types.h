@@ -38,6 +38,9 @@ struct alignas(16) TriShade {                                        // Triangle
   float t11, t12, t21, t22;   // tuvTrans _11 _12 _21 _22 (_13 = _23 = 0 by construction)
   float tv0; int32_t tex; int32_t dielectric; int32_t obj;
 };
+// Bounding sphere of an object for the wave-bundle cull (rfx_kernels.hip): spheres first, then triangles.
+// r = +inf marks an object that is never culled (an ill-conditioned triangle, see rfx_host.cpp).
+struct alignas(16) Bound { float x, y, z, r; };
 struct alignas(16) LightRec { float ox, oy, oz, radius, r, g, b, power; }; // OmniLight.h
 struct alignas(16) TexRec { uint32_t offset, w, h, pad; };
 
@@ -52,6 +55,7 @@ struct DevScene {
   const LightRec *lights;     // n_light
   const TexRec *texs;         // n_tex
   const uint32_t *texels;     // texel pool, ARGB
+  const Bound *bound;         // n_sph + n_tri bounding spheres
   int32_t n_sph, n_tri, n_light, skybox_tex;
   float amb_r, amb_g, amb_b;  // diffLightColor * diffLightPower (Scene.cpp:186, host-folded)
   float env_r, env_g, env_b;  // envColor (Scene.cpp:12,55)
