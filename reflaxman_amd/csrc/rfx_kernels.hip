@@ -222,7 +222,7 @@ __device__ __forceinline__ bool sphere_tail(float b, float d, v3 ray, const RayC
 // ((aox, aoy), (arx, ary), (u, v)), each half rounding exactly as the scalar expression.
 template <bool STATS, bool SHADOW>
 __device__ __forceinline__ bool tri_hit(const TriGeo &g, v3 o, v3 ray, float &t_out, float &u_out, float &v_out,
-                                        float &sq_out, Cnt &cnt)
+                                        float &sq_out, Cnt &cnt, float a2 = 0.0f, float best_sq = INFINITY)
 {
   RFX_CNT(SHADOW ? C_SH_TRI_TESTS : C_TRI_TESTS);
   const float dx = o.x - g.v0x, dy = o.y - g.v0y, dz = o.z - g.v0z;
@@ -238,6 +238,15 @@ __device__ __forceinline__ bool tri_hit(const TriGeo &g, v3 o, v3 ray, float &t_
   // exact reject before the division: with opposite signs or a zero (or NaN) numerator, t <= 0 or NaN,
   // which `t > VERY_SMALL_NUMBER` rejects anyway; the divide is skipped when no lane of the wave needs it
   if (!same_sign) return false;
+#if !defined(RFX_DIST_CMP) && !defined(RFX_NO_TRI_DIST)
+  if constexpr (!SHADOW && !STATS)
+  {
+    // exact reject of a plane hit beyond the current closest hit: |ray t|^2 = a nz^2 / arz^2 (real), and
+    // a 2^-16 margin over the float rounding of both sides leaves |ray t| strictly above the best
+    // distance after rounding, so the reference could neither take it nor tie (a2 = 2a exactly)
+    if (nz * nz * a2 > best_sq * (arz * arz) * 2.0000305f) return false;
+  }
+#endif
   const float t = nz / arz;
   if (!(t > kVerySmall)) return false;
   RFX_CNT(SHADOW ? C_SH_TRI_T : C_TRI_T);
@@ -457,7 +466,7 @@ __device__ __forceinline__ void closest_hit(const DevScene &S, v3 origin, v3 ray
       m &= m - 1ull;
       if (!live) continue;
       float t, u, v, sq;
-      if (tri_hit<STATS, false>(S.tri_geo[i], origin, ray, t, u, v, sq, cnt))
+      if (tri_hit<STATS, false>(S.tri_geo[i], origin, ray, t, u, v, sq, cnt, k.a2, h.sq))
       {
         RFX_CNT(C_TRI_D);
         const int obj = S.tri_shade[i].obj;
@@ -521,7 +530,7 @@ __device__ __forceinline__ void closest_hit_small(const DevScene &S, v3 origin, 
     const int i = __builtin_ctzll(tm);
     tm &= tm - 1ull;
     float t, u, v, sq;
-    if (tri_hit<STATS, false>(S.tri_geo[i], origin, ray, t, u, v, sq, cnt))
+    if (tri_hit<STATS, false>(S.tri_geo[i], origin, ray, t, u, v, sq, cnt, k.a2, h.sq))
     {
       RFX_CNT(C_TRI_D);
       const int obj = S.tri_shade[i].obj;

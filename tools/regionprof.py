@@ -20,7 +20,7 @@ REGIONS = ["sphere_loop", "triangle_loop", "winner", "light_loop", "shadow_anyhi
 
 
 def main():
-    path = os.path.join(_build.LIBDIR, "diag", "librfx_prof.so")
+    path = os.path.join(_build.LIBDIR, "diag", sys.argv[2] if len(sys.argv) > 2 else "librfx_prof.so")
     scene = sys.argv[1] if len(sys.argv) > 1 else "synth16"
     r = ab.Runner("prof", path, scenes.get_scene(scene), 3840, 2160, 8, 1350490027)
     r.render(2)
@@ -31,7 +31,7 @@ def main():
     assert r.L.rfx_synchronize(r.r) == 0
     assert r.L.rfx_debug_prof_read(buf, 1) == 16
     tot = buf[7]
-    print(json.dumps({"scene": scene, "cycles": {k: int(v) for k, v in zip(REGIONS, buf[:8])},
+    print(json.dumps({"scene": scene, "lib": os.path.basename(path), "cycles": {k: int(v) for k, v in zip(REGIONS, buf[:8])},
                       "wave_executions": {k: int(v) for k, v in zip(REGIONS, buf[8:])},
                       "share_of_trace": {k: round(v / tot, 4) for k, v in zip(REGIONS, buf[:8])}}))
 
