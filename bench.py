@@ -273,7 +273,7 @@ def main():
                    "parallelism": f"row-strips{rb}x{world}" if world > 1 else "single-gpu"},
         "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": metrics.PEAK_FP32_VALU_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved / metrics.PEAK_FP32_VALU_TFLOPS, 4),
-                     "traffic": traffic, "kernel": "rfx::trace_kernel<false>",
+                     "traffic": traffic, "kernel": "rfx::trace_kernel (plain pixel mode, wave-bundle culling)",
                      "flops_per_launch": int(flops_launch), "avg_launch_ms": round(trace_avg, 4),
                      "frac_vs_nofma_peak": round(achieved / metrics.PEAK_FP32_NOFMA_TFLOPS, 4),
                      "algo_hbm_bytes_per_launch": px_launch * metrics.ALGO_BYTES_PER_PIXEL,

@@ -1,11 +1,21 @@
-"""Summarise rocprofv3 --pmc CSVs for the trace kernel (per-launch means of each counter)."""
+"""Summarise rocprofv3 --pmc CSVs for one kernel (per-launch means of each counter).
+
+    python tools/pmc_summary.py [--kernel SUBSTR] [--out profiles/pmc_trace_kernel.json
+                                 --config SCENE W H DEPTH NGPUS] CSV...
+
+With --out, also writes the HBM traffic record bench.py reads for `roofline.traffic`:
+FETCH_SIZE and WRITE_SIZE are reported by rocprofv3 in KiB per dispatch; the bytes are
+taken as read + write.  (MI355X_MICROARCH.md: FETCH_SIZE counts exactly half the bytes of
+16-B-per-lane streaming reads; this kernel's reads -- randDir dwords, texels, the scene --
+are other widths, so FETCH_SIZE is used as reported, and the record says so.)
+"""
+import argparse
 import collections
 import csv
 import json
-import sys
 
 
-def summarise(paths, kernel="trace_kernel"):
+def summarise(paths, kernel="trace_kernel<false"):
     agg = collections.defaultdict(list)
     for p in paths:
         for r in csv.DictReader(open(p)):
@@ -14,8 +24,29 @@ def summarise(paths, kernel="trace_kernel"):
     return {k: sum(v) / len(v) for k, v in sorted(agg.items())}
 
 
-if __name__ == "__main__":
-    s = summarise(sys.argv[1:])
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--kernel", default="trace_kernel<false")
+    ap.add_argument("--out")
+    ap.add_argument("--config", nargs=5)
+    ap.add_argument("csv", nargs="+")
+    a = ap.parse_args()
+    s = summarise(a.csv, a.kernel)
     if "SQ_ACTIVE_INST_VALU" in s and "SQ_THREAD_CYCLES_VALU" in s:
         s["valu_lane_util"] = s["SQ_THREAD_CYCLES_VALU"] / (64 * s["SQ_ACTIVE_INST_VALU"])
     print(json.dumps(s, indent=1))
+    if a.out:
+        scene, W, H, depth, n = a.config
+        rec = {
+            "kernel": a.kernel, "config": [scene, int(W), int(H), int(depth), int(n)],
+            "fetch_bytes_per_launch": int(s["FETCH_SIZE"] * 1024), "write_bytes_per_launch": int(s["WRITE_SIZE"] * 1024),
+            "hbm_bytes_per_launch": int((s["FETCH_SIZE"] + s["WRITE_SIZE"]) * 1024),
+            "note": "rocprofv3 FETCH_SIZE + WRITE_SIZE (KiB) per dispatch, separate --pmc passes; FETCH_SIZE uncorrected "
+                    "(non-16B reads); Infinity-Cache hits may be counted",
+            "counters": s,
+        }
+        json.dump(rec, open(a.out, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
