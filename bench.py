@@ -17,7 +17,9 @@ N > 1 (weak scaling): the frame grows with N at 16:9 (N=4 is C4, 7680x4320);
 rows are dealt to ranks in block-cyclic 8-row strips, each rank traces its
 strips; the RNG pre-pass is sliced too (each rank counts 1/N of the random
 stream, one all-gather of ~1K block counts over RCCL), and the ARGB8 strips
-are gathered to rank 0 over RCCL (xGMI) and un-interleaved on device.  value = traces of the whole frame / step time
+are gathered to rank 0 over RCCL (xGMI) and un-interleaved on device.  The
+gather of frame i runs on its own communicator while frame i+1 renders
+(double-buffered strips; --no-pipeline serialises them).  value = traces of the whole frame / step time
 (max over ranks).
 
 Also reported: the trace kernel's algorithmic TFLOP/s against the FP32 VALU
@@ -127,6 +129,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (gloo: multi-rank rehearsal)")
     ap.add_argument("--one-device", action="store_true", help="all ranks on cuda:0 (rehearsal on a 1-GPU box)")
+    ap.add_argument("--no-pipeline", action="store_true", help="N > 1: gather each frame's strips before the next frame")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -167,7 +170,8 @@ def main():
         # sliced RNG pre-pass (count own slice -> all-gather block counts -> emit own strips), trace of
         # the own strips, ARGB8 strip gather to rank 0 + device un-interleave (reflaxman_amd/dist.py)
         from reflaxman_amd.dist import RfxStripOps, StripFrame
-        sf = StripFrame(RfxStripOps(rr, frame, stream.cuda_stream), W, H, rb, rank, world, dev)
+        sf = StripFrame(RfxStripOps(rr, frame, stream.cuda_stream), W, H, rb, rank, world, dev,
+                        pipeline=False if args.no_pipeline else None)
         rows, img, argb = sf.rows, sf.img, sf.argb
     else:
         rows = H
@@ -270,7 +274,8 @@ def main():
         "config": {"workload": f"C3 {args.scene}: 16 spheres + 4 textured triangles + sun, {W}x{H}, depth {depth}, 1 spp"
                                + (" (C4 family, weak-scaled 16:9 frame)" if world > 1 else ""),
                    "scene": args.scene, "width": W, "height": H, "depth": depth, "spp": 1,
-                   "parallelism": f"row-strips{rb}x{world}" if world > 1 else "single-gpu"},
+                   "parallelism": (f"row-strips{rb}x{world}" + ("+pipelined-gather" if sf.pipeline else ""))
+                                  if world > 1 else "single-gpu"},
         "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": metrics.PEAK_FP32_VALU_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved / metrics.PEAK_FP32_VALU_TFLOPS, 4),
                      "traffic": traffic, "kernel": "rfx::trace_kernel (plain pixel mode, wave-bundle culling)",

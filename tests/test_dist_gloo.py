@@ -22,6 +22,7 @@ class FakeOps:
     def __init__(self, W, H, rb, rank, world, bps=5):
         self.W, self.H, self.rb, self.rank, self.world, self.bps = W, H, rb, rank, world, bps
         self.seen_counts = None
+        self.frame = 0
 
     def blocks_per_slice(self, nslices):
         return self.bps
@@ -41,23 +42,27 @@ class FakeOps:
         argb = np.ctypeslib.as_array((ctypes.c_int32 * (rows * self.W)).from_address(d_argb)) if rows else None
         for i in range(rows):
             y = rdist.strip_row_to_y(i, self.rb, self.rank, self.world)
-            argb[i * self.W:(i + 1) * self.W] = (y << 12) | np.arange(self.W)
+            argb[i * self.W:(i + 1) * self.W] = (self.frame << 24) | (y << 12) | np.arange(self.W)
+        self.frame += 1
 
 
-def _worker(rank, world, port, W, H, rb, q):
+def _worker(rank, world, port, W, H, rb, pipeline, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         ops = FakeOps(W, H, rb, rank, world)
-        sf = rdist.StripFrame(ops, W, H, rb, rank, world, torch.device("cpu"))
-        out = sf.step()
+        sf = rdist.StripFrame(ops, W, H, rb, rank, world, torch.device("cpu"), pipeline=pipeline)
+        assert sf.pipeline == pipeline
         expect = [s * 1000 + b for s in range(world) for b in range(ops.bps)]
-        ok_counts = ops.seen_counts.tolist() == expect
-        if rank == 0:
-            ys, xs = torch.meshgrid(torch.arange(H), torch.arange(W), indexing="ij")
-            ok_frame = bool(torch.equal(out, ((ys << 12) | xs).to(torch.int32)))
-        else:
-            ok_frame = out is None
+        ok_counts = ok_frame = True
+        for frame in range(3):  # three frames: both buffer sets of the pipeline, one of them reused
+            out = sf.step()
+            ok_counts &= ops.seen_counts.tolist() == expect
+            if rank == 0:
+                ys, xs = torch.meshgrid(torch.arange(H), torch.arange(W), indexing="ij")
+                ok_frame &= bool(torch.equal(out, ((frame << 24) | (ys << 12) | xs).to(torch.int32)))
+            else:
+                ok_frame &= out is None
         q.put((rank, ok_counts, ok_frame))
     finally:
         dist.destroy_process_group()
@@ -71,12 +76,13 @@ def _free_port():
     return p
 
 
+@pytest.mark.parametrize("pipeline", [False, True])
 @pytest.mark.parametrize("W,H,rb", [(16, 37, 4), (8, 64, 8), (5, 3, 8)])
-def test_strip_frame_world2_gloo(W, H, rb):
+def test_strip_frame_world2_gloo(W, H, rb, pipeline):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, W, H, rb, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, W, H, rb, pipeline, q)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:
