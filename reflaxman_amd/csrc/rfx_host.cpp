@@ -595,6 +595,43 @@ extern "C" int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *s)
     if (!(t.cond < 1000.0)) r = INFINITY;
     bd.push_back({(float)cx, (float)cy, (float)cz, r});
   }
+  // small-scene lane table (rfx_types.h CullRec)
+  std::vector<CullRec> cs;
+  uint64_t cull_valid = 0;
+  const bool small = s->spheres.size() <= 32 && s->tris.size() <= 32;
+  if (small)
+  {
+    cs.assign(64, CullRec{0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f});
+    for (size_t i = 0; i < s->spheres.size(); ++i)
+    {
+      const int lane = (int)(i & 1u) * 16 + (int)(i >> 1);
+      const Bound &b = bd[i];
+      cs[lane] = CullRec{b.x, b.y, b.z, b.r, 0.0f, 0.0f, 0.0f, 0.0f};
+      cull_valid |= 1ull << lane;
+    }
+    for (size_t i = 0; i < s->tris.size(); ++i)
+    {
+      const HostTri &t = s->tris[i];
+      const Bound &b = bd[s->spheres.size() + i];
+      CullRec c{b.x, b.y, b.z, b.r, 0.0f, 0.0f, 0.0f, 0.0f};
+      if (t.cond < 1000.0)
+      {
+        // plane of the triangle in double: unit normal of (v1 - v0) x (v2 - v0), offset n . v0
+        const double ax = (double)t.v1.x - t.v0.x, ay = (double)t.v1.y - t.v0.y, az = (double)t.v1.z - t.v0.z;
+        const double bx = (double)t.v2.x - t.v0.x, by = (double)t.v2.y - t.v0.y, bz = (double)t.v2.z - t.v0.z;
+        double nx = ay * bz - az * by, ny = az * bx - ax * bz, nz = ax * by - ay * bx;
+        const double nl = sqrt(nx * nx + ny * ny + nz * nz);
+        if (nl > 0.0)
+        {
+          nx /= nl; ny /= nl; nz /= nl;
+          c.nx = (float)nx; c.ny = (float)ny; c.nz = (float)nz;
+          c.d = (float)(nx * t.v0.x + ny * t.v0.y + nz * t.v0.z);
+        }
+      }
+      cs[32 + i] = c;
+      cull_valid |= 1ull << (32 + i);
+    }
+  }
   std::vector<LightRec> lr;
   for (const HostLight &l : s->lights) lr.push_back({l.origin.x, l.origin.y, l.origin.z, l.radius, l.r, l.g, l.b, l.power});
   std::vector<TexRec> tr;
@@ -609,11 +646,12 @@ extern "C" int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *s)
       (rc = upload(r, si, &d.sph_info)) ||
       (rc = upload(r, tg, &d.tri_geo)) || (rc = upload(r, ts, &d.tri_shade)) || (rc = upload(r, tm, &d.tri_mat)) ||
       (rc = upload(r, lr, &d.lights)) || (rc = upload(r, tr, &d.texs)) || (rc = upload(r, pool, &d.texels)) ||
-      (rc = upload(r, bd, &d.bound)))
+      (rc = upload(r, bd, &d.bound)) || (rc = upload(r, cs, &d.cull_small)))
     return rc;
   d.n_sph = (int32_t)sg.size();
   d.n_tri = (int32_t)tg.size();
   d.n_light = (int32_t)lr.size();
+  d.cull_valid = cull_valid;
   d.skybox_tex = s->skybox;
   const col amb = cscale(s->diff, s->diff_power);                                    // Scene.cpp:186 (first factor)
   d.amb_r = amb.r; d.amb_g = amb.g; d.amb_b = amb.b;

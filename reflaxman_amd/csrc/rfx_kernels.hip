@@ -360,6 +360,29 @@ constexpr int kChunkLimit = 64;
 constexpr int kChunkLimit = 0x7fffffff;
 #endif
 
+// Small scenes: lane l tests cull record l (rfx_types.h CullRec) -- the cone test of cull_chunk, and
+// for a triangle also its plane: when every origin lies more than rw (plus a margin) on one side and
+// every direction leaves that side (axis . n beyond sin of the cone's half-angle, plus a margin), every
+// ray has t <= 0 for the plane.  The reference's float test then sees -ao.z and ar.z of opposite signs
+// too: for a basis with cond <= 1000 their rounding error stays below 2e-4 of |o - v0| and |ray|, inside
+// the 1e-3 margins.  Bits of lanes without an object are cleared.
+__device__ __forceinline__ uint64_t cull_small(const CullRec *tab, uint64_t valid, const Bundle &B)
+{
+  const CullRec g = tab[threadIdx.x & 63u];
+  const float vx = g.x - B.cx, vy = g.y - B.cy, vz = g.z - B.cz;
+  const float L2 = vx * vx + vy * vy + vz * vz;
+  const float L = __builtin_amdgcn_sqrtf(L2);
+  const float rp = g.r + B.rw + kCullRel * (L + B.rw);
+  const float va = vx * B.ax + vy * B.ay + vz * B.az;
+  const float lim = B.cosa * __builtin_amdgcn_sqrtf(fmaxf(L2 - rp * rp, 0.0f)) - B.sina * rp;
+  const float side = g.nx * B.cx + g.ny * B.cy + g.nz * B.cz - g.d;
+  const float an = g.nx * B.ax + g.ny * B.ay + g.nz * B.az;
+  const float ms = B.rw + 1e-3f * (L + g.r + B.rw) + 1e-6f, ma = B.sina + 1e-3f;
+  const bool away = (side > ms && an > ma) || (side < -ms && an < -ma);
+  const bool keep = !(L > rp && va < lim) && !away;
+  return __ballot(keep) & valid;
+}
+
 __device__ __forceinline__ uint64_t all_bits(int n) { return n >= 64 ? ~0ull : ((1ull << n) - 1ull); }
 
 // sphere bits (2q, 2q+1) -> pair bit q
@@ -485,7 +508,9 @@ __device__ __forceinline__ void closest_hit(const DevScene &S, v3 origin, v3 ray
 // One cull mask covers the whole scene (bit l: object l of the bound array, spheres then triangles), so
 // the object loops need no wave-wide step and run only in the lanes that trace -- a lane leaves the
 // any-hit loop at its first occluder.
-__device__ __forceinline__ uint64_t tri_bits(uint64_t om, int n_sph) { return n_sph >= 64 ? 0ull : om >> n_sph; }
+// lane-layout masks (CullRec): pair q <- lanes q and 16 + q; triangle i <- lane 32 + i
+__device__ __forceinline__ uint32_t small_pairs(uint64_t om) { return (uint32_t)((om | (om >> 16)) & 0xFFFFull); }
+__device__ __forceinline__ uint64_t small_tris(uint64_t om) { return om >> 32; }
 
 template <bool STATS>
 __device__ __forceinline__ void closest_hit_small(const DevScene &S, v3 origin, v3 ray, uint64_t om, Hit &h, Cnt &cnt)
@@ -496,7 +521,7 @@ __device__ __forceinline__ void closest_hit_small(const DevScene &S, v3 origin, 
   RFX_PROF_BEGIN(P_SPH);
   // spheres in index order carry increasing object indices, so among spheres a strict `<` already keeps
   // the first of equal distances
-  uint32_t pm = pair_bits(om & all_bits(S.n_sph));
+  uint32_t pm = small_pairs(om);
   while (pm)
   {
     const int j = __builtin_ctz(pm);
@@ -524,7 +549,7 @@ __device__ __forceinline__ void closest_hit_small(const DevScene &S, v3 origin, 
   }
   RFX_PROF_END(P_SPH);
   RFX_PROF_BEGIN(P_TRI);
-  uint64_t tm = tri_bits(om, S.n_sph);
+  uint64_t tm = small_tris(om);
   while (tm)
   {
     const int i = __builtin_ctzll(tm);
@@ -551,7 +576,7 @@ __device__ __forceinline__ bool occluded_small(const DevScene &S, v3 o, v3 ray, 
 {
   const RayConst k = ray_const(ray);
   float t, sq, u, v;
-  uint32_t pm = pair_bits(om & all_bits(S.n_sph));
+  uint32_t pm = small_pairs(om);
   while (pm)
   {
     const int j = __builtin_ctz(pm);
@@ -573,7 +598,7 @@ __device__ __forceinline__ bool occluded_small(const DevScene &S, v3 o, v3 ray, 
       if (sphere_tail<STATS, true>(b.y, d.y, ray, k, t, sq, cnt) && 2 * j + 1 != skip_sph) return true;
     }
   }
-  uint64_t tm = tri_bits(om, S.n_sph);
+  uint64_t tm = small_tris(om);
   while (tm)
   {
     const int i = __builtin_ctzll(tm);
@@ -685,12 +710,11 @@ __device__ __forceinline__ col trace(const DevScene &S, v3 origin, v3 ray, int d
     Hit h;
     if constexpr (SMALL)
     {
-      const int n_obj = S.n_sph + S.n_tri;
-      uint64_t om = all_bits(n_obj);
+      uint64_t om = S.cull_valid;
       if constexpr (CULL)
       {
         const Bundle B = make_bundle(origin, ray, alive);
-        if (B.ok) om = cull_chunk(S.bound, 0, n_obj, B);
+        if (B.ok) om = cull_small(S.cull_small, S.cull_valid, B);
       }
       if (alive) closest_hit_small<STATS>(S, origin, ray, om, h, cnt);
       else h.obj = -1;
@@ -752,12 +776,11 @@ __device__ __forceinline__ col trace(const DevScene &S, v3 origin, v3 ray, int d
         {
           if constexpr (SMALL)
           {
-            const int n_obj = S.n_sph + S.n_tri;
-            uint64_t om = all_bits(n_obj);
+            uint64_t om = S.cull_valid;
             if constexpr (CULL)
             {
               const Bundle SB = make_bundle(drop, sray, facing);
-              if (SB.ok) om = cull_chunk(S.bound, 0, n_obj, SB);
+              if (SB.ok) om = cull_small(S.cull_small, S.cull_valid, SB);
             }
             if (facing && !occluded_small<STATS>(S, drop, sray, skip_sph, skip_tri, om, cnt)) lit |= 1u << q;
           }
@@ -923,7 +946,7 @@ __device__ __forceinline__ v3 load_rd(const FrameParams &P, uint64_t i)
 // loop.  The plain variant drops the sample loops and their live state (no spills before the bounce loop).
 enum TraceMode { kModeSsaa = 0, kModeBlock = 1, kModePlain = 2 };
 // CFG bits: kCfgCull -- wave-bundle culling (every non-stats launch); kCfgManyLights -- more than 32 lights;
-// kCfgSmall -- at most 64 objects (one cull mask for the whole scene)
+// kCfgSmall -- at most 32 spheres and 32 triangles (one lane-layout cull mask for the whole scene)
 constexpr int kCfgCull = 1, kCfgManyLights = 2, kCfgSmall = 4;
 
 // one workgroup = 16x16 output pixels (block mode: block corners), one wave = an 8x8 tile (ray coherence).
@@ -1321,7 +1344,7 @@ hipError_t launch_trace(const DevScene &S, const FrameParams &P, bool stats, hip
   const int mode = P.ss < 0 ? kModeBlock : (P.ss == 1 && !P.additive && !P.accumulate) ? kModePlain : kModeSsaa;
   // the stats build counts the reference's every test, so it never culls
   int cfg = (S.n_light > 32 ? kCfgManyLights : 0) | (stats ? 0 : kCfgCull) |
-            (S.n_sph + S.n_tri <= 64 ? kCfgSmall : 0);
+            (S.n_sph <= 32 && S.n_tri <= 32 ? kCfgSmall : 0);
 #ifdef RFX_NO_CULL
   cfg &= ~kCfgCull;
 #endif

@@ -41,6 +41,11 @@ struct alignas(16) TriShade {                                        // Triangle
 // Bounding sphere of an object for the wave-bundle cull (rfx_kernels.hip): spheres first, then triangles.
 // r = +inf marks an object that is never culled (an ill-conditioned triangle, see rfx_host.cpp).
 struct alignas(16) Bound { float x, y, z, r; };
+// Small scenes (<= 32 spheres, <= 32 triangles): one cull record per lane of a wave.  Lanes 0-15 hold
+// spheres 0, 2, .., 30, lanes 16-31 spheres 1, 3, .., 31 (so a ballot folds into the pair mask with one
+// shift), lanes 32-63 triangles 0-31.  A triangle record also carries its plane (unit normal n, n . v0);
+// a sphere's or an empty lane's plane is zero.
+struct alignas(16) CullRec { float x, y, z, r, nx, ny, nz, d; };
 struct alignas(16) LightRec { float ox, oy, oz, radius, r, g, b, power; }; // OmniLight.h
 struct alignas(16) TexRec { uint32_t offset, w, h, pad; };
 
@@ -56,6 +61,8 @@ struct DevScene {
   const TexRec *texs;         // n_tex
   const uint32_t *texels;     // texel pool, ARGB
   const Bound *bound;         // n_sph + n_tri bounding spheres
+  const CullRec *cull_small;  // 64 lane records (small scenes only, else null)
+  uint64_t cull_valid;        // lanes of cull_small that hold an object
   int32_t n_sph, n_tri, n_light, skybox_tex;
   float amb_r, amb_g, amb_b;  // diffLightColor * diffLightPower (Scene.cpp:186, host-folded)
   float env_r, env_g, env_b;  // envColor (Scene.cpp:12,55)
