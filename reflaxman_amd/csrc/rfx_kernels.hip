@@ -86,6 +86,30 @@ __device__ __forceinline__ col from_argb_lut(uint32_t c, const float *lut)
 #endif
 }
 
+// glibc powf's tables (rfx_powf.h) copied to LDS by each workgroup: the lookups index them per lane,
+// and LDS answers such gathers in ~100 cycles where the constant/global path takes several hundred.
+__shared__ double s_powf_log[16][2];
+__shared__ uint64_t s_powf_exp[32];
+
+__device__ __forceinline__ void stage_powf_tables()
+{
+  const uint32_t t = threadIdx.x;
+  if (t < 32)
+  {
+    s_powf_exp[t] = kExp2fTab[t];
+    s_powf_log[t >> 1][t & 1u] = kPowfLog2Tab[t >> 1][t & 1u];
+  }
+}
+
+__device__ __forceinline__ float powf_dev(float x, float y)
+{
+#ifdef RFX_POW_GLOBAL
+  return powf_glibc(x, y);
+#else
+  return powf_glibc_t(x, y, s_powf_log, s_powf_exp);
+#endif
+}
+
 // ------------------------------------------------------------- sampling
 template <bool STATS>
 __device__ __forceinline__ col texel_uv(const DevScene &S, int tex, float u, float v, const float *lut, Cnt &cnt)
@@ -844,7 +868,7 @@ __device__ __forceinline__ col trace(const DevScene &S, v3 origin, v3 ray, int d
             if (sc > kVerySmall && L.radius > kVerySmall)
             {
               RFX_CNT(C_L_POW);
-              const float sp = powf_glibc(sc, 1 + 3 * m.refl * dlen / L.radius) * m.refl;
+              const float sp = powf_dev(sc, 1 + 3 * m.refl * dlen / L.radius) * m.refl;
               sumS = cadd(sumS, cscale(lc, sp));
             }
           }
@@ -864,7 +888,7 @@ __device__ __forceinline__ col trace(const DevScene &S, v3 origin, v3 ray, int d
         RFX_CNT(C_DIELECTRIC);
         const float aa = rayLen * normLen;
         const float cosA = (aa > kVerySmall) ? clampf(dot(ray, neg(norm)) / aa, 0.0f, 1.0f) : 0.0f;
-        const float r = 0.2f + 0.8f * powf_glibc(1.0f - cosA, 3.0f);
+        const float r = 0.2f + 0.8f * powf_dev(1.0f - cosA, 3.0f);
         fin = cadd(cmul(cscale(color, 1.0f - r), sumL), sumS);
         fin = cmul(fin, mulc);
         mulc = cscale(mulc, r);
@@ -958,6 +982,7 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
   constexpr bool CULL = (CFG & kCfgCull) != 0, MANYL = (CFG & kCfgManyLights) != 0, SMALL = (CFG & kCfgSmall) != 0;
   __shared__ float lut[256];
   lut[threadIdx.x] = (float)threadIdx.x / 255.0f;                               // Color.cpp:11-13
+  stage_powf_tables();
   RFX_PROF_INIT();
   __syncthreads();
   Cnt cnt;

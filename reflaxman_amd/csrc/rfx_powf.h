@@ -80,7 +80,8 @@ RFX_PHD int pw_checkint(uint32_t iy)
 }
 RFX_PHD int pw_zeroinfnan(uint32_t ix) { return 2 * ix - 1 >= 2u * 0x7f800000 - 1; }
 
-RFX_PHD float powf_glibc(float x, float y)
+// logtab / exptab: kPowfLog2Tab / kExp2fTab or copies of them (the trace kernel keeps copies in LDS)
+RFX_PHD float powf_glibc_t(float x, float y, const double (*logtab)[2], const uint64_t *exptab)
 {
   uint32_t sign_bias = 0;
   uint32_t ix = pw_asuint(x), iy = pw_asuint(y);
@@ -121,7 +122,7 @@ RFX_PHD float powf_glibc(float x, float y)
   const uint32_t top = tmp & 0xff800000u;
   const uint32_t iz = ix - top;
   const int k = (int32_t)top >> 23;
-  const double invc = kPowfLog2Tab[i][0], logc = kPowfLog2Tab[i][1];
+  const double invc = logtab[i][0], logc = logtab[i][1];
   const double z = (double)pw_asfloat(iz);
   const double r = pw_fma(z, invc, -1.0);
   const double y0 = logc + (double)k;
@@ -148,7 +149,7 @@ RFX_PHD float powf_glibc(float x, float y)
   const uint64_t ki = pw_asuint64(kd);
   kd -= shift;
   const double rr = ylogx - kd;
-  uint64_t t = kExp2fTab[ki % 32];
+  uint64_t t = exptab[ki % 32];
   t += (ki + sign_bias) << 47;
   const double s = pw_asdouble(t);
   const double zz = pw_fma(rr, 0x1.c6af84b912394p-5, 0x1.ebfce50fac4f3p-3);
@@ -158,5 +159,7 @@ RFX_PHD float powf_glibc(float x, float y)
   e = e * s;
   return (float)e;
 }
+
+RFX_PHD float powf_glibc(float x, float y) { return powf_glibc_t(x, y, kPowfLog2Tab, kExp2fTab); }
 
 }  // namespace rfx
