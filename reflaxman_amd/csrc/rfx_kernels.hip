@@ -110,6 +110,58 @@ __device__ __forceinline__ float powf_dev(float x, float y)
 #endif
 }
 
+// Small scenes (<= 32 spheres, <= 32 triangles): the per-object records the hit lanes gather by their
+// own object index (winner geometry and material, the cull lane table) staged in LDS per workgroup.
+__shared__ SphereGeo s_sph_geo[32];
+__shared__ MatRec s_sph_mat[32];
+__shared__ int32_t s_sph_info[64];
+__shared__ TriShade s_tri_shade[32];
+__shared__ MatRec s_tri_mat[32];
+__shared__ CullRec s_cull[64];
+
+template <bool SMALL>
+struct Tabs {
+  const DevScene &S;
+  __device__ __forceinline__ SphereGeo sph_geo(int i) const { return S.sph_geo[i]; }
+  __device__ __forceinline__ MatRec sph_mat(int i) const { return S.sph_mat[i]; }
+  __device__ __forceinline__ int32_t sph_info(int k) const { return S.sph_info[k]; }
+  __device__ __forceinline__ TriShade tri_shade(int i) const { return S.tri_shade[i]; }
+  __device__ __forceinline__ MatRec tri_mat(int i) const { return S.tri_mat[i]; }
+  __device__ __forceinline__ const CullRec *cull() const { return S.cull_small; }
+};
+#ifndef RFX_NO_LDS_SMALL
+template <>
+struct Tabs<true> {
+  const DevScene &S;
+  __device__ __forceinline__ SphereGeo sph_geo(int i) const { return s_sph_geo[i]; }
+  __device__ __forceinline__ MatRec sph_mat(int i) const { return s_sph_mat[i]; }
+  __device__ __forceinline__ int32_t sph_info(int k) const { return s_sph_info[k]; }
+  __device__ __forceinline__ TriShade tri_shade(int i) const { return s_tri_shade[i]; }
+  __device__ __forceinline__ MatRec tri_mat(int i) const { return s_tri_mat[i]; }
+  __device__ __forceinline__ const CullRec *cull() const { return s_cull; }
+};
+#endif
+
+__device__ __forceinline__ void stage_small_scene(const DevScene &S)
+{
+#ifndef RFX_NO_LDS_SMALL
+  const int t = (int)threadIdx.x;
+  if (t < S.n_sph)
+  {
+    s_sph_geo[t] = S.sph_geo[t];
+    s_sph_mat[t] = S.sph_mat[t];
+    s_sph_info[2 * t] = S.sph_info[2 * t];
+    s_sph_info[2 * t + 1] = S.sph_info[2 * t + 1];
+  }
+  if (t < S.n_tri)
+  {
+    s_tri_shade[t] = S.tri_shade[t];
+    s_tri_mat[t] = S.tri_mat[t];
+  }
+  if (t < 64) s_cull[t] = S.cull_small[t];
+#endif
+}
+
 // ------------------------------------------------------------- sampling
 template <bool STATS>
 __device__ __forceinline__ col texel_uv(const DevScene &S, int tex, float u, float v, const float *lut, Cnt &cnt)
@@ -569,7 +621,7 @@ __device__ __forceinline__ void closest_hit_small(const DevScene &S, v3 origin, 
   if (h.obj >= 0)
   {
     h.i = h.obj;
-    h.obj = S.sph_info[2 * h.i];
+    h.obj = Tabs<true>{S}.sph_info(2 * h.i);
   }
   RFX_PROF_END(P_SPH);
   RFX_PROF_BEGIN(P_TRI);
@@ -719,6 +771,7 @@ __device__ __forceinline__ col trace(const DevScene &S, v3 origin, v3 ray, int d
                                      Cnt &cnt, bool valid)
 {
   if (valid) RFX_CNT(C_RAYS);
+  const Tabs<SMALL> T{S};
   col mulc = mkc(1.0f, 1.0f, 1.0f), pix = mkc(0.0f, 0.0f, 0.0f);
   int refl = 0;
   bool alive = valid && depth > 0;
@@ -738,7 +791,7 @@ __device__ __forceinline__ col trace(const DevScene &S, v3 origin, v3 ray, int d
       if constexpr (CULL)
       {
         const Bundle B = make_bundle(origin, ray, alive);
-        if (B.ok) om = cull_small(S.cull_small, S.cull_valid, B);
+        if (B.ok) om = cull_small(T.cull(), S.cull_valid, B);
       }
       if (alive) closest_hit_small<STATS>(S, origin, ray, om, h, cnt);
       else h.obj = -1;
@@ -759,13 +812,14 @@ __device__ __forceinline__ col trace(const DevScene &S, v3 origin, v3 ray, int d
       if (h.kind == 0)
       {
         RFX_CNT(C_HIT_SPH);
-        const SphereGeo g = S.sph_geo[h.i];
+        const SphereGeo g = T.sph_geo(h.i);
         norm = sub(drop, mk(g.cx, g.cy, g.cz));                                // Sphere.cpp:67
       }
       else
       {
         RFX_CNT(C_HIT_TRI);
-        norm = mk(S.tri_shade[h.i].nx, S.tri_shade[h.i].ny, S.tri_shade[h.i].nz);
+        const TriShade sh = T.tri_shade(h.i);
+        norm = mk(sh.nx, sh.ny, sh.nz);
       }
     }
     RFX_PROF_END(P_WIN);
@@ -804,7 +858,7 @@ __device__ __forceinline__ col trace(const DevScene &S, v3 origin, v3 ray, int d
             if constexpr (CULL)
             {
               const Bundle SB = make_bundle(drop, sray, facing);
-              if (SB.ok) om = cull_small(S.cull_small, S.cull_valid, SB);
+              if (SB.ok) om = cull_small(T.cull(), S.cull_valid, SB);
             }
             if (facing && !occluded_small<STATS>(S, drop, sray, skip_sph, skip_tri, om, cnt)) lit |= 1u << q;
           }
@@ -826,13 +880,13 @@ __device__ __forceinline__ col trace(const DevScene &S, v3 origin, v3 ray, int d
           // the hit object's material, texel, reflection and lengths (Sphere.cpp:66-80, Triangle.cpp:86-105)
           if (h.kind == 0)
           {
-            m = S.sph_mat[h.i];
-            diel = S.sph_info[2 * h.i + 1];
+            m = T.sph_mat(h.i);
+            diel = T.sph_info(2 * h.i + 1);
           }
           else
           {
-            const TriShade sh = S.tri_shade[h.i];
-            m = S.tri_mat[h.i];
+            const TriShade sh = T.tri_shade(h.i);
+            m = T.tri_mat(h.i);
             diel = sh.dielectric;
             if (sh.tex >= 0)                                                   // Triangle.cpp:89-96
             {
@@ -983,6 +1037,7 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
   __shared__ float lut[256];
   lut[threadIdx.x] = (float)threadIdx.x / 255.0f;                               // Color.cpp:11-13
   stage_powf_tables();
+  if constexpr (SMALL) stage_small_scene(S);
   RFX_PROF_INIT();
   __syncthreads();
   Cnt cnt;
