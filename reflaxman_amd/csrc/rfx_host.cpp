@@ -601,19 +601,22 @@ extern "C" int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *s)
   const bool small = s->spheres.size() <= 32 && s->tris.size() <= 32;
   if (small)
   {
-    cs.assign(64, CullRec{0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f});
+    cs.assign(64, CullRec{});
     for (size_t i = 0; i < s->spheres.size(); ++i)
     {
       const int lane = (int)(i & 1u) * 16 + (int)(i >> 1);
       const Bound &b = bd[i];
-      cs[lane] = CullRec{b.x, b.y, b.z, b.r, 0.0f, 0.0f, 0.0f, 0.0f};
+      CullRec c{};
+      c.x = b.x; c.y = b.y; c.z = b.z; c.r = b.r;
+      cs[lane] = c;
       cull_valid |= 1ull << lane;
     }
     for (size_t i = 0; i < s->tris.size(); ++i)
     {
       const HostTri &t = s->tris[i];
       const Bound &b = bd[s->spheres.size() + i];
-      CullRec c{b.x, b.y, b.z, b.r, 0.0f, 0.0f, 0.0f, 0.0f};
+      CullRec c{};
+      c.x = b.x; c.y = b.y; c.z = b.z; c.r = b.r;
       if (t.cond < 1000.0)
       {
         // plane of the triangle in double: unit normal of (v1 - v0) x (v2 - v0), offset n . v0

@@ -50,6 +50,22 @@ __shared__ unsigned long long s_prof[2 * P_COUNT];  // per workgroup, flushed to
       atomicAdd(&s_prof[P_COUNT + k], 1ull);                                              \
     }                                                                                     \
   } while (0)
+// cull statistics (diagnostic build): per bundle kind (0 closest hit, 1 shadow): bundles, usable bundles,
+// live lanes, kept sphere pairs, kept triangles, valid pairs, valid triangles
+__device__ unsigned long long g_cull[16];
+#define RFX_CULL_STAT(kind, ok, live_mask, om, valid)                                                 \
+  do {                                                                                              \
+    if ((threadIdx.x & 63u) == 0u)                                                                  \
+    {                                                                                               \
+      atomicAdd(&g_cull[8 * (kind) + 0], 1ull);                                                     \
+      atomicAdd(&g_cull[8 * (kind) + 1], (ok) ? 1ull : 0ull);                                       \
+      atomicAdd(&g_cull[8 * (kind) + 2], (unsigned long long)__popcll(live_mask));                 \
+      atomicAdd(&g_cull[8 * (kind) + 3], (unsigned long long)__popc(small_pairs(om)));             \
+      atomicAdd(&g_cull[8 * (kind) + 4], (unsigned long long)__popcll(small_tris(om)));            \
+      atomicAdd(&g_cull[8 * (kind) + 5], (unsigned long long)__popc(small_pairs(valid)));          \
+      atomicAdd(&g_cull[8 * (kind) + 6], (unsigned long long)__popcll(small_tris(valid)));         \
+    }                                                                                               \
+  } while (0)
 #define RFX_PROF_INIT()                                          \
   do {                                                           \
     if (threadIdx.x < 2 * P_COUNT) s_prof[threadIdx.x] = 0ull;   \
@@ -71,6 +87,9 @@ __shared__ unsigned long long s_prof[2 * P_COUNT];  // per workgroup, flushed to
   } while (0)
 #define RFX_PROF_END(k) \
   do {                  \
+  } while (0)
+#define RFX_CULL_STAT(kind, ok, live_mask, om, valid) \
+  do {                                                \
   } while (0)
 #endif
 
@@ -792,6 +811,7 @@ __device__ __forceinline__ col trace(const DevScene &S, v3 origin, v3 ray, int d
       {
         const Bundle B = make_bundle(origin, ray, alive);
         if (B.ok) om = cull_small(T.cull(), S.cull_valid, B);
+        RFX_CULL_STAT(0, B.ok, __ballot(alive), om, S.cull_valid);
       }
       if (alive) closest_hit_small<STATS>(S, origin, ray, om, h, cnt);
       else h.obj = -1;
@@ -859,6 +879,7 @@ __device__ __forceinline__ col trace(const DevScene &S, v3 origin, v3 ray, int d
             {
               const Bundle SB = make_bundle(drop, sray, facing);
               if (SB.ok) om = cull_small(T.cull(), S.cull_valid, SB);
+              RFX_CULL_STAT(1, SB.ok, __ballot(facing), om, S.cull_valid);
             }
             if (facing && !occluded_small<STATS>(S, drop, sray, skip_sph, skip_tri, om, cnt)) lit |= 1u << q;
           }
@@ -1312,6 +1333,17 @@ __global__ __launch_bounds__(kRngBlock) void rng_emit(const uint32_t *seed, cons
 }  // namespace rfx
 
 #ifdef RFX_DEBUG_PROF
+extern "C" int rfx_debug_cull_read(unsigned long long *out, int reset)
+{
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rfx::g_cull), sizeof(rfx::g_cull)) != hipSuccess) return -1;
+  if (reset)
+  {
+    static const unsigned long long zero[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(rfx::g_cull), zero, sizeof(zero)) != hipSuccess) return -1;
+  }
+  return 16;
+}
+
 extern "C" int rfx_debug_prof_read(unsigned long long *out, int reset)
 {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rfx::g_prof), sizeof(rfx::g_prof)) != hipSuccess) return -1;

@@ -31,9 +31,19 @@ def main():
     assert r.L.rfx_synchronize(r.r) == 0
     assert r.L.rfx_debug_prof_read(buf, 1) == 16
     tot = buf[7]
+    cb = (C.c_ulonglong * 16)()
+    cull = {}
+    if hasattr(r.L, "rfx_debug_cull_read") and r.L.rfx_debug_cull_read(cb, 1) == 16:
+        for k, name in ((0, "closest"), (1, "shadow")):
+            v = cb[8 * k: 8 * k + 7]
+            n = max(v[0], 1)
+            cull[name] = {"bundles": v[0], "usable": round(v[1] / n, 3), "live_lanes": round(v[2] / n, 1),
+                          "kept_pairs": round(v[3] / n, 2), "valid_pairs": round(v[5] / n, 2),
+                          "kept_tris": round(v[4] / n, 2), "valid_tris": round(v[6] / n, 2)}
     print(json.dumps({"scene": scene, "lib": os.path.basename(path), "cycles": {k: int(v) for k, v in zip(REGIONS, buf[:8])},
                       "wave_executions": {k: int(v) for k, v in zip(REGIONS, buf[8:])},
-                      "share_of_trace": {k: round(v / tot, 4) for k, v in zip(REGIONS, buf[:8])}}))
+                      "share_of_trace": {k: round(v / tot, 4) for k, v in zip(REGIONS, buf[:8])},
+                      "cull": cull}))
 
 
 if __name__ == "__main__":
