@@ -12,6 +12,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
+#include <cmath>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -541,8 +543,48 @@ extern "C" int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *s)
   std::vector<SphereGeo> sg;
   std::vector<MatRec> sm, tm;
   std::vector<int32_t> si;
-  for (const HostSphere &sp : s->spheres)
+  // Large scenes (more than 32 spheres): spheres in spatial order -- 30-bit Morton code of the centre in
+  // the centres' bounding box, ties by insertion index -- so each 64-sphere chunk of the device arrays is
+  // compact and its bounding sphere can cull it as a whole.  Every record keeps its object index (sph_info),
+  // and the large-scene kernel path compares (distance, object index), so the order changes no result.
+  const size_t nsph = s->spheres.size();
+  std::vector<uint32_t> order(nsph);
+  for (size_t i = 0; i < nsph; ++i) order[i] = (uint32_t)i;
+  if (nsph > 32)
   {
+    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (const HostSphere &sp : s->spheres)
+    {
+      const double c[3] = {sp.center.x, sp.center.y, sp.center.z};
+      for (int a = 0; a < 3; ++a) { lo[a] = fmin(lo[a], c[a]); hi[a] = fmax(hi[a], c[a]); }
+    }
+    auto spread = [](uint32_t v) {  // 10 bits -> every third bit
+      v &= 0x3FFu;
+      v = (v | (v << 16)) & 0x030000FFu;
+      v = (v | (v << 8)) & 0x0300F00Fu;
+      v = (v | (v << 4)) & 0x030C30C3u;
+      v = (v | (v << 2)) & 0x09249249u;
+      return v;
+    };
+    std::vector<uint32_t> code(nsph);
+    for (size_t i = 0; i < nsph; ++i)
+    {
+      const HostSphere &sp = s->spheres[i];
+      const double c[3] = {sp.center.x, sp.center.y, sp.center.z};
+      uint32_t q[3];
+      for (int a = 0; a < 3; ++a)
+      {
+        const double ext = hi[a] - lo[a];
+        const double f = ext > 0.0 && std::isfinite(ext) ? (c[a] - lo[a]) / ext : 0.0;
+        q[a] = (uint32_t)fmin(fmax(f * 1023.0, 0.0), 1023.0);
+      }
+      code[i] = spread(q[0]) | spread(q[1]) << 1 | spread(q[2]) << 2;
+    }
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return code[a] < code[b]; });
+  }
+  for (uint32_t oi : order)
+  {
+    const HostSphere &sp = s->spheres[oi];
     sg.push_back({sp.center.x, sp.center.y, sp.center.z, sp.sq_radius});
     sm.push_back({sp.mat.r, sp.mat.g, sp.mat.b, sp.mat.refl});
     si.push_back(sp.obj);
@@ -582,8 +624,27 @@ extern "C" int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *s)
   // falls back to the identity for a singular basis, Matrix33.cpp:58-79) may report hits far from its
   // vertices, so it gets r = +inf and is never culled
   std::vector<Bound> bd;
-  for (const HostSphere &sp : s->spheres)
+  for (uint32_t oi : order)
+  {
+    const HostSphere &sp = s->spheres[oi];
     bd.push_back({sp.center.x, sp.center.y, sp.center.z, sp.radius * 1.00001f});
+  }
+  // chunk bounds: 64 consecutive spheres of the device order, centred on their mean centre
+  std::vector<Bound> cb;
+  for (size_t first = 0; first < nsph; first += 64)
+  {
+    const size_t last = std::min(nsph, first + 64);
+    double m[3] = {0.0, 0.0, 0.0};
+    for (size_t i = first; i < last; ++i) { m[0] += bd[i].x; m[1] += bd[i].y; m[2] += bd[i].z; }
+    for (double &v : m) v /= (double)(last - first);
+    double r = 0.0;
+    for (size_t i = first; i < last; ++i)
+    {
+      const double dx = bd[i].x - m[0], dy = bd[i].y - m[1], dz = bd[i].z - m[2];
+      r = fmax(r, sqrt(dx * dx + dy * dy + dz * dz) + (double)bd[i].r);
+    }
+    cb.push_back({(float)m[0], (float)m[1], (float)m[2], (float)(r * 1.0001 + 1e-6)});
+  }
   for (const HostTri &t : s->tris)
   {
     const double cx = ((double)t.v0.x + t.v1.x + t.v2.x) / 3.0, cy = ((double)t.v0.y + t.v1.y + t.v2.y) / 3.0,
@@ -649,11 +710,12 @@ extern "C" int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *s)
       (rc = upload(r, si, &d.sph_info)) ||
       (rc = upload(r, tg, &d.tri_geo)) || (rc = upload(r, ts, &d.tri_shade)) || (rc = upload(r, tm, &d.tri_mat)) ||
       (rc = upload(r, lr, &d.lights)) || (rc = upload(r, tr, &d.texs)) || (rc = upload(r, pool, &d.texels)) ||
-      (rc = upload(r, bd, &d.bound)) || (rc = upload(r, cs, &d.cull_small)))
+      (rc = upload(r, bd, &d.bound)) || (rc = upload(r, cs, &d.cull_small)) || (rc = upload(r, cb, &d.chunk_bound)))
     return rc;
   d.n_sph = (int32_t)sg.size();
   d.n_tri = (int32_t)tg.size();
   d.n_light = (int32_t)lr.size();
+  d.n_chunk = (int32_t)cb.size();
   d.cull_valid = cull_valid;
   d.skybox_tex = s->skybox;
   const col amb = cscale(s->diff, s->diff_power);                                    // Scene.cpp:186 (first factor)

@@ -530,6 +530,9 @@ __device__ __forceinline__ bool tri_takes(float sq, float best_sq, int obj, int 
 #endif
 
 // Call with every lane of the wave active; `live` lanes trace (origin, ray).  B: the bundle, or null.
+// Large scenes: the spheres are stored in spatial (Morton) order, 64 to a chunk with a bounding sphere;
+// the bundle culls whole chunks (one lane per chunk), then the spheres of the surviving chunks.  The
+// visiting order is then not the insertion order, so spheres take the general (distance, object) rule.
 template <bool STATS>
 __device__ __forceinline__ void closest_hit(const DevScene &S, v3 origin, v3 ray, bool live, const Bundle *B, Hit &h,
                                             Cnt &cnt)
@@ -537,40 +540,43 @@ __device__ __forceinline__ void closest_hit(const DevScene &S, v3 origin, v3 ray
   if (live) RFX_CNT(C_SEGMENTS);
   h.obj = -1; h.kind = 0; h.i = 0; h.t = 0.0f; h.u = 0.0f; h.v = 0.0f; h.sq = kNoHitKey;
   const RayConst k = ray_const(ray);
+  const bool cull = B && B->ok;
   RFX_PROF_BEGIN(P_SPH);
-  // spheres in index order carry increasing object indices, so among spheres `strictly_closer` already
-  // keeps the first of equal distances
-  for (int first = 0; first < S.n_sph && first < kChunkLimit; first += 64)
+  for (int cfirst = 0; cfirst < S.n_chunk; cfirst += 64)
   {
-    const int n = min(64, S.n_sph - first);
-    const uint64_t m = (B && B->ok) ? cull_chunk(S.bound, first, n, *B) : all_bits(n);
-    uint32_t pm = pair_bits(m);
-    while (pm)
+    uint64_t cm = cull ? cull_chunk(S.chunk_bound, cfirst, min(64, S.n_chunk - cfirst), *B)
+                       : all_bits(min(64, S.n_chunk - cfirst));
+    while (cm)
     {
-      const int j = (first >> 1) + __builtin_ctz(pm);
-      pm &= pm - 1u;
-      f2 b, d;
-      pair_bd(S.sph_pair[j], origin, k, b, d);
-      if (!live) continue;
-      if constexpr (!STATS)
-        if (!pair_may_hit(b, d)) continue;  // both miss: one branch
-      float t, sq;
-      if (sphere_tail<STATS, false>(b.x, d.x, ray, k, t, sq, cnt))
+      const int first = 64 * (cfirst + __builtin_ctzll(cm));
+      cm &= cm - 1ull;
+      const int n = min(64, S.n_sph - first);
+      const uint64_t m = cull ? cull_chunk(S.bound, first, n, *B) : all_bits(n);
+      uint32_t pm = pair_bits(m);
+      while (pm)
       {
-        const float key = hit_key(sq);
-        if (sph_takes(key, h.sq)) { h.sq = key; h.obj = 2 * j; h.t = t; }
-      }
-      if ((!STATS || 2 * j + 1 < S.n_sph) && sphere_tail<STATS, false>(b.y, d.y, ray, k, t, sq, cnt))
-      {
-        const float key = hit_key(sq);
-        if (sph_takes(key, h.sq)) { h.sq = key; h.obj = 2 * j + 1; h.t = t; }
+        const int j = (first >> 1) + __builtin_ctz(pm);
+        pm &= pm - 1u;
+        f2 b, d;
+        pair_bd(S.sph_pair[j], origin, k, b, d);
+        if (!live) continue;
+        if constexpr (!STATS)
+          if (!pair_may_hit(b, d)) continue;  // both miss: one branch
+        float t, sq;
+        if (sphere_tail<STATS, false>(b.x, d.x, ray, k, t, sq, cnt))
+        {
+          const float key = hit_key(sq);
+          const int obj = S.sph_info[4 * j];
+          if (tri_takes(key, h.sq, obj, h.obj)) { h.sq = key; h.obj = obj; h.i = 2 * j; h.t = t; }
+        }
+        if ((!STATS || 2 * j + 1 < S.n_sph) && sphere_tail<STATS, false>(b.y, d.y, ray, k, t, sq, cnt))
+        {
+          const float key = hit_key(sq);
+          const int obj = S.sph_info[4 * j + 2];
+          if (tri_takes(key, h.sq, obj, h.obj)) { h.sq = key; h.obj = obj; h.i = 2 * j + 1; h.t = t; }
+        }
       }
     }
-  }
-  if (h.obj >= 0)
-  {
-    h.i = h.obj;
-    h.obj = S.sph_info[2 * h.i];
   }
   RFX_PROF_END(P_SPH);
   RFX_PROF_BEGIN(P_TRI);
@@ -720,37 +726,45 @@ __device__ __forceinline__ bool occluded(const DevScene &S, v3 o, v3 ray, bool l
                                          const Bundle *B, Cnt &cnt)
 {
   const RayConst k = ray_const(ray);
+  const bool cull = B && B->ok;
   bool occ = false;
   float t, sq, u, v;
-  for (int first = 0; first < S.n_sph && first < kChunkLimit; first += 64)
+  for (int cfirst = 0; cfirst < S.n_chunk; cfirst += 64)
   {
     if (__ballot(live && !occ) == 0) return occ;
-    const int n = min(64, S.n_sph - first);
-    const uint64_t m = (B && B->ok) ? cull_chunk(S.bound, first, n, *B) : all_bits(n);
-    uint32_t pm = pair_bits(m);
-    while (pm)
+    uint64_t cm = cull ? cull_chunk(S.chunk_bound, cfirst, min(64, S.n_chunk - cfirst), *B)
+                       : all_bits(min(64, S.n_chunk - cfirst));
+    while (cm)
     {
-      const int j = (first >> 1) + __builtin_ctz(pm);
-      pm &= pm - 1u;
-      f2 b, d;
-      pair_bd(S.sph_pair[j], o, k, b, d);
-      if (live && !occ)
+      const int first = 64 * (cfirst + __builtin_ctzll(cm));
+      cm &= cm - 1ull;
+      const int n = min(64, S.n_sph - first);
+      const uint64_t m = cull ? cull_chunk(S.bound, first, n, *B) : all_bits(n);
+      uint32_t pm = pair_bits(m);
+      while (pm)
       {
-        if constexpr (STATS)
+        const int j = (first >> 1) + __builtin_ctz(pm);
+        pm &= pm - 1u;
+        f2 b, d;
+        pair_bd(S.sph_pair[j], o, k, b, d);
+        if (live && !occ)
         {
-          if (2 * j != skip_sph && sphere_tail<STATS, true>(b.x, d.x, ray, k, t, sq, cnt)) occ = true;
-          else if (2 * j + 1 != skip_sph && 2 * j + 1 < S.n_sph &&
-                   sphere_tail<STATS, true>(b.y, d.y, ray, k, t, sq, cnt))
-            occ = true;
+          if constexpr (STATS)
+          {
+            if (2 * j != skip_sph && sphere_tail<STATS, true>(b.x, d.x, ray, k, t, sq, cnt)) occ = true;
+            else if (2 * j + 1 != skip_sph && 2 * j + 1 < S.n_sph &&
+                     sphere_tail<STATS, true>(b.y, d.y, ray, k, t, sq, cnt))
+              occ = true;
+          }
+          else if (pair_may_hit(b, d))
+          {
+            // the hit object is filtered out after its test, which does not change the boolean
+            if (sphere_tail<STATS, true>(b.x, d.x, ray, k, t, sq, cnt) && 2 * j != skip_sph) occ = true;
+            else if (sphere_tail<STATS, true>(b.y, d.y, ray, k, t, sq, cnt) && 2 * j + 1 != skip_sph) occ = true;
+          }
         }
-        else if (pair_may_hit(b, d))
-        {
-          // the hit object is filtered out after its test, which does not change the boolean
-          if (sphere_tail<STATS, true>(b.x, d.x, ray, k, t, sq, cnt) && 2 * j != skip_sph) occ = true;
-          else if (sphere_tail<STATS, true>(b.y, d.y, ray, k, t, sq, cnt) && 2 * j + 1 != skip_sph) occ = true;
-        }
+        if (__ballot(live && !occ) == 0) return occ;
       }
-      if (__ballot(live && !occ) == 0) return occ;
     }
   }
   for (int first = 0; first < S.n_tri && first < kChunkLimit; first += 64)
@@ -809,9 +823,11 @@ __device__ __forceinline__ col trace(const DevScene &S, v3 origin, v3 ray, int d
       uint64_t om = S.cull_valid;
       if constexpr (CULL)
       {
+#ifndef RFX_NO_CLOSEST_CULL
         const Bundle B = make_bundle(origin, ray, alive);
         if (B.ok) om = cull_small(T.cull(), S.cull_valid, B);
         RFX_CULL_STAT(0, B.ok, __ballot(alive), om, S.cull_valid);
+#endif
       }
       if (alive) closest_hit_small<STATS>(S, origin, ray, om, h, cnt);
       else h.obj = -1;
@@ -877,9 +893,11 @@ __device__ __forceinline__ col trace(const DevScene &S, v3 origin, v3 ray, int d
             uint64_t om = S.cull_valid;
             if constexpr (CULL)
             {
+#ifndef RFX_NO_SHADOW_CULL
               const Bundle SB = make_bundle(drop, sray, facing);
               if (SB.ok) om = cull_small(T.cull(), S.cull_valid, SB);
               RFX_CULL_STAT(1, SB.ok, __ballot(facing), om, S.cull_valid);
+#endif
             }
             if (facing && !occluded_small<STATS>(S, drop, sray, skip_sph, skip_tri, om, cnt)) lit |= 1u << q;
           }

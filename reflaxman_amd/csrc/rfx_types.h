@@ -61,9 +61,11 @@ struct DevScene {
   const TexRec *texs;         // n_tex
   const uint32_t *texels;     // texel pool, ARGB
   const Bound *bound;         // n_sph + n_tri bounding spheres
+  const Bound *chunk_bound;   // n_chunk bounding spheres of 64-sphere chunks (large scenes: Morton order)
   const CullRec *cull_small;  // 64 lane records (small scenes only, else null)
   uint64_t cull_valid;        // lanes of cull_small that hold an object
   int32_t n_sph, n_tri, n_light, skybox_tex;
+  int32_t n_chunk;            // (n_sph + 63) / 64
   float amb_r, amb_g, amb_b;  // diffLightColor * diffLightPower (Scene.cpp:186, host-folded)
   float env_r, env_g, env_b;  // envColor (Scene.cpp:12,55)
   float half_tile_w, half_tile_h;  // Skybox.cpp:21-37
