@@ -30,7 +30,7 @@ void rng_jump_table(uint64_t nblk, uint32_t *out);
 hipError_t launch_rng_count(const uint32_t *d_seed, const uint32_t *d_jump, uint32_t *d_blk_cnt, uint64_t blk0,
                             uint64_t nblk_slice, hipStream_t st);
 hipError_t launch_rng_finish(const uint32_t *d_seed, const uint32_t *d_jump, uint32_t *d_next_seed,
-                             const uint32_t *d_blk_cnt, uint64_t nblk, uint64_t traces, float *d_rd, uint64_t n_rd,
+                             const uint32_t *d_blk_cnt, uint64_t nblk, uint64_t traces, uint32_t *d_rd_state,
                              uint64_t *d_blk_off, int *d_err, uint64_t ss2, uint64_t W, uint32_t row_block,
                              uint32_t rank, uint32_t nranks, hipStream_t st);
 hipError_t launch_trace(const DevScene &S, const FrameParams &P, bool stats, hipStream_t st);
@@ -403,7 +403,7 @@ struct rfx_renderer {
   int *d_err = nullptr;
   uint32_t jitter_seed = 0;
   // workspaces
-  float *d_rd = nullptr; uint64_t rd_cap = 0;
+  uint32_t *d_rd = nullptr; uint64_t rd_cap = 0;  // per-trace LCG states (rng_emit)
   uint32_t *d_blk_cnt = nullptr; uint64_t *d_blk_off = nullptr; uint64_t blk_cap = 0;
   uint32_t *d_jump = nullptr;  // LCG jump table for blk_cap blocks (rng_jump_table)
   // host staging for rfx_render_frame_host
@@ -771,7 +771,7 @@ static int ensure_rng_workspace(rfx_renderer *r, uint64_t traces, uint64_t nblk)
     (void)hipFree(r->d_rd);
     r->d_rd = nullptr;
     r->rd_cap = 0;
-    HIP_CHECK(hipMalloc(&r->d_rd, traces * 3 * sizeof(float)));
+    HIP_CHECK(hipMalloc(&r->d_rd, traces * sizeof(uint32_t)));
     r->rd_cap = traces;
   }
   if (nblk > r->blk_cap)
@@ -797,7 +797,7 @@ static int enqueue_rng(rfx_renderer *r, uint64_t traces, hipStream_t st)
   const uint64_t nblk = rng_layout(traces, 1, nullptr);
   if ((rc = ensure_rng_workspace(r, traces, nblk)) != RFX_OK) return rc;
   HIP_CHECK(launch_rng_count(r->d_seed, r->d_jump, r->d_blk_cnt, 0, nblk, st));
-  HIP_CHECK(launch_rng_finish(r->d_seed, r->d_jump, r->d_seed + 1, r->d_blk_cnt, nblk, traces, r->d_rd, r->rd_cap,
+  HIP_CHECK(launch_rng_finish(r->d_seed, r->d_jump, r->d_seed + 1, r->d_blk_cnt, nblk, traces, r->d_rd,
                               r->d_blk_off, r->d_err, 1, 1, 1, 0, 1, st));
   HIP_CHECK(hipMemcpyAsync(r->d_seed, r->d_seed + 1, sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
   return RFX_OK;
@@ -843,14 +843,13 @@ static int finish_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *d_counts
   FrameParams &P = pl.P;
   const hipStream_t st = pl.st;
   const uint64_t ss2 = P.ss > 0 ? (uint64_t)(P.ss * P.ss) : 1;
-  HIP_CHECK(launch_rng_finish(r->d_seed, r->d_jump, r->d_seed + 1, d_counts, nblk, pl.traces, r->d_rd, r->rd_cap,
+  HIP_CHECK(launch_rng_finish(r->d_seed, r->d_jump, r->d_seed + 1, d_counts, nblk, pl.traces, r->d_rd,
                               r->d_blk_off, r->d_err, ss2, P.W, P.row_block, P.rank, P.nranks, st));
   HIP_CHECK(hipMemcpyAsync(r->d_seed, r->d_seed + 1, sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
   if ((rc = timing_event(r, st)) != RFX_OK) return rc;
   P.img = d_rgb;
   P.argb = d_argb;
-  P.rd = r->d_rd;
-  P.n_rd = r->rd_cap;
+  P.rd_state = r->d_rd;
   P.counters = (unsigned long long *)d_counters;
   if (P.grid_rows) HIP_CHECK(launch_trace(r->dev, P, d_counters != nullptr, st));
   if ((rc = timing_event(r, st)) != RFX_OK) return rc;
@@ -1050,16 +1049,18 @@ extern "C" int rfx_rand_dirs(rfx_renderer *r, uint32_t seed, uint64_t n, float *
   HIP_CHECK(hipStreamSynchronize(r->stream));
   HIP_CHECK(hipMemcpyAsync(r->d_seed, &seed, sizeof(uint32_t), hipMemcpyHostToDevice, r->stream));
   if ((rc = enqueue_rng(r, n, r->stream)) != RFX_OK) return rc;
-  std::vector<float> soa(3 * n);
-  for (int k = 0; k < 3; ++k)
-    HIP_CHECK(hipMemcpyAsync(soa.data() + k * n, r->d_rd + k * r->rd_cap, n * sizeof(float), hipMemcpyDeviceToHost, r->stream));
+  std::vector<uint32_t> states(n);
+  HIP_CHECK(hipMemcpyAsync(states.data(), r->d_rd, n * sizeof(uint32_t), hipMemcpyDeviceToHost, r->stream));
   uint32_t after = 0;
   HIP_CHECK(hipMemcpyAsync(&after, r->d_seed, sizeof(uint32_t), hipMemcpyDeviceToHost, r->stream));
   HIP_CHECK(hipMemcpyAsync(r->d_seed, &saved, sizeof(uint32_t), hipMemcpyHostToDevice, r->stream));
   if ((rc = rfx_synchronize(r)) != RFX_OK) return rc;
-  for (uint64_t i = 0; i < n; ++i)
+  for (uint64_t i = 0; i < n; ++i)  // Vector3.cpp:182-184 from each trace's state
   {
-    out3[i * 3] = soa[i]; out3[i * 3 + 1] = soa[n + i]; out3[i * 3 + 2] = soa[2 * n + i];
+    const uint32_t s1 = lcg_step(states[i]), s2 = lcg_step(s1), s3 = lcg_step(s2);
+    out3[i * 3] = rand_component(lcg_out(s1));
+    out3[i * 3 + 1] = rand_component(lcg_out(s2));
+    out3[i * 3 + 2] = rand_component(lcg_out(s3));
   }
   if (seed_out) *seed_out = after;
   return RFX_OK;

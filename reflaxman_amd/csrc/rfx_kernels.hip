@@ -317,7 +317,7 @@ __device__ __forceinline__ bool sphere_tail(float b, float d, v3 ray, const RayC
 // ((aox, aoy), (arx, ary), (u, v)), each half rounding exactly as the scalar expression.
 template <bool STATS, bool SHADOW>
 __device__ __forceinline__ bool tri_hit(const TriGeo &g, v3 o, v3 ray, float &t_out, float &u_out, float &v_out,
-                                        float &sq_out, Cnt &cnt, float a2 = 0.0f, float best_sq = INFINITY)
+                                        float &sq_out, Cnt &cnt, const RayConst &k, float best_sq = INFINITY)
 {
   RFX_CNT(SHADOW ? C_SH_TRI_TESTS : C_TRI_TESTS);
   const float dx = o.x - g.v0x, dy = o.y - g.v0y, dz = o.z - g.v0z;
@@ -339,7 +339,7 @@ __device__ __forceinline__ bool tri_hit(const TriGeo &g, v3 o, v3 ray, float &t_
     // exact reject of a plane hit beyond the current closest hit: |ray t|^2 = a nz^2 / arz^2 (real), and
     // a 2^-16 margin over the float rounding of both sides leaves |ray t| strictly above the best
     // distance after rounding, so the reference could neither take it nor tie (a2 = 2a exactly)
-    if (nz * nz * a2 > best_sq * (arz * arz) * 2.0000305f) return false;
+    if (nz * nz * k.a2 > best_sq * (arz * arz) * 2.0000305f) return false;
   }
 #endif
   const float t = nz / arz;
@@ -590,7 +590,7 @@ __device__ __forceinline__ void closest_hit(const DevScene &S, v3 origin, v3 ray
       m &= m - 1ull;
       if (!live) continue;
       float t, u, v, sq;
-      if (tri_hit<STATS, false>(S.tri_geo[i], origin, ray, t, u, v, sq, cnt, k.a2, h.sq))
+      if (tri_hit<STATS, false>(S.tri_geo[i], origin, ray, t, u, v, sq, cnt, k, h.sq))
       {
         RFX_CNT(C_TRI_D);
         const int obj = S.tri_shade[i].obj;
@@ -656,7 +656,7 @@ __device__ __forceinline__ void closest_hit_small(const DevScene &S, v3 origin, 
     const int i = __builtin_ctzll(tm);
     tm &= tm - 1ull;
     float t, u, v, sq;
-    if (tri_hit<STATS, false>(S.tri_geo[i], origin, ray, t, u, v, sq, cnt, k.a2, h.sq))
+    if (tri_hit<STATS, false>(S.tri_geo[i], origin, ray, t, u, v, sq, cnt, k, h.sq))
     {
       RFX_CNT(C_TRI_D);
       const int obj = S.tri_shade[i].obj;
@@ -706,9 +706,9 @@ __device__ __forceinline__ bool occluded_small(const DevScene &S, v3 o, v3 ray, 
     tm &= tm - 1ull;
     if constexpr (STATS)
     {
-      if (i != skip_tri && tri_hit<STATS, true>(S.tri_geo[i], o, ray, t, u, v, sq, cnt)) return true;
+      if (i != skip_tri && tri_hit<STATS, true>(S.tri_geo[i], o, ray, t, u, v, sq, cnt, k)) return true;
     }
-    else if (tri_hit<STATS, true>(S.tri_geo[i], o, ray, t, u, v, sq, cnt) && i != skip_tri)
+    else if (tri_hit<STATS, true>(S.tri_geo[i], o, ray, t, u, v, sq, cnt, k) && i != skip_tri)
       return true;
   }
   return false;
@@ -780,9 +780,9 @@ __device__ __forceinline__ bool occluded(const DevScene &S, v3 o, v3 ray, bool l
       {
         if constexpr (STATS)
         {
-          if (i != skip_tri && tri_hit<STATS, true>(S.tri_geo[i], o, ray, t, u, v, sq, cnt)) occ = true;
+          if (i != skip_tri && tri_hit<STATS, true>(S.tri_geo[i], o, ray, t, u, v, sq, cnt, k)) occ = true;
         }
-        else if (tri_hit<STATS, true>(S.tri_geo[i], o, ray, t, u, v, sq, cnt) && i != skip_tri)
+        else if (tri_hit<STATS, true>(S.tri_geo[i], o, ray, t, u, v, sq, cnt, k) && i != skip_tri)
           occ = true;
       }
       if (__ballot(live && !occ) == 0) return occ;
@@ -1046,10 +1046,14 @@ __device__ __forceinline__ uint32_t strip_row_to_y(uint32_t r, const FrameParams
   return (blk * P.nranks + P.rank) * P.row_block + w;
 }
 
-__device__ __forceinline__ v3 load_rd(const FrameParams &P, uint64_t i)
+// trace i's randomInsideSphere draw (Vector3.cpp:176-188) from the LCG state before its accepted triple
+__device__ __forceinline__ v3 rd_from_state(uint32_t s)
 {
-  return mk(P.rd[i], P.rd[P.n_rd + i], P.rd[2 * P.n_rd + i]);
+  const uint32_t s1 = lcg_step(s), s2 = lcg_step(s1), s3 = lcg_step(s2);
+  return mk(rand_component_dev(lcg_out(s1)), rand_component_dev(lcg_out(s2)), rand_component_dev(lcg_out(s3)));
 }
+
+__device__ __forceinline__ v3 load_rd(const FrameParams &P, uint64_t i) { return rd_from_state(P.rd_state[i]); }
 
 // 6 waves per SIMD (<= 80 VGPRs): the kernel is VALU-issue bound; more waves hide the scene-load and
 // texel latencies better than spills cost (tools/ab.py: 4 -> 5 -> 6 each won)
@@ -1272,14 +1276,15 @@ __device__ __forceinline__ bool owned(uint64_t idx, const EmitFilter &f)
 }
 
 // Scatter of the accepted triples: a block's accepted triples are the contiguous trace range
-// [blk_off[b], blk_off[b] + blk_cnt[b]); each thread regenerates its 16 triples into registers, the block
-// scans the accept counts, places its accepted triples in LDS at their block-local rank, and then writes
-// the range out with coalesced stores (randDir SoA, one plane per component).
+// [blk_off[b], blk_off[b] + blk_cnt[b]); each thread regenerates its 16 triples, keeping for each the LCG
+// state before its three draws, the block scans the accept counts, places the accepted triples' states in
+// LDS at their block-local rank, and writes the range out with coalesced 4-byte stores.  Trace i then
+// re-derives its randDir from that state (rd_from_state): three LCG steps and three exact conversions.
 __global__ __launch_bounds__(kRngBlock) void rng_emit(const uint32_t *seed, const uint32_t *jump, const uint64_t *blk_off,
-                                                      const uint32_t *blk_cnt, uint64_t need, float *rd, uint64_t n_rd,
+                                                      const uint32_t *blk_cnt, uint64_t need, uint32_t *rd_state,
                                                       uint32_t *next_seed, EmitFilter flt)
 {
-  __shared__ float sx[kTriplesPerBlock], sy[kTriplesPerBlock], sz[kTriplesPerBlock];
+  __shared__ uint32_t sst[kTriplesPerBlock];
   __shared__ uint32_t wsum[kRngBlock / 64];
   const uint64_t off = blk_off[blockIdx.x];
   if (off >= need) return;
@@ -1295,12 +1300,14 @@ __global__ __launch_bounds__(kRngBlock) void rng_emit(const uint32_t *seed, cons
     if (!any) return;
   }
   uint32_t s = thread_state(*seed, jump, blockIdx.x, threadIdx.x);
-  float x[kTriplesPerThread], y[kTriplesPerThread], z[kTriplesPerThread];
+  uint32_t st[kTriplesPerThread];
   uint32_t acc = 0, c = 0;
+  float x, y, z;
 #pragma unroll
   for (int j = 0; j < kTriplesPerThread; ++j)
   {
-    const bool a = triple(s, x[j], y[j], z[j]);
+    st[j] = s;
+    const bool a = triple(s, x, y, z);
     acc |= (a ? 1u : 0u) << j;
     c += a ? 1u : 0u;
   }
@@ -1318,33 +1325,20 @@ __global__ __launch_bounds__(kRngBlock) void rng_emit(const uint32_t *seed, cons
   uint32_t wbase = 0;
   for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) wbase += wsum[w];
   uint32_t li = wbase + (inc - c);                                               // block-local rank
-  if (li < cnt && li + c >= cnt && off + cnt == need)
-  {
-    // this thread holds trace need-1: the stream state after it is the next frame's state
-    uint32_t st = thread_state(*seed, jump, blockIdx.x, threadIdx.x);
-    uint32_t k = li;
-    for (int j = 0; j < kTriplesPerThread; ++j)
-    {
-      st = lcg_step(lcg_step(lcg_step(st)));
-      if ((acc >> j) & 1u)
-        if (k++ == cnt - 1) { *next_seed = st; break; }
-    }
-  }
 #pragma unroll
   for (int j = 0; j < kTriplesPerThread; ++j)
     if ((acc >> j) & 1u)
     {
-      sx[li] = x[j]; sy[li] = y[j]; sz[li] = z[j];
+      // trace need-1's triple: the stream state after it is the next frame's state
+      if (off + li == need - 1) *next_seed = lcg_step(lcg_step(lcg_step(st[j])));
+      if (li < cnt) sst[li] = st[j];
       ++li;
     }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < cnt; i += kRngBlock)
   {
     const uint64_t idx = off + i;
-    if (flt.nranks <= 1 || owned(idx, flt))
-    {
-      rd[idx] = sx[i]; rd[n_rd + idx] = sy[i]; rd[2 * n_rd + idx] = sz[i];
-    }
+    if (flt.nranks <= 1 || owned(idx, flt)) rd_state[idx] = sst[i];
   }
 }
 
@@ -1416,14 +1410,14 @@ hipError_t launch_rng_count(const uint32_t *d_seed, const uint32_t *d_jump, uint
 
 // second half: scan all nblk counts, scatter the randDirs this rank needs, carry the stream state
 hipError_t launch_rng_finish(const uint32_t *d_seed, const uint32_t *d_jump, uint32_t *d_next_seed,
-                             const uint32_t *d_blk_cnt, uint64_t nblk, uint64_t traces, float *d_rd, uint64_t n_rd,
+                             const uint32_t *d_blk_cnt, uint64_t nblk, uint64_t traces, uint32_t *d_rd_state,
                              uint64_t *d_blk_off, int *d_err, uint64_t ss2, uint64_t W, uint32_t row_block,
                              uint32_t rank, uint32_t nranks, hipStream_t st)
 {
   hipLaunchKernelGGL(rng_scan, dim3(1), dim3(1024), 0, st, d_blk_cnt, (uint32_t)nblk, d_blk_off, traces, d_err);
   const EmitFilter flt{ss2 ? ss2 : 1, W ? W : 1, row_block ? row_block : 1, rank, nranks ? nranks : 1};
   hipLaunchKernelGGL(rng_emit, dim3((uint32_t)nblk), dim3(kRngBlock), 0, st, d_seed, d_jump, d_blk_off, d_blk_cnt,
-                     traces, d_rd, n_rd, d_next_seed, flt);
+                     traces, d_rd_state, d_next_seed, flt);
   return hipGetLastError();
 }
 

@@ -87,8 +87,7 @@ struct FrameParams {
   uint64_t trace_base;          // trace index of the first trace in the range (block mode: corner count)
   float *img;                   // W x H x 3 frame (nranks == 1) or strip_rows x W x 3 (in/out when accumulate)
   uint32_t *argb;               // same shape, or null
-  const float *rd;              // randDir SoA: rd[i], rd[n_rd + i], rd[2 n_rd + i]
-  uint64_t n_rd;
+  const uint32_t *rd_state;     // per trace: LCG state before its accepted randomInsideSphere triple
   unsigned long long *counters; // C_COUNT u64, stats build only
 };
 

@@ -29,11 +29,9 @@ from reflaxman_amd import _build, _lib, scenes  # noqa: E402
 
 VARIANTS = {
     "base": [],
+    "nonear": ["RFX_NO_NEAR_REJ"],
+    "skipafter": ["RFX_SKIP_AFTER"],
     "wpe5": ["RFX_WAVES_PER_EU=5"],
-    "lds": ["RFX_LDS_SCENE"],
-    "old": ["RFX_NO_TRI_SIGN", "RFX_NO_SPH_B"],
-    "notrisign": ["RFX_NO_TRI_SIGN"],
-    "nosphb": ["RFX_NO_SPH_B"],
 }
 
 
