@@ -1055,12 +1055,23 @@ __device__ __forceinline__ v3 rd_from_state(uint32_t s)
 
 __device__ __forceinline__ v3 load_rd(const FrameParams &P, uint64_t i) { return rd_from_state(P.rd_state[i]); }
 
-// 6 waves per SIMD (<= 80 VGPRs): the kernel is VALU-issue bound; more waves hide the scene-load and
-// texel latencies better than spills cost (tools/ab.py: 4 -> 5 -> 6 each won)
+// 7 waves per SIMD (<= 72 VGPRs, a few spills): the kernel is VALU-issue bound; more waves hide the
+// scene-load and texel latencies better than spills cost (tools/ab.py, C3 trace kernel: 6 -> 7 -2.6%;
+// 8 waves / 64 VGPRs spill enough to lose 4-7%)
 #ifndef RFX_WAVES_PER_EU
-#define RFX_WAVES_PER_EU 6
+#define RFX_WAVES_PER_EU 7
 #endif
-#define RFX_TRACE_BOUNDS __launch_bounds__(256, RFX_WAVES_PER_EU)
+// waves per workgroup (1, 2 or 4): a wave is an 8x8 pixel tile, a workgroup 8x8 / 16x8 / 16x16 pixels.
+// Two: a workgroup's slots free when its slower wave ends, and the per-workgroup LDS staging stays cheap
+// (tools/ab.py, C3 trace kernel: 4 -> 2 waves -2.5%, 1 wave +3.6%)
+#ifndef RFX_WG_WAVES
+#define RFX_WG_WAVES 2
+#endif
+constexpr uint32_t kWgWaves = RFX_WG_WAVES, kWgThreads = 64 * kWgWaves;
+constexpr uint32_t kTileWavesX = kWgWaves >= 2 ? 2 : 1, kTileWavesY = kWgWaves / kTileWavesX;
+constexpr uint32_t kTileW = 8 * kTileWavesX, kTileH = 8 * kTileWavesY;
+static_assert(kWgWaves == 1 || kWgWaves == 2 || kWgWaves == 4, "RFX_WG_WAVES: 1, 2 or 4");
+#define RFX_TRACE_BOUNDS __launch_bounds__(kWgThreads) __attribute__((amdgpu_waves_per_eu(RFX_WAVES_PER_EU)))
 
 // Pixel loop variants of Render::renderNext: block preview (sampleNum < 0), one plain trace per pixel
 // (sampleNum == 1, no jitter, no accumulation -- the benchmark frame), and the general SSAA / additive
@@ -1070,7 +1081,7 @@ enum TraceMode { kModeSsaa = 0, kModeBlock = 1, kModePlain = 2 };
 // kCfgSmall -- at most 32 spheres and 32 triangles (one lane-layout cull mask for the whole scene)
 constexpr int kCfgCull = 1, kCfgManyLights = 2, kCfgSmall = 4;
 
-// one workgroup = 16x16 output pixels (block mode: block corners), one wave = an 8x8 tile (ray coherence).
+// one workgroup = kTileW x kTileH output pixels (block mode: block corners), one wave = an 8x8 tile (ray coherence).
 // Every lane of a wave reaches trace() -- lanes outside the frame or the cursor span as invalid -- so the
 // bounce loop can use wave-wide bundles.
 template <bool STATS, int MODE, int CFG>
@@ -1078,7 +1089,7 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
 {
   constexpr bool CULL = (CFG & kCfgCull) != 0, MANYL = (CFG & kCfgManyLights) != 0, SMALL = (CFG & kCfgSmall) != 0;
   __shared__ float lut[256];
-  lut[threadIdx.x] = (float)threadIdx.x / 255.0f;                               // Color.cpp:11-13
+  for (uint32_t i = threadIdx.x; i < 256; i += kWgThreads) lut[i] = (float)i / 255.0f;  // Color.cpp:11-13
   stage_powf_tables();
   if constexpr (SMALL) stage_small_scene(S);
   RFX_PROF_INIT();
@@ -1090,8 +1101,8 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
     for (int k = 0; k < C_COUNT; ++k) cnt.c[k] = 0;
   }
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-  const uint32_t lx = (wave & 1u) * 8u + (lane & 7u), ly = (wave >> 1) * 8u + (lane >> 3);
-  const uint32_t gx = blockIdx.x * 16u + lx, gy = blockIdx.y * 16u + ly;
+  const uint32_t lx = (wave % kTileWavesX) * 8u + (lane & 7u), ly = (wave / kTileWavesX) * 8u + (lane >> 3);
+  const uint32_t gx = blockIdx.x * kTileW + lx, gy = blockIdx.y * kTileH + ly;
   m33 view;
   view.m11 = P.v11; view.m12 = P.v12; view.m13 = P.v13;
   view.m21 = P.v21; view.m22 = P.v22; view.m23 = P.v23;
@@ -1425,7 +1436,7 @@ template <bool STATS, int MODE, int CFG>
 static void launch_one(dim3 grid, const DevScene &S, const FrameParams &P, hipStream_t st)
 {
   if constexpr (!STATS || !(CFG & kCfgCull))  // the stats build never culls
-    hipLaunchKernelGGL((trace_kernel<STATS, MODE, CFG>), grid, dim3(256), 0, st, S, P);
+    hipLaunchKernelGGL((trace_kernel<STATS, MODE, CFG>), grid, dim3(kWgThreads), 0, st, S, P);
 }
 
 template <bool STATS, int MODE>
@@ -1464,7 +1475,7 @@ static void launch_mode_cfg(bool stats, int mode, int cfg, dim3 grid, const DevS
 hipError_t launch_trace(const DevScene &S, const FrameParams &P, bool stats, hipStream_t st)
 {
   const uint32_t cols = P.ss < 0 ? (P.W + (uint32_t)(-P.ss) - 1) / (uint32_t)(-P.ss) : P.W;
-  const dim3 grid((cols + 15) / 16, (P.grid_rows + 15) / 16);
+  const dim3 grid((cols + kTileW - 1) / kTileW, (P.grid_rows + kTileH - 1) / kTileH);
   const int mode = P.ss < 0 ? kModeBlock : (P.ss == 1 && !P.additive && !P.accumulate) ? kModePlain : kModeSsaa;
   // the stats build counts the reference's every test, so it never culls
   int cfg = (S.n_light > 32 ? kCfgManyLights : 0) | (stats ? 0 : kCfgCull) |

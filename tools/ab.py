@@ -29,9 +29,10 @@ from reflaxman_amd import _build, _lib, scenes  # noqa: E402
 
 VARIANTS = {
     "base": [],
-    "nonear": ["RFX_NO_NEAR_REJ"],
-    "skipafter": ["RFX_SKIP_AFTER"],
-    "wpe5": ["RFX_WAVES_PER_EU=5"],
+    "wg2": ["RFX_WG_WAVES=2"],
+    "wg1": ["RFX_WG_WAVES=1"],
+    "wpe7": ["RFX_WAVES_PER_EU=7"],
+    "wg2wpe7": ["RFX_WG_WAVES=2", "RFX_WAVES_PER_EU=7"],
 }
 
 
