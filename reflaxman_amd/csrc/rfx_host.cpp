@@ -31,7 +31,7 @@ hipError_t launch_rng_count(const uint32_t *d_seed, const uint32_t *d_jump, uint
                             uint64_t nblk_slice, hipStream_t st);
 hipError_t launch_rng_finish(const uint32_t *d_seed, const uint32_t *d_jump, uint32_t *d_next_seed,
                              const uint32_t *d_blk_cnt, uint64_t nblk, uint64_t traces, uint32_t *d_rd_state,
-                             uint64_t *d_blk_off, int *d_err, uint64_t ss2, uint64_t W, uint32_t row_block,
+                             int *d_err, uint64_t ss2, uint64_t W, uint32_t row_block,
                              uint32_t rank, uint32_t nranks, hipStream_t st);
 hipError_t launch_trace(const DevScene &S, const FrameParams &P, bool stats, hipStream_t st);
 }  // namespace rfx
@@ -404,7 +404,7 @@ struct rfx_renderer {
   uint32_t jitter_seed = 0;
   // workspaces
   uint32_t *d_rd = nullptr; uint64_t rd_cap = 0;  // per-trace LCG states (rng_emit)
-  uint32_t *d_blk_cnt = nullptr; uint64_t *d_blk_off = nullptr; uint64_t blk_cap = 0;
+  uint32_t *d_blk_cnt = nullptr; uint64_t blk_cap = 0;
   uint32_t *d_jump = nullptr;  // LCG jump table for blk_cap blocks (rng_jump_table)
   // host staging for rfx_render_frame_host
   float *d_img = nullptr; uint32_t *d_argb = nullptr; uint64_t *d_cnt = nullptr; size_t img_cap = 0;
@@ -505,7 +505,7 @@ extern "C" void rfx_renderer_destroy(rfx_renderer *r)
   (void)hipStreamSynchronize(r->stream);
   free_scene(r);
   (void)hipFree(r->d_seed); (void)hipFree(r->d_err); (void)hipFree(r->d_rd);
-  (void)hipFree(r->d_blk_cnt); (void)hipFree(r->d_blk_off); (void)hipFree(r->d_jump);
+  (void)hipFree(r->d_blk_cnt); (void)hipFree(r->d_jump);
   (void)hipFree(r->d_img); (void)hipFree(r->d_argb); (void)hipFree(r->d_cnt);
   for (hipEvent_t e : r->events) (void)hipEventDestroy(e);
   if (r->own_stream) (void)hipStreamDestroy(r->own_stream);
@@ -776,10 +776,9 @@ static int ensure_rng_workspace(rfx_renderer *r, uint64_t traces, uint64_t nblk)
   }
   if (nblk > r->blk_cap)
   {
-    (void)hipFree(r->d_blk_cnt); (void)hipFree(r->d_blk_off); (void)hipFree(r->d_jump);
-    r->d_blk_cnt = nullptr; r->d_blk_off = nullptr; r->d_jump = nullptr; r->blk_cap = 0;
+    (void)hipFree(r->d_blk_cnt); (void)hipFree(r->d_jump);
+    r->d_blk_cnt = nullptr; r->d_jump = nullptr; r->blk_cap = 0;
     HIP_CHECK(hipMalloc(&r->d_blk_cnt, nblk * sizeof(uint32_t)));
-    HIP_CHECK(hipMalloc(&r->d_blk_off, nblk * sizeof(uint64_t)));
     std::vector<uint32_t> jump(2 * (256 + nblk));
     rng_jump_table(nblk, jump.data());
     HIP_CHECK(hipMalloc(&r->d_jump, jump.size() * sizeof(uint32_t)));
@@ -798,7 +797,7 @@ static int enqueue_rng(rfx_renderer *r, uint64_t traces, hipStream_t st)
   if ((rc = ensure_rng_workspace(r, traces, nblk)) != RFX_OK) return rc;
   HIP_CHECK(launch_rng_count(r->d_seed, r->d_jump, r->d_blk_cnt, 0, nblk, st));
   HIP_CHECK(launch_rng_finish(r->d_seed, r->d_jump, r->d_seed + 1, r->d_blk_cnt, nblk, traces, r->d_rd,
-                              r->d_blk_off, r->d_err, 1, 1, 1, 0, 1, st));
+                              r->d_err, 1, 1, 1, 0, 1, st));
   HIP_CHECK(hipMemcpyAsync(r->d_seed, r->d_seed + 1, sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
   return RFX_OK;
 }
@@ -844,7 +843,7 @@ static int finish_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *d_counts
   const hipStream_t st = pl.st;
   const uint64_t ss2 = P.ss > 0 ? (uint64_t)(P.ss * P.ss) : 1;
   HIP_CHECK(launch_rng_finish(r->d_seed, r->d_jump, r->d_seed + 1, d_counts, nblk, pl.traces, r->d_rd,
-                              r->d_blk_off, r->d_err, ss2, P.W, P.row_block, P.rank, P.nranks, st));
+                              r->d_err, ss2, P.W, P.row_block, P.rank, P.nranks, st));
   HIP_CHECK(hipMemcpyAsync(r->d_seed, r->d_seed + 1, sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
   if ((rc = timing_event(r, st)) != RFX_OK) return rc;
   P.img = d_rgb;

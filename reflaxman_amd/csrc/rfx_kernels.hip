@@ -1,6 +1,6 @@
 // gfx950 kernels for ReflaxMan's per-pixel trace loop.
 //
-//   rng_count / rng_scan / rng_emit : the reference's serial LCG stream
+//   rng_count / rng_emit : the reference's serial LCG stream
 //       (trace_math.h:34-39, Vector3.cpp:176-188) as a parallel pre-pass:
 //       LCG jump-ahead per thread, accept flags, block scan, scatter of the
 //       i-th accepted triple to trace i.
@@ -1246,33 +1246,6 @@ __global__ __launch_bounds__(kRngBlock) void rng_count(const uint32_t *seed, con
   }
 }
 
-// single workgroup: exclusive scan of block counts; flags a short stream
-__global__ __launch_bounds__(1024) void rng_scan(const uint32_t *blk_cnt, uint32_t nblk, uint64_t *blk_off,
-                                                 uint64_t need, int *err)
-{
-  __shared__ uint64_t part[1024];
-  const uint32_t per = (nblk + 1023) / 1024;
-  const uint32_t b0 = threadIdx.x * per, b1 = min(nblk, b0 + per);
-  uint64_t sum = 0;
-  for (uint32_t b = b0; b < b1; ++b) sum += blk_cnt[b];
-  part[threadIdx.x] = sum;
-  __syncthreads();
-  for (uint32_t off = 1; off < 1024; off <<= 1)
-  {
-    const uint64_t v = threadIdx.x >= off ? part[threadIdx.x - off] : 0;
-    __syncthreads();
-    part[threadIdx.x] += v;
-    __syncthreads();
-  }
-  uint64_t run = part[threadIdx.x] - sum;
-  for (uint32_t b = b0; b < b1; ++b)
-  {
-    blk_off[b] = run;
-    run += blk_cnt[b];
-  }
-  if (threadIdx.x == 1023 && part[1023] < need) *err = 1;
-}
-
 // Which traces a rank needs randDirs for: trace i -> pixel i / ss2 -> row -> strip (row / row_block)
 // -> owner strip % nranks (rfx_strip_row_to_y).  nranks <= 1: every trace.
 struct EmitFilter {
@@ -1286,18 +1259,32 @@ __device__ __forceinline__ bool owned(uint64_t idx, const EmitFilter &f)
   return ((idx / f.ss2 / f.W / f.row_block) % f.nranks) == f.rank;
 }
 
-// Scatter of the accepted triples: a block's accepted triples are the contiguous trace range
-// [blk_off[b], blk_off[b] + blk_cnt[b]); each thread regenerates its 16 triples, keeping for each the LCG
-// state before its three draws, the block scans the accept counts, places the accepted triples' states in
-// LDS at their block-local rank, and writes the range out with coalesced 4-byte stores.  Trace i then
-// re-derives its randDir from that state (rd_from_state): three LCG steps and three exact conversions.
-__global__ __launch_bounds__(kRngBlock) void rng_emit(const uint32_t *seed, const uint32_t *jump, const uint64_t *blk_off,
-                                                      const uint32_t *blk_cnt, uint64_t need, uint32_t *rd_state,
-                                                      uint32_t *next_seed, EmitFilter flt)
+// Scatter of the accepted triples: block b's accepted triples are the contiguous trace range
+// [off_b, off_b + blk_cnt[b]), off_b the sum of the counts before b.  Each thread regenerates its 16
+// triples, keeping for each the LCG state before its three draws; the block scans the accept counts,
+// places the accepted triples' states in LDS at their block-local rank, and writes the range out with
+// coalesced 4-byte stores.  Trace i then re-derives its randDir from that state (rd_from_state): three
+// LCG steps and three exact conversions.
+__global__ __launch_bounds__(kRngBlock) void rng_emit(const uint32_t *seed, const uint32_t *jump, const uint32_t *blk_cnt,
+                                                      uint64_t need, uint32_t *rd_state, uint32_t *next_seed, int *err,
+                                                      EmitFilter flt)
 {
   __shared__ uint32_t sst[kTriplesPerBlock];
   __shared__ uint32_t wsum[kRngBlock / 64];
-  const uint64_t off = blk_off[blockIdx.x];
+  // this block's first trace: the accept counts of the blocks before it, summed by the block (the count
+  // array is a few KB and L2-resident, so no separate scan pass)
+  uint32_t part = 0;
+  for (uint32_t k = threadIdx.x; k < blockIdx.x; k += kRngBlock) part += blk_cnt[k];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+  __shared__ uint64_t s_off;
+  if (threadIdx.x == 0) s_off = 0;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) atomicAdd((unsigned long long *)&s_off, (unsigned long long)part);
+  __syncthreads();
+  const uint64_t off = s_off;
+  // the last block flags a stream too short for the frame (host: RFX_ERR_RNG)
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0 && off + blk_cnt[blockIdx.x] < need) *err = 1;
   if (off >= need) return;
   const uint32_t cnt = (uint32_t)min((uint64_t)blk_cnt[blockIdx.x], need - off);  // triples this block emits
   const uint64_t last = off + cnt - 1;
@@ -1422,13 +1409,12 @@ hipError_t launch_rng_count(const uint32_t *d_seed, const uint32_t *d_jump, uint
 // second half: scan all nblk counts, scatter the randDirs this rank needs, carry the stream state
 hipError_t launch_rng_finish(const uint32_t *d_seed, const uint32_t *d_jump, uint32_t *d_next_seed,
                              const uint32_t *d_blk_cnt, uint64_t nblk, uint64_t traces, uint32_t *d_rd_state,
-                             uint64_t *d_blk_off, int *d_err, uint64_t ss2, uint64_t W, uint32_t row_block,
+                             int *d_err, uint64_t ss2, uint64_t W, uint32_t row_block,
                              uint32_t rank, uint32_t nranks, hipStream_t st)
 {
-  hipLaunchKernelGGL(rng_scan, dim3(1), dim3(1024), 0, st, d_blk_cnt, (uint32_t)nblk, d_blk_off, traces, d_err);
   const EmitFilter flt{ss2 ? ss2 : 1, W ? W : 1, row_block ? row_block : 1, rank, nranks ? nranks : 1};
-  hipLaunchKernelGGL(rng_emit, dim3((uint32_t)nblk), dim3(kRngBlock), 0, st, d_seed, d_jump, d_blk_off, d_blk_cnt,
-                     traces, d_rd_state, d_next_seed, flt);
+  hipLaunchKernelGGL(rng_emit, dim3((uint32_t)nblk), dim3(kRngBlock), 0, st, d_seed, d_jump, d_blk_cnt, traces,
+                     d_rd_state, d_next_seed, d_err, flt);
   return hipGetLastError();
 }
 
