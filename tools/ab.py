@@ -19,6 +19,7 @@ import json
 import os
 import statistics
 import sys
+import time
 
 import numpy as np
 
@@ -26,6 +27,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 from reflaxman_amd import _build, _lib, scenes  # noqa: E402
+
+_HIP = C.CDLL("libamdhip64.so")
 
 VARIANTS = {
     "base": [],
@@ -106,11 +109,15 @@ class Runner:
 
     def timed(self, frames):
         self.L.rfx_renderer_set_timing(self.r, 1)
+        _HIP.hipDeviceSynchronize()
+        t0 = time.perf_counter()
         self.render(frames)
+        _HIP.hipDeviceSynchronize()   # every stream: a speculative pre-pass counts too
+        wall = (time.perf_counter() - t0) * 1e3 / frames
         pre, tr, n = C.c_double(), C.c_double(), C.c_uint64()
         self.L.rfx_renderer_get_timing(self.r, C.byref(pre), C.byref(tr), C.byref(n))
         self.L.rfx_renderer_set_timing(self.r, 0)
-        return pre.value / n.value, tr.value / n.value
+        return pre.value / n.value, tr.value / n.value, wall
 
 
 def cmd_build(names):
@@ -136,11 +143,13 @@ def cmd_run(args):
         r.render(args.warmup)
     times = {r.name: [] for r in runners}
     pre = {r.name: [] for r in runners}
+    wall = {r.name: [] for r in runners}
     for _ in range(args.rounds):
         for r in runners:
-            p, t = r.timed(args.frames)
+            p, t, w = r.timed(args.frames)
             times[r.name].append(t)
             pre[r.name].append(p)
+            wall[r.name].append(w)
     base = statistics.median(times[runners[0].name])
     out = []
     for r in runners:
@@ -148,6 +157,7 @@ def cmd_run(args):
         out.append({"variant": r.name, "defines": VARIANTS.get(r.name), "parity_sha_ok": parity[r.name],
                     "trace_ms_median": round(med, 4), "trace_ms_min": round(min(times[r.name]), 4),
                     "prepass_ms_median": round(statistics.median(pre[r.name]), 4),
+                    "frame_ms_median": round(statistics.median(wall[r.name]), 4),
                     "vs_first": round(med / base, 4),
                     "mrays_trace_only": round(args.width * args.height / (med * 1e-3) / 1e6, 1)})
     for o in out:
@@ -164,7 +174,7 @@ def main():
     ap.add_argument("--height", type=int, default=2160)
     ap.add_argument("--depth", type=int, default=8)
     ap.add_argument("--rounds", type=int, default=12)
-    ap.add_argument("--frames", type=int, default=3)
+    ap.add_argument("--frames", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     args = ap.parse_args()
     if args.cmd == "build":
