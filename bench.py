@@ -71,6 +71,27 @@ def ulp_diff(a: np.ndarray, b: np.ndarray) -> int:
     return int(np.abs(ai - bi).max()) if a.size else 0
 
 
+def ulp_hist(a: np.ndarray, b: np.ndarray) -> dict:
+    """Histogram of per-channel float ULP distances (buckets 0, 1, 2-15, 16-255, >=256)."""
+    ai = a.reshape(-1).view(np.int32).astype(np.int64)
+    bi = b.reshape(-1).view(np.int32).astype(np.int64)
+    ai = np.where(ai < 0, np.int64(-2 ** 31) - ai, ai)
+    bi = np.where(bi < 0, np.int64(-2 ** 31) - bi, bi)
+    d = np.abs(ai - bi)
+    edges = [("0", 0, 0), ("1", 1, 1), ("2-15", 2, 15), ("16-255", 16, 255), (">=256", 256, None)]
+    return {k: int(((d >= lo) & (d <= hi)).sum()) if hi is not None else int((d >= lo).sum()) for k, lo, hi in edges}
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def u8_diff(a: np.ndarray, b: np.ndarray) -> int:
     ch = lambda x, s: ((x >> s) & 0xFF).astype(np.int32)
     return int(max(np.abs(ch(a, s) - ch(b, s)).max() for s in (0, 8, 16))) if a.size else 0
@@ -110,9 +131,10 @@ def cpu_baseline(desc, W, H, depth, gpu_rgb, gpu_argb, stride):
               else f"rows {ys.start}..{ys.stop - 1} of the first frame")
     return {
         "value": round(px / secs / 1e6, 4), "unit": "Mrays/s", "cores": 1, "kind": kind,
-        "sample": f"{sample}; {secs:.1f} s of single-thread trace time; "
+        "sample": f"{sample}; {secs:.1f} s of single-thread trace time; {cpu_model()}; "
                   f"{subprocess.run(['nproc'], capture_output=True, text=True).stdout.strip()} host CPUs visible",
-    }, {"max_u8": u8_diff(g_argb, argb), "max_f32_ulp": ulp_diff(g_rgb, rgb), "pixels": int(px)}
+    }, {"max_u8": u8_diff(g_argb, argb), "max_f32_ulp": ulp_diff(g_rgb, rgb),
+        "f32_ulp_histogram": ulp_hist(g_rgb, rgb), "pixels": int(px)}
 
 
 def main():
@@ -251,6 +273,24 @@ def main():
     else:
         trace_avg, pre_avg = trace_ms / max(nfr, 1), pre_ms / max(nfr, 1)
 
+    e2e = None
+    if world == 1:
+        # end to end with the frame handed back to the host (pinned buffers, PCIe D2H of the f32 RGB and
+        # ARGB8 frames): reported beside `value`, never as it
+        h_rgb = torch.empty(img.numel(), dtype=img.dtype, pin_memory=True)
+        h_argb = torch.empty(argb.numel(), dtype=argb.dtype, pin_memory=True)
+        n_e2e = min(args.steps, 5)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(n_e2e):
+            step()
+            h_rgb.copy_(img, non_blocking=True)
+            h_argb.copy_(argb, non_blocking=True)
+            torch.cuda.current_stream().synchronize()
+        e2e_s = (time.perf_counter() - t1) / n_e2e
+        e2e = {"ms_per_frame": round(e2e_s * 1e3, 4), "Mrays_per_s": round(traces / e2e_s / 1e6, 2),
+               "d2h_bytes_per_frame": int(img.numel() * 4 + argb.numel() * 4), "frames": n_e2e}
+
     if rank != 0:
         dist.destroy_process_group()
         return
@@ -285,6 +325,10 @@ def main():
                      "algo_hbm_GBps": round(px_launch * metrics.ALGO_BYTES_PER_PIXEL / (trace_avg * 1e-3) / 1e9, 1)},
         "phases_ms": {"rng_prepass": round(pre_avg, 4), "trace": round(trace_avg, 4)},
         "work_per_ray": {k: round(v, 3) for k, v in work.items() if k != "flops"},
+        # SURVEY §8(d) secondary metric: bounce segments + shadow rays per second (counted, frame 0's rates)
+        "secondary_Msegments_per_s": round((work["segments_per_ray"] + work["shadow_rays_per_ray"]) * traces
+                                           * args.steps / elapsed / 1e6, 1),
+        "end_to_end_incl_d2h": e2e,
         "parity": parity,
     }
     if world == 1 and not args.no_cpu_baseline:
