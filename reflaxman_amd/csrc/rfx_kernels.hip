@@ -109,6 +109,7 @@ __device__ __forceinline__ col from_argb_lut(uint32_t c, const float *lut)
 // and LDS answers such gathers in ~100 cycles where the constant/global path takes several hundred.
 __shared__ double s_powf_log[16][2];
 __shared__ uint64_t s_powf_exp[32];
+__shared__ double s_powf_add[2][4];
 
 __device__ __forceinline__ void stage_powf_tables()
 {
@@ -117,6 +118,7 @@ __device__ __forceinline__ void stage_powf_tables()
   {
     s_powf_exp[t] = kExp2fTab[t];
     s_powf_log[t >> 1][t & 1u] = kPowfLog2Tab[t >> 1][t & 1u];
+    if (t < 8) s_powf_add[t >> 2][t & 3u] = kPowfAdd[t >> 2][t & 3u];
   }
 }
 
@@ -125,7 +127,11 @@ __device__ __forceinline__ float powf_dev(float x, float y)
 #ifdef RFX_POW_GLOBAL
   return powf_glibc(x, y);
 #else
-  return powf_glibc_t(x, y, s_powf_log, s_powf_exp);
+#ifdef RFX_POW_ADD_LIT
+  return powf_glibc_t(x, y, s_powf_log, s_powf_exp, kPowfAdd);
+#else
+  return powf_glibc_t(x, y, s_powf_log, s_powf_exp, s_powf_add);
+#endif
 #endif
 }
 

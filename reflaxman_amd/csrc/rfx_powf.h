@@ -80,8 +80,17 @@ RFX_PHD int pw_checkint(uint32_t iy)
 }
 RFX_PHD int pw_zeroinfnan(uint32_t ix) { return 2 * ix - 1 >= 2u * 0x7f800000 - 1; }
 
-// logtab / exptab: kPowfLog2Tab / kExp2fTab or copies of them (the trace kernel keeps copies in LDS)
-RFX_PHD float powf_glibc_t(float x, float y, const double (*logtab)[2], const uint64_t *exptab)
+// The three polynomial addends that are not inline constants.  An f64 fma on gfx950 reads at most one
+// scalar operand, so with the multiplier in SGPRs each addend needs a VGPR pair; as literals they are
+// hoisted out of the trace loop and spilled to scratch.  Read from a table (the trace kernel's LDS copy)
+// at an index the compiler cannot fold -- (ix >> 31), always 0 there -- they are loaded at the call.
+RFX_PCONST double kPowfAdd[2][4] = {{-0x1.71969a075c67ap-2, -0x1.7154748bef6c8p-1, 0x1.ebfce50fac4f3p-3, 0.0},
+                                    {-0x1.71969a075c67ap-2, -0x1.7154748bef6c8p-1, 0x1.ebfce50fac4f3p-3, 0.0}};
+
+// logtab / exptab / addtab: kPowfLog2Tab / kExp2fTab / kPowfAdd or copies of them (the trace kernel keeps
+// copies in LDS)
+RFX_PHD float powf_glibc_t(float x, float y, const double (*logtab)[2], const uint64_t *exptab,
+                           const double (*addtab)[4])
 {
   uint32_t sign_bias = 0;
   uint32_t ix = pw_asuint(x), iy = pw_asuint(y);
@@ -123,12 +132,13 @@ RFX_PHD float powf_glibc_t(float x, float y, const double (*logtab)[2], const ui
   const uint32_t iz = ix - top;
   const int k = (int32_t)top >> 23;
   const double invc = logtab[i][0], logc = logtab[i][1];
+  const double *add = addtab[ix >> 31];  // ix < 2^31 here: row 0
   const double z = (double)pw_asfloat(iz);
   const double r = pw_fma(z, invc, -1.0);
   const double y0 = logc + (double)k;
   const double r2 = r * r;
-  double yy = pw_fma(r, 0x1.27616c9496e0bp-2, -0x1.71969a075c67ap-2);
-  const double p = pw_fma(r, 0x1.ec70a6ca7baddp-2, -0x1.7154748bef6c8p-1);
+  double yy = pw_fma(r, 0x1.27616c9496e0bp-2, add[0]);      // -0x1.71969a075c67ap-2
+  const double p = pw_fma(r, 0x1.ec70a6ca7baddp-2, add[1]);  // -0x1.7154748bef6c8p-1
   const double r4 = r2 * r2;
   double q = pw_fma(r, 0x1.71547652ab82bp+0, y0);
   q = pw_fma(r2, p, q);
@@ -152,7 +162,7 @@ RFX_PHD float powf_glibc_t(float x, float y, const double (*logtab)[2], const ui
   uint64_t t = exptab[ki % 32];
   t += (ki + sign_bias) << 47;
   const double s = pw_asdouble(t);
-  const double zz = pw_fma(rr, 0x1.c6af84b912394p-5, 0x1.ebfce50fac4f3p-3);
+  const double zz = pw_fma(rr, 0x1.c6af84b912394p-5, add[2]);  // 0x1.ebfce50fac4f3p-3
   const double rr2 = rr * rr;
   double e = pw_fma(rr, 0x1.62e42ff0c52d6p-1, 1.0);
   e = pw_fma(zz, rr2, e);
@@ -160,6 +170,6 @@ RFX_PHD float powf_glibc_t(float x, float y, const double (*logtab)[2], const ui
   return (float)e;
 }
 
-RFX_PHD float powf_glibc(float x, float y) { return powf_glibc_t(x, y, kPowfLog2Tab, kExp2fTab); }
+RFX_PHD float powf_glibc(float x, float y) { return powf_glibc_t(x, y, kPowfLog2Tab, kExp2fTab, kPowfAdd); }
 
 }  // namespace rfx
