@@ -1108,7 +1108,17 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
   }
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const uint32_t lx = (wave % kTileWavesX) * 8u + (lane & 7u), ly = (wave / kTileWavesX) * 8u + (lane >> 3);
-  const uint32_t gx = blockIdx.x * kTileW + lx, gy = blockIdx.y * kTileH + ly;
+  // the tile this workgroup renders: with a tile order (longest-processing-time first, from the previous
+  // frame's measured tile costs) the most expensive tiles start first and the cheap ones fill the tail
+  uint32_t bx = blockIdx.x, by = blockIdx.y;
+  if (P.tile_order)
+  {
+    const uint32_t t = P.tile_order[blockIdx.y * gridDim.x + blockIdx.x];
+    bx = t % gridDim.x;
+    by = t / gridDim.x;
+  }
+  const uint64_t clk0 = P.tile_cost ? __builtin_readcyclecounter() : 0;
+  const uint32_t gx = bx * kTileW + lx, gy = by * kTileH + ly;
   m33 view;
   view.m11 = P.v11; view.m12 = P.v12; view.m13 = P.v13;
   view.m21 = P.v21; view.m22 = P.v22; view.m23 = P.v23;
@@ -1202,6 +1212,82 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
   }
   flush_counters<STATS>(P, cnt);
   RFX_PROF_FLUSH();
+  if (P.tile_cost && lane == 0 && wave < 2u)  // a vector store from one lane of each of the first two waves
+  {
+    uint32_t *tc = P.tile_cost + 2u * (by * gridDim.x + bx);
+    tc[wave] = (uint32_t)min(__builtin_readcyclecounter() - clk0, 0xFFFFFFFFull);
+    if (kWgWaves == 1) tc[1] = 0;
+  }
+}
+
+// ------------------------------------------------------------- LPT tile order
+// The tile costs of a frame (two waves' clock cycles per tile) become the next launch's tile order, most
+// expensive first: a counting sort on a log-scale key (exponent and 3 mantissa bits: buckets ~9% wide) over
+// kLptGroups workgroups -- per-group LDS histograms, one scan of (bucket, group) offsets, a scatter.  The
+// order within a bucket is whatever the LDS atomics give: any permutation renders the same pixels, only
+// the schedule changes.
+constexpr int kLptThreads = 1024, kLptBuckets = 256, kLptGroups = 64;
+
+__device__ __forceinline__ uint32_t lpt_key(const uint32_t *cost, uint32_t i)
+{
+  const uint32_t c = max(cost[2u * i] + cost[2u * i + 1u], 1u);
+  const uint32_t e = 31u - (uint32_t)__clz(c);
+  const uint32_t m = e >= 3u ? (c >> (e - 3u)) & 7u : (c << (3u - e)) & 7u;
+  return (uint32_t)(kLptBuckets - 1) - min(e * 8u + m, (uint32_t)(kLptBuckets - 1));  // descending cost
+}
+
+// histogram of group g's tiles [g chunk, (g + 1) chunk) into hist[g][bucket]
+__global__ __launch_bounds__(kLptThreads) void lpt_hist(const uint32_t *cost, uint32_t n, uint32_t chunk, uint32_t *hist)
+{
+  __shared__ uint32_t h[kLptBuckets];
+  for (uint32_t b = threadIdx.x; b < kLptBuckets; b += kLptThreads) h[b] = 0;
+  __syncthreads();
+  const uint32_t i0 = blockIdx.x * chunk, i1 = min(n, i0 + chunk);
+  for (uint32_t i = i0 + threadIdx.x; i < i1; i += kLptThreads) atomicAdd(&h[lpt_key(cost, i)], 1u);
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < kLptBuckets; b += kLptThreads) hist[blockIdx.x * kLptBuckets + b] = h[b];
+}
+
+// hist[g][b] <- first slot of group g's tiles of bucket b (buckets in order, groups in order within one)
+__global__ __launch_bounds__(kLptBuckets) void lpt_scan(uint32_t *hist)
+{
+  __shared__ uint32_t tot[kLptBuckets];
+  const uint32_t b = threadIdx.x;
+  uint32_t run = 0;
+  for (int g = 0; g < kLptGroups; ++g) { const uint32_t v = hist[g * kLptBuckets + b]; hist[g * kLptBuckets + b] = run; run += v; }
+  tot[b] = run;
+  __syncthreads();
+  if (b == 0)
+  {
+    uint32_t acc = 0;
+    for (int k = 0; k < kLptBuckets; ++k) { const uint32_t v = tot[k]; tot[k] = acc; acc += v; }
+  }
+  __syncthreads();
+  for (int g = 0; g < kLptGroups; ++g) hist[g * kLptBuckets + b] += tot[b];
+}
+
+__global__ __launch_bounds__(kLptThreads) void lpt_scatter(const uint32_t *cost, uint32_t n, uint32_t chunk,
+                                                            const uint32_t *hist, uint32_t *order)
+{
+  __shared__ uint32_t off[kLptBuckets];
+  for (uint32_t b = threadIdx.x; b < kLptBuckets; b += kLptThreads) off[b] = hist[blockIdx.x * kLptBuckets + b];
+  __syncthreads();
+  const uint32_t i0 = blockIdx.x * chunk, i1 = min(n, i0 + chunk);
+  for (uint32_t i = i0 + threadIdx.x; i < i1; i += kLptThreads) order[atomicAdd(&off[lpt_key(cost, i)], 1u)] = i;
+}
+
+uint32_t trace_tiles(const FrameParams &P);
+
+// bytes of scratch launch_tile_order needs
+size_t tile_order_scratch() { return (size_t)kLptGroups * kLptBuckets * sizeof(uint32_t); }
+
+hipError_t launch_tile_order(const uint32_t *cost, uint32_t n, uint32_t *order, uint32_t *scratch, hipStream_t st)
+{
+  const uint32_t chunk = (n + kLptGroups - 1) / kLptGroups;
+  hipLaunchKernelGGL(lpt_hist, dim3(kLptGroups), dim3(kLptThreads), 0, st, cost, n, chunk, scratch);
+  hipLaunchKernelGGL(lpt_scan, dim3(1), dim3(kLptBuckets), 0, st, scratch);
+  hipLaunchKernelGGL(lpt_scatter, dim3(kLptGroups), dim3(kLptThreads), 0, st, cost, n, chunk, scratch, order);
+  return hipGetLastError();
 }
 
 // ------------------------------------------------------------- RNG pre-pass
@@ -1464,10 +1550,22 @@ static void launch_mode_cfg(bool stats, int mode, int cfg, dim3 grid, const DevS
   }
 }
 
-hipError_t launch_trace(const DevScene &S, const FrameParams &P, bool stats, hipStream_t st)
+static dim3 trace_grid(const FrameParams &P)
 {
   const uint32_t cols = P.ss < 0 ? (P.W + (uint32_t)(-P.ss) - 1) / (uint32_t)(-P.ss) : P.W;
-  const dim3 grid((cols + kTileW - 1) / kTileW, (P.grid_rows + kTileH - 1) / kTileH);
+  return dim3((cols + kTileW - 1) / kTileW, (P.grid_rows + kTileH - 1) / kTileH);
+}
+
+// workgroups (tiles) of the frame's trace launch
+uint32_t trace_tiles(const FrameParams &P)
+{
+  const dim3 g = trace_grid(P);
+  return g.x * g.y;
+}
+
+hipError_t launch_trace(const DevScene &S, const FrameParams &P, bool stats, hipStream_t st)
+{
+  const dim3 grid = trace_grid(P);
   const int mode = P.ss < 0 ? kModeBlock : (P.ss == 1 && !P.additive && !P.accumulate) ? kModePlain : kModeSsaa;
   // the stats build counts the reference's every test, so it never culls
   int cfg = (S.n_light > 32 ? kCfgManyLights : 0) | (stats ? 0 : kCfgCull) |

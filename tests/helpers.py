@@ -19,7 +19,7 @@ def sha(a) -> str:
 
 
 def gpu_render(desc, W, H, depth, ss=1, additive=False, frames=1, sphere_seed=1350490027, jitter_seed=0,
-               chunks=None, device=0):
+               chunks=None, device=0, tile_order=None, each_frame=None):
     """Render through the Python mirror of Render (reflaxman_amd.render.Render) on the GPU.
 
     chunks: None -> one renderNext(W*H) per frame; else a list of renderNext sizes cycled until done.
@@ -28,6 +28,8 @@ def gpu_render(desc, W, H, depth, ss=1, additive=False, frames=1, sphere_seed=13
     r = Render(device=device, sphere_seed=sphere_seed, jitter_seed=jitter_seed, load_default_scene=False)
     r.scene, r.camera = build_scene(desc)
     r.setImageSize(W, H)
+    if tile_order is not None:
+        r._r.set_tile_order(tile_order)
     for _ in range(frames):
         r.renderBegin(depth, ss, additive)
         if chunks is None:
@@ -37,5 +39,8 @@ def gpu_render(desc, W, H, depth, ss=1, additive=False, frames=1, sphere_seed=13
             i = 0
             while r.renderNext(chunks[i % len(chunks)]):
                 i += 1
+        if each_frame is not None:
+            r.synchronize()
+            each_frame(r.imagePixels(), r.copyImage())
     r.synchronize()
     return r.imagePixels(), r.copyImage(), r

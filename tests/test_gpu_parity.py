@@ -96,6 +96,24 @@ def test_rand_dirs_prepass():
     rr.close()
 
 
+@pytest.mark.parametrize("name,W,H,depth,ss,additive,chunks", [
+    ("synth16", 640, 360, 8, 1, False, None),      # plain frames: record, reuse the sorted order, re-sort
+    ("default", 200, 150, 4, 2, True, None),       # SSAA + additive accumulation
+    ("default", 161, 121, 4, -4, False, None),     # block preview
+    ("synth16", 320, 180, 8, 1, False, [5000, 777]),  # chunked renderNext: the grid changes every call
+])
+def test_tile_order_changes_no_pixel(name, W, H, depth, ss, additive, chunks):
+    """The longest-tile-first schedule (default) renders every frame exactly as raster order does."""
+    frames = []
+    for mode in (0, 1):
+        got = []
+        _, _, r = gpu_render(scene(name), W, H, depth, ss, additive, 9, tile_order=mode, chunks=chunks,
+                             each_frame=lambda rgb, argb: got.append((rgb.tobytes(), argb.tobytes())))
+        r.close()
+        frames.append(got)
+    assert len(frames[0]) == 9 and frames[0] == frames[1]
+
+
 def test_rng_state_carries_across_frames():
     """Two back-to-back frames (non-additive) continue the global stream like the reference."""
     import oracle as orc

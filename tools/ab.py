@@ -36,6 +36,10 @@ VARIANTS = {
     "wg1": ["RFX_WG_WAVES=1"],
     "wpe7": ["RFX_WAVES_PER_EU=7"],
     "wg2wpe7": ["RFX_WG_WAVES=2", "RFX_WAVES_PER_EU=7"],
+    "raster": ["RFX_TILE_ORDER_DEFAULT=0"],
+    "rastercost": ["RFX_TILE_ORDER_DEFAULT=2"],
+    "every1": ["RFX_TILE_SORT_EVERY=1"],
+    "every16": ["RFX_TILE_SORT_EVERY=16"],
 }
 
 
