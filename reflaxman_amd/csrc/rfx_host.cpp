@@ -891,12 +891,12 @@ static int tile_schedule(rfx_renderer *r, FrameParams &P, hipStream_t st, uint64
     r->tile_cap = 0;
     r->tile_n = 0;
     r->tile_pending = false;
-    HIP_CHECK(hipMalloc(&r->d_tile_cost, 2ull * n * sizeof(uint32_t)));
+    HIP_CHECK(hipMalloc(&r->d_tile_cost, (size_t)n * sizeof(uint32_t)));
     HIP_CHECK(hipMalloc(&r->d_tile_order, (size_t)n * sizeof(uint32_t)));
     r->tile_cap = n;
   }
-  // the last sort must have read the costs this launch may overwrite (every workgroup writes both of its
-  // tile's slots) and written the order it reads
+  // the last sort must have read the costs this launch may overwrite (every workgroup writes its tile's)
+  // and written the order it reads
   if (r->tile_pending && r->tile_waited != st)
   {
     HIP_CHECK(hipStreamWaitEvent(st, r->tile_join, 0));

@@ -1061,6 +1061,16 @@ __device__ __forceinline__ v3 rd_from_state(uint32_t s)
 
 __device__ __forceinline__ v3 load_rd(const FrameParams &P, uint64_t i) { return rd_from_state(P.rd_state[i]); }
 
+// Shader clock, low 32 bits.  A plain asm statement (no side effects declared, so the compiler may still
+// serve the scene loads that follow through the scalar cache -- __builtin_readcyclecounter would count as a
+// memory clobber for them); it waits for its own result.
+__device__ __forceinline__ uint32_t clock32()
+{
+  uint64_t c;
+  asm("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(c));
+  return (uint32_t)c;
+}
+
 // 7 waves per SIMD (<= 72 VGPRs, a few spills): the kernel is VALU-issue bound; more waves hide the
 // scene-load and texel latencies better than spills cost (tools/ab.py, C3 trace kernel: 6 -> 7 -2.6%;
 // 8 waves / 64 VGPRs spill enough to lose 4-7%)
@@ -1099,6 +1109,17 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
   stage_powf_tables();
   if constexpr (SMALL) stage_small_scene(S);
   RFX_PROF_INIT();
+  // the tile this workgroup renders: with a tile order (longest-processing-time first, from the previous
+  // frame's measured tile costs) the most expensive tiles start first and the cheap ones fill the tail
+  const uint32_t tile = P.tile_order ? P.tile_order[blockIdx.y * gridDim.x + blockIdx.x] : blockIdx.y * gridDim.x + blockIdx.x;
+  // tile cost: the start clock (low 32 bits) and the tile index wait in LDS, so the bounce loop keeps no
+  // register for them
+  __shared__ uint32_t s_clk0, s_tile;
+  if (P.tile_cost && threadIdx.x == 0)
+  {
+    s_clk0 = clock32();
+    s_tile = tile;
+  }
   __syncthreads();
   Cnt cnt;
   if constexpr (STATS)
@@ -1108,16 +1129,7 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
   }
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const uint32_t lx = (wave % kTileWavesX) * 8u + (lane & 7u), ly = (wave / kTileWavesX) * 8u + (lane >> 3);
-  // the tile this workgroup renders: with a tile order (longest-processing-time first, from the previous
-  // frame's measured tile costs) the most expensive tiles start first and the cheap ones fill the tail
-  uint32_t bx = blockIdx.x, by = blockIdx.y;
-  if (P.tile_order)
-  {
-    const uint32_t t = P.tile_order[blockIdx.y * gridDim.x + blockIdx.x];
-    bx = t % gridDim.x;
-    by = t / gridDim.x;
-  }
-  const uint64_t clk0 = P.tile_cost ? __builtin_readcyclecounter() : 0;
+  const uint32_t bx = tile % gridDim.x, by = tile / gridDim.x;
   const uint32_t gx = bx * kTileW + lx, gy = by * kTileH + ly;
   m33 view;
   view.m11 = P.v11; view.m12 = P.v12; view.m13 = P.v13;
@@ -1151,6 +1163,7 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
           if (P.argb) P.argb[(size_t)qy * P.W + qx] = a;
         }
     }
+    if (P.tile_cost && __lane_id() == 0) P.tile_cost[s_tile] = clock32() - s_clk0;  // one lane per wave, the last stays
   }
   else
   {
@@ -1209,19 +1222,15 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
       d[0] = out.r; d[1] = out.g; d[2] = out.b;
       if (P.argb) P.argb[o] = argb(out);                                           // Render::copyImage
     }
+    if (P.tile_cost && __lane_id() == 0) P.tile_cost[s_tile] = clock32() - s_clk0;  // one lane per wave, the last stays
   }
   flush_counters<STATS>(P, cnt);
   RFX_PROF_FLUSH();
-  if (P.tile_cost && lane == 0 && wave < 2u)  // a vector store from one lane of each of the first two waves
-  {
-    uint32_t *tc = P.tile_cost + 2u * (by * gridDim.x + bx);
-    tc[wave] = (uint32_t)min(__builtin_readcyclecounter() - clk0, 0xFFFFFFFFull);
-    if (kWgWaves == 1) tc[1] = 0;
-  }
+
 }
 
 // ------------------------------------------------------------- LPT tile order
-// The tile costs of a frame (two waves' clock cycles per tile) become the next launch's tile order, most
+// The tile costs of a frame (clock cycles per tile) become the next launch's tile order, most
 // expensive first: a counting sort on a log-scale key (exponent and 3 mantissa bits: buckets ~9% wide) over
 // kLptGroups workgroups -- per-group LDS histograms, one scan of (bucket, group) offsets, a scatter.  The
 // order within a bucket is whatever the LDS atomics give: any permutation renders the same pixels, only
@@ -1230,7 +1239,7 @@ constexpr int kLptThreads = 1024, kLptBuckets = 256, kLptGroups = 64;
 
 __device__ __forceinline__ uint32_t lpt_key(const uint32_t *cost, uint32_t i)
 {
-  const uint32_t c = max(cost[2u * i] + cost[2u * i + 1u], 1u);
+  const uint32_t c = max(cost[i], 1u);  // clock cycles from the workgroup's start to a wave's end (mod 2^32)
   const uint32_t e = 31u - (uint32_t)__clz(c);
   const uint32_t m = e >= 3u ? (c >> (e - 3u)) & 7u : (c << (3u - e)) & 7u;
   return (uint32_t)(kLptBuckets - 1) - min(e * 8u + m, (uint32_t)(kLptBuckets - 1));  // descending cost
@@ -1253,8 +1262,12 @@ __global__ __launch_bounds__(kLptBuckets) void lpt_scan(uint32_t *hist)
 {
   __shared__ uint32_t tot[kLptBuckets];
   const uint32_t b = threadIdx.x;
+  uint32_t v[kLptGroups];  // all loads first (independent), then the running sum in registers
+#pragma unroll
+  for (int g = 0; g < kLptGroups; ++g) v[g] = hist[g * kLptBuckets + b];
   uint32_t run = 0;
-  for (int g = 0; g < kLptGroups; ++g) { const uint32_t v = hist[g * kLptBuckets + b]; hist[g * kLptBuckets + b] = run; run += v; }
+#pragma unroll
+  for (int g = 0; g < kLptGroups; ++g) { const uint32_t c = v[g]; v[g] = run; run += c; }
   tot[b] = run;
   __syncthreads();
   if (b == 0)
@@ -1263,7 +1276,9 @@ __global__ __launch_bounds__(kLptBuckets) void lpt_scan(uint32_t *hist)
     for (int k = 0; k < kLptBuckets; ++k) { const uint32_t v = tot[k]; tot[k] = acc; acc += v; }
   }
   __syncthreads();
-  for (int g = 0; g < kLptGroups; ++g) hist[g * kLptBuckets + b] += tot[b];
+  const uint32_t base = tot[b];
+#pragma unroll
+  for (int g = 0; g < kLptGroups; ++g) hist[g * kLptBuckets + b] = v[g] + base;
 }
 
 __global__ __launch_bounds__(kLptThreads) void lpt_scatter(const uint32_t *cost, uint32_t n, uint32_t chunk,

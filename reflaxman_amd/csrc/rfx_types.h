@@ -90,7 +90,7 @@ struct FrameParams {
   const uint32_t *rd_state;     // per trace: LCG state before its accepted randomInsideSphere triple
   unsigned long long *counters; // C_COUNT u64, stats build only
   const uint32_t *tile_order;   // workgroup i renders tile tile_order[i] (previous frame's LPT order), or null: tile i
-  uint32_t *tile_cost;          // per tile and wave: its clock cycles this frame (the next frame's order), or null
+  uint32_t *tile_cost;          // per tile: its clock cycles this frame (the next frame's order), or null
 };
 
 }  // namespace rfx

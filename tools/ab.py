@@ -33,6 +33,9 @@ _HIP = C.CDLL("libamdhip64.so")
 VARIANTS = {
     "base": [],
     "wg2": ["RFX_WG_WAVES=2"],
+    "wg4": ["RFX_WG_WAVES=4"],
+    "wpe8": ["RFX_WAVES_PER_EU=8"],
+    "wpe6": ["RFX_WAVES_PER_EU=6"],
     "wg1": ["RFX_WG_WAVES=1"],
     "wpe7": ["RFX_WAVES_PER_EU=7"],
     "wg2wpe7": ["RFX_WG_WAVES=2", "RFX_WAVES_PER_EU=7"],
