@@ -396,6 +396,9 @@ extern "C" uint32_t rfx_strip_row_to_y(uint32_t r, uint32_t rb, uint32_t rank, u
 #ifndef RFX_TILE_ORDER_DEFAULT
 #define RFX_TILE_ORDER_DEFAULT 1
 #endif
+#ifndef RFX_TILE_ORDER_MIN_TILES
+#define RFX_TILE_ORDER_MIN_TILES 32768  // C3 (3840x2160) has 64,800 tiles of 16x8; C2 (1920x1080) 16,200
+#endif
 #ifndef RFX_TILE_SORT_EVERY
 #define RFX_TILE_SORT_EVERY 4  // tools/ab.py, C3: every launch -7.5% trace time vs raster order, every 4th -9.4%, every 16th -9.8%
 #endif
@@ -542,7 +545,7 @@ extern "C" int rfx_renderer_device(const rfx_renderer *r) { return r ? r->device
 
 extern "C" int rfx_renderer_set_tile_order(rfx_renderer *r, int mode)
 {
-  if (!r || mode < 0 || mode > 2) return fail(RFX_ERR_ARG, "renderer_set_tile_order: mode 0, 1 or 2");
+  if (!r || mode < 0 || mode > 3) return fail(RFX_ERR_ARG, "renderer_set_tile_order: mode 0, 1, 2 or 3");
   r->tile_mode = mode;
   return RFX_OK;
 }
@@ -903,7 +906,7 @@ static int tile_schedule(rfx_renderer *r, FrameParams &P, hipStream_t st, uint64
     r->tile_waited = st;
   }
   const bool same = r->tile_pending && r->tile_n == n && r->tile_key == key;
-  P.tile_order = (same && r->tile_mode == 1) ? r->d_tile_order : nullptr;
+  P.tile_order = (same && r->tile_mode != 2) ? r->d_tile_order : nullptr;
   // record (and re-sort) every RFX_TILE_SORT_EVERY-th launch, and at once after a grid change
   record = !same || r->tile_count % RFX_TILE_SORT_EVERY == 0;
   P.tile_cost = record ? r->d_tile_cost : nullptr;
@@ -926,7 +929,10 @@ static int finish_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *d_counts
   P.argb = d_argb;
   P.rd_state = r->d_rd;
   P.counters = (unsigned long long *)d_counters;
-  const bool sched = P.grid_rows && r->tile_mode && !d_counters;
+  // mode 1 schedules only launches of at least RFX_TILE_ORDER_MIN_TILES tiles: on shorter ones the sort's
+  // latency (three small launches and a cross-stream wait, ~15 us) is not hidden by the RNG pre-pass
+  const bool sched = P.grid_rows && r->tile_mode && !d_counters &&
+                     (r->tile_mode != 1 || trace_tiles(P) >= RFX_TILE_ORDER_MIN_TILES);
   uint64_t key = 0;
   bool record = false;
   if (sched && (rc = tile_schedule(r, P, st, key, record)) != RFX_OK) return rc;

@@ -105,13 +105,26 @@ def test_rand_dirs_prepass():
 def test_tile_order_changes_no_pixel(name, W, H, depth, ss, additive, chunks):
     """The longest-tile-first schedule (default) renders every frame exactly as raster order does."""
     frames = []
-    for mode in (0, 1):
+    for mode in (0, 3):  # raster order vs longest-first on every launch size
         got = []
         _, _, r = gpu_render(scene(name), W, H, depth, ss, additive, 9, tile_order=mode, chunks=chunks,
                              each_frame=lambda rgb, argb: got.append((rgb.tobytes(), argb.tobytes())))
         r.close()
         frames.append(got)
     assert len(frames[0]) == 9 and frames[0] == frames[1]
+
+
+def test_tile_order_default_full_size():
+    """C3 at full size, where the default schedule is on: 6 frames, bit-identical to raster order."""
+    frames = []
+    for mode in (0, 1):
+        got = []
+        _, _, r = gpu_render(scene("synth16"), 3840, 2160, 8, frames=6, tile_order=mode,
+                             each_frame=lambda rgb, argb: got.append((sha(rgb), sha(argb))))
+        r.close()
+        frames.append(got)
+    assert len(frames[0]) == 6 and frames[0] == frames[1]
+    assert frames[0][0] == (CASES["hash_synth16_3840x2160_d8"]["sha_f32"], CASES["hash_synth16_3840x2160_d8"]["sha_argb"])
 
 
 def test_rng_state_carries_across_frames():
