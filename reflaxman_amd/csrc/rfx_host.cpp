@@ -410,8 +410,10 @@ struct rfx_renderer {
   DevScene dev{};
   std::vector<void *> scene_allocs;
   bool has_scene = false;
-  // RNG state: d_seed[0] current, d_seed[1] next; d_err
+  // RNG state: d_seed[seed_idx] current; the pre-pass writes the next frame's state to the other word and
+  // the host flips seed_idx (no device copy between frames); d_err
   uint32_t *d_seed = nullptr;
+  uint32_t seed_idx = 0;
   int *d_err = nullptr;
   uint32_t jitter_seed = 0;
   // workspaces
@@ -437,6 +439,9 @@ struct rfx_renderer {
   std::vector<hipEvent_t> events;
   size_t events_used = 0;
 };
+
+static uint32_t *seed_cur(rfx_renderer *r) { return r->d_seed + r->seed_idx; }
+static uint32_t *seed_next(rfx_renderer *r) { return r->d_seed + (r->seed_idx ^ 1u); }
 
 static int timing_event(rfx_renderer *r, hipStream_t st)
 {
@@ -769,7 +774,7 @@ extern "C" int rfx_renderer_set_rng(rfx_renderer *r, uint32_t sphere_seed, uint3
   if (!r) return fail(RFX_ERR_ARG, "set_rng: null renderer");
   int rc;
   if ((rc = set_dev(r)) != RFX_OK) return rc;
-  HIP_CHECK(hipMemcpyAsync(r->d_seed, &sphere_seed, sizeof(uint32_t), hipMemcpyHostToDevice, r->stream));
+  HIP_CHECK(hipMemcpyAsync(seed_cur(r), &sphere_seed, sizeof(uint32_t), hipMemcpyHostToDevice, r->stream));
   HIP_CHECK(hipStreamSynchronize(r->stream));
   r->jitter_seed = jitter_seed;
   return RFX_OK;
@@ -782,7 +787,7 @@ extern "C" int rfx_renderer_get_rng(rfx_renderer *r, uint32_t *sphere_seed, uint
   if ((rc = set_dev(r)) != RFX_OK) return rc;
   uint32_t s = 0;
   int err = 0;
-  HIP_CHECK(hipMemcpyAsync(&s, r->d_seed, sizeof(uint32_t), hipMemcpyDeviceToHost, r->stream));
+  HIP_CHECK(hipMemcpyAsync(&s, seed_cur(r), sizeof(uint32_t), hipMemcpyDeviceToHost, r->stream));
   HIP_CHECK(hipMemcpyAsync(&err, r->d_err, sizeof(int), hipMemcpyDeviceToHost, r->stream));
   HIP_CHECK(hipStreamSynchronize(r->stream));
   if (err) return fail(RFX_ERR_RNG, "RNG pre-pass ran short of accepted triples");
@@ -825,16 +830,16 @@ static int ensure_rng_workspace(rfx_renderer *r, uint64_t traces, uint64_t nblk)
 }
 
 // Whole pre-pass on one device: every block counted here (the 1-GPU path, and the redundant form of the
-// multi-GPU one).  Sphere stream: d_seed[0] -> pre-pass -> d_seed[1] -> copied back to d_seed[0].
+// multi-GPU one).  Sphere stream: d_seed[seed_idx] -> pre-pass -> the other word, which becomes current.
 static int enqueue_rng(rfx_renderer *r, uint64_t traces, hipStream_t st)
 {
   int rc;
   const uint64_t nblk = rng_layout(traces, 1, nullptr);
   if ((rc = ensure_rng_workspace(r, traces, nblk)) != RFX_OK) return rc;
-  HIP_CHECK(launch_rng_count(r->d_seed, r->d_jump, r->d_blk_cnt, 0, nblk, st));
-  HIP_CHECK(launch_rng_finish(r->d_seed, r->d_jump, r->d_seed + 1, r->d_blk_cnt, nblk, traces, r->d_rd,
+  HIP_CHECK(launch_rng_count(seed_cur(r), r->d_jump, r->d_blk_cnt, 0, nblk, st));
+  HIP_CHECK(launch_rng_finish(seed_cur(r), r->d_jump, seed_next(r), r->d_blk_cnt, nblk, traces, r->d_rd,
                               r->d_err, 1, 1, 1, 0, 1, st));
-  HIP_CHECK(hipMemcpyAsync(r->d_seed, r->d_seed + 1, sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+  r->seed_idx ^= 1u;
   return RFX_OK;
 }
 
@@ -867,7 +872,7 @@ extern "C" int rfx_frame_rng_count(rfx_renderer *r, const rfx_frame *f, uint32_t
   uint64_t bps = 0;
   const uint64_t nblk = rng_layout(pl.traces, nslices, &bps);
   if ((rc = ensure_rng_workspace(r, pl.traces, nblk)) != RFX_OK) return rc;
-  HIP_CHECK(launch_rng_count(r->d_seed, r->d_jump, d_blk_counts, (uint64_t)slice * bps, bps, pl.st));
+  HIP_CHECK(launch_rng_count(seed_cur(r), r->d_jump, d_blk_counts, (uint64_t)slice * bps, bps, pl.st));
   return RFX_OK;
 }
 
@@ -921,9 +926,9 @@ static int finish_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *d_counts
   FrameParams &P = pl.P;
   const hipStream_t st = pl.st;
   const uint64_t ss2 = P.ss > 0 ? (uint64_t)(P.ss * P.ss) : 1;
-  HIP_CHECK(launch_rng_finish(r->d_seed, r->d_jump, r->d_seed + 1, d_counts, nblk, pl.traces, r->d_rd,
+  HIP_CHECK(launch_rng_finish(seed_cur(r), r->d_jump, seed_next(r), d_counts, nblk, pl.traces, r->d_rd,
                               r->d_err, ss2, P.W, P.row_block, P.rank, P.nranks, st));
-  HIP_CHECK(hipMemcpyAsync(r->d_seed, r->d_seed + 1, sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+  r->seed_idx ^= 1u;
   if ((rc = timing_event(r, st)) != RFX_OK) return rc;
   P.img = d_rgb;
   P.argb = d_argb;
@@ -981,7 +986,7 @@ extern "C" int rfx_render_frame(rfx_renderer *r, const rfx_frame *f, float *d_rg
   const uint64_t nblk = rng_layout(pl.traces, 1, nullptr);
   if ((rc = ensure_rng_workspace(r, pl.traces, nblk)) != RFX_OK) return rc;
   if ((rc = timing_event(r, pl.st)) != RFX_OK) return rc;
-  HIP_CHECK(launch_rng_count(r->d_seed, r->d_jump, r->d_blk_cnt, 0, nblk, pl.st));
+  HIP_CHECK(launch_rng_count(seed_cur(r), r->d_jump, r->d_blk_cnt, 0, nblk, pl.st));
   return finish_frame(r, pl, r->d_blk_cnt, nblk, d_rgb, d_argb, d_counters);
 }
 
@@ -1142,15 +1147,15 @@ extern "C" int rfx_rand_dirs(rfx_renderer *r, uint32_t seed, uint64_t n, float *
   int rc;
   if ((rc = set_dev(r)) != RFX_OK) return rc;
   uint32_t saved = 0;
-  HIP_CHECK(hipMemcpyAsync(&saved, r->d_seed, sizeof(uint32_t), hipMemcpyDeviceToHost, r->stream));
+  HIP_CHECK(hipMemcpyAsync(&saved, seed_cur(r), sizeof(uint32_t), hipMemcpyDeviceToHost, r->stream));
   HIP_CHECK(hipStreamSynchronize(r->stream));
-  HIP_CHECK(hipMemcpyAsync(r->d_seed, &seed, sizeof(uint32_t), hipMemcpyHostToDevice, r->stream));
+  HIP_CHECK(hipMemcpyAsync(seed_cur(r), &seed, sizeof(uint32_t), hipMemcpyHostToDevice, r->stream));
   if ((rc = enqueue_rng(r, n, r->stream)) != RFX_OK) return rc;
   std::vector<uint32_t> states(n);
   HIP_CHECK(hipMemcpyAsync(states.data(), r->d_rd, n * sizeof(uint32_t), hipMemcpyDeviceToHost, r->stream));
   uint32_t after = 0;
-  HIP_CHECK(hipMemcpyAsync(&after, r->d_seed, sizeof(uint32_t), hipMemcpyDeviceToHost, r->stream));
-  HIP_CHECK(hipMemcpyAsync(r->d_seed, &saved, sizeof(uint32_t), hipMemcpyHostToDevice, r->stream));
+  HIP_CHECK(hipMemcpyAsync(&after, seed_cur(r), sizeof(uint32_t), hipMemcpyDeviceToHost, r->stream));  // flipped
+  HIP_CHECK(hipMemcpyAsync(seed_cur(r), &saved, sizeof(uint32_t), hipMemcpyHostToDevice, r->stream));
   if ((rc = rfx_synchronize(r)) != RFX_OK) return rc;
   for (uint64_t i = 0; i < n; ++i)  // Vector3.cpp:182-184 from each trace's state
   {
