@@ -1330,16 +1330,33 @@ __device__ __forceinline__ bool triple(uint32_t &s, float &x, float &y, float &z
   return !(x * x + y * y + z * z > 1.f);                                        // Vector3.cpp:185
 }
 
+// A thread's 16-triple run as two chains of 8 triples each (the second starts 24 draws later: one affine
+// jump), so two independent LCG dependency chains interleave -- the same states, half the serial latency.
+constexpr int kHalfRun = kTriplesPerThread / 2;
+struct LcgJump { uint32_t a, c; };
+constexpr LcgJump lcg_jump_const(int draws)
+{
+  uint32_t a = 1u, c = 0u;
+  for (int i = 0; i < draws; ++i) { a = 214013u * a; c = 214013u * c + 2531011u; }
+  return LcgJump{a, c};
+}
+constexpr LcgJump kHalfJump = lcg_jump_const(3 * kHalfRun);
+
 // accepted-triple count of blocks [blk0, blk0 + gridDim.x): one slice of the stream (multi-GPU: one per rank)
 __global__ __launch_bounds__(kRngBlock) void rng_count(const uint32_t *seed, const uint32_t *jump, uint32_t *blk_cnt,
                                                        uint64_t blk0)
 {
   const uint64_t b = blk0 + blockIdx.x;
   uint32_t s = thread_state(*seed, jump, b, threadIdx.x);
+  uint32_t s2 = kHalfJump.a * s + kHalfJump.c;
   uint32_t c = 0;
   float x, y, z;
-#pragma unroll 4
-  for (int j = 0; j < kTriplesPerThread; ++j) c += triple(s, x, y, z) ? 1u : 0u;
+#pragma unroll
+  for (int j = 0; j < kHalfRun; ++j)
+  {
+    c += triple(s, x, y, z) ? 1u : 0u;
+    c += triple(s2, x, y, z) ? 1u : 0u;
+  }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
   __shared__ uint32_t wsum[kRngBlock / 64];
@@ -1405,16 +1422,18 @@ __global__ __launch_bounds__(kRngBlock) void rng_emit(const uint32_t *seed, cons
     if (!any) return;
   }
   uint32_t s = thread_state(*seed, jump, blockIdx.x, threadIdx.x);
+  uint32_t s2 = kHalfJump.a * s + kHalfJump.c;
   uint32_t st[kTriplesPerThread];
   uint32_t acc = 0, c = 0;
   float x, y, z;
 #pragma unroll
-  for (int j = 0; j < kTriplesPerThread; ++j)
+  for (int j = 0; j < kHalfRun; ++j)
   {
     st[j] = s;
-    const bool a = triple(s, x, y, z);
-    acc |= (a ? 1u : 0u) << j;
-    c += a ? 1u : 0u;
+    st[j + kHalfRun] = s2;
+    const bool a = triple(s, x, y, z), a2 = triple(s2, x, y, z);
+    acc |= (a ? 1u : 0u) << j | (a2 ? 1u : 0u) << (j + kHalfRun);
+    c += (a ? 1u : 0u) + (a2 ? 1u : 0u);
   }
   // exclusive scan of c across the workgroup
   const uint32_t lane = threadIdx.x & 63;

@@ -190,9 +190,22 @@ RFX_HD uint32_t lcg_jump(uint32_t s, uint64_t n)
 }
 // one component of Vector3::randomInsideSphere (Vector3.cpp:182-184)
 RFX_HD float rand_component(uint32_t k) { return (float)k / ((float)0x7FFF / 2) - 1.f; }
-// The same value without the f32 divide (the RNG pre-pass kernels): for every k in [0, 0x7FFF],
-// (float)k / 16383.5f == (float)((double)k * (1.0 / 16383.5)) -- checked exhaustively by
-// tests/test_rng_exact.py -- and the subtraction of 1 is the reference's own.
-RFX_HD float rand_component_dev(uint32_t k) { return (float)((double)k * (1.0 / 16383.5)) - 1.f; }
+// The same value without the f32 divide (the RNG pre-pass kernels), and the subtraction of 1 is the
+// reference's own.  For every k in [0, 0x7FFF] the quotient (float)k / 16383.5f equals
+//   host:   (float)((double)k * (1.0 / 16383.5))
+//   device: q = k * r, e = fma(-q, 16383.5, k), q + e * r as one fma (r = f32(1 / 16383.5)),
+// f32 only (f64 multiplies and conversions run at a fraction of the f32 rate) -- both checked
+// exhaustively by tests/test_rng_exact.py.
+RFX_HD float rand_component_dev(uint32_t k)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+  const float kf = (float)k, r = 1.0f / 16383.5f;
+  const float q = kf * r;
+  const float e = __builtin_fmaf(-q, 16383.5f, kf);
+  return __builtin_fmaf(e, r, q) - 1.f;
+#else
+  return (float)((double)k * (1.0 / 16383.5)) - 1.f;
+#endif
+}
 
 }  // namespace rfx
