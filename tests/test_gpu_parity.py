@@ -240,6 +240,59 @@ def test_sliced_rng_prepass_multi_rank(nranks, row_block, ss):
     whole.close()
 
 
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_strips_with_tile_order_over_frames(nranks):
+    """Strip frames (the multi-GPU path, ranks emulated in one process) with the longest-first schedule on
+    every launch (mode 3): each of 5 consecutive frames assembles to the raster-order 1-GPU frame."""
+    import ctypes as C
+    from reflaxman_amd import _lib
+    from reflaxman_amd.render import Renderer, build_scene, make_frame
+    desc = scene("synth16")
+    W, H, depth, rb, frames = 200, 120, 8, 8, 5
+    s, cam = build_scene(desc)
+    L = _lib.load()
+
+    def fetch(rr, d, n):
+        a = np.empty(n, np.uint32)
+        _lib.check(L.rfx_memcpy_d2h(rr._h, a.ctypes.data_as(C.c_void_p), d, a.nbytes))
+        return a
+
+    whole = Renderer(sphere_seed=4242)
+    whole.set_scene(s)
+    whole.set_tile_order(0)
+    d_img, d_argb = C.c_void_p(), C.c_void_p()
+    _lib.check(L.rfx_device_alloc(whole._h, W * H * 12, C.byref(d_img)))
+    _lib.check(L.rfx_device_alloc(whole._h, W * H * 4, C.byref(d_argb)))
+    refs = []
+    for _ in range(frames):
+        whole.render_frame(make_frame(cam, W, H, depth, 1), d_img.value, d_argb.value)
+        refs.append(fetch(whole, d_argb, W * H).reshape(H, W))
+    got = [np.zeros((H, W), np.uint32) for _ in range(frames)]
+    for rank in range(nranks):
+        rr = Renderer(sphere_seed=4242)
+        rr.set_scene(s)
+        rr.set_tile_order(3)
+        f = make_frame(cam, W, H, depth, 1, row_block=rb, rank=rank, nranks=nranks)
+        bps = C.c_uint64()
+        _lib.check(L.rfx_frame_rng_blocks(rr._h, C.byref(f), nranks, C.byref(bps)))
+        d_cnt = C.c_void_p()
+        _lib.check(L.rfx_device_alloc(rr._h, nranks * bps.value * 4, C.byref(d_cnt)))
+        rows = L.rfx_strip_rows(H, rb, rank, nranks)
+        p_img, p_argb = C.c_void_p(), C.c_void_p()
+        _lib.check(L.rfx_device_alloc(rr._h, rows * W * 12, C.byref(p_img)))
+        _lib.check(L.rfx_device_alloc(rr._h, rows * W * 4, C.byref(p_argb)))
+        ys = [L.rfx_strip_row_to_y(i, rb, rank, nranks) for i in range(rows)]
+        for k in range(frames):
+            for sl in range(nranks):  # what the all-gather assembles from every rank's slice
+                _lib.check(L.rfx_frame_rng_count(rr._h, C.byref(f), sl, nranks, d_cnt, None))
+            _lib.check(L.rfx_render_frame_counted(rr._h, C.byref(f), nranks, d_cnt, p_img, p_argb, None, None))
+            got[k][ys] = fetch(rr, p_argb, rows * W).reshape(rows, W)
+        rr.close()
+    for k in range(frames):
+        assert np.array_equal(got[k], refs[k]), k
+    whole.close()
+
+
 def test_event_counters_match_oracle():
     """The stats kernel's event counts equal the CPU restatement's (same algorithm, same branches)."""
     import ctypes as C
