@@ -97,11 +97,12 @@ int rfx_renderer_device(const rfx_renderer *r);
 int rfx_renderer_set_stream(rfx_renderer *r, void *hip_stream);
 /* upload the scene (host precompute already done by the builder calls) */
 int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *scene);
-/* Trace-launch schedule (no effect on any pixel): 1 (default) = on launches of >= 32768 tiles (16x8 pixels
- * each; 3840x2160 has 64,800) workgroups take the tiles longest-first, in the order sorted from an earlier
- * launch's measured per-tile clock costs of the same grid (re-sorted every 4th launch; the first launch, or
- * one after a grid change, runs tiles in raster order); 3 = the same on every launch size; 0 = raster
- * order, no cost recording; 2 = raster order with cost recording (A/B of the sort's overhead). */
+/* Trace-launch schedule (no effect on any pixel): 1 (default) = on launches of >= 65536 tiles (8x8 pixels,
+ * one wave each; 3840x2160 has 129,600) waves take the tiles longest-first, in the order sorted from an
+ * earlier launch's measured per-tile clock costs of the same grid (re-sorted every 4th launch; the first
+ * launch, or one after a grid change, runs tiles in raster order); 3 = the same on every launch size;
+ * 0 = raster order, no cost recording; 2 = raster order with cost recording (A/B of the sort's overhead).
+ * Block-preview frames (sample_num < 0) always run in raster order. */
 int rfx_renderer_set_tile_order(rfx_renderer *r, int mode);
 /* The reference's two LCG streams (trace_math.h:34-39): Vector3.cpp's (randomInsideSphere) and
  * Render.cpp's (additive jitter).  Both persist across frames exactly as the reference's would. */

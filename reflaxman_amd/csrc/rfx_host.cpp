@@ -397,7 +397,10 @@ extern "C" uint32_t rfx_strip_row_to_y(uint32_t r, uint32_t rb, uint32_t rank, u
 #define RFX_TILE_ORDER_DEFAULT 1
 #endif
 #ifndef RFX_TILE_ORDER_MIN_TILES
-#define RFX_TILE_ORDER_MIN_TILES 32768  // C3 (3840x2160) has 64,800 tiles of 16x8; C2 (1920x1080) 16,200
+#define RFX_TILE_ORDER_MIN_TILES 65536  // 8x8 wave tiles: C3 (3840x2160) has 129,600, C2 (1920x1080) 32,400
+#endif
+#ifndef RFX_WAVE_TILES  // schedule unit: the wave's 8x8 tile (1) or the workgroup's 16x8 (0); tools/ab.py, C3: -2.7% trace
+#define RFX_WAVE_TILES 1
 #endif
 #ifndef RFX_TILE_SORT_EVERY
 #define RFX_TILE_SORT_EVERY 4  // tools/ab.py, C3: every launch -7.5% trace time vs raster order, every 4th -9.4%, every 16th -9.8%
@@ -936,7 +939,7 @@ static int finish_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *d_counts
   P.counters = (unsigned long long *)d_counters;
   // mode 1 schedules only launches of at least RFX_TILE_ORDER_MIN_TILES tiles: on shorter ones the sort's
   // latency (three small launches and a cross-stream wait, ~15 us) is not hidden by the RNG pre-pass
-  const bool sched = P.grid_rows && r->tile_mode && !d_counters &&
+  const bool sched = P.grid_rows && r->tile_mode && !d_counters && !(RFX_WAVE_TILES && P.ss < 0) &&
                      (r->tile_mode != 1 || trace_tiles(P) >= RFX_TILE_ORDER_MIN_TILES);
   uint64_t key = 0;
   bool record = false;

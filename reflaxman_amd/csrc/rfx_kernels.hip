@@ -1061,6 +1061,10 @@ __device__ __forceinline__ v3 rd_from_state(uint32_t s)
 
 __device__ __forceinline__ v3 load_rd(const FrameParams &P, uint64_t i) { return rd_from_state(P.rd_state[i]); }
 
+#ifndef RFX_WAVE_TILES  // schedule unit: the wave's 8x8 tile (1) or the workgroup's 16x8 (0); tools/ab.py, C3: -2.7% trace
+#define RFX_WAVE_TILES 1
+#endif
+
 // Shader clock, low 32 bits.  A plain asm statement (no side effects declared, so the compiler may still
 // serve the scene loads that follow through the scalar cache -- __builtin_readcyclecounter would count as a
 // memory clobber for them); it waits for its own result.
@@ -1128,9 +1132,19 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
     for (int k = 0; k < C_COUNT; ++k) cnt.c[k] = 0;
   }
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+#if RFX_WAVE_TILES
+  // the schedule's unit is the wave's 8x8 tile: wave v of workgroup w renders tile tile_order[2w + v] of the
+  // (2 gridDim.x) x gridDim.y tile grid (identity: the workgroup's own two tiles side by side)
+  static_assert(kWgWaves == 2 && kTileWavesX == 2, "RFX_WAVE_TILES: two waves side by side");
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(wave), wid = blockIdx.y * gridDim.x + blockIdx.x;
+  const uint32_t t8 = P.tile_order ? P.tile_order[2u * wid + wv] : 2u * wid + wv;
+  const uint32_t gx = (t8 % (2u * gridDim.x)) * 8u + (lane & 7u), gy = (t8 / (2u * gridDim.x)) * 8u + (lane >> 3);
+  (void)tile;
+#else
   const uint32_t lx = (wave % kTileWavesX) * 8u + (lane & 7u), ly = (wave / kTileWavesX) * 8u + (lane >> 3);
   const uint32_t bx = tile % gridDim.x, by = tile / gridDim.x;
   const uint32_t gx = bx * kTileW + lx, gy = by * kTileH + ly;
+#endif
   m33 view;
   view.m11 = P.v11; view.m12 = P.v12; view.m13 = P.v13;
   view.m21 = P.v21; view.m22 = P.v22; view.m23 = P.v23;
@@ -1222,7 +1236,12 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
       d[0] = out.r; d[1] = out.g; d[2] = out.b;
       if (P.argb) P.argb[o] = argb(out);                                           // Render::copyImage
     }
+#if RFX_WAVE_TILES
+    if (P.tile_cost && __lane_id() == 0)  // per wave tile, located from the live pixel (x, orow)
+      P.tile_cost[(P.nranks > 1 ? orow : orow - P.row0) / 8u * P.tiles_x + x / 8u] = clock32() - s_clk0;
+#else
     if (P.tile_cost && __lane_id() == 0) P.tile_cost[s_tile] = clock32() - s_clk0;  // one lane per wave, the last stays
+#endif
   }
   flush_counters<STATS>(P, cnt);
   RFX_PROF_FLUSH();
@@ -1594,12 +1613,14 @@ static dim3 trace_grid(const FrameParams &P)
 uint32_t trace_tiles(const FrameParams &P)
 {
   const dim3 g = trace_grid(P);
-  return g.x * g.y;
+  return (RFX_WAVE_TILES ? 2u : 1u) * g.x * g.y;
 }
 
 hipError_t launch_trace(const DevScene &S, const FrameParams &P, bool stats, hipStream_t st)
 {
   const dim3 grid = trace_grid(P);
+  FrameParams Pt = P;
+  Pt.tiles_x = 2u * grid.x;  // wave tiles per row (RFX_WAVE_TILES)
   const int mode = P.ss < 0 ? kModeBlock : (P.ss == 1 && !P.additive && !P.accumulate) ? kModePlain : kModeSsaa;
   // the stats build counts the reference's every test, so it never culls
   int cfg = (S.n_light > 32 ? kCfgManyLights : 0) | (stats ? 0 : kCfgCull) |
@@ -1607,7 +1628,7 @@ hipError_t launch_trace(const DevScene &S, const FrameParams &P, bool stats, hip
 #ifdef RFX_NO_CULL
   cfg &= ~kCfgCull;
 #endif
-  launch_mode_cfg(stats, mode, cfg, grid, S, P, st);
+  launch_mode_cfg(stats, mode, cfg, grid, S, Pt, st);
   return hipGetLastError();
 }
 

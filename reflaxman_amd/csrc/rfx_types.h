@@ -91,6 +91,7 @@ struct FrameParams {
   unsigned long long *counters; // C_COUNT u64, stats build only
   const uint32_t *tile_order;   // workgroup i renders tile tile_order[i] (previous frame's LPT order), or null: tile i
   uint32_t *tile_cost;          // per tile: its clock cycles this frame (the next frame's order), or null
+  uint32_t tiles_x;             // schedule tiles per grid row (set by launch_trace)
 };
 
 }  // namespace rfx

@@ -267,9 +267,9 @@ class Renderer:
         check(_lib.load().rfx_synchronize(self._h), "rfx_synchronize")
 
     def set_tile_order(self, mode: int):
-        """Trace-launch schedule (rfx.h rfx_renderer_set_tile_order): 1 longest-tile-first from earlier
-        launches' tile costs on large launches (default), 3 on every launch, 0 raster order, 2 raster order
-        with cost recording.  No pixel changes."""
+        """Trace-launch schedule (rfx.h rfx_renderer_set_tile_order): 1 longest-tile-first (8x8 wave tiles)
+        from earlier launches' tile costs on large launches (default), 3 on every launch, 0 raster order,
+        2 raster order with cost recording.  No pixel changes."""
         check(_lib.load().rfx_renderer_set_tile_order(self._h, int(mode)), "set_tile_order")
 
     def set_timing(self, enable: bool):
