@@ -1133,12 +1133,13 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
   }
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
 #if RFX_WAVE_TILES
-  // the schedule's unit is the wave's 8x8 tile: wave v of workgroup w renders tile tile_order[2w + v] of the
-  // (2 gridDim.x) x gridDim.y tile grid (identity: the workgroup's own two tiles side by side)
-  static_assert(kWgWaves == 2 && kTileWavesX == 2, "RFX_WAVE_TILES: two waves side by side");
+  // the schedule's unit is the wave's 8x8 tile: wave v of workgroup w renders tile tile_order[kWgWaves w + v]
+  // of the (kTileWavesX gridDim.x) x (kTileWavesY gridDim.y) tile grid (identity: the workgroup's own tiles)
   const uint32_t wv = __builtin_amdgcn_readfirstlane(wave), wid = blockIdx.y * gridDim.x + blockIdx.x;
-  const uint32_t t8 = P.tile_order ? P.tile_order[2u * wid + wv] : 2u * wid + wv;
-  const uint32_t gx = (t8 % (2u * gridDim.x)) * 8u + (lane & 7u), gy = (t8 / (2u * gridDim.x)) * 8u + (lane >> 3);
+  const uint32_t w8 = kTileWavesX * gridDim.x;
+  const uint32_t t8 = P.tile_order ? P.tile_order[kWgWaves * wid + wv]
+                                   : (blockIdx.y * kTileWavesY + wv / kTileWavesX) * w8 + blockIdx.x * kTileWavesX + wv % kTileWavesX;
+  const uint32_t gx = (t8 % w8) * 8u + (lane & 7u), gy = (t8 / w8) * 8u + (lane >> 3);
   (void)tile;
 #else
   const uint32_t lx = (wave % kTileWavesX) * 8u + (lane & 7u), ly = (wave / kTileWavesX) * 8u + (lane >> 3);
@@ -1613,14 +1614,14 @@ static dim3 trace_grid(const FrameParams &P)
 uint32_t trace_tiles(const FrameParams &P)
 {
   const dim3 g = trace_grid(P);
-  return (RFX_WAVE_TILES ? 2u : 1u) * g.x * g.y;
+  return (RFX_WAVE_TILES ? kWgWaves : 1u) * g.x * g.y;
 }
 
 hipError_t launch_trace(const DevScene &S, const FrameParams &P, bool stats, hipStream_t st)
 {
   const dim3 grid = trace_grid(P);
   FrameParams Pt = P;
-  Pt.tiles_x = 2u * grid.x;  // wave tiles per row (RFX_WAVE_TILES)
+  Pt.tiles_x = kTileWavesX * grid.x;  // wave tiles per row (RFX_WAVE_TILES)
   const int mode = P.ss < 0 ? kModeBlock : (P.ss == 1 && !P.additive && !P.accumulate) ? kModePlain : kModeSsaa;
   // the stats build counts the reference's every test, so it never culls
   int cfg = (S.n_light > 32 ? kCfgManyLights : 0) | (stats ? 0 : kCfgCull) |
