@@ -42,6 +42,8 @@ VARIANTS = {
     "raster": ["RFX_TILE_ORDER_DEFAULT=0"],
     "rastercost": ["RFX_TILE_ORDER_DEFAULT=2"],
     "every1": ["RFX_TILE_SORT_EVERY=1"],
+    "every2": ["RFX_TILE_SORT_EVERY=2"],
+    "every8": ["RFX_TILE_SORT_EVERY=8"],
     "wgtiles": ["RFX_WAVE_TILES=0"],
     "every16": ["RFX_TILE_SORT_EVERY=16"],
 }
