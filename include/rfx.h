@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define RFX_ABI_VERSION 1
+#define RFX_ABI_VERSION 2
 
 typedef enum {
   RFX_OK = 0,
@@ -56,6 +56,13 @@ int rfx_scene_add_sphere(rfx_scene *scene, const float center[3], float radius, 
 /* Scene::addTriangle(v1, v2, v3, material) -- Scene.cpp:41-46, Triangle.cpp:11-21.  Returns the object index. */
 int rfx_scene_add_triangle(rfx_scene *scene, const float v1[3], const float v2[3], const float v3[3],
                            int material_type, const float rgb[3], float reflectivity, float transparency);
+/* Plane(pos, norm, material) -- Plane.cpp:9-14, traced by Plane::trace (Plane.cpp:36-73).  The reference's
+ * Scene cannot hold a Plane (no addPlane); this is its natural extension: the plane takes an
+ * object index in insertion order like any other object (closest-hit ties, shadow self-skip).  The normal is
+ * used as given (the reference never normalises it).  Returns the object index. */
+int rfx_scene_add_plane(rfx_scene *scene, const float pos[3], const float norm[3], int material_type,
+                        const float rgb[3], float reflectivity, float transparency);
+int rfx_scene_plane_count(const rfx_scene *scene);
 /* Triangle::setTexture(texture, u1, v1, u2, v2, u3, v3) -- Triangle.cpp:110-120.  uv = {u1,v1,u2,v2,u3,v3}. */
 int rfx_triangle_set_texture(rfx_scene *scene, int object_index, int texture_index, const float uv[6]);
 /* Scene::addLight(origin, radius, color, power) -- Scene.cpp:48-59, OmniLight.cpp:8-14.  Returns the light index. */
@@ -136,7 +143,7 @@ uint32_t rfx_strip_row_to_y(uint32_t r, uint32_t row_block, uint32_t rank, uint3
  *   d_argb : device uint32, strip_rows x W, Color::argb of the stored value (copyImage), or NULL
  *   d_counters : device uint64[RFX_NCOUNTERS] accumulated event counters (stats kernel), or NULL
  */
-#define RFX_NCOUNTERS 35
+#define RFX_NCOUNTERS 40
 int rfx_render_frame(rfx_renderer *r, const rfx_frame *frame, float *d_rgb, uint32_t *d_argb,
                      uint64_t *d_counters, void *stream);
 
@@ -176,6 +183,23 @@ int rfx_synchronize(rfx_renderer *r);
 /* Sample the RNG stream: the first n randomInsideSphere draws from `seed` (Vector3.cpp:176-188),
  * computed by the device pre-pass, n x 3 floats to host.  *seed_out = state after them. */
 int rfx_rand_dirs(rfx_renderer *r, uint32_t seed, uint64_t n, float *out3, uint32_t *seed_out);
+
+/*
+ * Device known-answer entry points (validation).  Each runs the trace kernel's own device code on host
+ * arrays and returns host results, synchronously, on the scene last uploaded by rfx_renderer_set_scene:
+ *   rfx_kat_objects: ray i = rays[6i..6i+5] (origin, direction) against object objects[i] alone ->
+ *       out[15i..]: hit, drop3, normal3, reflected ray3, distance, material colour3 (texel of a textured
+ *       triangle), any-hit -- SceneObject::trace with and without out-parameters (Sphere.cpp:44-85,
+ *       Triangle.cpp:53-108, Plane.cpp:36-73);
+ *   rfx_kat_texels: texture >= 0: Texture::getTexelColor(u, v) (in n x 2, Texture.cpp:231-269) of that scene
+ *       texture; texture < 0: Skybox::getTexelColor(ray) (in n x 3, Skybox.cpp:39-106) -> out n x 3;
+ *   rfx_kat_powf: powf(x, y) as Scene.cpp:175,196 evaluate it (in n x 2 -> out n);
+ *   rfx_kat_argb: Color::argb (Color.cpp:114-117) (in n x 3 -> out n).
+ */
+int rfx_kat_objects(rfx_renderer *r, const float *rays, const int32_t *objects, uint64_t n, float *out);
+int rfx_kat_texels(rfx_renderer *r, int texture, const float *in, uint64_t n, float *out);
+int rfx_kat_powf(rfx_renderer *r, const float *xy, uint64_t n, float *out);
+int rfx_kat_argb(rfx_renderer *r, const float *rgb, uint64_t n, uint32_t *out);
 
 #ifdef __cplusplus
 }

@@ -26,6 +26,7 @@ COUNTER_NAMES = [
     "l_eval", "l_facing", "l_lit", "l_spec", "l_pow",
     "dielectric", "metal", "continue", "sky",
     "tex_bilinear", "tex_checker", "tex_other",
+    "pln_tests", "pln_t", "hit_pln", "sh_pln_tests", "sh_pln_t",
 ]
 
 _fp = C.POINTER(C.c_float)
@@ -55,6 +56,7 @@ def lib():
         L.orc_add_light.argtypes = [C.c_void_p, _fp, C.c_float, _fp, C.c_float]
         L.orc_add_sphere.argtypes = [C.c_void_p, _fp, C.c_float, C.c_int, _fp, C.c_float, C.c_float]
         L.orc_add_triangle.argtypes = [C.c_void_p, _fp, _fp, _fp, C.c_int, _fp, C.c_float, C.c_float]
+        L.orc_add_plane.argtypes = [C.c_void_p, _fp, _fp, C.c_int, _fp, C.c_float, C.c_float]
         L.orc_triangle_set_texture.argtypes = [C.c_void_p, C.c_int, C.c_int, _fp]
         L.orc_camera_view.argtypes = [_fp, _fp, _fp]
         L.orc_render.argtypes = [C.c_void_p, _fp, _fp, C.c_float, C.c_uint32, C.c_uint32, C.c_int, C.c_int,
@@ -108,6 +110,8 @@ class OracleScene:
             mt, rgb, refl, tr = ob[-1]
             if ob[0] == "sphere":
                 L.orc_add_sphere(self.h, _f(ob[1])[1], ob[2], mt, _f(rgb)[1], refl, tr)
+            elif ob[0] == "plane":
+                L.orc_add_plane(self.h, _f(ob[1])[1], _f(ob[2])[1], mt, _f(rgb)[1], refl, tr)
             else:
                 L.orc_add_triangle(self.h, _f(ob[1])[1], _f(ob[2])[1], _f(ob[3])[1], mt, _f(rgb)[1], refl, tr)
         for (oi, ti, uv) in desc.settex:

@@ -10,6 +10,10 @@
  *       (src/common/Scene.cpp:10-71), Triangle::setTexture (Triangle.cpp:110-120)
  *   Sphere/Triangle/Plane::trace, Skybox::getTexelColor, Texture::getTexelColor,
  *   Color::argb, Vector3::randomInsideSphere, Camera ctor  (KAT modes)
+ *   Texture(fileName) / loadFromFile, Texture(w, h) + saveToFile (file-format modes)
+ * Scene has no addPlane; a scene file's "plane" line puts a reference Plane (Plane.cpp) into the Scene's
+ * object list through a pointer to that private member (formed by the explicit-instantiation rule of
+ * [temp.explicit], no source change), so the reference's own Scene::trace renders it.
  * Used to generate tests/golden/* and, on the GPU box, as the timed
  * "reference" CPU baseline of bench.py.
  *
@@ -28,6 +32,16 @@
 #include "Render.h"
 #include "Plane.h"
 #include "Skybox.h"
+
+// Scene::sceneObjects (Scene.h:15-19) is private and Scene has no addPlane: a pointer to the member, formed in
+// an explicit template instantiation (where access checking does not apply), lets the harness append a Plane.
+typedef std::vector<SceneObject *> Scene::*SceneObjectsPtr;
+template <SceneObjectsPtr M>
+struct SceneObjectsAccess {
+  friend SceneObjectsPtr scene_objects_member() { return M; }
+};
+SceneObjectsPtr scene_objects_member();
+template struct SceneObjectsAccess<&Scene::sceneObjects>;
 
 static void die(const char *msg) { fprintf(stderr, "refharness: %s\n", msg); exit(2); }
 
@@ -113,6 +127,14 @@ static void load_scene(Render &r, const char *scene_arg)
       if (f.size() != 15) die("triangle");
       objects_tri.push_back(r.scene.addTriangle(Vector3(f[0], f[1], f[2]), Vector3(f[3], f[4], f[5]), Vector3(f[6], f[7], f[8]),
                         Material(f[9] != 0.0f ? Material::mtDielectric : Material::mtMetal, Color(f[10], f[11], f[12]), f[13], f[14])));
+    }
+    else if (!strcmp(kw, "plane"))
+    {
+      if (f.size() != 12) die("plane");
+      Plane *pl = new Plane(Vector3(f[0], f[1], f[2]), Vector3(f[3], f[4], f[5]),
+                            Material(f[6] != 0.0f ? Material::mtDielectric : Material::mtMetal, Color(f[7], f[8], f[9]), f[10], f[11]));
+      (r.scene.*scene_objects_member()).push_back(pl);  // owned and deleted by ~Scene (Scene.cpp:17-27)
+      objects_tri.push_back(NULL);
     }
     else if (!strcmp(kw, "settex"))
     {
@@ -383,6 +405,36 @@ int main(int argc, char **argv)
     std::vector<float> out(n);
     for (size_t i = 0; i < n; ++i) out[i] = pow(f[i * 2], f[i * 2 + 1]);
     write_file(argv[3], n ? &out[0] : NULL, out.size() * 4);
+    return 0;
+  }
+  if (mode == "savetex")
+  {
+    // savetex W H IN OUT : Texture(W, H) filled with IN's W*H ARGB words, saveToFile(OUT) (.bmp / .tga)
+    if (argc != 6) die("savetex W H IN OUT");
+    unsigned W = atoi(argv[2]), H = atoi(argv[3]);
+    std::vector<char> in = read_file(argv[4]);
+    if (in.size() != (size_t)W * H * 4) die("savetex: input size");
+    Texture t(W, H);
+    memcpy(t.getColorBuffer(), &in[0], in.size());
+    printf("%d\n", t.saveToFile(argv[5]) ? 1 : 0);
+    return 0;
+  }
+  if (mode == "loadtex")
+  {
+    // loadtex IN OUT : Texture::loadFromFile(IN) (what Scene::addTexture does) -> OUT: ok, w, h, texels
+    if (argc != 4) die("loadtex IN OUT");
+    Texture t;
+    const bool ok = t.loadFromFile(argv[2]);
+    std::vector<uint32_t> out;
+    out.push_back(ok ? 1u : 0u);
+    out.push_back(t.getWidth());
+    out.push_back(t.getHeight());
+    if ((size_t)t.getWidth() * t.getHeight())
+    {
+      const ARGB *p = t.getColorBuffer();
+      out.insert(out.end(), p, p + (size_t)t.getWidth() * t.getHeight());
+    }
+    write_file(argv[3], &out[0], out.size() * 4);
     return 0;
   }
   die("unknown mode");

@@ -121,7 +121,8 @@ typedef struct {
   v3 v0, norm; m33 ax; m33 tuv; float tu0, tv0; int tex; mat_t mat;
 } tri_t;
 typedef struct { v3 origin; float radius; col color; float power; } light_t;
-typedef struct { int kind; int idx; } obj_t; /* kind 0 sphere, 1 triangle */
+typedef struct { v3 pos, norm; mat_t mat; } plane_t;
+typedef struct { int kind; int idx; } obj_t; /* kind 0 sphere, 1 triangle, 2 plane */
 
 struct orc_scene {
   col diff_color, env_color;
@@ -130,6 +131,7 @@ struct orc_scene {
   int skybox_tex;
   sphere_t *spheres; int n_spheres;
   tri_t *tris; int n_tris;
+  plane_t *planes; int n_planes;
   obj_t *objs; int n_objs;
   light_t *lights; int n_lights;
   tex_t *texs; int n_texs;
@@ -153,7 +155,7 @@ void orc_scene_free(orc_scene *s)
 {
   if (!s) return;
   for (int i = 0; i < s->n_texs; ++i) free(s->texs[i].texels);
-  free(s->texs); free(s->spheres); free(s->tris); free(s->objs); free(s->lights);
+  free(s->texs); free(s->spheres); free(s->tris); free(s->planes); free(s->objs); free(s->lights);
   free(s);
 }
 
@@ -242,6 +244,20 @@ int orc_add_triangle(orc_scene *s, const float a[3], const float b[3], const flo
   GROW(s->objs, s->n_objs);
   s->objs[s->n_objs].kind = 1;
   s->objs[s->n_objs].idx = s->n_tris++;
+  return s->n_objs++;
+}
+
+int orc_add_plane(orc_scene *s, const float pos[3], const float norm[3], int diel, const float rgb[3], float refl,
+                  float transp)                                              /* Plane.cpp:9-14 */
+{
+  GROW(s->planes, s->n_planes);
+  plane_t *p = &s->planes[s->n_planes];
+  p->pos = V(pos[0], pos[1], pos[2]);
+  p->norm = V(norm[0], norm[1], norm[2]);
+  p->mat = make_mat(diel, rgb, refl, transp);
+  GROW(s->objs, s->n_objs);
+  s->objs[s->n_objs].kind = 2;
+  s->objs[s->n_objs].idx = s->n_planes++;
   return s->n_objs++;
 }
 
@@ -427,9 +443,10 @@ static int tri_trace(const orc_scene *s, const tri_t *tr, v3 o, v3 ray, hit_t *o
   return 0;
 }
 
-/* Plane::trace (Plane.cpp:36-73) -- KAT only: Scene cannot hold a Plane */
-static int plane_trace(v3 pos, v3 norm, v3 o, v3 ray, hit_t *out)
+/* Plane::trace (Plane.cpp:36-73); in a scene through the addPlane extension (the reference's Scene has none) */
+static int plane_trace(v3 pos, v3 norm, v3 o, v3 ray, hit_t *out, uint64_t *cnt, int shadow)
 {
+  if (cnt) cnt[shadow ? ORC_SH_PLN_TESTS : ORC_PLN_TESTS]++;
   const v3 vop = vsub(pos, o);
   const float a = vdot(norm, ray);
   if (fabsf(a) > VSN)
@@ -437,6 +454,7 @@ static int plane_trace(v3 pos, v3 norm, v3 o, v3 ray, hit_t *out)
     const float t = vdot(norm, vop) / a;
     if (t > VSN)
     {
+      if (cnt) cnt[shadow ? ORC_SH_PLN_T : ORC_PLN_T]++;
       const v3 full = vmul(ray, t);
       const float sq = vsqlen(full);
       if (sq > DELTA * DELTA)
@@ -447,6 +465,7 @@ static int plane_trace(v3 pos, v3 norm, v3 o, v3 ray, hit_t *out)
           out->norm = norm;
           out->refl = tm_reflect(full, norm);
           out->dist = sqrtf(sq);
+          out->tex_cat = -1;
         }
         return 1;
       }
@@ -470,8 +489,15 @@ static col scene_trace(const orc_scene *s, v3 origin, v3 ray, int depth, v3 rand
     for (int i = 0; i < s->n_objs; ++i)                                       /* :86-106, strict '<' keeps the first */
     {
       const obj_t *ob = &s->objs[i];
-      int h = ob->kind == 0 ? sphere_trace(&s->spheres[ob->idx], origin, ray, &cur, cnt, 0)
-                            : tri_trace(s, &s->tris[ob->idx], origin, ray, &cur, cnt, 0);
+      int h;
+      if (ob->kind == 0) h = sphere_trace(&s->spheres[ob->idx], origin, ray, &cur, cnt, 0);
+      else if (ob->kind == 1) h = tri_trace(s, &s->tris[ob->idx], origin, ray, &cur, cnt, 0);
+      else
+      {
+        const plane_t *pl = &s->planes[ob->idx];
+        h = plane_trace(pl->pos, pl->norm, origin, ray, &cur, cnt, 0);
+        cur.mat = pl->mat;
+      }
       if (h && cur.dist < minDistance)
       {
         minDistance = cur.dist;
@@ -483,7 +509,8 @@ static col scene_trace(const orc_scene *s, v3 origin, v3 ray, int depth, v3 rand
     {
       if (cnt)
       {
-        cnt[s->objs[hitObj].kind == 0 ? ORC_HIT_SPH : ORC_HIT_TRI]++;
+        const int k = s->objs[hitObj].kind;
+        cnt[k == 0 ? ORC_HIT_SPH : k == 1 ? ORC_HIT_TRI : ORC_HIT_PLN]++;
         if (best.tex_cat >= 0) cnt[best.tex_cat]++;
       }
       const v3 drop = best.drop, norm = best.norm, reflect = best.refl;
@@ -506,7 +533,8 @@ static col scene_trace(const orc_scene *s, v3 origin, v3 ray, int depth, v3 rand
             if (i == hitObj) continue;
             const obj_t *ob = &s->objs[i];
             if (ob->kind == 0 ? sphere_trace(&s->spheres[ob->idx], drop, shadowRay, NULL, cnt, 1)
-                              : tri_trace(s, &s->tris[ob->idx], drop, shadowRay, NULL, cnt, 1))
+                : ob->kind == 1 ? tri_trace(s, &s->tris[ob->idx], drop, shadowRay, NULL, cnt, 1)
+                                : plane_trace(s->planes[ob->idx].pos, s->planes[ob->idx].norm, drop, shadowRay, NULL, cnt, 1))
             {
               inShadow = 1;
               break;
@@ -830,9 +858,9 @@ void orc_kat_plane(const float *f, uint64_t n, float *out)
     hit_t h;
     memset(&h, 0, sizeof(h));
     v3 pos = V(f[6], f[7], f[8]), nn = V(f[9], f[10], f[11]), o = V(f[0], f[1], f[2]), r = V(f[3], f[4], f[5]);
-    int hit = plane_trace(pos, nn, o, r, &h);
+    int hit = plane_trace(pos, nn, o, r, &h, NULL, 0);
     h.mat.color = C(KAT_RGB[0], KAT_RGB[1], KAT_RGB[2]);
-    int any = plane_trace(pos, nn, o, r, NULL);
+    int any = plane_trace(pos, nn, o, r, NULL, NULL, 1);
     write_hit(out + i * 15, hit, &h, any);
   }
 }

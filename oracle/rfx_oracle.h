@@ -28,6 +28,7 @@ enum {
   ORC_L_EVAL, ORC_L_FACING, ORC_L_LIT, ORC_L_SPEC, ORC_L_POW,
   ORC_DIELECTRIC, ORC_METAL, ORC_CONTINUE, ORC_SKY,
   ORC_TEX_BILINEAR, ORC_TEX_CHECKER, ORC_TEX_OTHER,
+  ORC_PLN_TESTS, ORC_PLN_T, ORC_HIT_PLN, ORC_SH_PLN_TESTS, ORC_SH_PLN_T,
   ORC_NCOUNTERS
 };
 
@@ -40,6 +41,8 @@ int orc_add_light(orc_scene *s, const float origin[3], float radius, const float
 int orc_add_sphere(orc_scene *s, const float center[3], float radius, int dielectric, const float rgb[3], float refl, float transp);
 int orc_add_triangle(orc_scene *s, const float v0[3], const float v1[3], const float v2[3], int dielectric,
                      const float rgb[3], float refl, float transp);
+int orc_add_plane(orc_scene *s, const float pos[3], const float norm[3], int dielectric, const float rgb[3],
+                  float refl, float transp);
 int orc_triangle_set_texture(orc_scene *s, int object_id, int texture_id, const float uv[6]);
 
 /* Camera(eye, at, fov) -> view, row-major _11.._33 (Camera.cpp:24-56) */

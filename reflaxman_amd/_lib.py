@@ -12,7 +12,8 @@ import os
 from . import _build
 
 RFX_OK = 0
-RFX_NCOUNTERS = 35
+RFX_NCOUNTERS = 40
+RFX_ABI_VERSION = 2
 METAL, DIELECTRIC = 0, 1
 
 _fp = C.POINTER(C.c_float)
@@ -44,6 +45,8 @@ SIGNATURES = [
     ("rfx_scene_destroy", None, [C.c_void_p]),
     ("rfx_scene_add_sphere", C.c_int, [C.c_void_p, _fp, C.c_float, C.c_int, _fp, C.c_float, C.c_float]),
     ("rfx_scene_add_triangle", C.c_int, [C.c_void_p, _fp, _fp, _fp, C.c_int, _fp, C.c_float, C.c_float]),
+    ("rfx_scene_add_plane", C.c_int, [C.c_void_p, _fp, _fp, C.c_int, _fp, C.c_float, C.c_float]),
+    ("rfx_scene_plane_count", C.c_int, [C.c_void_p]),
     ("rfx_triangle_set_texture", C.c_int, [C.c_void_p, C.c_int, C.c_int, _fp]),
     ("rfx_scene_add_light", C.c_int, [C.c_void_p, _fp, C.c_float, _fp, C.c_float]),
     ("rfx_scene_add_texture_argb", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, _u32p]),
@@ -81,6 +84,10 @@ SIGNATURES = [
     ("rfx_memcpy_h2d", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]),
     ("rfx_synchronize", C.c_int, [C.c_void_p]),
     ("rfx_rand_dirs", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint64, _fp, _u32p]),
+    ("rfx_kat_objects", C.c_int, [C.c_void_p, _fp, C.POINTER(C.c_int32), C.c_uint64, _fp]),
+    ("rfx_kat_texels", C.c_int, [C.c_void_p, C.c_int, _fp, C.c_uint64, _fp]),
+    ("rfx_kat_powf", C.c_int, [C.c_void_p, _fp, C.c_uint64, _fp]),
+    ("rfx_kat_argb", C.c_int, [C.c_void_p, _fp, C.c_uint64, _u32p]),
 ]
 
 _lib = None
@@ -119,7 +126,7 @@ def load(build_if_missing: bool = True):
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
-    if L.rfx_abi_version() != 1:
+    if L.rfx_abi_version() != RFX_ABI_VERSION:
         raise RfxError("librfx.so ABI version mismatch")
     _lib = L
     return L

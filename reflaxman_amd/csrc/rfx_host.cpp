@@ -37,6 +37,8 @@ hipError_t launch_trace(const DevScene &S, const FrameParams &P, bool stats, hip
 uint32_t trace_tiles(const FrameParams &P);
 size_t tile_order_scratch();
 hipError_t launch_tile_order(const uint32_t *cost, uint32_t n, uint32_t *order, uint32_t *scratch, hipStream_t st);
+hipError_t launch_kat(int what, const DevScene &S, int tex, const void *in, const int32_t *objs, uint32_t n, void *out,
+                      hipStream_t st);
 }  // namespace rfx
 
 using namespace rfx;
@@ -64,7 +66,9 @@ extern "C" int rfx_abi_version(void) { return RFX_ABI_VERSION; }
 extern "C" const char *rfx_last_error(void) { return g_last_error.c_str(); }
 
 // ============================================================== scene (host)
-struct HostTexture { uint32_t w = 0, h = 0; std::vector<uint32_t> texels; };
+// w x h as loaded; no texels = the reference's empty colorBuf (procedural checker).  loaded: the file was read
+// (Skybox::loadTexture then derives its half tiles from w and h, Skybox.cpp:21-37).
+struct HostTexture { uint32_t w = 0, h = 0; bool loaded = false; std::vector<uint32_t> texels; };
 struct HostMat { int dielectric; float r, g, b, refl, transp; };
 struct HostSphere { v3 center; float radius, sq_radius; HostMat mat; int obj; };
 struct HostTri {
@@ -77,6 +81,7 @@ struct HostTri {
   int obj;
 };
 struct HostLight { v3 origin; float radius; float r, g, b, power; };
+struct HostPlane { v3 pos, norm; HostMat mat; int obj; };
 
 struct rfx_scene {
   col diff, env;
@@ -85,7 +90,8 @@ struct rfx_scene {
   int skybox = -1;
   std::vector<HostSphere> spheres;
   std::vector<HostTri> tris;
-  std::vector<int> obj_kind, obj_idx;  // insertion order
+  std::vector<HostPlane> planes;
+  std::vector<int> obj_kind, obj_idx;  // insertion order: kind 0 sphere, 1 triangle, 2 plane
   std::vector<HostLight> lights;
   std::vector<HostTexture> textures;
 };
@@ -166,6 +172,22 @@ extern "C" int rfx_scene_add_triangle(rfx_scene *s, const float a[3], const floa
   return t.obj;
 }
 
+extern "C" int rfx_scene_add_plane(rfx_scene *s, const float pos[3], const float norm[3], int type, const float rgb[3],
+                                   float refl, float transp)                         // Plane.cpp:9-14
+{
+  if (!s || !pos || !norm || !rgb || (type != RFX_METAL && type != RFX_DIELECTRIC))
+    return fail(RFX_ERR_ARG, "add_plane: bad args");
+  HostPlane p;
+  p.pos = mk(pos[0], pos[1], pos[2]);
+  p.norm = mk(norm[0], norm[1], norm[2]);
+  p.mat = make_mat(type, rgb, refl, transp);
+  p.obj = (int)s->obj_kind.size();
+  s->obj_kind.push_back(2);
+  s->obj_idx.push_back((int)s->planes.size());
+  s->planes.push_back(p);
+  return p.obj;
+}
+
 extern "C" int rfx_triangle_set_texture(rfx_scene *s, int obj, int tex, const float uv[6])  // Triangle.cpp:110-120
 {
   if (!s || !uv || obj < 0 || obj >= (int)s->obj_kind.size() || s->obj_kind[obj] != 1)
@@ -202,6 +224,7 @@ extern "C" int rfx_scene_add_texture_argb(rfx_scene *s, uint32_t w, uint32_t h, 
   if (argb && w && h)
   {
     t.w = w; t.h = h;
+    t.loaded = true;
     t.texels.assign(argb, argb + (size_t)w * h);
   }
   s->textures.push_back(std::move(t));
@@ -215,6 +238,9 @@ struct BmpFileHeader { uint16_t bfType; uint32_t bfSize; uint16_t r1, r2; uint32
 struct BmpInfoHeader { uint32_t biSize; int32_t biWidth, biHeight; uint16_t biPlanes, biBitCount; uint32_t biCompression, biSizeImage; int32_t xppm, yppm; uint32_t clrUsed, clrImportant; };
 #pragma pack(pop)
 
+// Texture::loadFromTGAFile (Texture.cpp:34-108): type 2, 24/32 bpp, rows in file order (origin bit ignored).
+// As in the reference a header with a zero width or height loads successfully as an empty texture (w x h kept,
+// no texels).  Negative (int16) sizes, which the reference cannot allocate, fail.
 static bool tga_read(const char *path, uint32_t &w, uint32_t &h, std::vector<uint32_t> &out)
 {
   w = h = 0;
@@ -223,16 +249,16 @@ static bool tga_read(const char *path, uint32_t &w, uint32_t &h, std::vector<uin
   if (!f) return false;
   TgaHeader hd;
   bool ok = false;
-  if (fread(&hd, sizeof(hd), 1, f) == 1 && hd.imagetype == 2)
+  if (fread(&hd, sizeof(hd), 1, f) == 1 && hd.imagetype == 2 && hd.xsize >= 0 && hd.ysize >= 0)
   {
-    const uint32_t W = (uint32_t)(uint16_t)hd.xsize, H = (uint32_t)(uint16_t)hd.ysize;
+    const uint32_t W = (uint32_t)hd.xsize, H = (uint32_t)hd.ysize;
     const int bpp = hd.bpix;
     const long off = (long)sizeof(hd) + hd.idlen + hd.cmlen * hd.cmbits / 8;
-    if (!fseek(f, off, SEEK_SET) && (bpp == 24 || bpp == 32) && W && H)
+    if (!fseek(f, off, SEEK_SET) && (bpp == 24 || bpp == 32))
     {
       const size_t n = (size_t)W * H, ps = (size_t)bpp / 8;
       std::vector<uint8_t> raw(n * ps);
-      if (fread(raw.data(), 1, raw.size(), f) == raw.size())
+      if (!n || fread(raw.data(), 1, raw.size(), f) == raw.size())
       {
         out.resize(n);
         for (size_t i = 0; i < n; ++i)
@@ -307,6 +333,7 @@ extern "C" int rfx_scene_add_texture_file(rfx_scene *s, const char *path, int *l
   if (!s || !path) return fail(RFX_ERR_ARG, "add_texture_file: bad args");
   HostTexture t;
   const bool ok = has_ext(path, ".tga") && tga_read(path, t.w, t.h, t.texels);     // Texture.cpp:175-189
+  t.loaded = ok;
   if (loaded) *loaded = ok ? 1 : 0;
   s->textures.push_back(std::move(t));
   return (int)s->textures.size() - 1;
@@ -316,7 +343,7 @@ static void set_skybox_index(rfx_scene *s, int idx)                             
 {
   s->skybox = idx;
   const HostTexture &t = s->textures[idx];
-  if (t.w)
+  if (t.loaded)
   {
     s->half_tile_w = 1.0f / 8.0f - 1.0f / (float)t.w - kFltEpsilon;
     s->half_tile_h = 1.0f / 6.0f - 1.0f / (float)t.h - kFltEpsilon;
@@ -339,7 +366,13 @@ extern "C" int rfx_scene_set_skybox_argb(rfx_scene *s, uint32_t w, uint32_t h, c
   if (!s) return fail(RFX_ERR_ARG, "set_skybox_argb: null scene");
   const int idx = rfx_scene_add_texture_argb(s, w, h, argb);
   set_skybox_index(s, idx);
-  return s->textures[idx].w ? 1 : 0;
+  return s->textures[idx].loaded ? 1 : 0;
+}
+
+extern "C" int rfx_scene_plane_count(const rfx_scene *s)
+{
+  if (!s) return fail(RFX_ERR_ARG, "plane_count: null scene");
+  return (int)s->planes.size();
 }
 
 extern "C" int rfx_scene_counts(const rfx_scene *s, int *ns, int *nt, int *nl, int *nx)
@@ -740,13 +773,32 @@ extern "C" int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *s)
       cull_valid |= 1ull << (32 + i);
     }
   }
+  std::vector<PlaneGeo> pg;
+  std::vector<MatRec> pm;
+  for (const HostPlane &p : s->planes)
+  {
+    pg.push_back({p.pos.x, p.pos.y, p.pos.z, p.norm.x, p.norm.y, p.norm.z, p.obj, p.mat.dielectric});
+    pm.push_back({p.mat.r, p.mat.g, p.mat.b, p.mat.refl});
+  }
+  // object index -> (kind, index in the device arrays): spheres through the Morton order
+  std::vector<int32_t> loc(s->obj_kind.size());
+  {
+    std::vector<int32_t> sph_dev(nsph);
+    for (size_t di = 0; di < nsph; ++di) sph_dev[order[di]] = (int32_t)di;
+    for (size_t o = 0; o < loc.size(); ++o)
+    {
+      const int kind = s->obj_kind[o], idx = s->obj_idx[o];
+      loc[o] = kind << 28 | (kind == 0 ? sph_dev[idx] : idx);
+    }
+  }
   std::vector<LightRec> lr;
   for (const HostLight &l : s->lights) lr.push_back({l.origin.x, l.origin.y, l.origin.z, l.radius, l.r, l.g, l.b, l.power});
   std::vector<TexRec> tr;
   std::vector<uint32_t> pool;
   for (const HostTexture &t : s->textures)
   {
-    tr.push_back({(uint32_t)pool.size(), t.w, t.h, 0});
+    const bool empty = t.texels.empty();  // the reference's empty colorBuf: checker (Texture.cpp:242-243)
+    tr.push_back({(uint32_t)pool.size(), empty ? 0u : t.w, empty ? 0u : t.h, 0});
     pool.insert(pool.end(), t.texels.begin(), t.texels.end());
   }
   DevScene d{};
@@ -754,12 +806,16 @@ extern "C" int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *s)
       (rc = upload(r, si, &d.sph_info)) ||
       (rc = upload(r, tg, &d.tri_geo)) || (rc = upload(r, ts, &d.tri_shade)) || (rc = upload(r, tm, &d.tri_mat)) ||
       (rc = upload(r, lr, &d.lights)) || (rc = upload(r, tr, &d.texs)) || (rc = upload(r, pool, &d.texels)) ||
-      (rc = upload(r, bd, &d.bound)) || (rc = upload(r, cs, &d.cull_small)) || (rc = upload(r, cb, &d.chunk_bound)))
+      (rc = upload(r, bd, &d.bound)) || (rc = upload(r, cs, &d.cull_small)) || (rc = upload(r, cb, &d.chunk_bound)) ||
+      (rc = upload(r, pg, &d.pln_geo)) || (rc = upload(r, pm, &d.pln_mat)) || (rc = upload(r, loc, &d.obj_loc)))
     return rc;
   d.n_sph = (int32_t)sg.size();
   d.n_tri = (int32_t)tg.size();
   d.n_light = (int32_t)lr.size();
   d.n_chunk = (int32_t)cb.size();
+  d.n_pln = (int32_t)pg.size();
+  d.n_tex = (int32_t)tr.size();
+  d.n_obj = (int32_t)loc.size();
   d.cull_valid = cull_valid;
   d.skybox_tex = s->skybox;
   const col amb = cscale(s->diff, s->diff_power);                                    // Scene.cpp:186 (first factor)
@@ -1169,4 +1225,66 @@ extern "C" int rfx_rand_dirs(rfx_renderer *r, uint32_t seed, uint64_t n, float *
   }
   if (seed_out) *seed_out = after;
   return RFX_OK;
+}
+
+// ============================================================== device known-answer entry points
+// Each runs the trace kernel's own device code (rfx_kernels.hip kat_*) on host arrays, synchronously.
+template <class T>
+static int kat_buffer(size_t n, const T *src, T **dev)
+{
+  *dev = nullptr;
+  HIP_CHECK(hipMalloc((void **)dev, n ? n * sizeof(T) : sizeof(T)));
+  if (src && n) HIP_CHECK(hipMemcpy(*dev, src, n * sizeof(T), hipMemcpyHostToDevice));
+  return RFX_OK;
+}
+
+static int kat_run(rfx_renderer *r, int what, int tex, const void *in, size_t in_elems, const int32_t *objs,
+                   uint64_t n, void *out, size_t out_elems)
+{
+  int rc;
+  if ((rc = set_dev(r)) != RFX_OK) return rc;
+  if (n >= (1ull << 31)) return fail(RFX_ERR_ARG, "kat: n too large");
+  float *d_in = nullptr, *d_out = nullptr;
+  int32_t *d_obj = nullptr;
+  rc = kat_buffer(in_elems, (const float *)in, &d_in);
+  if (rc == RFX_OK && objs) rc = kat_buffer((size_t)n, objs, &d_obj);
+  if (rc == RFX_OK) rc = kat_buffer(out_elems, (const float *)nullptr, &d_out);
+  if (rc == RFX_OK)
+  {
+    hipError_t e = launch_kat(what, r->dev, tex, d_in, d_obj, (uint32_t)n, d_out, r->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(r->stream);
+    if (e == hipSuccess) e = hipMemcpy(out, d_out, out_elems * 4, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) rc = fail(RFX_ERR_HIP, "kat: %s", hipGetErrorString(e));
+  }
+  (void)hipFree(d_in); (void)hipFree(d_obj); (void)hipFree(d_out);
+  return rc;
+}
+
+extern "C" int rfx_kat_objects(rfx_renderer *r, const float *rays, const int32_t *objects, uint64_t n, float *out)
+{
+  if (!r || (n && (!rays || !objects || !out))) return fail(RFX_ERR_ARG, "kat_objects: bad args");
+  if (!r->has_scene) return fail(RFX_ERR_STATE, "kat_objects: no scene uploaded");
+  for (uint64_t i = 0; i < n; ++i)
+    if (objects[i] < 0 || objects[i] >= r->dev.n_obj) return fail(RFX_ERR_ARG, "kat_objects: object %d", objects[i]);
+  return kat_run(r, 0, 0, rays, (size_t)n * 6, objects, n, out, (size_t)n * 15);
+}
+
+extern "C" int rfx_kat_texels(rfx_renderer *r, int texture, const float *in, uint64_t n, float *out)
+{
+  if (!r || (n && (!in || !out))) return fail(RFX_ERR_ARG, "kat_texels: bad args");
+  if (!r->has_scene) return fail(RFX_ERR_STATE, "kat_texels: no scene uploaded");
+  if (texture >= r->dev.n_tex) return fail(RFX_ERR_ARG, "kat_texels: texture %d", texture);
+  return kat_run(r, 1, texture, in, (size_t)n * (texture >= 0 ? 2 : 3), nullptr, n, out, (size_t)n * 3);
+}
+
+extern "C" int rfx_kat_powf(rfx_renderer *r, const float *xy, uint64_t n, float *out)
+{
+  if (!r || (n && (!xy || !out))) return fail(RFX_ERR_ARG, "kat_powf: bad args");
+  return kat_run(r, 2, 0, xy, (size_t)n * 2, nullptr, n, out, (size_t)n);
+}
+
+extern "C" int rfx_kat_argb(rfx_renderer *r, const float *rgb, uint64_t n, uint32_t *out)
+{
+  if (!r || (n && (!rgb || !out))) return fail(RFX_ERR_ARG, "kat_argb: bad args");
+  return kat_run(r, 3, 0, rgb, (size_t)n * 3, nullptr, n, out, (size_t)n);
 }

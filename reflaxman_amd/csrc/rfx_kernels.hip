@@ -97,12 +97,7 @@ __device__ unsigned long long g_cull[16];
 // the table holds exactly the quotients the reference computes per channel.
 __device__ __forceinline__ col from_argb_lut(uint32_t c, const float *lut)
 {
-#ifdef RFX_NO_LUT
-  (void)lut;
-  return from_argb(c);
-#else
   return mkc(lut[(c >> 16) & 0xFFu], lut[(c >> 8) & 0xFFu], lut[c & 0xFFu]);
-#endif
 }
 
 // glibc powf's tables (rfx_powf.h) copied to LDS by each workgroup: the lookups index them per lane,
@@ -124,15 +119,7 @@ __device__ __forceinline__ void stage_powf_tables()
 
 __device__ __forceinline__ float powf_dev(float x, float y)
 {
-#ifdef RFX_POW_GLOBAL
-  return powf_glibc(x, y);
-#else
-#ifdef RFX_POW_ADD_LIT
-  return powf_glibc_t(x, y, s_powf_log, s_powf_exp, kPowfAdd);
-#else
   return powf_glibc_t(x, y, s_powf_log, s_powf_exp, s_powf_add);
-#endif
-#endif
 }
 
 // Small scenes (<= 32 spheres, <= 32 triangles): the per-object records the hit lanes gather by their
@@ -154,7 +141,6 @@ struct Tabs {
   __device__ __forceinline__ MatRec tri_mat(int i) const { return S.tri_mat[i]; }
   __device__ __forceinline__ const CullRec *cull() const { return S.cull_small; }
 };
-#ifndef RFX_NO_LDS_SMALL
 template <>
 struct Tabs<true> {
   const DevScene &S;
@@ -165,11 +151,9 @@ struct Tabs<true> {
   __device__ __forceinline__ MatRec tri_mat(int i) const { return s_tri_mat[i]; }
   __device__ __forceinline__ const CullRec *cull() const { return s_cull; }
 };
-#endif
 
 __device__ __forceinline__ void stage_small_scene(const DevScene &S)
 {
-#ifndef RFX_NO_LDS_SMALL
   const int t = (int)threadIdx.x;
   if (t < S.n_sph)
   {
@@ -184,7 +168,6 @@ __device__ __forceinline__ void stage_small_scene(const DevScene &S)
     s_tri_mat[t] = S.tri_mat[t];
   }
   if (t < 64) s_cull[t] = S.cull_small[t];
-#endif
 }
 
 // ------------------------------------------------------------- sampling
@@ -249,6 +232,17 @@ __device__ __forceinline__ col skybox_texel(const DevScene &S, v3 ray, const flo
     else { u = uBottom + x / ay * hw; v = vBottom + z / ay * hh; }
   }
   return texel_uv<STATS>(S, S.skybox_tex, u, v, lut, cnt);
+}
+
+// A textured triangle's material colour at barycentrics (u, v) (Triangle.cpp:89-96): tuvTrans * (u, v, 0)
+// (whose _13 and _23 are 0) offset by (tu[0], tv[0]).
+template <bool STATS>
+__device__ __forceinline__ col tri_texel(const DevScene &S, const TriShade &sh, float u, float v, const float *lut,
+                                         Cnt &cnt)
+{
+  const float tvx = u * sh.t11 + v * sh.t12 + 0.0f;
+  const float tvy = u * sh.t21 + v * sh.t22 + 0.0f;
+  return texel_uv<STATS>(S, sh.tex, sh.tu0 + tvx, sh.tv0 + tvy, lut, cnt);
 }
 
 // ------------------------------------------------------------- primitives
@@ -339,7 +333,6 @@ __device__ __forceinline__ bool tri_hit(const TriGeo &g, v3 o, v3 ray, float &t_
   // exact reject before the division: with opposite signs or a zero (or NaN) numerator, t <= 0 or NaN,
   // which `t > VERY_SMALL_NUMBER` rejects anyway; the divide is skipped when no lane of the wave needs it
   if (!same_sign) return false;
-#if !defined(RFX_DIST_CMP) && !defined(RFX_NO_TRI_DIST)
   if constexpr (!SHADOW && !STATS)
   {
     // exact reject of a plane hit beyond the current closest hit: |ray t|^2 = a nz^2 / arz^2 (real), and
@@ -347,7 +340,6 @@ __device__ __forceinline__ bool tri_hit(const TriGeo &g, v3 o, v3 ray, float &t_
     // distance after rounding, so the reference could neither take it nor tie (a2 = 2a exactly)
     if (nz * nz * k.a2 > best_sq * (arz * arz) * 2.0000305f) return false;
   }
-#endif
   const float t = nz / arz;
   if (!(t > kVerySmall)) return false;
   RFX_CNT(SHADOW ? C_SH_TRI_T : C_TRI_T);
@@ -361,6 +353,30 @@ __device__ __forceinline__ bool tri_hit(const TriGeo &g, v3 o, v3 ray, float &t_
   const float sq = sqlen(mul(ray, t));
   if (!(sq > kDelta * kDelta)) return false;
   t_out = t; u_out = u; v_out = v; sq_out = sq;
+  return true;
+}
+
+// Plane::trace (Plane.cpp:36-73) up to its hit decision; on a hit returns t and |ray t|^2.  a = norm . ray,
+// t = norm . (pos - origin) / a, with tri_hit's two exact rejects before the division (opposite signs or a
+// zero numerator give t <= 0; a plane hit beyond the closest hit so far cannot win or tie).
+template <bool STATS, bool SHADOW>
+__device__ __forceinline__ bool plane_hit(const PlaneGeo &g, v3 o, v3 ray, float &t_out, float &sq_out, Cnt &cnt,
+                                          const RayConst &k, float best_sq = INFINITY)
+{
+  RFX_CNT(SHADOW ? C_SH_PLN_TESTS : C_PLN_TESTS);
+  const v3 n = mk(g.nx, g.ny, g.nz);
+  const float a = dot(n, ray);                                                     // Plane.cpp:41
+  if (!(fabsf(a) > kVerySmall)) return false;
+  const float num = dot(n, sub(mk(g.px, g.py, g.pz), o));                          // Plane.cpp:40,45
+  if (!((num > 0.0f && a > 0.0f) || (num < 0.0f && a < 0.0f))) return false;
+  if constexpr (!SHADOW && !STATS)
+    if (num * num * k.a2 > best_sq * (a * a) * 2.0000305f) return false;
+  const float t = num / a;
+  if (!(t > kVerySmall)) return false;
+  RFX_CNT(SHADOW ? C_SH_PLN_T : C_PLN_T);
+  const float sq = sqlen(mul(ray, t));
+  if (!(sq > kDelta * kDelta)) return false;                                       // Plane.cpp:50-53
+  t_out = t; sq_out = sq;
   return true;
 }
 
@@ -393,11 +409,6 @@ __device__ __forceinline__ float lane_bcast(float v, int lane)
 __device__ __forceinline__ float wave_max_nonneg(float v)
 {
   uint32_t u = __float_as_uint(v);
-#ifdef RFX_BPERM_REDUCE
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) u = max(u, (uint32_t)__shfl_xor((int)u, off, 64));
-  return __uint_as_float(u);
-#else
   u = max(u, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x111, 0xf, 0xf, false));  // row_shr:1
   u = max(u, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x112, 0xf, 0xf, false));  // row_shr:2
   u = max(u, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x114, 0xf, 0xf, false));  // row_shr:4
@@ -405,7 +416,6 @@ __device__ __forceinline__ float wave_max_nonneg(float v)
   u = max(u, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x142, 0xa, 0xf, false));  // row_bcast:15
   u = max(u, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x143, 0xc, 0xf, false));  // row_bcast:31
   return __int_as_float(__builtin_amdgcn_readlane((int)u, 63));
-#endif
 }
 
 // Bundle of the rays (o, d) of the `live` lanes.  Call with every lane of the wave active and at least
@@ -455,12 +465,6 @@ __device__ __forceinline__ uint64_t cull_chunk(const Bound *bound, int first, in
   return __ballot(keep);
 }
 
-#ifdef RFX_ONE_CHUNK  // A/B only: scenes of at most 64 spheres and 64 triangles
-constexpr int kChunkLimit = 64;
-#else
-constexpr int kChunkLimit = 0x7fffffff;
-#endif
-
 // Small scenes: lane l tests cull record l (rfx_types.h CullRec) -- the cone test of cull_chunk, and
 // for a triangle also its plane: when every origin lies more than rw (plus a margin) on one side and
 // every direction leaves that side (axis . n beyond sin of the cone's half-angle, plus a margin), every
@@ -505,7 +509,7 @@ __device__ __forceinline__ uint32_t pair_bits(uint64_t m)
 // Triangle.cpp:70-85): for sq < best_sq, dist < best unless both round to the same float, i.e. unless
 // sq >= sq_lower_bound(best); for sq >= best_sq, dist >= best (tests/test_sqrt_bounds.py).
 struct Hit {
-  int obj, kind, i;  // object index (-1: none), 0 sphere / 1 triangle, index within its kind
+  int obj, kind, i;  // object index (-1: none), 0 sphere / 1 triangle / 2 plane, index within its kind
   float t, u, v, sq;
 };
 
@@ -515,15 +519,6 @@ __device__ __forceinline__ bool strictly_closer(float sq, float best_sq)
 }
 
 // the comparison key of a candidate and the two decisions on it (Hit::sq holds the winner's key)
-#ifdef RFX_DIST_CMP  // A/B reference: compare the rounded distances themselves
-constexpr float kNoHitKey = kFltMax;
-__device__ __forceinline__ float hit_key(float sq) { return sqrt_rn(sq); }
-__device__ __forceinline__ bool sph_takes(float key, float best) { return key < best; }
-__device__ __forceinline__ bool tri_takes(float key, float best, int obj, int best_obj)
-{
-  return key < best || (key == best && obj < best_obj);
-}
-#else
 constexpr float kNoHitKey = INFINITY;
 __device__ __forceinline__ float hit_key(float sq) { return sq; }
 __device__ __forceinline__ bool sph_takes(float sq, float best_sq) { return strictly_closer(sq, best_sq); }
@@ -533,13 +528,45 @@ __device__ __forceinline__ bool tri_takes(float sq, float best_sq, int obj, int 
   return sq < best_sq ? (obj < best_obj || strictly_closer(sq, best_sq))
                       : (obj < best_obj && sqrt_rn(sq) == sqrt_rn(best_sq));
 }
-#endif
+
+// The planes (Scene::addPlane extension, Plane.cpp:36-73) for one lane, after the other kinds: every lane that
+// traces tests every plane (an infinite plane has no bounding sphere to cull with).
+template <bool STATS>
+__device__ __forceinline__ void closest_planes(const DevScene &S, v3 origin, v3 ray, const RayConst &k, Hit &h, Cnt &cnt)
+{
+  for (int i = 0; i < S.n_pln; ++i)
+  {
+    const PlaneGeo g = S.pln_geo[i];
+    float t, sq;
+    if (plane_hit<STATS, false>(g, origin, ray, t, sq, cnt, k, h.sq) && tri_takes(sq, h.sq, g.obj, h.obj))
+    {
+      h.sq = sq; h.obj = g.obj; h.kind = 2; h.i = i; h.t = t;
+    }
+  }
+}
+
+// any-hit over the planes but the hit one (skip_pln)
+template <bool STATS>
+__device__ __forceinline__ bool occluded_planes(const DevScene &S, v3 o, v3 ray, const RayConst &k, int skip_pln, Cnt &cnt)
+{
+  float t, sq;
+  for (int i = 0; i < S.n_pln; ++i)
+  {
+    if constexpr (STATS)
+    {
+      if (i != skip_pln && plane_hit<STATS, true>(S.pln_geo[i], o, ray, t, sq, cnt, k)) return true;
+    }
+    else if (plane_hit<STATS, true>(S.pln_geo[i], o, ray, t, sq, cnt, k) && i != skip_pln)
+      return true;
+  }
+  return false;
+}
 
 // Call with every lane of the wave active; `live` lanes trace (origin, ray).  B: the bundle, or null.
 // Large scenes: the spheres are stored in spatial (Morton) order, 64 to a chunk with a bounding sphere;
 // the bundle culls whole chunks (one lane per chunk), then the spheres of the surviving chunks.  The
 // visiting order is then not the insertion order, so spheres take the general (distance, object) rule.
-template <bool STATS>
+template <bool STATS, bool PLANES>
 __device__ __forceinline__ void closest_hit(const DevScene &S, v3 origin, v3 ray, bool live, const Bundle *B, Hit &h,
                                             Cnt &cnt)
 {
@@ -586,7 +613,7 @@ __device__ __forceinline__ void closest_hit(const DevScene &S, v3 origin, v3 ray
   }
   RFX_PROF_END(P_SPH);
   RFX_PROF_BEGIN(P_TRI);
-  for (int first = 0; first < S.n_tri && first < kChunkLimit; first += 64)
+  for (int first = 0; first < S.n_tri; first += 64)
   {
     const int n = min(64, S.n_tri - first);
     uint64_t m = (B && B->ok) ? cull_chunk(S.bound, S.n_sph + first, n, *B) : all_bits(n);
@@ -608,6 +635,8 @@ __device__ __forceinline__ void closest_hit(const DevScene &S, v3 origin, v3 ray
       }
     }
   }
+  if constexpr (PLANES)
+    if (live) closest_planes<STATS>(S, origin, ray, k, h, cnt);
   RFX_PROF_END(P_TRI);
 }
 
@@ -619,7 +648,7 @@ __device__ __forceinline__ void closest_hit(const DevScene &S, v3 origin, v3 ray
 __device__ __forceinline__ uint32_t small_pairs(uint64_t om) { return (uint32_t)((om | (om >> 16)) & 0xFFFFull); }
 __device__ __forceinline__ uint64_t small_tris(uint64_t om) { return om >> 32; }
 
-template <bool STATS>
+template <bool STATS, bool PLANES>
 __device__ __forceinline__ void closest_hit_small(const DevScene &S, v3 origin, v3 ray, uint64_t om, Hit &h, Cnt &cnt)
 {
   RFX_CNT(C_SEGMENTS);
@@ -673,13 +702,14 @@ __device__ __forceinline__ void closest_hit_small(const DevScene &S, v3 origin, 
       }
     }
   }
+  if constexpr (PLANES) closest_planes<STATS>(S, origin, ray, k, h, cnt);
   RFX_PROF_END(P_TRI);
 }
 
 // Scene.cpp:129-141 for a small scene (see occluded below for the order and counter notes)
-template <bool STATS>
-__device__ __forceinline__ bool occluded_small(const DevScene &S, v3 o, v3 ray, int skip_sph, int skip_tri, uint64_t om,
-                                               Cnt &cnt)
+template <bool STATS, bool PLANES>
+__device__ __forceinline__ bool occluded_small(const DevScene &S, v3 o, v3 ray, int skip_sph, int skip_tri, int skip_pln,
+                                               uint64_t om, Cnt &cnt)
 {
   const RayConst k = ray_const(ray);
   float t, sq, u, v;
@@ -717,6 +747,7 @@ __device__ __forceinline__ bool occluded_small(const DevScene &S, v3 o, v3 ray, 
     else if (tri_hit<STATS, true>(S.tri_geo[i], o, ray, t, u, v, sq, cnt, k) && i != skip_tri)
       return true;
   }
+  if constexpr (PLANES) return occluded_planes<STATS>(S, o, ray, k, skip_pln, cnt);
   return false;
 }
 
@@ -727,9 +758,9 @@ __device__ __forceinline__ bool occluded_small(const DevScene &S, v3 o, v3 ray, 
 // lane has one.  (Spheres precede triangles, the reference's order for scenes whose objects are added
 // spheres-first -- then even the event counters match it: the second sphere of a pair is counted only
 // when the first did not occlude.)
-template <bool STATS>
+template <bool STATS, bool PLANES>
 __device__ __forceinline__ bool occluded(const DevScene &S, v3 o, v3 ray, bool live, int skip_sph, int skip_tri,
-                                         const Bundle *B, Cnt &cnt)
+                                         int skip_pln, const Bundle *B, Cnt &cnt)
 {
   const RayConst k = ray_const(ray);
   const bool cull = B && B->ok;
@@ -773,7 +804,7 @@ __device__ __forceinline__ bool occluded(const DevScene &S, v3 o, v3 ray, bool l
       }
     }
   }
-  for (int first = 0; first < S.n_tri && first < kChunkLimit; first += 64)
+  for (int first = 0; first < S.n_tri; first += 64)
   {
     if (__ballot(live && !occ) == 0) return occ;
     const int n = min(64, S.n_tri - first);
@@ -794,6 +825,8 @@ __device__ __forceinline__ bool occluded(const DevScene &S, v3 o, v3 ray, bool l
       if (__ballot(live && !occ) == 0) return occ;
     }
   }
+  if constexpr (PLANES)
+    if (live && !occ) occ = occluded_planes<STATS>(S, o, ray, k, skip_pln, cnt);
   return occ;
 }
 
@@ -803,9 +836,9 @@ __device__ __forceinline__ bool occluded(const DevScene &S, v3 o, v3 ray, bool l
 // shadow any-hit (Scene.cpp:117-141; the occlusion tests depend on nothing the shading computes, so
 // they run first, with few registers live), then material, shading and the next ray or the sky.
 // CULL: wave bundles skip objects no live lane can hit (closest hit and shadow rays); MANYL: more than
-// 32 lights (shadow masks and shading in blocks of 32).  Call with every lane of the wave active;
-// `valid` lanes trace.  Returns the trace's colour (zero for invalid lanes).
-template <bool STATS, bool CULL, bool MANYL, bool SMALL>
+// 32 lights (shadow masks and shading in blocks of 32); PLANES: the scene holds planes.  Call with every lane
+// of the wave active; `valid` lanes trace.  Returns the trace's colour (zero for invalid lanes).
+template <bool STATS, bool CULL, bool MANYL, bool SMALL, bool PLANES>
 __device__ __forceinline__ col trace(const DevScene &S, v3 origin, v3 ray, int depth, v3 rd, const float *lut,
                                      Cnt &cnt, bool valid)
 {
@@ -829,20 +862,18 @@ __device__ __forceinline__ col trace(const DevScene &S, v3 origin, v3 ray, int d
       uint64_t om = S.cull_valid;
       if constexpr (CULL)
       {
-#ifndef RFX_NO_CLOSEST_CULL
         const Bundle B = make_bundle(origin, ray, alive);
         if (B.ok) om = cull_small(T.cull(), S.cull_valid, B);
         RFX_CULL_STAT(0, B.ok, __ballot(alive), om, S.cull_valid);
-#endif
       }
-      if (alive) closest_hit_small<STATS>(S, origin, ray, om, h, cnt);
+      if (alive) closest_hit_small<STATS, PLANES>(S, origin, ray, om, h, cnt);
       else h.obj = -1;
     }
     else
     {
       Bundle B;
       if constexpr (CULL) B = make_bundle(origin, ray, alive);
-      closest_hit<STATS>(S, origin, ray, alive, CULL ? &B : nullptr, h, cnt);
+      closest_hit<STATS, PLANES>(S, origin, ray, alive, CULL ? &B : nullptr, h, cnt);
     }
     const bool hit = alive && h.obj >= 0;
     // re-derive the winner's outputs with the reference's expressions
@@ -857,15 +888,22 @@ __device__ __forceinline__ col trace(const DevScene &S, v3 origin, v3 ray, int d
         const SphereGeo g = T.sph_geo(h.i);
         norm = sub(drop, mk(g.cx, g.cy, g.cz));                                // Sphere.cpp:67
       }
-      else
+      else if (!PLANES || h.kind == 1)
       {
         RFX_CNT(C_HIT_TRI);
         const TriShade sh = T.tri_shade(h.i);
         norm = mk(sh.nx, sh.ny, sh.nz);
       }
+      else
+      {
+        RFX_CNT(C_HIT_PLN);
+        const PlaneGeo g = S.pln_geo[h.i];
+        norm = mk(g.nx, g.ny, g.nz);                                               // Plane.cpp:58-59
+      }
     }
     RFX_PROF_END(P_WIN);
     const int skip_sph = h.kind == 0 ? h.i : -1, skip_tri = h.kind == 1 ? h.i : -1;
+    const int skip_pln = PLANES && h.kind == 2 ? h.i : -1;
     MatRec m{0.0f, 0.0f, 0.0f, 0.0f};
     int diel = 0;
     v3 reflv = mk(0.0f, 0.0f, 0.0f);
@@ -899,19 +937,19 @@ __device__ __forceinline__ col trace(const DevScene &S, v3 origin, v3 ray, int d
             uint64_t om = S.cull_valid;
             if constexpr (CULL)
             {
-#ifndef RFX_NO_SHADOW_CULL
               const Bundle SB = make_bundle(drop, sray, facing);
               if (SB.ok) om = cull_small(T.cull(), S.cull_valid, SB);
               RFX_CULL_STAT(1, SB.ok, __ballot(facing), om, S.cull_valid);
-#endif
             }
-            if (facing && !occluded_small<STATS>(S, drop, sray, skip_sph, skip_tri, om, cnt)) lit |= 1u << q;
+            if (facing && !occluded_small<STATS, PLANES>(S, drop, sray, skip_sph, skip_tri, skip_pln, om, cnt))
+              lit |= 1u << q;
           }
           else
           {
             Bundle SB;
             if constexpr (CULL) SB = make_bundle(drop, sray, facing);
-            const bool occ = occluded<STATS>(S, drop, sray, facing, skip_sph, skip_tri, CULL ? &SB : nullptr, cnt);
+            const bool occ = occluded<STATS, PLANES>(S, drop, sray, facing, skip_sph, skip_tri, skip_pln,
+                                                     CULL ? &SB : nullptr, cnt);
             if (facing && !occ) lit |= 1u << q;
           }
         }
@@ -928,16 +966,19 @@ __device__ __forceinline__ col trace(const DevScene &S, v3 origin, v3 ray, int d
             m = T.sph_mat(h.i);
             diel = T.sph_info(2 * h.i + 1);
           }
+          else if (PLANES && h.kind == 2)
+          {
+            m = S.pln_mat[h.i];                                                  // untextured (Plane.cpp:67-68)
+            diel = S.pln_geo[h.i].dielectric;
+          }
           else
           {
             const TriShade sh = T.tri_shade(h.i);
             m = T.tri_mat(h.i);
             diel = sh.dielectric;
-            if (sh.tex >= 0)                                                   // Triangle.cpp:89-96
+            if (sh.tex >= 0)
             {
-              const float tvx = h.u * sh.t11 + h.v * sh.t12 + 0.0f;
-              const float tvy = h.u * sh.t21 + h.v * sh.t22 + 0.0f;
-              const col c = texel_uv<STATS>(S, sh.tex, sh.tu0 + tvx, sh.tv0 + tvy, lut, cnt);
+              const col c = tri_texel<STATS>(S, sh, h.u, h.v, lut, cnt);
               m.r = c.r; m.g = c.g; m.b = c.b;
             }
           }
@@ -1099,7 +1140,8 @@ static_assert(kWgWaves == 1 || kWgWaves == 2 || kWgWaves == 4, "RFX_WG_WAVES: 1,
 enum TraceMode { kModeSsaa = 0, kModeBlock = 1, kModePlain = 2 };
 // CFG bits: kCfgCull -- wave-bundle culling (every non-stats launch); kCfgManyLights -- more than 32 lights;
 // kCfgSmall -- at most 32 spheres and 32 triangles (one lane-layout cull mask for the whole scene)
-constexpr int kCfgCull = 1, kCfgManyLights = 2, kCfgSmall = 4;
+// kCfgPlanes -- the scene holds planes (Scene::addPlane extension)
+constexpr int kCfgCull = 1, kCfgManyLights = 2, kCfgSmall = 4, kCfgPlanes = 8;
 
 // one workgroup = kTileW x kTileH output pixels (block mode: block corners), one wave = an 8x8 tile (ray coherence).
 // Every lane of a wave reaches trace() -- lanes outside the frame or the cursor span as invalid -- so the
@@ -1108,6 +1150,7 @@ template <bool STATS, int MODE, int CFG>
 __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
 {
   constexpr bool CULL = (CFG & kCfgCull) != 0, MANYL = (CFG & kCfgManyLights) != 0, SMALL = (CFG & kCfgSmall) != 0;
+  constexpr bool PLANES = (CFG & kCfgPlanes) != 0;
   __shared__ float lut[256];
   for (uint32_t i = threadIdx.x; i < 256; i += kWgThreads) lut[i] = (float)i / 255.0f;  // Color.cpp:11-13
   stage_powf_tables();
@@ -1165,7 +1208,7 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
     const v3 ray = mmul(view, mk((float)x - P.wh, (float)y - P.hh, P.rz));
     v3 rd = mk(0.0f, 0.0f, 0.0f);
     if (valid) rd = load_rd(P, (uint64_t)cy * bw + cx - P.trace_base);
-    const col c = trace<STATS, CULL, MANYL, SMALL>(S, eye, ray, P.depth, rd, lut, cnt, valid);
+    const col c = trace<STATS, CULL, MANYL, SMALL, PLANES>(S, eye, ray, P.depth, rd, lut, cnt, valid);
     if (valid)
     {
       const uint32_t ex = min(P.W, x + n), ey = min(P.H, y + n);
@@ -1196,7 +1239,7 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
       const v3 ray = mmul(view, mk(rx + 0.0f + 0.0f, ry + 0.0f + 0.0f, P.rz));
       v3 rd = mk(0.0f, 0.0f, 0.0f);
       if (valid) rd = load_rd(P, pr);
-      const col c = trace<STATS, CULL, MANYL, SMALL>(S, eye, ray, P.depth, rd, lut, cnt, valid);
+      const col c = trace<STATS, CULL, MANYL, SMALL, PLANES>(S, eye, ray, P.depth, rd, lut, cnt, valid);
       out = cadd(mkc(0.0f, 0.0f, 0.0f), c);                                      // Render.cpp:185 (/ 1.0f exact)
     }
     else
@@ -1220,7 +1263,7 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
           ray = mmul(view, ray);
           v3 rd = mk(0.0f, 0.0f, 0.0f);
           if (valid) rd = load_rd(P, pr * (uint64_t)(ss * ss) + (uint64_t)(sx * ss + sy));
-          fin = cadd(fin, trace<STATS, CULL, MANYL, SMALL>(S, eye, ray, P.depth, rd, lut, cnt, valid));
+          fin = cadd(fin, trace<STATS, CULL, MANYL, SMALL, PLANES>(S, eye, ray, P.depth, rd, lut, cnt, valid));
         }
       if (ss != 1)                                                                 // Render.cpp:189 (x / 1.0f == x)
       {
@@ -1486,6 +1529,129 @@ __global__ __launch_bounds__(kRngBlock) void rng_emit(const uint32_t *seed, cons
   }
 }
 
+// ------------------------------------------------------------- device known-answer kernels
+// Thread i runs the trace kernel's own device code on one case (rfx.h rfx_kat_*), so the reference's
+// known answers (tests/golden/kat_*.npz, outputs of the unmodified Sphere / Triangle / Plane / Skybox /
+// Texture / Color / powf code) pin every device primitive, edge cases no rendered frame reaches included.
+constexpr uint32_t kKatThreads = 256;
+
+__device__ __forceinline__ void stage_lut(float *lut)
+{
+  for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) lut[i] = (float)i / 255.0f;  // Color.cpp:11-13
+}
+
+// rays: n x 6 (origin, direction); objs: n object indices of S; out: n x 15 -- hit, drop, normal, reflected
+// ray, distance, material colour (the texel of a textured triangle), any-hit: the refharness kat_* layout.
+// The closest-hit derivation is the bounce loop's: the test up to t (and |ray t|^2), then the winner's
+// drop = origin + ray t, normal, reflect(ray t, normal) and distance sqrt(|ray t|^2).
+__global__ __launch_bounds__(kKatThreads) void kat_objects(DevScene S, const float *rays, const int32_t *objs, uint32_t n,
+                                                          float *out)
+{
+  __shared__ float lut[256];
+  stage_lut(lut);
+  __syncthreads();
+  const uint32_t i = blockIdx.x * kKatThreads + threadIdx.x;
+  if (i >= n) return;
+  Cnt cnt;
+  const float *q = rays + 6 * (size_t)i;
+  const v3 o = mk(q[0], q[1], q[2]), ray = mk(q[3], q[4], q[5]);
+  const int32_t loc = S.obj_loc[objs[i]];
+  const int kind = loc >> 28, idx = loc & 0x0FFFFFFF;
+  const RayConst k = ray_const(ray);
+  bool hit = false, any = false;
+  float t = 0.0f, sq = 0.0f, t2, sq2, u = 0.0f, v = 0.0f, u2, v2;
+  v3 norm = mk(0.0f, 0.0f, 0.0f), drop = o;
+  col c = mkc(0.0f, 0.0f, 0.0f);
+  if (kind == 0)
+  {
+    const SphereGeo g = S.sph_geo[idx];
+    SpherePair p;
+    p.cx[0] = g.cx; p.cy[0] = g.cy; p.cz[0] = g.cz; p.r2[0] = g.sq_radius;
+    p.cx[1] = 0.0f; p.cy[1] = 0.0f; p.cz[1] = 0.0f; p.r2[1] = -INFINITY;  // the padding of an odd count
+    f2 b, d;
+    pair_bd(p, o, k, b, d);
+    hit = pair_may_hit(b, d) && sphere_tail<false, false>(b.x, d.x, ray, k, t, sq, cnt);
+    any = pair_may_hit(b, d) && sphere_tail<false, true>(b.x, d.x, ray, k, t2, sq2, cnt);
+    if (hit)
+    {
+      drop = add(o, mul(ray, t));
+      norm = sub(drop, mk(g.cx, g.cy, g.cz));
+      const MatRec m = S.sph_mat[idx];
+      c = mkc(m.r, m.g, m.b);
+    }
+  }
+  else if (kind == 1)
+  {
+    hit = tri_hit<false, false>(S.tri_geo[idx], o, ray, t, u, v, sq, cnt, k);
+    any = tri_hit<false, true>(S.tri_geo[idx], o, ray, t2, u2, v2, sq2, cnt, k);
+    if (hit)
+    {
+      drop = add(o, mul(ray, t));
+      const TriShade sh = S.tri_shade[idx];
+      norm = mk(sh.nx, sh.ny, sh.nz);
+      const MatRec m = S.tri_mat[idx];
+      c = sh.tex >= 0 ? tri_texel<false>(S, sh, u, v, lut, cnt) : mkc(m.r, m.g, m.b);
+    }
+  }
+  else
+  {
+    const PlaneGeo g = S.pln_geo[idx];
+    hit = plane_hit<false, false>(g, o, ray, t, sq, cnt, k);
+    any = plane_hit<false, true>(g, o, ray, t2, sq2, cnt, k);
+    if (hit)
+    {
+      drop = add(o, mul(ray, t));
+      norm = mk(g.nx, g.ny, g.nz);
+      const MatRec m = S.pln_mat[idx];
+      c = mkc(m.r, m.g, m.b);
+    }
+  }
+  float *w = out + 15 * (size_t)i;
+  for (int j = 0; j < 15; ++j) w[j] = 0.0f;
+  w[0] = hit ? 1.0f : 0.0f;
+  if (hit)
+  {
+    const v3 rf = reflect(mul(ray, t), norm);
+    w[1] = drop.x; w[2] = drop.y; w[3] = drop.z;
+    w[4] = norm.x; w[5] = norm.y; w[6] = norm.z;
+    w[7] = rf.x; w[8] = rf.y; w[9] = rf.z;
+    w[10] = sqrt_rn(sq);
+    w[11] = c.r; w[12] = c.g; w[13] = c.b;
+  }
+  w[14] = any ? 1.0f : 0.0f;
+}
+
+// tex >= 0: Texture::getTexelColor(u, v) of texture tex (in: n x 2); tex < 0: Skybox::getTexelColor(ray)
+// (in: n x 3).  out: n x 3.
+__global__ __launch_bounds__(kKatThreads) void kat_texels(DevScene S, int tex, const float *in, uint32_t n, float *out)
+{
+  __shared__ float lut[256];
+  stage_lut(lut);
+  __syncthreads();
+  const uint32_t i = blockIdx.x * kKatThreads + threadIdx.x;
+  if (i >= n) return;
+  Cnt cnt;
+  const col c = tex >= 0 ? texel_uv<false>(S, tex, in[2 * (size_t)i], in[2 * (size_t)i + 1], lut, cnt)
+                         : skybox_texel<false>(S, mk(in[3 * (size_t)i], in[3 * (size_t)i + 1], in[3 * (size_t)i + 2]), lut, cnt);
+  out[3 * (size_t)i] = c.r; out[3 * (size_t)i + 1] = c.g; out[3 * (size_t)i + 2] = c.b;
+}
+
+// pow(x, y) as the bounce loop evaluates it (Scene.cpp:175,196): xy n x 2 -> out n
+__global__ __launch_bounds__(kKatThreads) void kat_powf(const float *xy, uint32_t n, float *out)
+{
+  stage_powf_tables();
+  __syncthreads();
+  const uint32_t i = blockIdx.x * kKatThreads + threadIdx.x;
+  if (i < n) out[i] = powf_dev(xy[2 * (size_t)i], xy[2 * (size_t)i + 1]);
+}
+
+// Color::argb (Color.cpp:114-117) as the epilogue evaluates it: rgb n x 3 -> out n
+__global__ __launch_bounds__(kKatThreads) void kat_argb(const float *rgb, uint32_t n, uint32_t *out)
+{
+  const uint32_t i = blockIdx.x * kKatThreads + threadIdx.x;
+  if (i < n) out[i] = argb(mkc(rgb[3 * (size_t)i], rgb[3 * (size_t)i + 1], rgb[3 * (size_t)i + 2]));
+}
+
 }  // namespace rfx
 
 #ifdef RFX_DEBUG_PROF
@@ -1584,6 +1750,14 @@ static void launch_cfg(int cfg, dim3 grid, const DevScene &S, const FrameParams 
     case 5: launch_one<STATS, MODE, 5>(grid, S, P, st); break;
     case 6: launch_one<STATS, MODE, 6>(grid, S, P, st); break;
     case 7: launch_one<STATS, MODE, 7>(grid, S, P, st); break;
+    case 8: launch_one<STATS, MODE, 8>(grid, S, P, st); break;
+    case 9: launch_one<STATS, MODE, 9>(grid, S, P, st); break;
+    case 10: launch_one<STATS, MODE, 10>(grid, S, P, st); break;
+    case 11: launch_one<STATS, MODE, 11>(grid, S, P, st); break;
+    case 12: launch_one<STATS, MODE, 12>(grid, S, P, st); break;
+    case 13: launch_one<STATS, MODE, 13>(grid, S, P, st); break;
+    case 14: launch_one<STATS, MODE, 14>(grid, S, P, st); break;
+    case 15: launch_one<STATS, MODE, 15>(grid, S, P, st); break;
   }
 }
 
@@ -1602,6 +1776,22 @@ static void launch_mode_cfg(bool stats, int mode, int cfg, dim3 grid, const DevS
     else if (mode == kModePlain) launch_cfg<false, kModePlain>(cfg, grid, S, P, st);
     else launch_cfg<false, kModeSsaa>(cfg, grid, S, P, st);
   }
+}
+
+static dim3 kat_grid(uint32_t n) { return dim3((n + kKatThreads - 1) / kKatThreads); }
+
+hipError_t launch_kat(int what, const DevScene &S, int tex, const void *in, const int32_t *objs, uint32_t n, void *out,
+                      hipStream_t st)
+{
+  if (!n) return hipSuccess;
+  switch (what)
+  {
+    case 0: hipLaunchKernelGGL(kat_objects, kat_grid(n), dim3(kKatThreads), 0, st, S, (const float *)in, objs, n, (float *)out); break;
+    case 1: hipLaunchKernelGGL(kat_texels, kat_grid(n), dim3(kKatThreads), 0, st, S, tex, (const float *)in, n, (float *)out); break;
+    case 2: hipLaunchKernelGGL(kat_powf, kat_grid(n), dim3(kKatThreads), 0, st, (const float *)in, n, (float *)out); break;
+    default: hipLaunchKernelGGL(kat_argb, kat_grid(n), dim3(kKatThreads), 0, st, (const float *)in, n, (uint32_t *)out); break;
+  }
+  return hipGetLastError();
 }
 
 static dim3 trace_grid(const FrameParams &P)
@@ -1624,11 +1814,8 @@ hipError_t launch_trace(const DevScene &S, const FrameParams &P, bool stats, hip
   Pt.tiles_x = kTileWavesX * grid.x;  // wave tiles per row (RFX_WAVE_TILES)
   const int mode = P.ss < 0 ? kModeBlock : (P.ss == 1 && !P.additive && !P.accumulate) ? kModePlain : kModeSsaa;
   // the stats build counts the reference's every test, so it never culls
-  int cfg = (S.n_light > 32 ? kCfgManyLights : 0) | (stats ? 0 : kCfgCull) |
-            (S.n_sph <= 32 && S.n_tri <= 32 ? kCfgSmall : 0);
-#ifdef RFX_NO_CULL
-  cfg &= ~kCfgCull;
-#endif
+  const int cfg = (S.n_light > 32 ? kCfgManyLights : 0) | (stats ? 0 : kCfgCull) |
+                  (S.n_sph <= 32 && S.n_tri <= 32 ? kCfgSmall : 0) | (S.n_pln > 0 ? kCfgPlanes : 0);
   launch_mode_cfg(stats, mode, cfg, grid, S, Pt, st);
   return hipGetLastError();
 }

@@ -33,7 +33,7 @@ constexpr float kFltMax = 3.402823466e+38f;
 // hence the same bits -- and keeps the full sequence for the other inputs.
 RFX_HD float sqrt_rn(float x)
 {
-#if defined(__HIP_DEVICE_COMPILE__) && !defined(RFX_PLAIN_SQRT)
+#if defined(__HIP_DEVICE_COMPILE__)
   if (x >= 0x1p-96f)
   {
     const float s = __builtin_amdgcn_sqrtf(x);

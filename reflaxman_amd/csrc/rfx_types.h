@@ -18,6 +18,7 @@ enum Counter {
   C_L_EVAL, C_L_FACING, C_L_LIT, C_L_SPEC, C_L_POW,
   C_DIELECTRIC, C_METAL, C_CONTINUE, C_SKY,
   C_TEX_BILINEAR, C_TEX_CHECKER, C_TEX_OTHER,
+  C_PLN_TESTS, C_PLN_T, C_HIT_PLN, C_SH_PLN_TESTS, C_SH_PLN_T,
   C_COUNT
 };
 
@@ -46,6 +47,8 @@ struct alignas(16) Bound { float x, y, z, r; };
 // shift), lanes 32-63 triangles 0-31.  A triangle record also carries its plane (unit normal n, n . v0);
 // a sphere's or an empty lane's plane is zero.
 struct alignas(16) CullRec { float x, y, z, r, nx, ny, nz, d; };
+// Plane(pos, norm, material) (Plane.h:6-14): the normal as given (the reference never normalises it)
+struct alignas(16) PlaneGeo { float px, py, pz, nx, ny, nz; int32_t obj, dielectric; };
 struct alignas(16) LightRec { float ox, oy, oz, radius, r, g, b, power; }; // OmniLight.h
 struct alignas(16) TexRec { uint32_t offset, w, h, pad; };
 
@@ -63,8 +66,12 @@ struct DevScene {
   const Bound *bound;         // n_sph + n_tri bounding spheres
   const Bound *chunk_bound;   // n_chunk bounding spheres of 64-sphere chunks (large scenes: Morton order)
   const CullRec *cull_small;  // 64 lane records (small scenes only, else null)
+  const PlaneGeo *pln_geo;    // n_pln (tested by every ray, never culled)
+  const MatRec *pln_mat;      // n_pln
+  const int32_t *obj_loc;     // n_obj: object index -> kind << 28 | index within its kind's device arrays
   uint64_t cull_valid;        // lanes of cull_small that hold an object
   int32_t n_sph, n_tri, n_light, skybox_tex;
+  int32_t n_pln, n_obj, n_tex;
   int32_t n_chunk;            // (n_sph + 63) / 64
   float amb_r, amb_g, amb_b;  // diffLightColor * diffLightPower (Scene.cpp:186, host-folded)
   float env_r, env_g, env_b;  // envColor (Scene.cpp:12,55)

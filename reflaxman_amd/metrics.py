@@ -26,6 +26,7 @@ COUNTER_NAMES = [
     "l_eval", "l_facing", "l_lit", "l_spec", "l_pow",
     "dielectric", "metal", "continue", "sky",
     "tex_bilinear", "tex_checker", "tex_other",
+    "pln_tests", "pln_t", "hit_pln", "sh_pln_tests", "sh_pln_t",
 ]
 
 # FLOPs per event (see module docstring for the rule)
@@ -58,6 +59,10 @@ FLOP_WEIGHTS = {
     "tex_bilinear": 45, # fx, fy, fractions (6), 4 texels ARGB/255 (12), lerp (27)
     "tex_checker": 2,   # u*50, v*50
     "tex_other": 3,
+    "pln_tests": 13,    # pos - o (3), norm . ray (5), norm . vop (5)            Plane.cpp:40-45
+    "pln_t": 9,         # t (1), ray * t (3), |.|^2 (5)                          Plane.cpp:45-50
+    "hit_pln": 45,      # sqrt (1), ray*t, drop (6), reflect (20), lengths (18)
+    "sh_pln_tests": 13, "sh_pln_t": 9,
 }
 
 POW_EVENTS = ("l_pow", "dielectric")  # one powf each
@@ -87,7 +92,7 @@ def summary(counts) -> dict:
         "flops_per_ray": flops(counts) / rays,
         "segments_per_ray": counts["segments"] / rays,
         "shadow_rays_per_ray": counts["l_facing"] / rays,
-        "isect_tests_per_ray": (counts["sph_tests"] + counts["tri_tests"]) / rays,
-        "shadow_tests_per_ray": (counts["sh_sph_tests"] + counts["sh_tri_tests"]) / rays,
+        "isect_tests_per_ray": (counts["sph_tests"] + counts["tri_tests"] + counts.get("pln_tests", 0)) / rays,
+        "shadow_tests_per_ray": (counts["sh_sph_tests"] + counts["sh_tri_tests"] + counts.get("sh_pln_tests", 0)) / rays,
         "pow_calls": sum(counts[k] for k in POW_EVENTS),
     }

@@ -64,6 +64,7 @@ class SceneDesc:
     textures: List[Texture] = field(default_factory=list)  # addTexture order
     lights: List[tuple] = field(default_factory=list)      # (origin3, radius, rgb3, power)
     objects: List[tuple] = field(default_factory=list)     # ('sphere', c3, r, mat) | ('triangle', v0, v1, v2, mat)
+                                                           # | ('plane', pos3, norm3, mat)
     settex: List[tuple] = field(default_factory=list)      # (object_index, texture_index, uv6)
 
     # ---- builders (mirroring the reference calls) ----
@@ -77,6 +78,11 @@ class SceneDesc:
 
     def add_triangle(self, v0, v1, v2, mat_type, rgb, refl, transp=0.0):
         self.objects.append(("triangle", tuple(map(f32, v0)), tuple(map(f32, v1)), tuple(map(f32, v2)),
+                             (int(mat_type), tuple(map(f32, rgb)), f32(refl), f32(transp))))
+        return len(self.objects) - 1
+
+    def add_plane(self, pos, norm, mat_type, rgb, refl, transp=0.0):
+        self.objects.append(("plane", tuple(map(f32, pos)), tuple(map(f32, norm)),
                              (int(mat_type), tuple(map(f32, rgb)), f32(refl), f32(transp))))
         return len(self.objects) - 1
 
@@ -124,6 +130,8 @@ class SceneDesc:
             mt, rgb, refl, tr = ob[-1]
             if ob[0] == "sphere":
                 lines.append("sphere " + " ".join(h(v) for v in (*ob[1], ob[2], mt, *rgb, refl, tr)))
+            elif ob[0] == "plane":
+                lines.append("plane " + " ".join(h(v) for v in (*ob[1], *ob[2], mt, *rgb, refl, tr)))
             else:
                 lines.append("triangle " + " ".join(h(v) for v in (*ob[1], *ob[2], *ob[3], mt, *rgb, refl, tr)))
         for (oi, ti, uv) in self.settex:
@@ -298,11 +306,93 @@ def stress_scene(n_spheres: int = 4096) -> SceneDesc:
     return s
 
 
+def _base(name: str) -> SceneDesc:
+    return SceneDesc(name, (f32(0.95), f32(0.95), f32(1.0), f32(0.15)),
+                     (tuple(map(f32, DEFAULT_CAMERA[0])), tuple(map(f32, DEFAULT_CAMERA[1])), f32(DEFAULT_CAMERA[2])))
+
+
+def lights_scene(n_lights: int) -> SceneDesc:
+    """Parity scene for the batched light loop: synth16 with n lights -- the sun, then lights at finite
+    distance (specular exponents 1 + 3 refl |L| / r far below the sun's) on a ring above the scene, each with
+    power 0.8 / n so envColor (the sum of colour x power, Scene.cpp:55) stays near the default's.
+    n > 32 takes the kernel's many-lights instantiation (shadow masks in blocks of 32)."""
+    s = synth16_scene()
+    s.name = f"lights{n_lights}"
+    s.lights = []
+    _add_sun(s)
+    g = Lcg(4040 + n_lights)
+    for k in range(n_lights - 1):
+        ang = 2.0 * np.pi * k / max(1, n_lights - 1)
+        o = (6.0 * np.cos(ang) + g.uniform(-1, 1), g.uniform(4.0, 9.0), 5.0 * np.sin(ang) + g.uniform(-1, 1))
+        s.add_light(o, g.uniform(0.2, 1.5), (g.uniform(0.4, 1), g.uniform(0.4, 1), g.uniform(0.4, 1)), 0.8 / n_lights)
+    return s
+
+
+def nolight_scene() -> SceneDesc:
+    """The default scene without a light: no shadow rays, ambient and sky only."""
+    s = default_scene()
+    s.name = "nolight"
+    s.lights = []
+    return s
+
+
+def mesh_scene(nx: int = 10, nz: int = 5) -> SceneDesc:
+    """More than 64 triangles (2 nx nz): the general (non-small) object loops with two 64-triangle chunks.  A
+    height-field ground mesh with per-triangle textures and materials, the 8 default spheres above it."""
+    s = _base(f"mesh{2 * nx * nz}")
+    _add_sun(s)
+    _add_default_spheres(s)
+    t0 = s.add_texture(synth_texture("ground", 256, 256, 1001))
+    t1 = s.add_texture(Texture("himiya", None))
+    g = Lcg(777)
+    x0, x1, z0, z1 = -14.0, 14.0, -10.0, 10.0
+    hgt = [[0.0 if (i in (0, nx) or j in (0, nz)) else g.uniform(-0.3, 0.3) for j in range(nz + 1)] for i in range(nx + 1)]
+    for i in range(nx):
+        for j in range(nz):
+            xa, xb = x0 + (x1 - x0) * i / nx, x0 + (x1 - x0) * (i + 1) / nx
+            za, zb = z0 + (z1 - z0) * j / nz, z0 + (z1 - z0) * (j + 1) / nz
+            p00, p01 = (xa, hgt[i][j], za), (xa, hgt[i][j + 1], zb)
+            p10, p11 = (xb, hgt[i + 1][j], za), (xb, hgt[i + 1][j + 1], zb)
+            mt = DIELECTRIC if (i + j) % 3 else METAL
+            rgb = (g.uniform(0.5, 1), g.uniform(0.5, 1), g.uniform(0.5, 1))
+            a = s.add_triangle(p00, p01, p10, mt, rgb, g.uniform(0.2, 0.95))
+            b = s.add_triangle(p01, p11, p10, mt, rgb, g.uniform(0.2, 0.95))
+            tex = t0 if (i + j) % 2 else t1
+            u0, u1, v0, v1 = i / nx, (i + 1) / nx, j / nz, (j + 1) / nz
+            s.set_texture(a, tex, (u0, v0, u0, v1, u1, v0))
+            s.set_texture(b, tex, (u0, v1, u1, v1, u1, v0))
+    return s
+
+
+def planes_scene(n_spheres: int = 0) -> SceneDesc:
+    """Planes in a scene (the addPlane extension of Plane.cpp:36-73): the 8 default spheres (or n LCG spheres,
+    the general object loops), a textured ground triangle pair, then a dielectric floor plane just below the
+    ground (normal not of unit length, as the reference allows) and a metal back-wall plane tilted towards the
+    camera.  Objects are added spheres, triangles, planes (the order the kernels visit them)."""
+    s = _base(f"planes{n_spheres}" if n_spheres else "planes")
+    _add_sun(s)
+    if n_spheres:
+        _lcg_spheres(s, n_spheres)
+    else:
+        _add_default_spheres(s)
+    ti = s.add_texture(synth_texture("ground", 128, 128, 1001))
+    _add_ground(s, ti)
+    s.add_plane((0.0, -0.05, 0.0), (0.0, 2.0, 0.0), DIELECTRIC, (0.8, 0.85, 0.9), 0.6)
+    s.add_plane((-16.0, 0.0, 0.0), (1.0, 0.05, 0.2), METAL, (0.9, 0.7, 0.5), 0.4)
+    return s
+
+
 SCENES = {
     "default": default_scene,
     "synth16": synth16_scene,
     "synth16_sky": lambda: synth16_scene(skybox=True),
     "stress4096": stress_scene,
+    "lights3": lambda: lights_scene(3),
+    "lights40": lambda: lights_scene(40),
+    "nolight": nolight_scene,
+    "mesh100": mesh_scene,
+    "planes": planes_scene,
+    "planes300": lambda: planes_scene(300),
 }
 
 
@@ -345,6 +435,8 @@ def parse_scene_file(path: str) -> SceneDesc:
             s.add_sphere(v[0:3], v[3], int(v[4] != 0), v[5:8], v[8], v[9])
         elif kw == "triangle":
             s.add_triangle(v[0:3], v[3:6], v[6:9], int(v[9] != 0), v[10:13], v[13], v[14])
+        elif kw == "plane":
+            s.add_plane(v[0:3], v[3:6], int(v[6] != 0), v[7:10], v[10], v[11])
         elif kw == "settex":
             s.set_texture(int(v[0]), int(v[1]), v[2:8])
         else:

@@ -23,6 +23,20 @@ static void check(float x, float y)
 
 int main(int argc, char **argv)
 {
+  if (argc == 4 && !strcmp(argv[1], "-f"))
+  {
+    // -f IN OUT: (x, y) f32 pairs from IN -> the restatement's powf(x, y) to OUT (KAT replay)
+    FILE *fi = fopen(argv[2], "rb"), *fo = fopen(argv[3], "wb");
+    if (!fi || !fo) return 2;
+    float xy[2];
+    while (fread(xy, sizeof(xy), 1, fi) == 1)
+    {
+      const float r = rfx::powf_glibc(xy[0], xy[1]);
+      fwrite(&r, sizeof(r), 1, fo);
+    }
+    fclose(fi); fclose(fo);
+    return 0;
+  }
   unsigned long long n_random = argc > 1 ? strtoull(argv[1], 0, 10) : 10000000ull;
   unsigned stride = argc > 2 ? (unsigned)strtoul(argv[2], 0, 10) : 7;
   // Scene.cpp:196 -- Fresnel: every stride-th float in [0, 1], y = 3

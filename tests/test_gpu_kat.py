@@ -1,0 +1,143 @@
+"""Device known answers: the trace kernel's own primitive code (rfx.h rfx_kat_*) against the outputs the
+unmodified reference computed for the same inputs (tests/golden/kat_*.npz, tools/gen_golden.py):
+
+* Sphere::trace / Triangle::trace (untextured, bilinear-textured, checker-textured) / Plane::trace with and
+  without out-parameters (Sphere.cpp:44-85, Triangle.cpp:53-108, Plane.cpp:36-73) on seeded rays built to hit
+  the edge cases -- inside-sphere origins, surface +- DELTA, tangents, rays pointing away, zero rays, the radius
+  clamp, barycentric edges, near-degenerate and parallel triangles, origins on a vertex, parallel planes;
+* Skybox::getTexelColor (checker and atlas) on the 6 faces, edges, corners, the zero ray;
+* Texture::getTexelColor(u, v) on the [0, 1] boundaries and 1 - FLT_EPSILON (32- and 24-bpp TGA texels);
+* powf at both Scene.cpp call sites' domains (glibc 2.35, kat_pow.npz) and Color::argb.
+
+Bar: bit-exact (0 ULP on every output float).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from helpers import GOLDEN
+from reflaxman_amd.render import DIELECTRIC, METAL, Color, Material, Renderer, Scene, Vector3
+
+pytestmark = pytest.mark.gpu
+
+KAT_MAT = Material(METAL, Color(0.25, 0.5, 0.75), 0.5, 0.0)  # oracle/ref_harness.cpp kat_material
+
+
+def load(key):
+    return np.load(os.path.join(GOLDEN, key + ".npz"))
+
+
+def run_objects(scene, rays, n):
+    r = Renderer()
+    r.set_scene(scene)
+    out = r.kat_objects(rays, np.arange(n, dtype=np.int32))
+    r.close()
+    return out
+
+
+def assert_same(out, ref, key):
+    bad = np.argwhere(out.view(np.uint32) != ref.view(np.uint32))
+    assert bad.size == 0, f"{key}: {len(bad)} values differ, first {bad[:5].tolist()}"
+
+
+def test_kat_sphere():
+    g = load("kat_sphere")
+    rec = g["inp"]
+    s = Scene()
+    for q in rec:
+        s.addSphere(Vector3(*q[6:9]), float(q[9]), KAT_MAT)
+    out = run_objects(s, rec[:, :6], rec.shape[0])
+    assert g["out"][:, 0].sum() > 100 and g["out"][:, 14].sum() > 100
+    assert_same(out, g["out"], "kat_sphere")
+
+
+@pytest.mark.parametrize("key,texture", [("kat_triangle", "none"), ("kat_triangle_tex", "tex"),
+                                         ("kat_triangle_checker", "empty")])
+def test_kat_triangle(key, texture):
+    g = load(key)
+    rec = g["inp"]
+    s = Scene()
+    tex = None
+    if texture != "none":
+        tex = s.addTextureArgb(g["tex"] if texture == "tex" else None)
+    for q in rec:
+        t = s.addTriangle(Vector3(*q[6:9]), Vector3(*q[9:12]), Vector3(*q[12:15]), KAT_MAT)
+        if tex is not None:
+            t.setTexture(tex, *[float(v) for v in q[15:21]])
+    out = run_objects(s, rec[:, :6], rec.shape[0])
+    assert g["out"][:, 0].sum() > 100
+    assert_same(out, g["out"], key)
+
+
+def test_kat_plane():
+    g = load("kat_plane")
+    rec = g["inp"]
+    s = Scene()
+    for q in rec:
+        s.addPlane(Vector3(*q[6:9]), Vector3(*q[9:12]), KAT_MAT)
+    out = run_objects(s, rec[:, :6], rec.shape[0])
+    assert g["out"][:, 0].sum() > 100
+    assert_same(out, g["out"], "kat_plane")
+
+
+def test_kat_mixed_objects_one_scene():
+    """Spheres, triangles and planes in ONE scene (the object map through the Morton sphere order)."""
+    gs, gt, gp = load("kat_sphere"), load("kat_triangle"), load("kat_plane")
+    s = Scene()
+    rays, objs, ref = [], [], []
+    n = 300
+    for i in range(n):
+        a, b, c = gs["inp"][i], gt["inp"][i], gp["inp"][i]
+        objs.append(s.addSphere(Vector3(*a[6:9]), float(a[9]), KAT_MAT).obj); rays.append(a[:6]); ref.append(gs["out"][i])
+        objs.append(s.addTriangle(Vector3(*b[6:9]), Vector3(*b[9:12]), Vector3(*b[12:15]), KAT_MAT).obj)
+        rays.append(b[:6]); ref.append(gt["out"][i])
+        objs.append(s.addPlane(Vector3(*c[6:9]), Vector3(*c[9:12]), KAT_MAT).obj); rays.append(c[:6]); ref.append(gp["out"][i])
+    r = Renderer()
+    r.set_scene(s)
+    perm = np.random.default_rng(5).permutation(len(objs))
+    out = r.kat_objects(np.array(rays)[perm], np.array(objs, np.int32)[perm])
+    r.close()
+    assert_same(out, np.array(ref)[perm], "mixed")
+
+
+@pytest.mark.parametrize("key,skybox", [("kat_skybox_checker", False), ("kat_skybox_tex", True)])
+def test_kat_skybox(key, skybox):
+    g = load(key)
+    s = Scene()
+    if skybox:
+        s.setSkyboxTextureArgb(g["tex"])
+    r = Renderer()
+    r.set_scene(s)
+    out = r.kat_texels(-1, g["inp"])
+    r.close()
+    assert_same(out, g["out"], key)
+
+
+@pytest.mark.parametrize("key,textured", [("kat_texture_checker", False), ("kat_texture_tex", True),
+                                          ("kat_texture_tex24", True)])
+def test_kat_texture(key, textured):
+    g = load(key)
+    s = Scene()
+    s.addTextureArgb(g["tex"] if textured else None)
+    r = Renderer()
+    r.set_scene(s)
+    out = r.kat_texels(0, g["inp"])
+    r.close()
+    assert_same(out, g["out"], key)
+
+
+def test_kat_powf():
+    g = load("kat_pow")
+    r = Renderer()
+    out = r.kat_powf(g["inp"])
+    r.close()
+    assert_same(out, g["out"], "kat_pow")
+
+
+def test_kat_argb():
+    g = load("kat_argb")
+    r = Renderer()
+    out = r.kat_argb(g["inp"])
+    r.close()
+    assert np.array_equal(out, g["out"])

@@ -44,9 +44,10 @@ def test_golden_bitexact(key):
 
 
 @pytest.mark.parametrize("key", ["hash_default_640x480_d4", "hash_default_1920x1080_d4",
-                                 "hash_synth16_3840x2160_d8", "hash_default_3840x2160_d8"])
+                                 "hash_synth16_3840x2160_d8", "hash_default_3840x2160_d8",
+                                 "hash_synth16_7680x4320_d8"])
 def test_full_size_hash(key):
-    """BASELINE configs C1, C2, C3 (and the default scene at 4K d8) at full size, bit-exact by SHA-256."""
+    """BASELINE configs C1, C2, C3, C4 (and the default scene at 4K d8) at full size, bit-exact by SHA-256."""
     c = CASES[key]
     rgb, argb, r = run_case(c)
     assert sha(argb) == c["sha_argb"], key
@@ -299,7 +300,9 @@ def test_event_counters_match_oracle():
     import oracle as orc
     from reflaxman_amd import _lib
     from reflaxman_amd.render import Renderer, build_scene, make_frame
-    for name, W, H, depth in (("default", 64, 48, 8), ("synth16", 64, 36, 8), ("synth16_sky", 48, 27, 6)):
+    for name, W, H, depth in (("default", 64, 48, 8), ("synth16", 64, 36, 8), ("synth16_sky", 48, 27, 6),
+                              ("planes", 64, 36, 8), ("planes300", 48, 27, 6), ("lights3", 48, 27, 8),
+                              ("lights40", 32, 18, 6), ("mesh100", 48, 27, 6), ("nolight", 48, 36, 4)):
         desc = scene(name)
         o = orc.OracleRender(desc, 4242, 0)
         o.set_image_size(W, H)
@@ -314,5 +317,74 @@ def test_event_counters_match_oracle():
         L = _lib.load()
         _lib.check(L.rfx_render_frame_host(rr._h, C.byref(f), _lib.fptr(img), None, _lib.u64ptr(gc)))
         assert img.tobytes() == o.image.tobytes()
-        assert gc.tolist() == oc.tolist(), dict(zip(orc.COUNTER_NAMES, zip(gc.tolist(), oc.tolist())))
+        # more than 32 spheres: the kernel visits them in Morton order, so the shadow any-hit (which stops at
+        # the first occluder) runs a different number of tests than the oracle's insertion order; its boolean
+        # and every other counter are order-independent
+        skip = {k for k in orc.COUNTER_NAMES if k.startswith("sh_")} if desc.n_spheres > 32 else set()
+        bad = {k: (int(a), int(b)) for k, a, b in zip(orc.COUNTER_NAMES, gc, oc) if a != b and k not in skip}
+        assert not bad, (name, bad)
         rr.close()
+
+
+@pytest.mark.parametrize("nranks", [2, 4, 8])
+def test_c4_strips_assemble_to_reference_hash(nranks):
+    """C4 (the C3 scene at 7680x4320 d8, BASELINE configs[3]) as the multi-GPU path renders it -- each rank
+    counts its slice of the random stream, the counts are exchanged (emulated: every rank counts every slice),
+    each rank emits and traces only its 8-row block-cyclic strips -- assembled in one process: SHA-256 of the
+    f32 frame and of the ARGB8 frame equal the reference's."""
+    import ctypes as C
+    from reflaxman_amd import _lib
+    from reflaxman_amd.render import Renderer, build_scene, make_frame
+    c = CASES["hash_synth16_7680x4320_d8"]
+    W, H, depth, rb = c["W"], c["H"], c["depth"], 8
+    s, cam = build_scene(scene("synth16"))
+    L = _lib.load()
+    img = np.zeros((H, W, 3), np.float32)
+    argb = np.zeros((H, W), np.uint32)
+    for rank in range(nranks):
+        rr = Renderer(sphere_seed=c["sphere_seed"])
+        rr.set_scene(s)
+        f = make_frame(cam, W, H, depth, 1, row_block=rb, rank=rank, nranks=nranks)
+        bps = C.c_uint64()
+        _lib.check(L.rfx_frame_rng_blocks(rr._h, C.byref(f), nranks, C.byref(bps)))
+        d_cnt = C.c_void_p()
+        _lib.check(L.rfx_device_alloc(rr._h, nranks * bps.value * 4, C.byref(d_cnt)))
+        for sl in range(nranks):
+            _lib.check(L.rfx_frame_rng_count(rr._h, C.byref(f), sl, nranks, d_cnt, None))
+        rows = L.rfx_strip_rows(H, rb, rank, nranks)
+        p_img, p_argb = C.c_void_p(), C.c_void_p()
+        _lib.check(L.rfx_device_alloc(rr._h, rows * W * 12, C.byref(p_img)))
+        _lib.check(L.rfx_device_alloc(rr._h, rows * W * 4, C.byref(p_argb)))
+        _lib.check(L.rfx_render_frame_counted(rr._h, C.byref(f), nranks, d_cnt, p_img, p_argb, None, None))
+        part = np.empty((rows, W, 3), np.float32)
+        part_argb = np.empty((rows, W), np.uint32)
+        _lib.check(L.rfx_memcpy_d2h(rr._h, part.ctypes.data_as(C.c_void_p), p_img, part.nbytes))
+        _lib.check(L.rfx_memcpy_d2h(rr._h, part_argb.ctypes.data_as(C.c_void_p), p_argb, part_argb.nbytes))
+        ys = np.array([L.rfx_strip_row_to_y(i, rb, rank, nranks) for i in range(rows)])
+        img[ys] = part
+        argb[ys] = part_argb
+        for p in (d_cnt, p_img, p_argb):
+            L.rfx_device_free(rr._h, p)
+        rr.close()
+    assert sha(argb) == c["sha_argb"]
+    assert sha(img) == c["sha_f32"]
+
+
+def test_textures_loaded_from_tga_files(tmp_path):
+    """The scene's textures read from TGA files by the library's loader (Scene.addTexture /
+    setSkyboxTexture, Texture.cpp:34-108) -- the files the reference read for the same golden."""
+    key = "render_synth16_sky_160x90_d8"
+    c = CASES[key]
+    from reflaxman_amd.render import Render, build_scene
+    r = Render(sphere_seed=c["sphere_seed"], jitter_seed=0, load_default_scene=False)
+    r.scene, r.camera = build_scene(scene(c["scene"]), texture_dir=str(tmp_path))
+    assert r.scene.counts() == (16, 4, 1, 3)
+    r.setImageSize(c["W"], c["H"])
+    r.renderBegin(c["depth"], 1, False)
+    while r.renderNext(c["W"] * c["H"]):
+        pass
+    r.synchronize()
+    g = np.load(os.path.join(GOLDEN, key + ".npz"))
+    assert np.array_equal(r.copyImage(), g["argb"])
+    assert r.imagePixels().tobytes() == g["rgb"].tobytes()
+    r.close()

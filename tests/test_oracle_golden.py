@@ -49,7 +49,8 @@ def test_render_bitexact(key):
 
 
 @pytest.mark.parametrize("key", ["hash_default_640x480_d4", "hash_default_1920x1080_d4",
-                                 "hash_synth16_3840x2160_d8", "hash_default_3840x2160_d8"])
+                                 "hash_synth16_3840x2160_d8", "hash_default_3840x2160_d8",
+                                 "hash_synth16_7680x4320_d8"])
 def test_full_size_hash(key):
     c = CASES[key]
     rgb, argb = render_oracle(c, nthreads=os.cpu_count() or 8)
@@ -118,7 +119,8 @@ def test_camera_kat():
     assert out.tobytes() == g["out"].tobytes()
 
 
-def test_pow_kat_is_libm():
-    """The fixture's pow values are glibc powf; numpy's float32 power is NOT used anywhere."""
+def test_pow_kat_shape():
+    """kat_pow.npz is compared value by value in tests/test_powf.py (host restatement and live libm) and
+    tests/test_gpu_kat.py (device powf)."""
     g = np.load(os.path.join(GOLDEN, "kat_pow.npz"))
-    assert g["out"].dtype == np.float32 and g["out"].shape[0] == g["inp"].shape[0]
+    assert g["out"].dtype == np.float32 and g["out"].shape[0] == g["inp"].shape[0] == 40007

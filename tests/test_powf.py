@@ -22,3 +22,22 @@ def test_powf_bitexact_vs_libm(checker):
     r = subprocess.run([checker, "20000000", "7"], capture_output=True, text=True)
     assert r.returncode == 0, r.stdout + r.stderr
     assert " 0 mismatches" in r.stdout
+
+
+def test_powf_restatement_matches_reference_kat(checker, tmp_path):
+    """kat_pow.npz: powf at both call sites' domains as the reference computed it (tools/gen_golden.py,
+    refharness kat_pow).  The fixture equals this host's live glibc powf and the product restatement."""
+    import ctypes
+    import numpy as np
+    g = np.load(os.path.join(ROOT, "tests", "golden", "kat_pow.npz"))
+    inp = np.ascontiguousarray(g["inp"], np.float32)
+    libm = ctypes.CDLL("libm.so.6")
+    libm.powf.restype = ctypes.c_float
+    libm.powf.argtypes = [ctypes.c_float, ctypes.c_float]
+    live = np.array([libm.powf(float(x), float(y)) for x, y in inp], np.float32)
+    assert live.tobytes() == g["out"].tobytes()
+    fi, fo = tmp_path / "in.bin", tmp_path / "out.bin"
+    inp.tofile(fi)
+    subprocess.run([checker, "-f", str(fi), str(fo)], check=True)
+    ours = np.fromfile(fo, np.float32)
+    assert ours.tobytes() == g["out"].tobytes(), np.argwhere(ours != g["out"])[:5]

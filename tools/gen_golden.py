@@ -163,6 +163,39 @@ def pow_inputs(rng, n=40000):
     return np.concatenate([np.stack([x1, y1], 1), np.stack([x2, y2], 1)]).astype(np.float32)
 
 
+def tga_cases() -> dict:
+    """Hand-made TGA files for Texture::loadFromTGAFile (Texture.cpp:34-108): file name -> bytes."""
+    import struct
+    tex = scenes.synth_texture("t", 5, 3, 5150).argb
+
+    def hdr(idlen=0, cmt=0, itype=2, cmorg=0, cmlen=0, cmbits=0, w=5, h=3, bpp=32, desc=0):
+        return struct.pack("<bbbhhbhhhhbb", idlen, cmt, itype, cmorg, cmlen, cmbits, 0, 0, w, h, bpp, desc)
+
+    def px(bpp, a=tex):
+        b, g, r, al = a & 0xFF, (a >> 8) & 0xFF, (a >> 16) & 0xFF, (a >> 24) & 0xFF
+        ch = [b, g, r, al] if bpp == 32 else [b, g, r]
+        return np.stack(ch, -1).astype(np.uint8).tobytes()
+
+    big = scenes.synth_texture("b", 300, 250, 6160).argb  # > 32768 pixels: the reader's buffer refills
+    c = {
+        "t32.tga": hdr() + px(32),
+        "t24.tga": hdr(bpp=24) + px(24),
+        "t32_id.tga": hdr(idlen=7) + b"ident!!" + px(32),
+        "t24_cmap.tga": hdr(cmlen=4, cmbits=24) + bytes(12) + px(24),
+        "t32_origin.tga": hdr(desc=0x20) + px(32),
+        "t32_big.tga": hdr(w=300, h=250) + px(32, big),
+        "t32_trailing.tga": hdr() + px(32) + b"extra bytes",
+        "short_pixels.tga": hdr() + px(32)[:-1],
+        "short_header.tga": hdr()[:10],
+        "type10.tga": hdr(itype=10) + px(32),
+        "bpp16.tga": hdr(bpp=16) + px(32),
+        "empty.tga": b"",
+        "not_tga.bmp": hdr() + px(32),
+        "zero_w.tga": hdr(w=0) + px(32),
+    }
+    return c
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="")
@@ -189,7 +222,8 @@ def main():
     with tempfile.TemporaryDirectory() as tmp:
         sc_dir = os.path.join(tmp, "scenes")
         scene_files = {}
-        for name in ("default", "synth16", "synth16_sky", "stress4096"):
+        for name in ("default", "synth16", "synth16_sky", "stress4096", "lights3", "lights40", "nolight", "mesh100",
+                     "planes", "planes300"):
             desc = scenes.get_scene(name)
             scene_files[name] = desc.write(sc_dir)
 
@@ -234,11 +268,63 @@ def main():
         save_render("render_synth16_sky_160x90_d8", "synth16_sky", 160, 90, 8)
         # 6. stress
         save_render("render_stress4096_64x36_d12", "stress4096", 64, 36, 12)
+        # light loop (3 lights; 40 > 32: the many-lights kernel), no light, > 64 triangles (general object loops),
+        # planes (the addPlane extension; the reference's Plane in the reference's Scene::trace)
+        save_render("render_lights3_160x90_d8", "lights3", 160, 90, 8)
+        save_render("render_lights40_96x54_d8", "lights40", 96, 54, 8)
+        save_render("render_nolight_160x120_d4", "nolight", 160, 120, 4)
+        save_render("render_mesh100_160x90_d8", "mesh100", 160, 90, 8)
+        save_render("render_planes_160x90_d8", "planes", 160, 90, 8)
+        save_render("render_planes_64x36_d6_ss2_add2", "planes", 64, 36, 6, ss=2, additive=True, frames=2, jseed=77)
+        save_render("render_planes300_96x54_d8", "planes300", 96, 54, 8)
         # full-size hashes only (C1, C3; the default 4K d8 too -- SURVEY Appendix B)
         save_render("hash_default_640x480_d4", "default", 640, 480, 4, store=False, use_file=False)
         save_render("hash_synth16_3840x2160_d8", "synth16", 3840, 2160, 8, store=False)
         save_render("hash_default_3840x2160_d8", "default", 3840, 2160, 8, store=False, use_file=False)
         save_render("hash_default_1920x1080_d4", "default", 1920, 1080, 4, store=False, use_file=False)
+        # C4: the C3 scene at 7680x4320 d8 (BASELINE configs[3])
+        save_render("hash_synth16_7680x4320_d8", "synth16", 7680, 4320, 8, store=False)
+
+        # C4 band: 4 rows at the middle of the 8K frame (stream advanced over the 2160 rows above)
+        key = "band_synth16_7680x4320_d8_y2160_r4"
+        if want(key):
+            t0 = time.time()
+            rgb, argb = band_case(tmp, scene_files["synth16"], 7680, 4320, 8, 2160, 4, DEFAULT_SEED)
+            np.savez_compressed(os.path.join(GOLDEN, key + ".npz"), rgb=rgb, argb=argb)
+            cases[key] = dict(kind="band", scene="synth16", W=7680, H=4320, depth=8, y0=2160, rows=4,
+                              sphere_seed=DEFAULT_SEED, sha_f32=sha(rgb.tobytes()), sha_argb=sha(argb.tobytes()))
+            print(f"{key}: {time.time() - t0:.1f}s", flush=True)
+
+        # file formats: the bytes Texture::saveToFile writes (BMP, TGA) and what Texture::loadFromFile reads
+        # back from hand-made TGA files (24/32 bpp, id field, colour-map fields, origin bit, broken files)
+        if want("file"):
+            img = scenes.synth_texture("img", 7, 5, 99).argb
+            src = os.path.join(tmp, "img.u32")
+            img.tofile(src)
+            outs = {}
+            for ext in ("bmp", "tga", "png"):
+                fn = os.path.join(tmp, "out." + ext)
+                r = subprocess.run([HARNESS, "savetex", "7", "5", src, fn], check=True, capture_output=True, text=True)
+                ok = int(r.stdout.strip())
+                outs[ext] = (ok, np.fromfile(fn, np.uint8) if ok else np.zeros(0, np.uint8))
+            np.savez_compressed(os.path.join(GOLDEN, "file_save.npz"), argb=img, bmp=outs["bmp"][1], tga=outs["tga"][1],
+                                ok=np.array([outs["bmp"][0], outs["tga"][0], outs["png"][0]], np.int32))
+            cases["file_save"] = dict(kind="file", what="Texture(7, 5) + saveToFile(.bmp / .tga / .png)")
+            loads = {}
+            for name, data in tga_cases().items():
+                fn = os.path.join(tmp, name)
+                open(fn, "wb").write(data)
+                fo = os.path.join(tmp, "load.out")
+                run(["loadtex", fn, fo])
+                loads[name] = (data, np.fromfile(fo, np.uint32))
+            arrays = {}
+            for i, (name, (data, out)) in enumerate(sorted(loads.items())):
+                arrays[f"in{i}"] = np.frombuffer(data, np.uint8)
+                arrays[f"out{i}"] = out
+            np.savez_compressed(os.path.join(GOLDEN, "file_load.npz"), names=np.array(sorted(loads)), **arrays)
+            cases["file_load"] = dict(kind="file", what="Texture::loadFromFile on hand-made TGA files",
+                                      names=sorted(loads))
+            print("file fixtures", flush=True)
 
         # stress bands (4K width) with stream advance
         for y0 in (0, 1080):
