@@ -1,11 +1,11 @@
 #!/usr/bin/env python3
 """bench.py -- Mrays/s of ReflaxMan's per-pixel trace loop on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1..c5]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
-Workload (BASELINE.json metric "Mrays/sec at 3840x2160 depth-8"): config C3 --
-the synth16 scene (16 spheres, ground + back-wall quads = 4 textured
+Workload (BASELINE.json metric "Mrays/sec at 3840x2160 depth-8"): at N = 1 config
+C3 -- the synth16 scene (16 spheres, ground + back-wall quads = 4 textured
 triangles, the default sun light => shadow rays), 3840x2160, depth 8, 1 spp,
 synthetic 512x512 TGA textures.  A step is one full frame of the hot path
 (Render::renderBegin + renderNext(W*H)): the RNG pre-pass, the trace kernel and
@@ -13,14 +13,16 @@ the ARGB8 epilogue, inputs and outputs resident in HBM.  Every step renders
 the *next* frame of the reference's global random stream, as the reference app
 does.
 
-N > 1 (weak scaling): the frame grows with N at 16:9 (N=4 is C4, 7680x4320);
-rows are dealt to ranks in block-cyclic 8-row strips, each rank traces its
-strips; the RNG pre-pass is sliced too (each rank counts 1/N of the random
-stream, one all-gather of ~1K block counts over RCCL), and the ARGB8 strips
-are gathered to rank 0 over RCCL (xGMI) and un-interleaved on device.  The
-gather of frame i runs on its own communicator while frame i+1 renders
-(double-buffered strips; --no-pipeline serialises them).  value = traces of the whole frame / step time
-(max over ranks).
+N > 1: config C4 (BASELINE configs[3]) -- the C3 scene at a FIXED 7680x4320 d8
+frame (strong scaling; --scaling weak grows the frame with N instead).  Rows
+are dealt to ranks in block-cyclic 8-row strips, each rank traces its strips;
+the RNG pre-pass is sliced too (each rank counts 1/N of the random stream, one
+all-gather of ~1K block counts over RCCL), and the ARGB8 strips (with
+--gather-rgb also the float RGB strips) are gathered to rank 0 over RCCL (xGMI)
+and un-interleaved on device.  The gather of frame i runs on its own
+communicator while frame i+1 renders (double-buffered strips; --no-pipeline
+serialises them).  value = traces of the whole frame / step time (max over
+ranks).
 
 Also reported: the trace kernel's algorithmic TFLOP/s against the FP32 VALU
 peak (roofline), its HIP-event time, full-frame parity (SHA-256 of the first
@@ -52,8 +54,18 @@ def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
 
-def frame_size(n: int, w0: int, h0: int):
-    if n == 1:
+# BASELINE.json configs: scene, width, height, depth, description
+CONFIGS = {
+    "c1": ("default", 640, 480, 4, "C1 default scene (Render::loadScene, textures absent -> checker)"),
+    "c2": ("default", 1920, 1080, 4, "C2 default scene"),
+    "c3": ("synth16", 3840, 2160, 8, "C3 synth16: 16 spheres + 4 textured triangles + sun"),
+    "c4": ("synth16", 7680, 4320, 8, "C4 synth16 (the C3 scene: 16 spheres + 4 textured triangles + sun)"),
+    "c5": ("stress4096", 3840, 2160, 12, "C5 stress4096: 4096 spheres + ground quad + sun"),
+}
+
+
+def frame_size(n: int, w0: int, h0: int, scaling: str):
+    if n == 1 or scaling == "strong":
         return w0, h0
     s = math.sqrt(n)
     return int(round(w0 * s)), int(round(h0 * s))
@@ -142,10 +154,15 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--scene", default="synth16")
-    ap.add_argument("--width", type=int, default=3840)
-    ap.add_argument("--height", type=int, default=2160)
-    ap.add_argument("--depth", type=int, default=8)
+    ap.add_argument("--config", choices=sorted(CONFIGS), default=None,
+                    help="BASELINE config (default: c3 on one GPU, c4 on more)")
+    ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
+                    help="N > 1: the config's fixed frame (strong) or a frame grown with N at its aspect (weak)")
+    ap.add_argument("--scene", default=None)
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--height", type=int, default=None)
+    ap.add_argument("--depth", type=int, default=None)
+    ap.add_argument("--gather-rgb", action="store_true", help="N > 1: gather the float RGB strips to rank 0 too")
     ap.add_argument("--row-block", type=int, default=8)
     ap.add_argument("--cpu-stride", type=int, default=2, help="cpu_baseline samples every n-th row")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -156,6 +173,13 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    cfg_name = args.config or ("c3" if world == 1 else "c4")
+    c_scene, c_w, c_h, c_depth, c_desc = CONFIGS[cfg_name]
+    custom = any(v is not None for v in (args.scene, args.width, args.height, args.depth))
+    args.scene = args.scene or c_scene
+    args.width = args.width or c_w
+    args.height = args.height or c_h
+    args.depth = args.depth or c_depth
     local = 0 if args.one_device else int(os.environ.get("LOCAL_RANK", str(rank)))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
@@ -174,7 +198,7 @@ def main():
             dist.init_process_group(args.backend)
     L = _lib.load()
 
-    W, H = frame_size(world, args.width, args.height)
+    W, H = frame_size(world, args.width, args.height, args.scaling)
     depth, rb = args.depth, args.row_block
     desc = scenes.get_scene(args.scene)
     scene, cam = build_scene(desc)
@@ -193,7 +217,7 @@ def main():
         # the own strips, ARGB8 strip gather to rank 0 + device un-interleave (reflaxman_amd/dist.py)
         from reflaxman_amd.dist import RfxStripOps, StripFrame
         sf = StripFrame(RfxStripOps(rr, frame, stream.cuda_stream), W, H, rb, rank, world, dev,
-                        pipeline=False if args.no_pipeline else None)
+                        pipeline=False if args.no_pipeline else None, gather_rgb=args.gather_rgb)
         rows, img, argb = sf.rows, sf.img, sf.argb
     else:
         rows = H
@@ -222,6 +246,14 @@ def main():
         r1.render_frame(f1, img1.data_ptr(), argb1.data_ptr(), 0, stream.cuda_stream)
         torch.cuda.synchronize()
         parity["multi_rank_frame_equals_single_gpu"] = bool(torch.equal(full0.reshape(-1), argb1))
+        if args.gather_rgb:
+            parity["multi_rank_rgb_equals_single_gpu"] = bool(torch.equal(sf.rgb_full.reshape(-1), img1))
+        man = json.load(open(os.path.join(ROOT, "tests", "golden", "manifest.json")))["cases"]
+        key = f"hash_{args.scene}_{W}x{H}_d{depth}"
+        if key in man:
+            parity["multi_rank_frame_vs_reference_sha256"] = {
+                "argb8": sha(full0.reshape(-1).cpu().numpy().view(np.uint32).tobytes()) == man[key]["sha_argb"],
+                "case": key}
         if os.environ.get("RFX_BENCH_DUMP"):
             np.save(os.path.join(os.environ["RFX_BENCH_DUMP"], "multi.npy"), full0.cpu().numpy())
             np.save(os.path.join(os.environ["RFX_BENCH_DUMP"], "single.npy"), argb1.view(H, W).cpu().numpy())
@@ -301,18 +333,20 @@ def main():
     flops_launch = flops_frame / world
     achieved = flops_launch / (trace_avg * 1e-3) / 1e12
     px_launch = rows * W
-    traffic = None
-    prof = os.path.join(ROOT, "profiles", "pmc_trace_kernel.json")
-    if os.path.exists(prof):
-        p = json.load(open(prof))
-        if p.get("config") == [args.scene, W, H, depth, world]:
-            traffic = p.get("hbm_bytes_per_launch")
+    # HBM traffic and executed VALU work of the trace kernel: rocprofv3 --pmc passes of this very workload
+    # and library build (tools/prof_round.sh -> profiles/pmc/), per launch; null when no such record exists
+    pmc = metrics.pmc_record(os.path.join(ROOT, "profiles", "pmc"), [args.scene, W, H, depth, world],
+                             _lib.lib_sha256())
+    traffic = pmc["hbm_bytes_per_launch"] if pmc else None
+    workload = (c_desc if not custom else f"{args.scene} scene") + f", {W}x{H}, depth {depth}, 1 spp"
+    if world > 1:
+        workload += f", {world} GPUs, fixed frame (strong scaling)" if args.scaling == "strong" else \
+            f", {world} GPUs, frame grown with N (weak scaling)"
     out = {
         "metric": METRIC, "value": round(mrays, 2), "unit": "Mrays/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-        "config": {"workload": f"C3 {args.scene}: 16 spheres + 4 textured triangles + sun, {W}x{H}, depth {depth}, 1 spp"
-                               + (" (C4 family, weak-scaled 16:9 frame)" if world > 1 else ""),
+        "scaling": args.scaling if world > 1 else "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": workload, "name": None if custom else cfg_name.upper(),
                    "scene": args.scene, "width": W, "height": H, "depth": depth, "spp": 1,
                    "parallelism": (f"row-strips{rb}x{world}" + ("+pipelined-gather" if sf.pipeline else ""))
                                   if world > 1 else "single-gpu"},
@@ -320,7 +354,12 @@ def main():
                      "unit": "TFLOP/s", "frac": round(achieved / metrics.PEAK_FP32_VALU_TFLOPS, 4),
                      "traffic": traffic, "kernel": "rfx::trace_kernel (plain pixel mode, wave-bundle culling)",
                      "flops_per_launch": int(flops_launch), "avg_launch_ms": round(trace_avg, 4),
+                     "frac_kind": "reference-equivalent algorithmic FLOPs (SURVEY 8(d) counting rule over the "
+                                  "reference's brute-force tests) / kernel time / FP32 VALU peak: exact culling skips "
+                                  "most of those tests, so this is effective work, not hardware utilisation -- "
+                                  "see `executed`",
                      "frac_vs_nofma_peak": round(achieved / metrics.PEAK_FP32_NOFMA_TFLOPS, 4),
+                     "executed": metrics.executed_work(pmc, trace_avg),
                      "algo_hbm_bytes_per_launch": px_launch * metrics.ALGO_BYTES_PER_PIXEL,
                      "algo_hbm_GBps": round(px_launch * metrics.ALGO_BYTES_PER_PIXEL / (trace_avg * 1e-3) / 1e9, 1)},
         "phases_ms": {"rng_prepass": round(pre_avg, 4), "trace": round(trace_avg, 4)},

@@ -1,0 +1,223 @@
+// reflaxman/dropin/Render.h -- drop-in replacement for the reference's src/common/Render.h.
+//
+// The reference's Render class (Render.h:7-42) with the same members and semantics, rendering on the MI355X
+// through the C-ABI (../../rfx.h) instead of the CPU loop of Render.cpp:136-215:
+//   * public camera (the caller's own Camera, Camera.h -- proceedControl/inMotion keep working), scene
+//     (./Scene.h), imageWidth, imageHeight, additiveCounter, inProgress;
+//   * renderBegin snapshots camera.view / camera.eye (Render.cpp:116-134); renderNext(pixels) renders exactly
+//     the raster span the reference's cursor would cover -- any chunk pattern (Pulse.cpp:102-209) gives the
+//     reference's image; renderAll keeps the reference's behaviour (imageHeight *pixels*, Render.cpp:217-221);
+//   * the float framebuffer (std::vector<Color> image, Render.h:10) lives in HBM and is read back on demand;
+//     imagePixel / copyImage then apply the caller's own Color::operator/ and Color::argb, as the reference.
+// Random streams: the reference seeds its two per-TU LCG streams from rand() at static init (trace_math.h:34),
+// so their values depend on link order; here they default to the harness link order's values and can be set
+// with RFX_SPHERE_SEED / RFX_JITTER_SEED in the environment (parity tests replay a given reference build).
+#pragma once
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "rfx.h"  // -I <repo>/include
+#include "Camera.h"
+#include "Scene.h"
+#include "Texture.h"
+
+class Render {
+ private:
+  std::vector<Color> image;  // host copy of the device framebuffer (read back on demand)
+
+  // staged render settings (Render.h:12-19)
+  unsigned int curx;
+  unsigned int cury;
+  int renderReflectNum;
+  int renderSampleNum;
+  bool renderAdditive;
+  Matrix33 renderCameraView;
+  Vector3 renderCameraEye;
+
+  rfx_renderer *r = nullptr;
+  void *d_image = nullptr;
+  size_t d_capacity = 0;
+  unsigned long long uploaded = ~0ull;
+  mutable bool host_valid = false;
+
+  static uint32_t seed_env(const char *name, uint32_t dflt)
+  {
+    const char *v = getenv(name);
+    return v && *v ? (uint32_t)strtoul(v, nullptr, 0) : dflt;
+  }
+  void sync_host() const
+  {
+    if (host_valid) return;
+    Render *self = const_cast<Render *>(this);
+    const size_t n = (size_t)imageWidth * imageHeight;
+    if (self->image.size() < n) self->image.resize(n);
+    if (n) rfx_dropin::check(rfx_memcpy_d2h(r, &self->image.front(), d_image, n * sizeof(float) * 3), "Render: read back");
+    host_valid = true;
+  }
+
+ public:
+  Camera camera;
+  Scene scene;
+  unsigned int imageWidth;
+  unsigned int imageHeight;
+  int additiveCounter;
+  bool inProgress;
+
+  Render(const char *exePath)  // Render.cpp:5-18
+      : curx(0), cury(0), renderReflectNum(0), renderSampleNum(0), renderAdditive(false), imageWidth(0), imageHeight(0),
+        additiveCounter(0), inProgress(false)
+  {
+    static_assert(sizeof(Color) == 3 * sizeof(float), "Color must be three floats (Color.h)");
+    rfx_dropin::check(rfx_renderer_create(&r, 0), "rfx_renderer_create");
+    rfx_dropin::check(rfx_renderer_set_rng(r, seed_env("RFX_SPHERE_SEED", 1350490027u), seed_env("RFX_JITTER_SEED", 424238335u)),
+                      "rfx_renderer_set_rng");
+    loadScene(exePath);
+  }
+  ~Render()
+  {
+    if (d_image) rfx_device_free(r, d_image);
+    rfx_renderer_destroy(r);
+  }
+  Render(const Render &) = delete;
+  Render &operator=(const Render &) = delete;
+
+  void loadScene(const char *exePath)  // Render.cpp:25-55
+  {
+    const std::string skyboxTextureFileName = std::string(exePath) + "./textures/skybox.tga";
+    const std::string planeTextureFileName = std::string(exePath) + "./textures/himiya.tga";
+    camera = Camera(Vector3(7.427f, 3.494f, -3.773f), Vector3(6.5981f, 3.127f, -3.352f), 1.05f);
+    scene = Scene(Color(0.95f, 0.95f, 1.0f), 0.15f);
+    scene.setSkyboxTexture(skyboxTextureFileName.c_str());
+    scene.addLight(Vector3(11.8e9f, 4.26e9f, 3.08e9f), 3.48e8f, Color(1.0f, 1.0f, 0.95f), 0.85f);
+    scene.addSphere(Vector3(-1.25f, 1.5f, -0.25f), 1.5f, Material(Material::mtMetal, Color(1.0f, 1.0f, 1.0f), 1.0f, 0.0f));
+    scene.addSphere(Vector3(0.15f, 1.0f, 1.75f), 1.0f, Material(Material::mtMetal, Color(1.0f, 1.0f, 1.0f), 0.95f, 0.0f));
+    scene.addSphere(Vector3(-3.0f, 0.6f, -3.0f), 0.6f, Material(Material::mtDielectric, Color(1.0f, 1.0f, 1.0f), 0.0f, 0.0f));
+    scene.addSphere(Vector3(-0.5f, 0.5f, -2.5f), 0.5f, Material(Material::mtDielectric, Color(0.5f, 1.0f, 0.15f), 0.75f, 0.0f));
+    scene.addSphere(Vector3(1.0f, 0.4f, -1.5f), 0.4f, Material(Material::mtDielectric, Color(0.0f, 0.5f, 1.0f), 1.0f, 0.0f));
+    scene.addSphere(Vector3(1.8f, 0.4f, 0.1f), 0.4f, Material(Material::mtMetal, Color(1.0f, 0.65f, 0.45f), 1.0f, 0.0f));
+    scene.addSphere(Vector3(1.7f, 0.5f, 1.9f), 0.5f, Material(Material::mtMetal, Color(1.0f, 0.90f, 0.60f), 0.75f, 0.0f));
+    scene.addSphere(Vector3(0.6f, 0.6f, 4.2f), 0.6f, Material(Material::mtMetal, Color(0.9f, 0.9f, 0.9f), 0.0f, 0.0f));
+    Texture *planeTexture = scene.addTexture(planeTextureFileName.c_str());
+    Triangle *tr1 = scene.addTriangle(Vector3(-14.0f, 0.0f, -10.0f), Vector3(-14.0f, 0.0f, 10.0f), Vector3(14.0f, 0.0f, -10.0f),
+                                      Material(Material::mtDielectric, Color(1.0f, 1.0f, 1.0f), 0.95f, 0.0f));
+    tr1->setTexture(planeTexture, 0.0f, 0.0f, 0.0f, 1.0f, 1.0f, 0.0f);
+    Triangle *tr2 = scene.addTriangle(Vector3(-14.0f, 0.0f, 10.0f), Vector3(14.0f, 0.0f, 10.0f), Vector3(14.0f, 0.0f, -10.0f),
+                                      Material(Material::mtDielectric, Color(1.0f, 1.0f, 1.0f), 0.95f, 0.0f));
+    tr2->setTexture(planeTexture, 0.0f, 1.0f, 1.0f, 1.0f, 1.0f, 0.0f);
+  }
+
+  void setImageSize(unsigned int width, unsigned int height)  // Render.cpp:57-80
+  {
+    if (width > 0 && height > 0)
+    {
+      const size_t bytes = (size_t)width * height * sizeof(float) * 3;
+      if (bytes > d_capacity)
+      {
+        if (d_image) rfx_device_free(r, d_image);
+        d_image = nullptr;
+        rfx_dropin::check(rfx_device_alloc(r, bytes, &d_image), "Render::setImageSize");
+        d_capacity = bytes;
+      }
+      std::vector<float> zero((size_t)width * height * 3, 0.0f);
+      rfx_dropin::check(rfx_memcpy_h2d(r, d_image, &zero.front(), bytes), "Render::setImageSize");
+      imageWidth = width;
+      imageHeight = height;
+      additiveCounter = 0;
+      inProgress = false;
+      curx = 0;
+      cury = 0;
+      host_valid = false;
+    }
+  }
+
+  void copyImage(Texture &texture) const  // Render.cpp:82-101
+  {
+    if (imageWidth == texture.getWidth() && imageHeight == texture.getHeight())
+    {
+      sync_host();
+      const Color *imagePixel = &image.front();
+      ARGB *texPixel = texture.getColorBuffer();
+      const ARGB *endTexPixel = texPixel + imageWidth * imageHeight;
+      while (texPixel < endTexPixel) *texPixel++ = (imagePixel++)->argb();
+    }
+    else
+      texture.clear(0);
+  }
+
+  Color imagePixel(int x, int y) const  // Render.cpp:103-114
+  {
+    if (x >= 0 && y >= 0)
+    {
+      sync_host();
+      return additiveCounter > 1 ? image[x + y * imageWidth] / float(additiveCounter) : image[x + y * imageWidth];
+    }
+    return Color(0, 0, 0);
+  }
+
+  void renderBegin(int reflectNum, int sampleNum, bool additive)  // Render.cpp:116-134
+  {
+    renderReflectNum = reflectNum;
+    renderSampleNum = sampleNum;
+    renderAdditive = additive;
+    inProgress = true;
+    curx = 0;
+    cury = 0;
+    renderCameraView = camera.view;
+    renderCameraEye = camera.eye;
+    if (additive)
+      additiveCounter++;
+    else
+      additiveCounter = 0;
+  }
+
+  bool renderNext(unsigned int pixels)  // Render.cpp:136-215, the cursor's span rendered on the device
+  {
+    if (!pixels || !inProgress || curx >= imageWidth || cury >= imageHeight || renderReflectNum <= 0 || !renderSampleNum)
+      return false;
+    const uint64_t total = (uint64_t)imageWidth * imageHeight;
+    const uint64_t p0 = (uint64_t)cury * imageWidth + curx;
+    const uint64_t p1 = p0 + pixels < total ? p0 + pixels : total;
+    if (uploaded != scene.revision())
+    {
+      rfx_dropin::check(rfx_renderer_set_scene(r, scene.handle()), "rfx_renderer_set_scene");
+      uploaded = scene.revision();
+    }
+    rfx_frame f;
+    memset(&f, 0, sizeof(f));
+    f.eye[0] = renderCameraEye.x; f.eye[1] = renderCameraEye.y; f.eye[2] = renderCameraEye.z;
+    memcpy(f.view, &renderCameraView.m[0][0], sizeof(f.view));
+    f.fov = camera.fov;  // rz = W/2/tanf(camera.fov/2): the live camera's fov, as Render.cpp:148
+    f.width = imageWidth;
+    f.height = imageHeight;
+    f.reflect_num = renderReflectNum;
+    f.sample_num = renderSampleNum;
+    f.additive = renderAdditive;
+    f.additive_counter = additiveCounter;
+    f.nranks = 1;
+    f.pixel_begin = p0;
+    f.pixel_end = p1;
+    rfx_dropin::check(rfx_render_frame(r, &f, (float *)d_image, nullptr, nullptr, nullptr), "Render::renderNext");
+    host_valid = false;
+    curx = (unsigned int)(p1 % imageWidth);
+    cury = (unsigned int)(p1 / imageWidth);
+    if (p1 == total) inProgress = false;
+    return inProgress;
+  }
+
+  void renderAll(int reflectNum, int sampleNum, bool additive)  // Render.cpp:217-221, as shipped
+  {
+    renderBegin(reflectNum, sampleNum, additive);
+    renderNext(imageHeight);
+  }
+
+  float getRenderProgress() const  // Render.cpp:223-226
+  {
+    return float(curx + cury * imageWidth) * 100.0f / imageWidth / imageHeight;
+  }
+
+  rfx_renderer *renderer() const { return r; }
+};

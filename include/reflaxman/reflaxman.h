@@ -1,4 +1,6 @@
-// reflaxman/reflaxman.h -- header-only C++ host shim over the C-ABI (../rfx.h).
+// reflaxman/reflaxman.h -- header-only C++ host shim over the C-ABI (../rfx.h), for hosts that do NOT
+// keep the reference's sources.  (A host that does -- the reference's own Pulse app -- uses the drop-in
+// headers reflaxman/dropin/{Render,Scene}.h instead, with its own Camera/Color/Texture/...; INTEGRATION.md.)
 //
 // Mirrors the reference's class API so host code written against
 // src/common/{Render,Scene,Camera,Material,Color,Vector3,Texture}.h recompiles
@@ -8,10 +10,10 @@
 //   Render (Render.h:7-42)   public camera/scene/imageWidth/imageHeight/additiveCounter/inProgress,
 //                            setImageSize, renderBegin, renderNext, renderAll, copyImage,
 //                            imagePixel, getRenderProgress, loadScene
-//   Scene (Scene.h:28-40)    ctor(Color, float), addSphere, addTriangle, addLight, addTexture,
-//                            setSkyboxTexture
+//   Scene (Scene.h:28-40)    ctor(Color, float), addSphere -> Sphere*, addTriangle -> Triangle*,
+//                            addLight -> OmniLight*, addTexture -> Texture*, setSkyboxTexture
 //   Triangle::setTexture (Triangle.h:16), Camera(eye, at, fov) (Camera.h:55), Material (Material.h),
-//   Texture (Texture.h): W x H ARGB buffer + saveToFile (.bmp / .tga)
+//   Texture (Texture.h): W x H ARGB buffer, Texture(fileName) (TGA), saveToFile (.bmp / .tga), clear
 //
 // Differences that are not visible to a well-behaved caller: Scene/Render are
 // non-copyable (the reference's implicit shallow copies double-free), and
@@ -23,6 +25,7 @@
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../rfx.h"
@@ -76,10 +79,27 @@ struct Camera {  // Camera.h:30-62 (rendering fields)
   }
 };
 
-class Texture {  // Texture.h:4-34 (image side: W x H ARGB + save)
+class Texture {  // Texture.h:4-34 (image side: W x H ARGB, TGA load, BMP/TGA save)
  public:
   Texture() : width(0), height(0) {}
   Texture(unsigned w, unsigned h) : width(w), height(h), buf((size_t)w * h, 0) {}
+  explicit Texture(const char *fileName) : width(0), height(0) { loadFromFile(fileName); }
+  bool loadFromFile(const char *fileName)  // Texture.cpp:175-189 (.tga only), Texture.cpp:34-108
+  {
+    const std::string f = fileName;
+    const size_t dot = f.find_last_of('.');
+    width = height = 0;
+    buf.clear();
+    if (dot == std::string::npos || f.substr(dot) != ".tga") return false;
+    uint32_t w = 0, h = 0;
+    if (rfx_tga_load(fileName, &w, &h, nullptr, 0) != RFX_OK) return false;
+    buf.assign((size_t)w * h, 0);
+    if ((size_t)w * h && rfx_tga_load(fileName, &w, &h, buf.data(), buf.size()) != RFX_OK) { buf.clear(); return false; }
+    width = w;
+    height = h;
+    return true;
+  }
+  void clear(ARGB bkColor) { for (ARGB &c : buf) c = bkColor; }  // Texture.cpp:278-283
   unsigned getWidth() const { return width; }
   unsigned getHeight() const { return height; }
   ARGB *getColorBuffer() { return buf.data(); }
@@ -102,11 +122,27 @@ class Texture {  // Texture.h:4-34 (image side: W x H ARGB + save)
 
 class Scene;
 
-struct TextureRef { Scene *scene; int index; };  // Scene::addTexture's Texture*
-class Triangle {                                 // Scene::addTriangle's Triangle*
+class Sphere {  // Scene::addSphere's Sphere*: a handle of the object index
+ public:
+  Sphere(Scene *s, int obj) : scene(s), object(obj) {}
+  int objectIndex() const { return object; }
+
+ private:
+  Scene *scene;
+  int object;
+};
+
+struct OmniLight {  // Scene::addLight's OmniLight* (OmniLight.h): the light as recorded (radius/power clamped)
+  Vector3 origin;
+  float radius;
+  Color color;
+  float power;
+};
+
+class Triangle {  // Scene::addTriangle's Triangle*
  public:
   Triangle(Scene *s, int obj) : scene(s), object(obj) {}
-  inline void setTexture(const TextureRef *texture, float u1, float v1, float u2, float v2, float u3, float v3);
+  inline void setTexture(const Texture *texture, float u1, float v1, float u2, float v2, float u3, float v3);
   int objectIndex() const { return object; }
 
  private:
@@ -125,19 +161,23 @@ class Scene {
   Scene &operator=(Scene &&o) noexcept
   {
     std::swap(h, o.h);
+    std::swap(spheres, o.spheres);
     std::swap(tris, o.tris);
+    std::swap(lights, o.lights);
     std::swap(texs, o.texs);
+    std::swap(tex_index, o.tex_index);
     ++version;
     return *this;
   }
 
-  int addSphere(const Vector3 &c, float radius, const Material &m)  // returns the object index
+  Sphere *addSphere(const Vector3 &c, float radius, const Material &m)  // Scene.cpp:29-39
   {
     const float cc[3] = {c.x, c.y, c.z}, rgb[3] = {m.color.r, m.color.g, m.color.b};
     const int obj = rfx_scene_add_sphere(h, cc, radius, m.type, rgb, m.reflectivity, m.transparency);
     rfx_check(obj, "Scene::addSphere");
     ++version;
-    return obj;
+    spheres.emplace_back(new Sphere(this, obj));
+    return spheres.back().get();
   }
   Triangle *addTriangle(const Vector3 &v1, const Vector3 &v2, const Vector3 &v3, const Material &m)
   {
@@ -149,21 +189,31 @@ class Scene {
     tris.emplace_back(new Triangle(this, obj));
     return tris.back().get();
   }
-  int addLight(const Vector3 &o, float radius, const Color &c, float power)
+  OmniLight *addLight(const Vector3 &o, float radius, const Color &c, float power)  // Scene.cpp:48-59
   {
     const float oo[3] = {o.x, o.y, o.z}, rgb[3] = {c.r, c.g, c.b};
     const int idx = rfx_scene_add_light(h, oo, radius, rgb, power);
     rfx_check(idx, "Scene::addLight");
     ++version;
-    return idx;
+    if (radius <= 1.0842021724855044e-19f) radius = 1.0842021724855044e-19f;  // Scene.cpp:50-53
+    const float p = power < 0.0f ? 0.0f : power > 1.0f ? 1.0f : power;     // OmniLight.cpp:13
+    lights.emplace_back(new OmniLight{o, radius, c, p});
+    return lights.back().get();
   }
-  TextureRef *addTexture(const char *fileName)  // failed loads give the checker texture, like the reference
+  Texture *addTexture(const char *fileName)  // Scene.cpp:61-66: failed loads give the checker texture
   {
     const int idx = rfx_scene_add_texture_file(h, fileName, nullptr);
     rfx_check(idx, "Scene::addTexture");
     ++version;
-    texs.emplace_back(new TextureRef{this, idx});
+    texs.emplace_back(new Texture(fileName));
+    tex_index.emplace_back(texs.back().get(), idx);
     return texs.back().get();
+  }
+  int textureIndex(const Texture *t) const
+  {
+    for (const auto &e : tex_index)
+      if (e.first == t) return e.second;
+    return -1;
   }
   bool setSkyboxTexture(const char *fileName)
   {
@@ -178,15 +228,18 @@ class Scene {
 
  private:
   rfx_scene *h;
+  std::vector<std::unique_ptr<Sphere>> spheres;
   std::vector<std::unique_ptr<Triangle>> tris;
-  std::vector<std::unique_ptr<TextureRef>> texs;
+  std::vector<std::unique_ptr<OmniLight>> lights;
+  std::vector<std::unique_ptr<Texture>> texs;
+  std::vector<std::pair<const Texture *, int>> tex_index;
   unsigned long long version = 0;
 };
 
-inline void Triangle::setTexture(const TextureRef *t, float u1, float v1, float u2, float v2, float u3, float v3)
+inline void Triangle::setTexture(const Texture *t, float u1, float v1, float u2, float v2, float u3, float v3)
 {
   const float uv[6] = {u1, v1, u2, v2, u3, v3};
-  rfx_check(rfx_triangle_set_texture(scene->handle(), object, t ? t->index : -1, uv), "Triangle::setTexture");
+  rfx_check(rfx_triangle_set_texture(scene->handle(), object, scene->textureIndex(t), uv), "Triangle::setTexture");
   scene->touch();
 }
 
@@ -228,7 +281,7 @@ class Render {  // Render.h:7-42
     scene.addSphere(Vector3(1.8f, 0.4f, 0.1f), 0.4f, Material(Material::mtMetal, Color(1.0f, 0.65f, 0.45f), 1.0f, 0.0f));
     scene.addSphere(Vector3(1.7f, 0.5f, 1.9f), 0.5f, Material(Material::mtMetal, Color(1.0f, 0.90f, 0.60f), 0.75f, 0.0f));
     scene.addSphere(Vector3(0.6f, 0.6f, 4.2f), 0.6f, Material(Material::mtMetal, Color(0.9f, 0.9f, 0.9f), 0.0f, 0.0f));
-    TextureRef *planeTexture = scene.addTexture(plane.c_str());
+    Texture *planeTexture = scene.addTexture(plane.c_str());
     Triangle *tr1 = scene.addTriangle(Vector3(-14.0f, 0.0f, -10.0f), Vector3(-14.0f, 0.0f, 10.0f), Vector3(14.0f, 0.0f, -10.0f),
                                       Material(Material::mtDielectric, Color(1.0f, 1.0f, 1.0f), 0.95f, 0.0f));
     tr1->setTexture(planeTexture, 0.0f, 0.0f, 0.0f, 1.0f, 1.0f, 0.0f);
@@ -321,7 +374,11 @@ class Render {  // Render.h:7-42
 
   void copyImage(Texture &texture) const  // Render.cpp:82-101
   {
-    if (texture.getWidth() != imageWidth || texture.getHeight() != imageHeight) return;
+    if (texture.getWidth() != imageWidth || texture.getHeight() != imageHeight)
+    {
+      texture.clear(0);
+      return;
+    }
     rfx_argb_from_rgb(host().data(), (size_t)imageWidth * imageHeight, texture.getColorBuffer());
   }
 

@@ -9,6 +9,7 @@ from __future__ import annotations
 import os
 import shutil
 import subprocess
+from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
@@ -17,8 +18,10 @@ LIB = os.path.join(LIBDIR, "librfx.so")
 ROOT = os.path.dirname(HERE)
 INCLUDE = os.path.join(ROOT, "include")
 
-SOURCES = ["rfx_kernels.hip", "rfx_host.cpp"]
-HEADERS = ["rfx_math.h", "rfx_powf.h", "rfx_types.h"]
+# the trace kernel families compile as separate TUs in parallel (one hipcc per source), then link
+SOURCES = ["rfx_kernels.hip", "rfx_host.cpp"] + [f"rfx_trace_{m}_{s}.hip" for m in ("plain", "ssaa", "block")
+                                                 for s in ("fast", "stats")]
+HEADERS = ["rfx_math.h", "rfx_powf.h", "rfx_types.h", "rfx_trace.h"]
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0] or "gfx950"
 
 FLAGS = [
@@ -26,8 +29,9 @@ FLAGS = [
     "-ffp-contract=off", "-fno-fast-math",
     "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-gpu-flush-denormals-to-zero",
     "-fno-slp-vectorize",  # auto-packing v3 code costs more v_mov than it saves (tools/ab.py: -7% trace time)
-    "-fPIC", "-shared", "-Wall", "-Wno-unknown-pragmas",
+    "-fPIC", "-Wall", "-Wno-unknown-pragmas",
 ]
+JOBS = min(8, os.cpu_count() or 1)
 
 
 def hipcc() -> str:
@@ -45,15 +49,36 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
+def _compile_link(out: str, extra, objdir: str) -> str:
+    """hipcc -c every source into objdir (in parallel), then hipcc -shared into out; returns compiler stderr."""
+    os.makedirs(objdir, exist_ok=True)
+
+    def one(src):
+        obj = os.path.join(objdir, os.path.splitext(src)[0] + ".o")
+        cmd = [hipcc(), *FLAGS, *extra, "-c", os.path.join(CSRC, src), "-o", obj]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError("build failed:\n" + " ".join(cmd) + "\n" + r.stdout + r.stderr)
+        return obj, r.stderr
+
+    with ThreadPoolExecutor(JOBS) as ex:
+        res = list(ex.map(one, SOURCES))
+    cmd = [hipcc(), *FLAGS, "-shared", *[o for o, _ in res], "-o", out]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError("link failed:\n" + " ".join(cmd) + "\n" + r.stdout + r.stderr)
+    return "".join(e for _, e in res)
+
+
 def build_variant(name: str, defines, verbose: bool = False) -> str:
     """Compile a variant librfx_<name>.so with extra -D defines / compiler flags (A/B timing builds, tools/ab.py)."""
     out = os.path.join(LIBDIR, "variants", f"librfx_{name}.so")
     os.makedirs(os.path.dirname(out), exist_ok=True)
     extra = [d if d.startswith("-") else f"-D{d}" for d in defines]  # "-..." entries are compiler flags
-    cmd = [hipcc(), *FLAGS, *extra, *[os.path.join(CSRC, s) for s in SOURCES], "-o", out]
-    r = subprocess.run(cmd, capture_output=True, text=True)
-    if r.returncode != 0:
-        raise RuntimeError(f"variant {name} build failed:\n" + r.stdout + r.stderr)
+    try:
+        _compile_link(out, extra, os.path.join(LIBDIR, "variants", "obj_" + name))
+    except RuntimeError as e:
+        raise RuntimeError(f"variant {name}: {e}") from None
     return out
 
 
@@ -63,12 +88,9 @@ def build(force: bool = False, verbose: bool = False) -> str:
         return LIB
     os.makedirs(LIBDIR, exist_ok=True)
     tmp = LIB + ".tmp"
-    cmd = [hipcc(), *FLAGS, *[os.path.join(CSRC, s) for s in SOURCES], "-o", tmp]
-    r = subprocess.run(cmd, capture_output=True, text=True)
-    if r.returncode != 0:
-        raise RuntimeError("librfx.so build failed:\n" + " ".join(cmd) + "\n" + r.stdout + r.stderr)
+    err = _compile_link(tmp, [], os.path.join(LIBDIR, "obj"))
     if verbose:
-        print(r.stderr)
+        print(err)
     os.replace(tmp, LIB)
     return LIB
 

@@ -132,6 +132,13 @@ def load(build_if_missing: bool = True):
     return L
 
 
+def lib_sha256(path: str = None) -> str:
+    """SHA-256 of the library file (keys the PMC records of profiles/pmc to the build they measured)."""
+    import hashlib
+    with open(path or _build.LIB, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
 def check(rc: int, what: str = "") -> int:
     if rc < 0:
         msg = load().rfx_last_error().decode(errors="replace")

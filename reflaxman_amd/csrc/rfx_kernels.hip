@@ -1,1296 +1,14 @@
-// gfx950 kernels for ReflaxMan's per-pixel trace loop.
-//
-//   rng_count / rng_emit : the reference's serial LCG stream
-//       (trace_math.h:34-39, Vector3.cpp:176-188) as a parallel pre-pass:
-//       LCG jump-ahead per thread, accept flags, block scan, scatter of the
-//       i-th accepted triple to trace i.
-//   trace_kernel<STATS, BLOCK> : Render::renderNext (Render.cpp:136-215) +
-//       Scene::trace (Scene.cpp:73-236), one lane per trace, 8x8-pixel wave
-//       tiles, the bounce "recursion" as the reference's own iterative loop.
-//       Scene arrays are walked in wave-uniform order (scalar loads);
-//       closest hit keeps only (dist, object, t, u, v) per candidate and
-//       re-derives drop/normal/reflection/texel for the winner with the same
-//       expressions; the shadow any-hit loop exits per lane on the first
-//       occluder and per wave once every lane has (exec-mask early out).
-//
-// Numerics: compiled with -ffp-contract=off, IEEE div/sqrt, f32 denormals on,
-// so every operation rounds exactly as the reference's x86-64 build does.
-// Work the reference does but whose result cannot matter is skipped only
-// where the skip is provably exact (each site says why).
-#include <hip/hip_runtime.h>
-
-#include "rfx_math.h"
-#include "rfx_powf.h"
-#include "rfx_types.h"
+// gfx950 kernels of librfx.so besides the trace kernel families (rfx_trace.h, rfx_trace_*.hip):
+//   rng_count / rng_emit : the reference's serial LCG stream (trace_math.h:34-39, Vector3.cpp:176-188) as a
+//       parallel pre-pass;
+//   lpt_hist / lpt_scan / lpt_scatter : the longest-tile-first schedule of the trace launch;
+//   kat_* : the trace kernel's primitive code on known-answer inputs (rfx.h rfx_kat_*);
+// and the library-internal launchers.
+#include "rfx_trace.h"
 
 #pragma clang fp contract(off)
 
 namespace rfx {
-
-struct Cnt { uint32_t c[C_COUNT]; };
-
-#define RFX_CNT(k)                   \
-  do {                               \
-    if constexpr (STATS) cnt.c[k]++; \
-  } while (0)
-
-// Diagnostic build only (RFX_DEBUG_PROF, tools/regionprof.py): wave clock cycles spent per region of
-// the bounce segment, summed by each region's first active lane into a device-global table.
-#ifdef RFX_DEBUG_PROF
-enum ProfRegion { P_SPH = 0, P_TRI, P_WIN, P_LIGHT, P_SHADOW, P_MAT, P_SKY, P_SEG, P_COUNT };
-__device__ unsigned long long g_prof[2 * P_COUNT];  // cycles, then wave executions
-__shared__ unsigned long long s_prof[2 * P_COUNT];  // per workgroup, flushed to g_prof at kernel end
-#define RFX_PROF_BEGIN(k) const uint64_t prof_t0_##k = __builtin_amdgcn_s_memtime()
-#define RFX_PROF_END(k)                                                                   \
-  do {                                                                                    \
-    const uint64_t dt_ = __builtin_amdgcn_s_memtime() - prof_t0_##k;                     \
-    if ((threadIdx.x & 63u) == (uint32_t)(__ffsll((long long)__ballot(1)) - 1))           \
-    {                                                                                     \
-      atomicAdd(&s_prof[k], (unsigned long long)dt_);                                     \
-      atomicAdd(&s_prof[P_COUNT + k], 1ull);                                              \
-    }                                                                                     \
-  } while (0)
-// cull statistics (diagnostic build): per bundle kind (0 closest hit, 1 shadow): bundles, usable bundles,
-// live lanes, kept sphere pairs, kept triangles, valid pairs, valid triangles
-__device__ unsigned long long g_cull[16];
-#define RFX_CULL_STAT(kind, ok, live_mask, om, valid)                                                 \
-  do {                                                                                              \
-    if ((threadIdx.x & 63u) == 0u)                                                                  \
-    {                                                                                               \
-      atomicAdd(&g_cull[8 * (kind) + 0], 1ull);                                                     \
-      atomicAdd(&g_cull[8 * (kind) + 1], (ok) ? 1ull : 0ull);                                       \
-      atomicAdd(&g_cull[8 * (kind) + 2], (unsigned long long)__popcll(live_mask));                 \
-      atomicAdd(&g_cull[8 * (kind) + 3], (unsigned long long)__popc(small_pairs(om)));             \
-      atomicAdd(&g_cull[8 * (kind) + 4], (unsigned long long)__popcll(small_tris(om)));            \
-      atomicAdd(&g_cull[8 * (kind) + 5], (unsigned long long)__popc(small_pairs(valid)));          \
-      atomicAdd(&g_cull[8 * (kind) + 6], (unsigned long long)__popcll(small_tris(valid)));         \
-    }                                                                                               \
-  } while (0)
-#define RFX_PROF_INIT()                                          \
-  do {                                                           \
-    if (threadIdx.x < 2 * P_COUNT) s_prof[threadIdx.x] = 0ull;   \
-  } while (0)
-#define RFX_PROF_FLUSH()                                                            \
-  do {                                                                              \
-    __syncthreads();                                                                \
-    if (threadIdx.x < 2 * P_COUNT) atomicAdd(&g_prof[threadIdx.x], s_prof[threadIdx.x]); \
-  } while (0)
-#else
-#define RFX_PROF_INIT() \
-  do {                  \
-  } while (0)
-#define RFX_PROF_FLUSH() \
-  do {                   \
-  } while (0)
-#define RFX_PROF_BEGIN(k) \
-  do {                    \
-  } while (0)
-#define RFX_PROF_END(k) \
-  do {                  \
-  } while (0)
-#define RFX_CULL_STAT(kind, ok, live_mask, om, valid) \
-  do {                                                \
-  } while (0)
-#endif
-
-// Color(ARGB) (Color.cpp:9-14) through a 256-entry LDS table of float(k) / 255.0f:
-// the table holds exactly the quotients the reference computes per channel.
-__device__ __forceinline__ col from_argb_lut(uint32_t c, const float *lut)
-{
-  return mkc(lut[(c >> 16) & 0xFFu], lut[(c >> 8) & 0xFFu], lut[c & 0xFFu]);
-}
-
-// glibc powf's tables (rfx_powf.h) copied to LDS by each workgroup: the lookups index them per lane,
-// and LDS answers such gathers in ~100 cycles where the constant/global path takes several hundred.
-__shared__ double s_powf_log[16][2];
-__shared__ uint64_t s_powf_exp[32];
-__shared__ double s_powf_add[2][4];
-
-__device__ __forceinline__ void stage_powf_tables()
-{
-  const uint32_t t = threadIdx.x;
-  if (t < 32)
-  {
-    s_powf_exp[t] = kExp2fTab[t];
-    s_powf_log[t >> 1][t & 1u] = kPowfLog2Tab[t >> 1][t & 1u];
-    if (t < 8) s_powf_add[t >> 2][t & 3u] = kPowfAdd[t >> 2][t & 3u];
-  }
-}
-
-__device__ __forceinline__ float powf_dev(float x, float y)
-{
-  return powf_glibc_t(x, y, s_powf_log, s_powf_exp, s_powf_add);
-}
-
-// Small scenes (<= 32 spheres, <= 32 triangles): the per-object records the hit lanes gather by their
-// own object index (winner geometry and material, the cull lane table) staged in LDS per workgroup.
-__shared__ SphereGeo s_sph_geo[32];
-__shared__ MatRec s_sph_mat[32];
-__shared__ int32_t s_sph_info[64];
-__shared__ TriShade s_tri_shade[32];
-__shared__ MatRec s_tri_mat[32];
-__shared__ CullRec s_cull[64];
-
-template <bool SMALL>
-struct Tabs {
-  const DevScene &S;
-  __device__ __forceinline__ SphereGeo sph_geo(int i) const { return S.sph_geo[i]; }
-  __device__ __forceinline__ MatRec sph_mat(int i) const { return S.sph_mat[i]; }
-  __device__ __forceinline__ int32_t sph_info(int k) const { return S.sph_info[k]; }
-  __device__ __forceinline__ TriShade tri_shade(int i) const { return S.tri_shade[i]; }
-  __device__ __forceinline__ MatRec tri_mat(int i) const { return S.tri_mat[i]; }
-  __device__ __forceinline__ const CullRec *cull() const { return S.cull_small; }
-};
-template <>
-struct Tabs<true> {
-  const DevScene &S;
-  __device__ __forceinline__ SphereGeo sph_geo(int i) const { return s_sph_geo[i]; }
-  __device__ __forceinline__ MatRec sph_mat(int i) const { return s_sph_mat[i]; }
-  __device__ __forceinline__ int32_t sph_info(int k) const { return s_sph_info[k]; }
-  __device__ __forceinline__ TriShade tri_shade(int i) const { return s_tri_shade[i]; }
-  __device__ __forceinline__ MatRec tri_mat(int i) const { return s_tri_mat[i]; }
-  __device__ __forceinline__ const CullRec *cull() const { return s_cull; }
-};
-
-__device__ __forceinline__ void stage_small_scene(const DevScene &S)
-{
-  const int t = (int)threadIdx.x;
-  if (t < S.n_sph)
-  {
-    s_sph_geo[t] = S.sph_geo[t];
-    s_sph_mat[t] = S.sph_mat[t];
-    s_sph_info[2 * t] = S.sph_info[2 * t];
-    s_sph_info[2 * t + 1] = S.sph_info[2 * t + 1];
-  }
-  if (t < S.n_tri)
-  {
-    s_tri_shade[t] = S.tri_shade[t];
-    s_tri_mat[t] = S.tri_mat[t];
-  }
-  if (t < 64) s_cull[t] = S.cull_small[t];
-}
-
-// ------------------------------------------------------------- sampling
-template <bool STATS>
-__device__ __forceinline__ col texel_uv(const DevScene &S, int tex, float u, float v, const float *lut, Cnt &cnt)
-{                                                                         // Texture.cpp:231-269
-  if (u < 0.0f || u > 1.0f || v < 0.0f || v > 1.0f) { RFX_CNT(C_TEX_OTHER); return mkc(0.0f, 0.0f, 0.0f); }
-  TexRec t;
-  t.w = 0; t.h = 0; t.offset = 0;
-  if (tex >= 0) t = S.texs[tex];
-  if (t.w == 0)
-  {
-    RFX_CNT(C_TEX_CHECKER);
-    return (((int)(u * 50) % 2) ^ ((int)(v * 50) % 2)) ? mkc(0.5f, 0.5f, 0.5f) : mkc(0.75f, 0.75f, 0.75f);
-  }
-  const float fx = clampf(u, 0.0f, 1.0f - kFltEpsilon) * (float)t.w;
-  const float fy = clampf(v, 0.0f, 1.0f - kFltEpsilon) * (float)t.h;
-  const uint32_t x = (uint32_t)fx, y = (uint32_t)fy;
-  const uint32_t *px = S.texels + t.offset;
-  if (x < t.w - 1 && y < t.h - 1)
-  {
-    RFX_CNT(C_TEX_BILINEAR);
-    const col c00 = from_argb_lut(px[x + t.w * y], lut), c01 = from_argb_lut(px[x + t.w * (y + 1)], lut);
-    const col c10 = from_argb_lut(px[x + 1 + t.w * y], lut), c11 = from_argb_lut(px[x + 1 + t.w * (y + 1)], lut);
-    const float uf = fx - floorf(fx), vf = fy - floorf(fy);
-    const float uo = 1 - uf, vo = 1 - vf;
-    return cadd(cscale(cadd(cscale(c00, uo), cscale(c10, uf)), vo), cscale(cadd(cscale(c01, uo), cscale(c11, uf)), vf));
-  }
-  RFX_CNT(C_TEX_OTHER);
-  const uint32_t xi = (uint32_t)fx, yi = (uint32_t)fy;                 // Texture.cpp:216-229
-  if (xi >= t.w || yi >= t.h) return mkc(0.0f, 0.0f, 0.0f);
-  return from_argb_lut(px[xi + t.w * yi], lut);
-}
-
-template <bool STATS>
-__device__ __forceinline__ col skybox_texel(const DevScene &S, v3 ray, const float *lut, Cnt &cnt)  // Skybox.cpp:39-106
-{
-  const float uLeft = 1.0f / 8.0f, vLeft = 3.0f / 6.0f;
-  const float uFront = 3.0f / 8.0f, vFront = 3.0f / 6.0f;
-  const float uRight = 5.0f / 8.0f, vRight = 3.0f / 6.0f;
-  const float uBack = 7.0f / 8.0f, vBack = 3.0f / 6.0f;
-  const float uTop = 3.0f / 8.0f, vTop = 5.0f / 6.0f;
-  const float uBottom = 3.0f / 8.0f, vBottom = 1.0f / 6.0f;
-  const float hw = S.half_tile_w, hh = S.half_tile_h;
-  const v3 n = normalized(ray);
-  const float x = n.x, y = n.y, z = n.z;
-  const float ax = fabsf(x) + kVerySmall, ay = fabsf(y) + kVerySmall, az = fabsf(z) + kVerySmall;
-  float u, v;
-  if (az >= ax && az >= ay)
-  {
-    if (z > 0) { u = uFront + x / az * hw; v = vFront + y / az * hh; }
-    else { u = uBack - x / az * hw; v = vBack + y / az * hh; }
-  }
-  else if (ax >= ay && ax >= az)
-  {
-    if (x > 0) { u = uRight - z / ax * hw; v = vRight + y / ax * hh; }
-    else { u = uLeft + z / ax * hw; v = vLeft + y / ax * hh; }
-  }
-  else
-  {
-    if (y > 0) { u = uTop + x / ay * hw; v = vTop - z / ay * hh; }
-    else { u = uBottom + x / ay * hw; v = vBottom + z / ay * hh; }
-  }
-  return texel_uv<STATS>(S, S.skybox_tex, u, v, lut, cnt);
-}
-
-// A textured triangle's material colour at barycentrics (u, v) (Triangle.cpp:89-96): tuvTrans * (u, v, 0)
-// (whose _13 and _23 are 0) offset by (tu[0], tv[0]).
-template <bool STATS>
-__device__ __forceinline__ col tri_texel(const DevScene &S, const TriShade &sh, float u, float v, const float *lut,
-                                         Cnt &cnt)
-{
-  const float tvx = u * sh.t11 + v * sh.t12 + 0.0f;
-  const float tvy = u * sh.t21 + v * sh.t22 + 0.0f;
-  return texel_uv<STATS>(S, sh.tex, sh.tu0 + tvx, sh.tv0 + tvy, lut, cnt);
-}
-
-// ------------------------------------------------------------- primitives
-// Per-ray constants of Sphere::trace (Sphere.cpp:50-52,58), hoisted out of the object loop.
-struct RayConst {
-  v3 ray2;      // 2.0f * ray
-  float a4, a2; // 4.0f * a, 2.0f * a  with a = |ray|^2
-  bool a_ok;    // a > VERY_SMALL_NUMBER
-};
-__device__ __forceinline__ RayConst ray_const(v3 ray)
-{
-  RayConst k;
-  const float a = sqlen(ray);
-  k.ray2 = mul(ray, 2.0f);
-  k.a4 = 4.0f * a;
-  k.a2 = 2.0f * a;
-  k.a_ok = a > kVerySmall;
-  return k;
-}
-
-// Sphere::trace (Sphere.cpp:44-85) for spheres 2j and 2j+1 at once, up to the discriminant: each half
-// of an f2 runs the reference's scalar expressions in the reference's order (vco = o - c,
-// b = 2ray . vco, c = |vco|^2 - r^2, d = b*b - 4a*c), so v_pk_* results round exactly as scalar ones.
-typedef float f2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ void pair_bd(const SpherePair &g, v3 o, const RayConst &k, f2 &b, f2 &d)
-{
-  const f2 vx = o.x - f2{g.cx[0], g.cx[1]};
-  const f2 vy = o.y - f2{g.cy[0], g.cy[1]};
-  const f2 vz = o.z - f2{g.cz[0], g.cz[1]};
-  b = k.ray2.x * vx + k.ray2.y * vy + k.ray2.z * vz;
-  const f2 c = vx * vx + vy * vy + vz * vz - f2{g.r2[0], g.r2[1]};
-  d = b * b - k.a4 * c;
-}
-
-// Can either sphere of a pair hit?  d < 0 misses; so does b >= 0 (or NaN), since then -b - sqrt(d) <= 0
-// gives t <= 0, which `t > VERY_SMALL_NUMBER` rejects (Sphere.cpp:58-60) -- both are exact rejects.
-__device__ __forceinline__ bool pair_may_hit(f2 b, f2 d)
-{
-  return (d.x >= 0.0f && b.x < 0.0f) || (d.y >= 0.0f && b.y < 0.0f);
-}
-
-// The rest of Sphere::trace for one sphere given its b and d: on a hit returns t and |ray t|^2.
-// `(ray * t).length() > DELTA` (Sphere.cpp:61-64) is tested as |ray t|^2 >= kSqDeltaSphere: the same
-// decision without the square root (rfx_math.h).
-template <bool STATS, bool SHADOW>
-__device__ __forceinline__ bool sphere_tail(float b, float d, v3 ray, const RayConst &k, float &t_out,
-                                            float &sq_out, Cnt &cnt)
-{
-  RFX_CNT(SHADOW ? C_SH_SPH_TESTS : C_SPH_TESTS);
-  if constexpr (STATS)
-    if (!(b > 0.0f)) RFX_CNT(SHADOW ? C_SH_SPH_B : C_SPH_B);
-  if (!(d >= 0.0f && k.a_ok)) return false;
-  // b >= 0 (or NaN): -b - sqrt(d) <= 0, so t <= 0 and `t > VERY_SMALL_NUMBER` rejects -- exact early out
-  if constexpr (!STATS)
-    if (!(b < 0.0f)) return false;
-  if constexpr (STATS)
-    if (!(b > 0.0f)) RFX_CNT(SHADOW ? C_SH_SPH_D : C_SPH_D);
-  const float t = (-b - sqrt_rn(d)) / k.a2;
-  if (!(t > kVerySmall)) return false;
-  RFX_CNT(SHADOW ? C_SH_SPH_T : C_SPH_T);
-  const float sq = sqlen(mul(ray, t));
-  if (!(sq >= kSqDeltaSphere)) return false;
-  t_out = t;
-  sq_out = sq;
-  return true;
-}
-
-// Triangle::trace (Triangle.cpp:53-108) up to its hit decision; on a hit returns t, u, v, |ray t|^2.
-// axTrans * (o - v0) and axTrans * ray are evaluated row by row with the reference's expressions: the
-// z row first, then -- only for t > VERY_SMALL_NUMBER -- the x and y rows as one packed chain
-// ((aox, aoy), (arx, ary), (u, v)), each half rounding exactly as the scalar expression.
-template <bool STATS, bool SHADOW>
-__device__ __forceinline__ bool tri_hit(const TriGeo &g, v3 o, v3 ray, float &t_out, float &u_out, float &v_out,
-                                        float &sq_out, Cnt &cnt, const RayConst &k, float best_sq = INFINITY)
-{
-  RFX_CNT(SHADOW ? C_SH_TRI_TESTS : C_TRI_TESTS);
-  const float dx = o.x - g.v0x, dy = o.y - g.v0y, dz = o.z - g.v0z;
-  const float aoz = dx * g.a31 + dy * g.a32 + dz * g.a33;
-  const float arz = ray.x * g.a31 + ray.y * g.a32 + ray.z * g.a33;
-  if (!(fabsf(arz) > kVerySmall)) return false;
-  RFX_CNT(SHADOW ? C_SH_TRI_Z : C_TRI_Z);
-  // t = -aoz / arz > VERY_SMALL_NUMBER needs -aoz and arz non-zero with equal signs (event counter only)
-  const float nz = -aoz;
-  const bool same_sign = (nz > 0.0f && arz > 0.0f) || (nz < 0.0f && arz < 0.0f);
-  if constexpr (STATS)
-    if (same_sign) RFX_CNT(SHADOW ? C_SH_TRI_S : C_TRI_S);
-  // exact reject before the division: with opposite signs or a zero (or NaN) numerator, t <= 0 or NaN,
-  // which `t > VERY_SMALL_NUMBER` rejects anyway; the divide is skipped when no lane of the wave needs it
-  if (!same_sign) return false;
-  if constexpr (!SHADOW && !STATS)
-  {
-    // exact reject of a plane hit beyond the current closest hit: |ray t|^2 = a nz^2 / arz^2 (real), and
-    // a 2^-16 margin over the float rounding of both sides leaves |ray t| strictly above the best
-    // distance after rounding, so the reference could neither take it nor tie (a2 = 2a exactly)
-    if (nz * nz * k.a2 > best_sq * (arz * arz) * 2.0000305f) return false;
-  }
-  const float t = nz / arz;
-  if (!(t > kVerySmall)) return false;
-  RFX_CNT(SHADOW ? C_SH_TRI_T : C_TRI_T);
-  const f2 c1{g.a11, g.a21}, c2{g.a12, g.a22}, c3{g.a13, g.a23};
-  const f2 ao = dx * c1 + dy * c2 + dz * c3;                  // (aox, aoy)
-  const f2 ar = ray.x * c1 + ray.y * c2 + ray.z * c3;         // (arx, ary)
-  const f2 uv = ao + t * ar;                                  // (u, v)
-  const float u = uv.x, v = uv.y;
-  if (!(u >= 0.0f && v >= 0.0f && u + v < 1.0f)) return false;
-  RFX_CNT(SHADOW ? C_SH_TRI_IN : C_TRI_IN);
-  const float sq = sqlen(mul(ray, t));
-  if (!(sq > kDelta * kDelta)) return false;
-  t_out = t; u_out = u; v_out = v; sq_out = sq;
-  return true;
-}
-
-// Plane::trace (Plane.cpp:36-73) up to its hit decision; on a hit returns t and |ray t|^2.  a = norm . ray,
-// t = norm . (pos - origin) / a, with tri_hit's two exact rejects before the division (opposite signs or a
-// zero numerator give t <= 0; a plane hit beyond the closest hit so far cannot win or tie).
-template <bool STATS, bool SHADOW>
-__device__ __forceinline__ bool plane_hit(const PlaneGeo &g, v3 o, v3 ray, float &t_out, float &sq_out, Cnt &cnt,
-                                          const RayConst &k, float best_sq = INFINITY)
-{
-  RFX_CNT(SHADOW ? C_SH_PLN_TESTS : C_PLN_TESTS);
-  const v3 n = mk(g.nx, g.ny, g.nz);
-  const float a = dot(n, ray);                                                     // Plane.cpp:41
-  if (!(fabsf(a) > kVerySmall)) return false;
-  const float num = dot(n, sub(mk(g.px, g.py, g.pz), o));                          // Plane.cpp:40,45
-  if (!((num > 0.0f && a > 0.0f) || (num < 0.0f && a < 0.0f))) return false;
-  if constexpr (!SHADOW && !STATS)
-    if (num * num * k.a2 > best_sq * (a * a) * 2.0000305f) return false;
-  const float t = num / a;
-  if (!(t > kVerySmall)) return false;
-  RFX_CNT(SHADOW ? C_SH_PLN_T : C_PLN_T);
-  const float sq = sqlen(mul(ray, t));
-  if (!(sq > kDelta * kDelta)) return false;                                       // Plane.cpp:50-53
-  t_out = t; sq_out = sq;
-  return true;
-}
-
-// ------------------------------------------------------------- wave ray bundles (exact culling)
-// The live rays of a wave form a bundle: origins within rw of (cx, cy, cz) -- the first live lane's
-// origin -- and directions within the half-angle acos(cosa) of that lane's direction (ax, ay, az).
-// A ray the reference's float test reports as hitting a sphere passes within r + 8.1e-4 |o - c| of the
-// centre (rounding of d = b^2 - 4ac, DESIGN.md "Exact culling"); kCullRel = 4e-3 covers that five times,
-// so an object whose bounding sphere, grown by rw and kCullRel (L + rw), lies outside the bundle's cone
-// is missed by every lane of the wave and its exact test is skipped for the whole wave.  Skipping a test
-// that misses changes no result: the closest hit and the any-hit only ever take hits.  Every cull
-// decision is a conjunction of comparisons, so a NaN anywhere keeps the object.
-constexpr float kCullRel = 4e-3f;
-
-struct Bundle {
-  float cx, cy, cz, rw;
-  float ax, ay, az, cosa, sina;
-  bool ok;  // wave-uniform: the bound is finite and the cone narrower than ~84 degrees
-};
-
-__device__ __forceinline__ float lane_bcast(float v, int lane)
-{
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
-}
-
-// max over the wave of a value >= 0 (every lane active): the bit patterns of non-negative floats order
-// like the floats, and a NaN pattern (above +inf) wins, which makes the bound unusable below.
-// DPP inclusive max-scan within each 16-lane row (row_shr 1, 2, 4, 8), then across rows (row_bcast 15,
-// row_bcast 31): lane 63 ends with the wave's maximum.  Lanes a shift leaves without a source keep 0.
-__device__ __forceinline__ float wave_max_nonneg(float v)
-{
-  uint32_t u = __float_as_uint(v);
-  u = max(u, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x111, 0xf, 0xf, false));  // row_shr:1
-  u = max(u, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x112, 0xf, 0xf, false));  // row_shr:2
-  u = max(u, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x114, 0xf, 0xf, false));  // row_shr:4
-  u = max(u, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x118, 0xf, 0xf, false));  // row_shr:8
-  u = max(u, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x142, 0xa, 0xf, false));  // row_bcast:15
-  u = max(u, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x143, 0xc, 0xf, false));  // row_bcast:31
-  return __int_as_float(__builtin_amdgcn_readlane((int)u, 63));
-}
-
-// Bundle of the rays (o, d) of the `live` lanes.  Call with every lane of the wave active and at least
-// one live lane.  Approximate square roots are fine here: every bound is widened well past their error.
-__device__ __forceinline__ Bundle make_bundle(v3 o, v3 d, bool live)
-{
-  Bundle B;
-  const int ref = __ffsll((long long)__ballot(live)) - 1;
-  B.cx = lane_bcast(o.x, ref); B.cy = lane_bcast(o.y, ref); B.cz = lane_bcast(o.z, ref);
-  const float dx = lane_bcast(d.x, ref), dy = lane_bcast(d.y, ref), dz = lane_bcast(d.z, ref);
-  const float inv = __builtin_amdgcn_rsqf(dx * dx + dy * dy + dz * dz);
-  B.ax = dx * inv; B.ay = dy * inv; B.az = dz * inv;
-  const float ex = o.x - B.cx, ey = o.y - B.cy, ez = o.z - B.cz;
-  const float e2 = ex * ex + ey * ey + ez * ez;
-  const float cosl = (d.x * B.ax + d.y * B.ay + d.z * B.az) * __builtin_amdgcn_rsqf(d.x * d.x + d.y * d.y + d.z * d.z);
-  const float dev = 1.0f - cosl;
-  // a live lane with a non-finite or degenerate ray disables the bound for the whole wave
-  const bool bad = live && !(e2 <= 1.0e30f && dev >= -0.5f && dev <= 2.5f);
-  const float e2m = wave_max_nonneg(live ? e2 : 0.0f);
-  const float devm = wave_max_nonneg(live ? fmaxf(dev, 0.0f) : 0.0f);
-  B.rw = __builtin_amdgcn_sqrtf(e2m) * 1.0001f;
-  B.cosa = 1.0f - devm - 4e-6f;                                                // approximate cosines: widen
-  B.sina = __builtin_amdgcn_sqrtf(fmaxf(1.0f - B.cosa * B.cosa, 0.0f) + 1e-7f) * 1.001f;
-  B.ok = __ballot(bad) == 0 && B.cosa > 0.1f && B.rw <= 1.0e15f;
-  return B;
-}
-
-// Bit l: object first + l (l < n <= 64) of the bounding-sphere array may be hit by a ray of the bundle.
-// Call with every lane of the wave active.  Cone test: the ray set meets the grown sphere (centre at
-// distance L, radius rp) only if the angle between (centre - c) and the axis is at most
-// acos(cosa) + asin(rp / L), i.e. va >= cosa sqrt(L^2 - rp^2) - sina rp.
-__device__ __forceinline__ uint64_t cull_chunk(const Bound *bound, int first, int n, const Bundle &B)
-{
-  const int l = (int)(threadIdx.x & 63u);
-  bool keep = false;
-  if (l < n)
-  {
-    const Bound g = bound[first + l];
-    const float vx = g.x - B.cx, vy = g.y - B.cy, vz = g.z - B.cz;
-    const float L2 = vx * vx + vy * vy + vz * vz;
-    const float L = __builtin_amdgcn_sqrtf(L2);
-    const float rp = g.r + B.rw + kCullRel * (L + B.rw);
-    const float va = vx * B.ax + vy * B.ay + vz * B.az;
-    const float lim = B.cosa * __builtin_amdgcn_sqrtf(fmaxf(L2 - rp * rp, 0.0f)) - B.sina * rp;
-    keep = !(L > rp && va < lim);
-  }
-  return __ballot(keep);
-}
-
-// Small scenes: lane l tests cull record l (rfx_types.h CullRec) -- the cone test of cull_chunk, and
-// for a triangle also its plane: when every origin lies more than rw (plus a margin) on one side and
-// every direction leaves that side (axis . n beyond sin of the cone's half-angle, plus a margin), every
-// ray has t <= 0 for the plane.  The reference's float test then sees -ao.z and ar.z of opposite signs
-// too: for a basis with cond <= 1000 their rounding error stays below 2e-4 of |o - v0| and |ray|, inside
-// the 1e-3 margins.  Bits of lanes without an object are cleared.
-__device__ __forceinline__ uint64_t cull_small(const CullRec *tab, uint64_t valid, const Bundle &B)
-{
-  const CullRec g = tab[threadIdx.x & 63u];
-  const float vx = g.x - B.cx, vy = g.y - B.cy, vz = g.z - B.cz;
-  const float L2 = vx * vx + vy * vy + vz * vz;
-  const float L = __builtin_amdgcn_sqrtf(L2);
-  const float rp = g.r + B.rw + kCullRel * (L + B.rw);
-  const float va = vx * B.ax + vy * B.ay + vz * B.az;
-  const float lim = B.cosa * __builtin_amdgcn_sqrtf(fmaxf(L2 - rp * rp, 0.0f)) - B.sina * rp;
-  const float side = g.nx * B.cx + g.ny * B.cy + g.nz * B.cz - g.d;
-  const float an = g.nx * B.ax + g.ny * B.ay + g.nz * B.az;
-  const float ms = B.rw + 1e-3f * (L + g.r + B.rw) + 1e-6f, ma = B.sina + 1e-3f;
-  const bool away = (side > ms && an > ma) || (side < -ms && an < -ma);
-  const bool keep = !(L > rp && va < lim) && !away;
-  return __ballot(keep) & valid;
-}
-
-__device__ __forceinline__ uint64_t all_bits(int n) { return n >= 64 ? ~0ull : ((1ull << n) - 1ull); }
-
-// sphere bits (2q, 2q+1) -> pair bit q
-__device__ __forceinline__ uint32_t pair_bits(uint64_t m)
-{
-  uint64_t x = (m | (m >> 1)) & 0x5555555555555555ull;
-  x = (x | (x >> 1)) & 0x3333333333333333ull;
-  x = (x | (x >> 2)) & 0x0F0F0F0F0F0F0F0Full;
-  x = (x | (x >> 4)) & 0x00FF00FF00FF00FFull;
-  x = (x | (x >> 8)) & 0x0000FFFF0000FFFFull;
-  x = (x | (x >> 16)) & 0x00000000FFFFFFFFull;
-  return (uint32_t)x;
-}
-
-// ------------------------------------------------------------- closest hit
-// Scene.cpp:86-106: the reference keeps the first object with the minimal distance, i.e. the
-// lexicographic minimum of (distance, insertion index); any visiting order gives it.  Distances are
-// compared through their squares (dist = sqrt_rn(sq) for both kinds, Sphere.cpp:61-62,
-// Triangle.cpp:70-85): for sq < best_sq, dist < best unless both round to the same float, i.e. unless
-// sq >= sq_lower_bound(best); for sq >= best_sq, dist >= best (tests/test_sqrt_bounds.py).
-struct Hit {
-  int obj, kind, i;  // object index (-1: none), 0 sphere / 1 triangle / 2 plane, index within its kind
-  float t, u, v, sq;
-};
-
-__device__ __forceinline__ bool strictly_closer(float sq, float best_sq)
-{
-  return sq < best_sq && (best_sq == INFINITY || sq < sq_lower_bound(sqrt_rn(best_sq)));
-}
-
-// the comparison key of a candidate and the two decisions on it (Hit::sq holds the winner's key)
-constexpr float kNoHitKey = INFINITY;
-__device__ __forceinline__ float hit_key(float sq) { return sq; }
-__device__ __forceinline__ bool sph_takes(float sq, float best_sq) { return strictly_closer(sq, best_sq); }
-// dist < best || (dist == best && obj < best_obj)
-__device__ __forceinline__ bool tri_takes(float sq, float best_sq, int obj, int best_obj)
-{
-  return sq < best_sq ? (obj < best_obj || strictly_closer(sq, best_sq))
-                      : (obj < best_obj && sqrt_rn(sq) == sqrt_rn(best_sq));
-}
-
-// The planes (Scene::addPlane extension, Plane.cpp:36-73) for one lane, after the other kinds: every lane that
-// traces tests every plane (an infinite plane has no bounding sphere to cull with).
-template <bool STATS>
-__device__ __forceinline__ void closest_planes(const DevScene &S, v3 origin, v3 ray, const RayConst &k, Hit &h, Cnt &cnt)
-{
-  for (int i = 0; i < S.n_pln; ++i)
-  {
-    const PlaneGeo g = S.pln_geo[i];
-    float t, sq;
-    if (plane_hit<STATS, false>(g, origin, ray, t, sq, cnt, k, h.sq) && tri_takes(sq, h.sq, g.obj, h.obj))
-    {
-      h.sq = sq; h.obj = g.obj; h.kind = 2; h.i = i; h.t = t;
-    }
-  }
-}
-
-// any-hit over the planes but the hit one (skip_pln)
-template <bool STATS>
-__device__ __forceinline__ bool occluded_planes(const DevScene &S, v3 o, v3 ray, const RayConst &k, int skip_pln, Cnt &cnt)
-{
-  float t, sq;
-  for (int i = 0; i < S.n_pln; ++i)
-  {
-    if constexpr (STATS)
-    {
-      if (i != skip_pln && plane_hit<STATS, true>(S.pln_geo[i], o, ray, t, sq, cnt, k)) return true;
-    }
-    else if (plane_hit<STATS, true>(S.pln_geo[i], o, ray, t, sq, cnt, k) && i != skip_pln)
-      return true;
-  }
-  return false;
-}
-
-// Call with every lane of the wave active; `live` lanes trace (origin, ray).  B: the bundle, or null.
-// Large scenes: the spheres are stored in spatial (Morton) order, 64 to a chunk with a bounding sphere;
-// the bundle culls whole chunks (one lane per chunk), then the spheres of the surviving chunks.  The
-// visiting order is then not the insertion order, so spheres take the general (distance, object) rule.
-template <bool STATS, bool PLANES>
-__device__ __forceinline__ void closest_hit(const DevScene &S, v3 origin, v3 ray, bool live, const Bundle *B, Hit &h,
-                                            Cnt &cnt)
-{
-  if (live) RFX_CNT(C_SEGMENTS);
-  h.obj = -1; h.kind = 0; h.i = 0; h.t = 0.0f; h.u = 0.0f; h.v = 0.0f; h.sq = kNoHitKey;
-  const RayConst k = ray_const(ray);
-  const bool cull = B && B->ok;
-  RFX_PROF_BEGIN(P_SPH);
-  for (int cfirst = 0; cfirst < S.n_chunk; cfirst += 64)
-  {
-    uint64_t cm = cull ? cull_chunk(S.chunk_bound, cfirst, min(64, S.n_chunk - cfirst), *B)
-                       : all_bits(min(64, S.n_chunk - cfirst));
-    while (cm)
-    {
-      const int first = 64 * (cfirst + __builtin_ctzll(cm));
-      cm &= cm - 1ull;
-      const int n = min(64, S.n_sph - first);
-      const uint64_t m = cull ? cull_chunk(S.bound, first, n, *B) : all_bits(n);
-      uint32_t pm = pair_bits(m);
-      while (pm)
-      {
-        const int j = (first >> 1) + __builtin_ctz(pm);
-        pm &= pm - 1u;
-        f2 b, d;
-        pair_bd(S.sph_pair[j], origin, k, b, d);
-        if (!live) continue;
-        if constexpr (!STATS)
-          if (!pair_may_hit(b, d)) continue;  // both miss: one branch
-        float t, sq;
-        if (sphere_tail<STATS, false>(b.x, d.x, ray, k, t, sq, cnt))
-        {
-          const float key = hit_key(sq);
-          const int obj = S.sph_info[4 * j];
-          if (tri_takes(key, h.sq, obj, h.obj)) { h.sq = key; h.obj = obj; h.i = 2 * j; h.t = t; }
-        }
-        if ((!STATS || 2 * j + 1 < S.n_sph) && sphere_tail<STATS, false>(b.y, d.y, ray, k, t, sq, cnt))
-        {
-          const float key = hit_key(sq);
-          const int obj = S.sph_info[4 * j + 2];
-          if (tri_takes(key, h.sq, obj, h.obj)) { h.sq = key; h.obj = obj; h.i = 2 * j + 1; h.t = t; }
-        }
-      }
-    }
-  }
-  RFX_PROF_END(P_SPH);
-  RFX_PROF_BEGIN(P_TRI);
-  for (int first = 0; first < S.n_tri; first += 64)
-  {
-    const int n = min(64, S.n_tri - first);
-    uint64_t m = (B && B->ok) ? cull_chunk(S.bound, S.n_sph + first, n, *B) : all_bits(n);
-    while (m)
-    {
-      const int i = first + __builtin_ctzll(m);
-      m &= m - 1ull;
-      if (!live) continue;
-      float t, u, v, sq;
-      if (tri_hit<STATS, false>(S.tri_geo[i], origin, ray, t, u, v, sq, cnt, k, h.sq))
-      {
-        RFX_CNT(C_TRI_D);
-        const int obj = S.tri_shade[i].obj;
-        const float key = hit_key(sq);
-        if (tri_takes(key, h.sq, obj, h.obj))
-        {
-          h.sq = key; h.obj = obj; h.kind = 1; h.i = i; h.t = t; h.u = u; h.v = v;
-        }
-      }
-    }
-  }
-  if constexpr (PLANES)
-    if (live) closest_planes<STATS>(S, origin, ray, k, h, cnt);
-  RFX_PROF_END(P_TRI);
-}
-
-// ------------------------------------------------------------- small scenes (<= 64 objects)
-// One cull mask covers the whole scene (bit l: object l of the bound array, spheres then triangles), so
-// the object loops need no wave-wide step and run only in the lanes that trace -- a lane leaves the
-// any-hit loop at its first occluder.
-// lane-layout masks (CullRec): pair q <- lanes q and 16 + q; triangle i <- lane 32 + i
-__device__ __forceinline__ uint32_t small_pairs(uint64_t om) { return (uint32_t)((om | (om >> 16)) & 0xFFFFull); }
-__device__ __forceinline__ uint64_t small_tris(uint64_t om) { return om >> 32; }
-
-template <bool STATS, bool PLANES>
-__device__ __forceinline__ void closest_hit_small(const DevScene &S, v3 origin, v3 ray, uint64_t om, Hit &h, Cnt &cnt)
-{
-  RFX_CNT(C_SEGMENTS);
-  h.obj = -1; h.kind = 0; h.i = 0; h.t = 0.0f; h.u = 0.0f; h.v = 0.0f; h.sq = kNoHitKey;
-  const RayConst k = ray_const(ray);
-  RFX_PROF_BEGIN(P_SPH);
-  // spheres in index order carry increasing object indices, so among spheres a strict `<` already keeps
-  // the first of equal distances
-  uint32_t pm = small_pairs(om);
-  while (pm)
-  {
-    const int j = __builtin_ctz(pm);
-    pm &= pm - 1u;
-    f2 b, d;
-    pair_bd(S.sph_pair[j], origin, k, b, d);
-    if constexpr (!STATS)
-      if (!pair_may_hit(b, d)) continue;  // both miss: one branch
-    float t, sq;
-    if (sphere_tail<STATS, false>(b.x, d.x, ray, k, t, sq, cnt))
-    {
-      const float key = hit_key(sq);
-      if (sph_takes(key, h.sq)) { h.sq = key; h.obj = 2 * j; h.t = t; }
-    }
-    if ((!STATS || 2 * j + 1 < S.n_sph) && sphere_tail<STATS, false>(b.y, d.y, ray, k, t, sq, cnt))
-    {
-      const float key = hit_key(sq);
-      if (sph_takes(key, h.sq)) { h.sq = key; h.obj = 2 * j + 1; h.t = t; }
-    }
-  }
-  if (h.obj >= 0)
-  {
-    h.i = h.obj;
-    h.obj = Tabs<true>{S}.sph_info(2 * h.i);
-  }
-  RFX_PROF_END(P_SPH);
-  RFX_PROF_BEGIN(P_TRI);
-  uint64_t tm = small_tris(om);
-  while (tm)
-  {
-    const int i = __builtin_ctzll(tm);
-    tm &= tm - 1ull;
-    float t, u, v, sq;
-    if (tri_hit<STATS, false>(S.tri_geo[i], origin, ray, t, u, v, sq, cnt, k, h.sq))
-    {
-      RFX_CNT(C_TRI_D);
-      const int obj = S.tri_shade[i].obj;
-      const float key = hit_key(sq);
-      if (tri_takes(key, h.sq, obj, h.obj))
-      {
-        h.sq = key; h.obj = obj; h.kind = 1; h.i = i; h.t = t; h.u = u; h.v = v;
-      }
-    }
-  }
-  if constexpr (PLANES) closest_planes<STATS>(S, origin, ray, k, h, cnt);
-  RFX_PROF_END(P_TRI);
-}
-
-// Scene.cpp:129-141 for a small scene (see occluded below for the order and counter notes)
-template <bool STATS, bool PLANES>
-__device__ __forceinline__ bool occluded_small(const DevScene &S, v3 o, v3 ray, int skip_sph, int skip_tri, int skip_pln,
-                                               uint64_t om, Cnt &cnt)
-{
-  const RayConst k = ray_const(ray);
-  float t, sq, u, v;
-  uint32_t pm = small_pairs(om);
-  while (pm)
-  {
-    const int j = __builtin_ctz(pm);
-    pm &= pm - 1u;
-    f2 b, d;
-    pair_bd(S.sph_pair[j], o, k, b, d);
-    if constexpr (STATS)
-    {
-      if (2 * j != skip_sph && sphere_tail<STATS, true>(b.x, d.x, ray, k, t, sq, cnt)) return true;
-      if (2 * j + 1 != skip_sph && 2 * j + 1 < S.n_sph && sphere_tail<STATS, true>(b.y, d.y, ray, k, t, sq, cnt))
-        return true;
-    }
-    else
-    {
-      // a miss on both spheres (the common case) costs one branch; the hit object is filtered out after
-      // its test, which does not change the boolean
-      if (!pair_may_hit(b, d)) continue;
-      if (sphere_tail<STATS, true>(b.x, d.x, ray, k, t, sq, cnt) && 2 * j != skip_sph) return true;
-      if (sphere_tail<STATS, true>(b.y, d.y, ray, k, t, sq, cnt) && 2 * j + 1 != skip_sph) return true;
-    }
-  }
-  uint64_t tm = small_tris(om);
-  while (tm)
-  {
-    const int i = __builtin_ctzll(tm);
-    tm &= tm - 1ull;
-    if constexpr (STATS)
-    {
-      if (i != skip_tri && tri_hit<STATS, true>(S.tri_geo[i], o, ray, t, u, v, sq, cnt, k)) return true;
-    }
-    else if (tri_hit<STATS, true>(S.tri_geo[i], o, ray, t, u, v, sq, cnt, k) && i != skip_tri)
-      return true;
-  }
-  if constexpr (PLANES) return occluded_planes<STATS>(S, o, ray, k, skip_pln, cnt);
-  return false;
-}
-
-// ------------------------------------------------------------- shadow any-hit
-// Scene.cpp:129-141: every object but the hit one (skip_sph / skip_tri: its sphere or triangle index,
-// -1 for the other kind); the boolean does not depend on the order.  Call with every lane of the wave
-// active; `live` lanes test (o, ray).  A lane stops at its first occluder and the wave once every live
-// lane has one.  (Spheres precede triangles, the reference's order for scenes whose objects are added
-// spheres-first -- then even the event counters match it: the second sphere of a pair is counted only
-// when the first did not occlude.)
-template <bool STATS, bool PLANES>
-__device__ __forceinline__ bool occluded(const DevScene &S, v3 o, v3 ray, bool live, int skip_sph, int skip_tri,
-                                         int skip_pln, const Bundle *B, Cnt &cnt)
-{
-  const RayConst k = ray_const(ray);
-  const bool cull = B && B->ok;
-  bool occ = false;
-  float t, sq, u, v;
-  for (int cfirst = 0; cfirst < S.n_chunk; cfirst += 64)
-  {
-    if (__ballot(live && !occ) == 0) return occ;
-    uint64_t cm = cull ? cull_chunk(S.chunk_bound, cfirst, min(64, S.n_chunk - cfirst), *B)
-                       : all_bits(min(64, S.n_chunk - cfirst));
-    while (cm)
-    {
-      const int first = 64 * (cfirst + __builtin_ctzll(cm));
-      cm &= cm - 1ull;
-      const int n = min(64, S.n_sph - first);
-      const uint64_t m = cull ? cull_chunk(S.bound, first, n, *B) : all_bits(n);
-      uint32_t pm = pair_bits(m);
-      while (pm)
-      {
-        const int j = (first >> 1) + __builtin_ctz(pm);
-        pm &= pm - 1u;
-        f2 b, d;
-        pair_bd(S.sph_pair[j], o, k, b, d);
-        if (live && !occ)
-        {
-          if constexpr (STATS)
-          {
-            if (2 * j != skip_sph && sphere_tail<STATS, true>(b.x, d.x, ray, k, t, sq, cnt)) occ = true;
-            else if (2 * j + 1 != skip_sph && 2 * j + 1 < S.n_sph &&
-                     sphere_tail<STATS, true>(b.y, d.y, ray, k, t, sq, cnt))
-              occ = true;
-          }
-          else if (pair_may_hit(b, d))
-          {
-            // the hit object is filtered out after its test, which does not change the boolean
-            if (sphere_tail<STATS, true>(b.x, d.x, ray, k, t, sq, cnt) && 2 * j != skip_sph) occ = true;
-            else if (sphere_tail<STATS, true>(b.y, d.y, ray, k, t, sq, cnt) && 2 * j + 1 != skip_sph) occ = true;
-          }
-        }
-        if (__ballot(live && !occ) == 0) return occ;
-      }
-    }
-  }
-  for (int first = 0; first < S.n_tri; first += 64)
-  {
-    if (__ballot(live && !occ) == 0) return occ;
-    const int n = min(64, S.n_tri - first);
-    uint64_t m = (B && B->ok) ? cull_chunk(S.bound, S.n_sph + first, n, *B) : all_bits(n);
-    while (m)
-    {
-      const int i = first + __builtin_ctzll(m);
-      m &= m - 1ull;
-      if (live && !occ)
-      {
-        if constexpr (STATS)
-        {
-          if (i != skip_tri && tri_hit<STATS, true>(S.tri_geo[i], o, ray, t, u, v, sq, cnt, k)) occ = true;
-        }
-        else if (tri_hit<STATS, true>(S.tri_geo[i], o, ray, t, u, v, sq, cnt, k) && i != skip_tri)
-          occ = true;
-      }
-      if (__ballot(live && !occ) == 0) return occ;
-    }
-  }
-  if constexpr (PLANES)
-    if (live && !occ) occ = occluded_planes<STATS>(S, o, ray, k, skip_pln, cnt);
-  return occ;
-}
-
-// ------------------------------------------------------------- Scene::trace
-// Scene::trace (Scene.cpp:73-236) for one trace per lane, the bounce loop run wave-wide: every
-// iteration is one segment of every live lane -- closest hit, then per light the facing test and the
-// shadow any-hit (Scene.cpp:117-141; the occlusion tests depend on nothing the shading computes, so
-// they run first, with few registers live), then material, shading and the next ray or the sky.
-// CULL: wave bundles skip objects no live lane can hit (closest hit and shadow rays); MANYL: more than
-// 32 lights (shadow masks and shading in blocks of 32); PLANES: the scene holds planes.  Call with every lane
-// of the wave active; `valid` lanes trace.  Returns the trace's colour (zero for invalid lanes).
-template <bool STATS, bool CULL, bool MANYL, bool SMALL, bool PLANES>
-__device__ __forceinline__ col trace(const DevScene &S, v3 origin, v3 ray, int depth, v3 rd, const float *lut,
-                                     Cnt &cnt, bool valid)
-{
-  if (valid) RFX_CNT(C_RAYS);
-  const Tabs<SMALL> T{S};
-  col mulc = mkc(1.0f, 1.0f, 1.0f), pix = mkc(0.0f, 0.0f, 0.0f);
-  int refl = 0;
-  bool alive = valid && depth > 0;
-#ifdef RFX_DEBUG_SEGS
-  int nseg = 0;  // diagnostic build only (tools/segstats.py): the trace's segment count replaces its colour
-#endif
-  RFX_PROF_BEGIN(P_SEG);
-  while (__ballot(alive))
-  {
-#ifdef RFX_DEBUG_SEGS
-    if (alive) ++nseg;
-#endif
-    Hit h;
-    if constexpr (SMALL)
-    {
-      uint64_t om = S.cull_valid;
-      if constexpr (CULL)
-      {
-        const Bundle B = make_bundle(origin, ray, alive);
-        if (B.ok) om = cull_small(T.cull(), S.cull_valid, B);
-        RFX_CULL_STAT(0, B.ok, __ballot(alive), om, S.cull_valid);
-      }
-      if (alive) closest_hit_small<STATS, PLANES>(S, origin, ray, om, h, cnt);
-      else h.obj = -1;
-    }
-    else
-    {
-      Bundle B;
-      if constexpr (CULL) B = make_bundle(origin, ray, alive);
-      closest_hit<STATS, PLANES>(S, origin, ray, alive, CULL ? &B : nullptr, h, cnt);
-    }
-    const bool hit = alive && h.obj >= 0;
-    // re-derive the winner's outputs with the reference's expressions
-    v3 drop = origin, norm = mk(0.0f, 0.0f, 0.0f);
-    RFX_PROF_BEGIN(P_WIN);
-    if (hit)
-    {
-      drop = add(origin, mul(ray, h.t));
-      if (h.kind == 0)
-      {
-        RFX_CNT(C_HIT_SPH);
-        const SphereGeo g = T.sph_geo(h.i);
-        norm = sub(drop, mk(g.cx, g.cy, g.cz));                                // Sphere.cpp:67
-      }
-      else if (!PLANES || h.kind == 1)
-      {
-        RFX_CNT(C_HIT_TRI);
-        const TriShade sh = T.tri_shade(h.i);
-        norm = mk(sh.nx, sh.ny, sh.nz);
-      }
-      else
-      {
-        RFX_CNT(C_HIT_PLN);
-        const PlaneGeo g = S.pln_geo[h.i];
-        norm = mk(g.nx, g.ny, g.nz);                                               // Plane.cpp:58-59
-      }
-    }
-    RFX_PROF_END(P_WIN);
-    const int skip_sph = h.kind == 0 ? h.i : -1, skip_tri = h.kind == 1 ? h.i : -1;
-    const int skip_pln = PLANES && h.kind == 2 ? h.i : -1;
-    MatRec m{0.0f, 0.0f, 0.0f, 0.0f};
-    int diel = 0;
-    v3 reflv = mk(0.0f, 0.0f, 0.0f);
-    float rayLen = 0.0f, normLen = 0.0f, reflectLen = 0.0f;
-    col sumL = mkc(0.0f, 0.0f, 0.0f), sumS = mkc(0.0f, 0.0f, 0.0f);
-    for (int base = 0;; base += 32)                                            // Scene.cpp:117-181
-    {
-      RFX_PROF_BEGIN(P_SHADOW);
-      uint32_t lit = 0;
-      const int nl = min(32, S.n_light - base);
-      for (int q = 0; q < nl; ++q)
-      {
-        const LightRec L = S.lights[base + q];
-        bool facing = false;
-        v3 sray = mk(0.0f, 0.0f, 0.0f);
-        if (hit)
-        {
-          RFX_CNT(C_L_EVAL);
-          const v3 dtl = sub(mk(L.ox, L.oy, L.oz), drop);
-          if (dot(dtl, norm) > kVerySmall)
-          {
-            RFX_CNT(C_L_FACING);
-            facing = true;
-            sray = add(dtl, mul(rd, L.radius));                                  // Scene.cpp:129
-          }
-        }
-        if (__ballot(facing))
-        {
-          if constexpr (SMALL)
-          {
-            uint64_t om = S.cull_valid;
-            if constexpr (CULL)
-            {
-              const Bundle SB = make_bundle(drop, sray, facing);
-              if (SB.ok) om = cull_small(T.cull(), S.cull_valid, SB);
-              RFX_CULL_STAT(1, SB.ok, __ballot(facing), om, S.cull_valid);
-            }
-            if (facing && !occluded_small<STATS, PLANES>(S, drop, sray, skip_sph, skip_tri, skip_pln, om, cnt))
-              lit |= 1u << q;
-          }
-          else
-          {
-            Bundle SB;
-            if constexpr (CULL) SB = make_bundle(drop, sray, facing);
-            const bool occ = occluded<STATS, PLANES>(S, drop, sray, facing, skip_sph, skip_tri, skip_pln,
-                                                     CULL ? &SB : nullptr, cnt);
-            if (facing && !occ) lit |= 1u << q;
-          }
-        }
-      }
-      RFX_PROF_END(P_SHADOW);
-      RFX_PROF_BEGIN(P_LIGHT);
-      if (hit)
-      {
-        if (!MANYL || base == 0)
-        {
-          // the hit object's material, texel, reflection and lengths (Sphere.cpp:66-80, Triangle.cpp:86-105)
-          if (h.kind == 0)
-          {
-            m = T.sph_mat(h.i);
-            diel = T.sph_info(2 * h.i + 1);
-          }
-          else if (PLANES && h.kind == 2)
-          {
-            m = S.pln_mat[h.i];                                                  // untextured (Plane.cpp:67-68)
-            diel = S.pln_geo[h.i].dielectric;
-          }
-          else
-          {
-            const TriShade sh = T.tri_shade(h.i);
-            m = T.tri_mat(h.i);
-            diel = sh.dielectric;
-            if (sh.tex >= 0)
-            {
-              const col c = tri_texel<STATS>(S, sh, h.u, h.v, lut, cnt);
-              m.r = c.r; m.g = c.g; m.b = c.b;
-            }
-          }
-          reflv = reflect(mul(ray, h.t), norm);                                // trace_math.cpp:14-23
-          rayLen = len(ray); normLen = len(norm); reflectLen = len(reflv);
-        }
-        for (int q = 0; q < nl; ++q)
-        {
-          if (!((lit >> q) & 1u)) continue;
-          RFX_CNT(C_L_LIT);
-          const LightRec L = S.lights[base + q];
-          const v3 dtl = sub(mk(L.ox, L.oy, L.oz), drop);
-          const float dlen = len(dtl);
-          float aa = dlen * normLen;
-          const float cosl = (aa > kVerySmall) ? dot(dtl, norm) / aa : 0.0f;
-          const col lc = mkc(L.r, L.g, L.b);
-          if (L.power > kVerySmall) sumL = cadd(sumL, cscale(cscale(lc, cosl), L.power));
-          aa = sqlen(dtl);
-          const float ang = (aa > kVerySmall) ? 1.0f - L.radius * L.radius / aa : 0.0f;
-          if (ang > 0)
-          {
-            RFX_CNT(C_L_SPEC);
-            const v3 dlr = add(normalized(dtl), mul(rd, 1.0f - m.refl));
-            aa = len(dlr) * reflectLen;
-            float sc = (aa > kVerySmall) ? dot(dlr, reflv) / aa : 0.0f;
-            sc = clampf(sc + (1.0f - sqrt_rn(ang)), 0.0f, 1.0f);
-            if (sc > kVerySmall && L.radius > kVerySmall)
-            {
-              RFX_CNT(C_L_POW);
-              const float sp = powf_dev(sc, 1 + 3 * m.refl * dlen / L.radius) * m.refl;
-              sumS = cadd(sumS, cscale(lc, sp));
-            }
-          }
-        }
-      }
-      RFX_PROF_END(P_LIGHT);
-      if (!MANYL || base + 32 >= S.n_light) break;
-    }
-    if (hit)
-    {
-      RFX_PROF_BEGIN(P_MAT);
-      sumL = cadd(mkc(S.amb_r, S.amb_g, S.amb_b), sumL);                        // Scene.cpp:186
-      const col color = mkc(m.r, m.g, m.b);
-      col fin;
-      if (diel)                                                                  // Scene.cpp:189-201
-      {
-        RFX_CNT(C_DIELECTRIC);
-        const float aa = rayLen * normLen;
-        const float cosA = (aa > kVerySmall) ? clampf(dot(ray, neg(norm)) / aa, 0.0f, 1.0f) : 0.0f;
-        const float r = 0.2f + 0.8f * powf_dev(1.0f - cosA, 3.0f);
-        fin = cadd(cmul(cscale(color, 1.0f - r), sumL), sumS);
-        fin = cmul(fin, mulc);
-        mulc = cscale(mulc, r);
-      }
-      else                                                                       // Scene.cpp:202-212
-      {
-        RFX_CNT(C_METAL);
-        const float r = 0.8f;
-        fin = cadd(cmul(cscale(color, 1.0f - r), sumL), sumS);
-        fin = cmul(fin, mulc);
-        mulc = cmul(mulc, cscale(color, r));
-      }
-      pix = cclamp(cadd(pix, fin));                                              // Scene.cpp:215-216
-      RFX_PROF_END(P_MAT);
-      if (mulc.r < 0.01f && mulc.g < 0.01f && mulc.b < 0.01f)                    // Scene.cpp:219-220
-        alive = false;
-      else
-      {
-        RFX_CNT(C_CONTINUE);
-        origin = drop;                                                           // Scene.cpp:223-224
-        ray = add(normalized(reflv), mul(rd, 1.0f - m.refl));
-        if (++refl >= depth) alive = false;                                      // Scene.cpp:78
-      }
-    }
-    else if (alive)                                                              // Scene.cpp:226-231
-    {
-      RFX_CNT(C_SKY);
-      RFX_PROF_BEGIN(P_SKY);
-      pix = cclamp(cadd(pix, cmul(cmul(mulc, skybox_texel<STATS>(S, ray, lut, cnt)), mkc(S.env_r, S.env_g, S.env_b))));
-      RFX_PROF_END(P_SKY);
-      alive = false;
-    }
-  }
-  RFX_PROF_END(P_SEG);
-#ifdef RFX_DEBUG_SEGS
-  return mkc((float)nseg, 0.0f, 0.0f);
-#else
-  return pix;
-#endif
-}
-
-template <bool STATS>
-__device__ __forceinline__ void flush_counters(const FrameParams &P, Cnt &cnt)
-{
-  if constexpr (STATS)
-  {
-#pragma unroll
-    for (int k = 0; k < C_COUNT; ++k)
-    {
-      unsigned long long v = cnt.c[k];
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-      if ((threadIdx.x & 63) == 0 && v) atomicAdd(&P.counters[k], v);
-    }
-  }
-}
-
-__device__ __forceinline__ uint32_t strip_row_to_y(uint32_t r, const FrameParams &P)
-{
-  if (P.nranks <= 1) return r;
-  const uint32_t blk = r / P.row_block, w = r % P.row_block;
-  return (blk * P.nranks + P.rank) * P.row_block + w;
-}
-
-// trace i's randomInsideSphere draw (Vector3.cpp:176-188) from the LCG state before its accepted triple
-__device__ __forceinline__ v3 rd_from_state(uint32_t s)
-{
-  const uint32_t s1 = lcg_step(s), s2 = lcg_step(s1), s3 = lcg_step(s2);
-  return mk(rand_component_dev(lcg_out(s1)), rand_component_dev(lcg_out(s2)), rand_component_dev(lcg_out(s3)));
-}
-
-__device__ __forceinline__ v3 load_rd(const FrameParams &P, uint64_t i) { return rd_from_state(P.rd_state[i]); }
-
-#ifndef RFX_WAVE_TILES  // schedule unit: the wave's 8x8 tile (1) or the workgroup's 16x8 (0); tools/ab.py, C3: -2.7% trace
-#define RFX_WAVE_TILES 1
-#endif
-
-// Shader clock, low 32 bits.  A plain asm statement (no side effects declared, so the compiler may still
-// serve the scene loads that follow through the scalar cache -- __builtin_readcyclecounter would count as a
-// memory clobber for them); it waits for its own result.
-__device__ __forceinline__ uint32_t clock32()
-{
-  uint64_t c;
-  asm("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(c));
-  return (uint32_t)c;
-}
-
-// 7 waves per SIMD (<= 72 VGPRs, a few spills): the kernel is VALU-issue bound; more waves hide the
-// scene-load and texel latencies better than spills cost (tools/ab.py, C3 trace kernel: 6 -> 7 -2.6%;
-// 8 waves / 64 VGPRs spill enough to lose 4-7%)
-#ifndef RFX_WAVES_PER_EU
-#define RFX_WAVES_PER_EU 7
-#endif
-// waves per workgroup (1, 2 or 4): a wave is an 8x8 pixel tile, a workgroup 8x8 / 16x8 / 16x16 pixels.
-// Two: a workgroup's slots free when its slower wave ends, and the per-workgroup LDS staging stays cheap
-// (tools/ab.py, C3 trace kernel: 4 -> 2 waves -2.5%, 1 wave +3.6%)
-#ifndef RFX_WG_WAVES
-#define RFX_WG_WAVES 2
-#endif
-constexpr uint32_t kWgWaves = RFX_WG_WAVES, kWgThreads = 64 * kWgWaves;
-constexpr uint32_t kTileWavesX = kWgWaves >= 2 ? 2 : 1, kTileWavesY = kWgWaves / kTileWavesX;
-constexpr uint32_t kTileW = 8 * kTileWavesX, kTileH = 8 * kTileWavesY;
-static_assert(kWgWaves == 1 || kWgWaves == 2 || kWgWaves == 4, "RFX_WG_WAVES: 1, 2 or 4");
-#define RFX_TRACE_BOUNDS __launch_bounds__(kWgThreads) __attribute__((amdgpu_waves_per_eu(RFX_WAVES_PER_EU)))
-
-// Pixel loop variants of Render::renderNext: block preview (sampleNum < 0), one plain trace per pixel
-// (sampleNum == 1, no jitter, no accumulation -- the benchmark frame), and the general SSAA / additive
-// loop.  The plain variant drops the sample loops and their live state (no spills before the bounce loop).
-enum TraceMode { kModeSsaa = 0, kModeBlock = 1, kModePlain = 2 };
-// CFG bits: kCfgCull -- wave-bundle culling (every non-stats launch); kCfgManyLights -- more than 32 lights;
-// kCfgSmall -- at most 32 spheres and 32 triangles (one lane-layout cull mask for the whole scene)
-// kCfgPlanes -- the scene holds planes (Scene::addPlane extension)
-constexpr int kCfgCull = 1, kCfgManyLights = 2, kCfgSmall = 4, kCfgPlanes = 8;
-
-// one workgroup = kTileW x kTileH output pixels (block mode: block corners), one wave = an 8x8 tile (ray coherence).
-// Every lane of a wave reaches trace() -- lanes outside the frame or the cursor span as invalid -- so the
-// bounce loop can use wave-wide bundles.
-template <bool STATS, int MODE, int CFG>
-__global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
-{
-  constexpr bool CULL = (CFG & kCfgCull) != 0, MANYL = (CFG & kCfgManyLights) != 0, SMALL = (CFG & kCfgSmall) != 0;
-  constexpr bool PLANES = (CFG & kCfgPlanes) != 0;
-  __shared__ float lut[256];
-  for (uint32_t i = threadIdx.x; i < 256; i += kWgThreads) lut[i] = (float)i / 255.0f;  // Color.cpp:11-13
-  stage_powf_tables();
-  if constexpr (SMALL) stage_small_scene(S);
-  RFX_PROF_INIT();
-  // the tile this workgroup renders: with a tile order (longest-processing-time first, from the previous
-  // frame's measured tile costs) the most expensive tiles start first and the cheap ones fill the tail
-  const uint32_t tile = P.tile_order ? P.tile_order[blockIdx.y * gridDim.x + blockIdx.x] : blockIdx.y * gridDim.x + blockIdx.x;
-  // tile cost: the start clock (low 32 bits) and the tile index wait in LDS, so the bounce loop keeps no
-  // register for them
-  __shared__ uint32_t s_clk0, s_tile;
-  if (P.tile_cost && threadIdx.x == 0)
-  {
-    s_clk0 = clock32();
-    s_tile = tile;
-  }
-  __syncthreads();
-  Cnt cnt;
-  if constexpr (STATS)
-  {
-#pragma unroll
-    for (int k = 0; k < C_COUNT; ++k) cnt.c[k] = 0;
-  }
-  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-#if RFX_WAVE_TILES
-  // the schedule's unit is the wave's 8x8 tile: wave v of workgroup w renders tile tile_order[kWgWaves w + v]
-  // of the (kTileWavesX gridDim.x) x (kTileWavesY gridDim.y) tile grid (identity: the workgroup's own tiles)
-  const uint32_t wv = __builtin_amdgcn_readfirstlane(wave), wid = blockIdx.y * gridDim.x + blockIdx.x;
-  const uint32_t w8 = kTileWavesX * gridDim.x;
-  const uint32_t t8 = P.tile_order ? P.tile_order[kWgWaves * wid + wv]
-                                   : (blockIdx.y * kTileWavesY + wv / kTileWavesX) * w8 + blockIdx.x * kTileWavesX + wv % kTileWavesX;
-  const uint32_t gx = (t8 % w8) * 8u + (lane & 7u), gy = (t8 / w8) * 8u + (lane >> 3);
-  (void)tile;
-#else
-  const uint32_t lx = (wave % kTileWavesX) * 8u + (lane & 7u), ly = (wave / kTileWavesX) * 8u + (lane >> 3);
-  const uint32_t bx = tile % gridDim.x, by = tile / gridDim.x;
-  const uint32_t gx = bx * kTileW + lx, gy = by * kTileH + ly;
-#endif
-  m33 view;
-  view.m11 = P.v11; view.m12 = P.v12; view.m13 = P.v13;
-  view.m21 = P.v21; view.m22 = P.v22; view.m23 = P.v23;
-  view.m31 = P.v31; view.m32 = P.v32; view.m33 = P.v33;
-  const v3 eye = mk(P.eye_x, P.eye_y, P.eye_z);
-
-  if constexpr (MODE == kModeBlock)
-  {
-    // block preview (Render.cpp:158-172): only block corners inside the cursor span are traced;
-    // trace order = raster order of corners, so corner (cx, cy) is trace cy * bw + cx.
-    const uint32_t n = (uint32_t)(-P.ss);
-    const uint32_t bw = (P.W + n - 1) / n, bh = (P.H + n - 1) / n;
-    const uint32_t cx = gx, cy = gy + P.row0;
-    const uint32_t x = cx * n, y = cy * n;
-    const uint64_t p = (uint64_t)y * P.W + x;
-    const bool valid = gy < P.grid_rows && cx < bw && cy < bh && p >= P.p_begin && p < P.p_end;
-    const v3 ray = mmul(view, mk((float)x - P.wh, (float)y - P.hh, P.rz));
-    v3 rd = mk(0.0f, 0.0f, 0.0f);
-    if (valid) rd = load_rd(P, (uint64_t)cy * bw + cx - P.trace_base);
-    const col c = trace<STATS, CULL, MANYL, SMALL, PLANES>(S, eye, ray, P.depth, rd, lut, cnt, valid);
-    if (valid)
-    {
-      const uint32_t ex = min(P.W, x + n), ey = min(P.H, y + n);
-      const uint32_t a = argb(c);
-      for (uint32_t qy = y; qy < ey; ++qy)
-        for (uint32_t qx = x; qx < ex; ++qx)
-        {
-          float *d = P.img + ((size_t)qy * P.W + qx) * 3;
-          d[0] = c.r; d[1] = c.g; d[2] = c.b;
-          if (P.argb) P.argb[(size_t)qy * P.W + qx] = a;
-        }
-    }
-    if (P.tile_cost && __lane_id() == 0) P.tile_cost[s_tile] = clock32() - s_clk0;  // one lane per wave, the last stays
-  }
-  else
-  {
-    const uint32_t x = gx;
-    const uint32_t y = P.nranks > 1 ? strip_row_to_y(gy, P) : gy + P.row0;
-    const uint32_t orow = P.nranks > 1 ? gy : y;
-    const uint64_t p = (uint64_t)y * P.W + x;
-    const bool valid = gx < P.W && gy < P.grid_rows && p >= P.p_begin && p < P.p_end;
-    const uint64_t pr = p - P.p_begin;
-    const float rx = (float)x - P.wh, ry = (float)y - P.hh;                       // Render.cpp:152-153
-    col out;
-    if constexpr (MODE == kModePlain)
-    {
-      // Render.cpp:183 with ssx = ssy = 0, sampleNum = 1, no jitter: float(0) / 1 == +0, rnd == 0
-      const v3 ray = mmul(view, mk(rx + 0.0f + 0.0f, ry + 0.0f + 0.0f, P.rz));
-      v3 rd = mk(0.0f, 0.0f, 0.0f);
-      if (valid) rd = load_rd(P, pr);
-      const col c = trace<STATS, CULL, MANYL, SMALL, PLANES>(S, eye, ray, P.depth, rd, lut, cnt, valid);
-      out = cadd(mkc(0.0f, 0.0f, 0.0f), c);                                      // Render.cpp:185 (/ 1.0f exact)
-    }
-    else
-    {
-      float rndx = 0.0f, rndy = 0.0f;
-      if (P.additive && valid)                                                     // Render.cpp:177-178
-      {
-        const uint32_t s1 = lcg_jump(P.jitter_seed, 2 * pr + 1);
-        rndx = (float)lcg_out(s1) / (float)0x7FFF;
-        rndy = (float)lcg_out(lcg_step(s1)) / (float)0x7FFF;
-      }
-      const int ss = P.ss;
-      const float ssf = (float)ss;
-      col fin = mkc(0.0f, 0.0f, 0.0f);
-      for (int sx = 0; sx < ss; ++sx)                                              // Render.cpp:181-187
-        for (int sy = 0; sy < ss; ++sy)
-        {
-          // float(0) / ss == +0 exactly, so the first sample's offsets need no division
-          const float ox = sx ? (float)sx / ssf : 0.0f, oy = sy ? (float)sy / ssf : 0.0f;
-          v3 ray = mk(rx + ox + rndx, ry + oy + rndy, P.rz);
-          ray = mmul(view, ray);
-          v3 rd = mk(0.0f, 0.0f, 0.0f);
-          if (valid) rd = load_rd(P, pr * (uint64_t)(ss * ss) + (uint64_t)(sx * ss + sy));
-          fin = cadd(fin, trace<STATS, CULL, MANYL, SMALL, PLANES>(S, eye, ray, P.depth, rd, lut, cnt, valid));
-        }
-      if (ss != 1)                                                                 // Render.cpp:189 (x / 1.0f == x)
-      {
-        const float sq = (float)(ss * ss);
-        if (fabsf(sq) > kVerySmall) fin = mkc(fin.r / sq, fin.g / sq, fin.b / sq);
-      }
-      out = fin;
-    }
-    if (valid)
-    {
-      const size_t o = (size_t)orow * P.W + x;
-      float *d = P.img + o * 3;
-      if (MODE == kModeSsaa && P.accumulate) out = mkc(d[0] + out.r, d[1] + out.g, d[2] + out.b);  // Render.cpp:191-194
-      d[0] = out.r; d[1] = out.g; d[2] = out.b;
-      if (P.argb) P.argb[o] = argb(out);                                           // Render::copyImage
-    }
-#if RFX_WAVE_TILES
-    if (P.tile_cost && __lane_id() == 0)  // per wave tile, located from the live pixel (x, orow)
-      P.tile_cost[(P.nranks > 1 ? orow : orow - P.row0) / 8u * P.tiles_x + x / 8u] = clock32() - s_clk0;
-#else
-    if (P.tile_cost && __lane_id() == 0) P.tile_cost[s_tile] = clock32() - s_clk0;  // one lane per wave, the last stays
-#endif
-  }
-  flush_counters<STATS>(P, cnt);
-  RFX_PROF_FLUSH();
-
-}
 
 // ------------------------------------------------------------- LPT tile order
 // The tile costs of a frame (clock cycles per tile) become the next launch's tile order, most
@@ -1654,29 +372,7 @@ __global__ __launch_bounds__(kKatThreads) void kat_argb(const float *rgb, uint32
 
 }  // namespace rfx
 
-#ifdef RFX_DEBUG_PROF
-extern "C" int rfx_debug_cull_read(unsigned long long *out, int reset)
-{
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rfx::g_cull), sizeof(rfx::g_cull)) != hipSuccess) return -1;
-  if (reset)
-  {
-    static const unsigned long long zero[16] = {};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(rfx::g_cull), zero, sizeof(zero)) != hipSuccess) return -1;
-  }
-  return 16;
-}
 
-extern "C" int rfx_debug_prof_read(unsigned long long *out, int reset)
-{
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rfx::g_prof), sizeof(rfx::g_prof)) != hipSuccess) return -1;
-  if (reset)
-  {
-    static const unsigned long long zero[2 * rfx::P_COUNT] = {};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(rfx::g_prof), zero, sizeof(zero)) != hipSuccess) return -1;
-  }
-  return 2 * rfx::P_COUNT;
-}
-#endif
 
 // ------------------------------------------------------------- launchers (library-internal)
 namespace rfx {
@@ -1730,52 +426,12 @@ hipError_t launch_rng_finish(const uint32_t *d_seed, const uint32_t *d_jump, uin
   return hipGetLastError();
 }
 
-template <bool STATS, int MODE, int CFG>
-static void launch_one(dim3 grid, const DevScene &S, const FrameParams &P, hipStream_t st)
-{
-  if constexpr (!STATS || !(CFG & kCfgCull))  // the stats build never culls
-    hipLaunchKernelGGL((trace_kernel<STATS, MODE, CFG>), grid, dim3(kWgThreads), 0, st, S, P);
-}
-
-template <bool STATS, int MODE>
-static void launch_cfg(int cfg, dim3 grid, const DevScene &S, const FrameParams &P, hipStream_t st)
-{
-  switch (cfg)
-  {
-    case 0: launch_one<STATS, MODE, 0>(grid, S, P, st); break;
-    case 1: launch_one<STATS, MODE, 1>(grid, S, P, st); break;
-    case 2: launch_one<STATS, MODE, 2>(grid, S, P, st); break;
-    case 3: launch_one<STATS, MODE, 3>(grid, S, P, st); break;
-    case 4: launch_one<STATS, MODE, 4>(grid, S, P, st); break;
-    case 5: launch_one<STATS, MODE, 5>(grid, S, P, st); break;
-    case 6: launch_one<STATS, MODE, 6>(grid, S, P, st); break;
-    case 7: launch_one<STATS, MODE, 7>(grid, S, P, st); break;
-    case 8: launch_one<STATS, MODE, 8>(grid, S, P, st); break;
-    case 9: launch_one<STATS, MODE, 9>(grid, S, P, st); break;
-    case 10: launch_one<STATS, MODE, 10>(grid, S, P, st); break;
-    case 11: launch_one<STATS, MODE, 11>(grid, S, P, st); break;
-    case 12: launch_one<STATS, MODE, 12>(grid, S, P, st); break;
-    case 13: launch_one<STATS, MODE, 13>(grid, S, P, st); break;
-    case 14: launch_one<STATS, MODE, 14>(grid, S, P, st); break;
-    case 15: launch_one<STATS, MODE, 15>(grid, S, P, st); break;
-  }
-}
-
 static void launch_mode_cfg(bool stats, int mode, int cfg, dim3 grid, const DevScene &S, const FrameParams &P,
                             hipStream_t st)
 {
-  if (stats)
-  {
-    if (mode == kModeBlock) launch_cfg<true, kModeBlock>(cfg, grid, S, P, st);
-    else if (mode == kModePlain) launch_cfg<true, kModePlain>(cfg, grid, S, P, st);
-    else launch_cfg<true, kModeSsaa>(cfg, grid, S, P, st);
-  }
-  else
-  {
-    if (mode == kModeBlock) launch_cfg<false, kModeBlock>(cfg, grid, S, P, st);
-    else if (mode == kModePlain) launch_cfg<false, kModePlain>(cfg, grid, S, P, st);
-    else launch_cfg<false, kModeSsaa>(cfg, grid, S, P, st);
-  }
+  if (mode == kModeBlock) (stats ? launch_trace_block_stats : launch_trace_block_fast)(cfg, grid, S, P, st);
+  else if (mode == kModePlain) (stats ? launch_trace_plain_stats : launch_trace_plain_fast)(cfg, grid, S, P, st);
+  else (stats ? launch_trace_ssaa_stats : launch_trace_ssaa_fast)(cfg, grid, S, P, st);
 }
 
 static dim3 kat_grid(uint32_t n) { return dim3((n + kKatThreads - 1) / kKatThreads); }

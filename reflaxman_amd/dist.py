@@ -73,47 +73,57 @@ def strip_row_to_y(i: int, row_block: int, rank: int, world: int) -> int:
 
 
 class StripFrame:
-    """Rank `rank`'s part of a W x H frame rendered by `world` ranks; rank 0 ends with the ARGB8 frame.
+    """Rank `rank`'s part of a W x H frame rendered by `world` ranks; rank 0 ends with the ARGB8 frame and,
+    with gather_rgb, the float RGB frame too (the reference's std::vector<Color> image, Render.h:10, that
+    Render::imagePixel reads, Render.cpp:103-114).
 
-    pipeline (default: on for the nccl backend): the strip gather of frame i runs on its own communicator
-    (a second process group, so its RCCL stream does not serialise with the next frame's count
+    pipeline (default: on for the nccl backend): the strip gathers of frame i run on their own communicator
+    (a second process group, so their RCCL stream does not serialise with the next frame's count
     all-gather) while frame i+1 renders; strip and gather buffers are double-buffered, and rank 0
     un-interleaves on a side stream.  A frame's assembled image is complete once the device is
     synchronised (every step's work, gathers included, is on the device's streams).
     """
 
     def __init__(self, ops, W: int, H: int, row_block: int, rank: int, world: int, device: torch.device,
-                 gather_to_root: bool = True, pipeline: Optional[bool] = None):
+                 gather_to_root: bool = True, pipeline: Optional[bool] = None, gather_rgb: bool = False):
         self.ops, self.W, self.H, self.rb = ops, W, H, row_block
         self.rank, self.world, self.device = rank, world, device
         self.gather_to_root = gather_to_root
+        self.gather_rgb = bool(gather_rgb) and gather_to_root and world > 1
         self.rows = strip_rows(H, row_block, rank, world)
         self.max_rows = max(strip_rows(H, row_block, r, world) for r in range(world))
         self.bps = ops.blocks_per_slice(world)
         self.counts = torch.zeros(world * self.bps, dtype=torch.int32, device=device)
-        self.img = torch.zeros(max(self.rows, 1) * W * 3, dtype=torch.float32, device=device)
         if pipeline is None:
             pipeline = world > 1 and gather_to_root and dist.get_backend() == "nccl"
         self.pipeline = bool(pipeline) and world > 1 and gather_to_root and not self._host_staged()
         nbuf = 2 if self.pipeline else 1
+        # per-rank strip buffers (every rank the same size for the gather): ARGB8, float RGB
         self.argb_bufs = [torch.zeros(self.max_rows * W, dtype=torch.int32, device=device) for _ in range(nbuf)]
-        self.argb = self.argb_bufs[0]
-        self.fulls: List[torch.Tensor] = []
-        self.gather_lists: List[List[torch.Tensor]] = []
+        self.img_bufs = [torch.zeros(max(self.max_rows, 1) * W * 3, dtype=torch.float32, device=device)
+                         for _ in range(nbuf if self.gather_rgb else 1)]
+        self.argb, self.img = self.argb_bufs[0], self.img_bufs[0]
+        # what rank 0 gathers: (strip buffers, values per frame row, dtype)
+        self.planes = [(self.argb_bufs, W, torch.int32)]
+        if self.gather_rgb:
+            self.planes.append((self.img_bufs, 3 * W, torch.float32))
+        self.fulls: List[List[torch.Tensor]] = []         # [plane][k]: H x per_row frame on rank 0
+        self.gather_lists: List[List[List[torch.Tensor]]] = []  # [plane][k][rank]
         self.row_index: List[torch.Tensor] = []
         if gather_to_root and rank == 0:
-            self.fulls = [torch.zeros(H * W, dtype=torch.int32, device=device) for _ in range(nbuf)]
-            self.gather_lists = [[torch.empty_like(self.argb) for _ in range(world)] for _ in range(nbuf)]
+            for bufs, per_row, dt in self.planes:
+                self.fulls.append([torch.zeros(H * per_row, dtype=dt, device=device) for _ in range(nbuf)])
+                self.gather_lists.append([[torch.empty_like(bufs[0]) for _ in range(world)] for _ in range(nbuf)])
             for r in range(world):
                 n = strip_rows(H, row_block, r, world)
                 self.row_index.append(torch.tensor([strip_row_to_y(i, row_block, r, world) for i in range(n)],
                                                    dtype=torch.int64, device=device))
-        self.full: Optional[torch.Tensor] = self.fulls[0] if self.fulls else None
-        self.gather_list = self.gather_lists[0] if self.gather_lists else None
+        self.full: Optional[torch.Tensor] = self.fulls[0][0] if self.fulls else None
+        self.rgb_full: Optional[torch.Tensor] = self.fulls[1][0] if self.gather_rgb and self.fulls else None
         self.group = dist.new_group(list(range(world))) if self.pipeline else None
         cuda = device.type == "cuda"
         self.side = torch.cuda.Stream(device=device) if self.pipeline and cuda and rank == 0 else None
-        self.works = [None] * nbuf
+        self.works: List[list] = [[] for _ in range(nbuf)]
         self.done: List[Optional[torch.cuda.Event]] = [None] * nbuf
         self.frame = 0
 
@@ -133,56 +143,69 @@ class StripFrame:
             dist.all_gather(list(self.counts.split(self.bps)), mine.clone())
 
     def _gather_strips(self, k: int):
-        if not self._host_staged():
-            dist.gather(self.argb_bufs[k], self.gather_lists[k] if self.rank == 0 else None, dst=0)
-            return
-        lst = [torch.empty(self.argb.shape, dtype=self.argb.dtype) for _ in range(self.world)] if self.rank == 0 else None
-        dist.gather(self.argb_bufs[k].cpu(), lst, dst=0)
-        if self.rank == 0:
-            for d, h in zip(self.gather_lists[k], lst):
-                d.copy_(h)
+        for pi, (bufs, _, _) in enumerate(self.planes):
+            lst = self.gather_lists[pi][k] if self.rank == 0 else None
+            if not self._host_staged():
+                dist.gather(bufs[k], lst, dst=0)
+                continue
+            hl = [torch.empty(bufs[k].shape, dtype=bufs[k].dtype) for _ in range(self.world)] if self.rank == 0 else None
+            dist.gather(bufs[k].cpu(), hl, dst=0)
+            if self.rank == 0:
+                for d, h in zip(lst, hl):
+                    d.copy_(h)
 
     def _assemble(self, k: int) -> torch.Tensor:
-        fv = self.fulls[k].view(self.H, self.W)
-        for r in range(self.world):
-            n = self.row_index[r].numel()
-            if n:
-                fv.index_copy_(0, self.row_index[r], self.gather_lists[k][r][: n * self.W].view(n, self.W))
-        return fv
+        out = []
+        for pi, (_, per_row, _) in enumerate(self.planes):
+            fv = self.fulls[pi][k].view(self.H, per_row)
+            for r in range(self.world):
+                n = self.row_index[r].numel()
+                if n:
+                    fv.index_copy_(0, self.row_index[r], self.gather_lists[pi][k][r][: n * per_row].view(n, per_row))
+            out.append(fv)
+        self.full = out[0]
+        if self.gather_rgb:
+            self.rgb_full = out[1].view(self.H, self.W, 3)
+        return out[0]
 
     def step(self, d_counters: int = 0) -> Optional[torch.Tensor]:
         """Render this rank's strips of one frame; rank 0 returns the (H, W) int32 ARGB frame (with
-        pipeline: complete once the device is synchronised)."""
+        pipeline: complete once the device is synchronised; with gather_rgb also in self.rgb_full)."""
         k = self.frame % len(self.argb_bufs)
         self.frame += 1
         cuda = self.device.type == "cuda"
         if self.pipeline:
-            # buffer set k was last used two frames ago: its gather and (rank 0) un-interleave must be done
-            if self.works[k] is not None:
-                self.works[k].wait()
+            # buffer set k was last used two frames ago: its gathers and (rank 0) un-interleave must be done
+            for w in self.works[k]:
+                w.wait()
+            self.works[k] = []
             if cuda and self.done[k] is not None:
                 torch.cuda.current_stream(self.device).wait_event(self.done[k])
         argb = self.argb_bufs[k]
-        self.argb = argb
+        img = self.img_bufs[k % len(self.img_bufs)]
+        self.argb, self.img = argb, img
         self.ops.rng_count(self.rank, self.world, self.counts.data_ptr())
         if self.world > 1:
             self._all_gather_counts()
-        self.ops.render_counted(self.world, self.counts.data_ptr(), self.img.data_ptr(), argb.data_ptr(), d_counters)
+        self.ops.render_counted(self.world, self.counts.data_ptr(), img.data_ptr(), argb.data_ptr(), d_counters)
         if self.world == 1 or not self.gather_to_root:
             return argb[: self.rows * self.W].view(self.rows, self.W) if self.world == 1 else None
         if not self.pipeline:
             self._gather_strips(k)
             return self._assemble(k) if self.rank == 0 else None
-        self.works[k] = dist.gather(argb, self.gather_lists[k] if self.rank == 0 else None, dst=0, group=self.group,
-                                    async_op=True)
+        for pi, (bufs, _, _) in enumerate(self.planes):
+            self.works[k].append(dist.gather(bufs[k], self.gather_lists[pi][k] if self.rank == 0 else None, dst=0,
+                                             group=self.group, async_op=True))
         if self.rank != 0:
             return None
         if not cuda:
-            self.works[k].wait()
-            self.works[k] = None
+            for w in self.works[k]:
+                w.wait()
+            self.works[k] = []
             return self._assemble(k)
         with torch.cuda.stream(self.side):
-            self.works[k].wait()  # the side stream waits for the gather
+            for w in self.works[k]:
+                w.wait()  # the side stream waits for the gathers
             fv = self._assemble(k)
             ev = torch.cuda.Event()
             ev.record(self.side)

@@ -9,12 +9,23 @@ follows Scene.cpp:73-236 operation for operation.  The event counts come from
 the stats build of the same kernel (``trace_kernel<true>``) and are tested
 equal to the CPU restatement's (tests/test_gpu_parity.py).
 
-Correctly rounded f32 division and sqrt expand to ~10-15 VALU instructions
-on gfx950 (v_div_scale/v_rcp/v_fma.../v_div_fixup; scaled v_sqrt + two fma
-corrections), so VALU instructions per FLOP is well above 1: the FLOP-based
-roofline fraction understates how busy the VALU is.  bench.py reports both.
+Two views of the trace kernel's work (bench.py reports both):
+
+* algorithmic FLOPs (``flops``): the reference's brute-force work -- every
+  intersection test Scene::trace runs -- priced per event.  The kernel skips
+  most of those tests exactly (wave-bundle culling), and a correctly rounded
+  f32 divide or sqrt expands to ~10-15 VALU instructions, so FLOPs / time is an
+  *effective* rate: it can exceed what the VALU executes (C5) or fall far
+  below it (C1).  It is not a hardware utilisation.
+* executed VALU work (``executed_work``): the instructions the kernel really
+  issued, from a rocprofv3 --pmc record of the same workload and library build
+  -- VALU lane-operations per second against the 78.6 T lane-op/s peak, and
+  wave-instruction issue slots against 1024 SIMDs x 2.4 GHz / 2 cycles.
 """
 from __future__ import annotations
+
+import json
+import os
 
 COUNTER_NAMES = [
     "rays", "segments",
@@ -71,6 +82,10 @@ POW_EVENTS = ("l_pow", "dielectric")  # one powf each
 PEAK_FP32_VALU_TFLOPS = 157.3   # spec, packed-FMA rate
 PEAK_FP32_NOFMA_TFLOPS = 78.6   # separate v_mul/v_add (parity forbids contraction)
 PEAK_HBM_GBS = 8000.0
+# executed-work peaks: 256 CU x 4 SIMD-32 x 2.4 GHz -- one lane-op per lane per clock; a wave64 VALU
+# instruction issues over 2 clocks (MI355X_MICROARCH.md, Wave scheduling)
+PEAK_VALU_LANE_OPS = 256 * 4 * 32 * 2.4e9
+PEAK_VALU_WAVE_INSTS = 256 * 4 * 2.4e9 / 2
 
 # algorithmic HBM bytes per pixel: f32 RGB framebuffer (12) + ARGB8 (4) written once
 ALGO_BYTES_PER_PIXEL = 16
@@ -96,3 +111,35 @@ def summary(counts) -> dict:
         "shadow_tests_per_ray": (counts["sh_sph_tests"] + counts["sh_tri_tests"] + counts.get("sh_pln_tests", 0)) / rays,
         "pow_calls": sum(counts[k] for k in POW_EVENTS),
     }
+
+
+def pmc_record(directory: str, config, lib_sha: str):
+    """The rocprofv3 --pmc record (tools/pmc_summary.py --out) of this workload and library build, or None."""
+    if not os.path.isdir(directory):
+        return None
+    for name in sorted(os.listdir(directory)):
+        if not name.endswith(".json"):
+            continue
+        rec = json.load(open(os.path.join(directory, name)))
+        if rec.get("config") == list(config) and rec.get("lib_sha256") == lib_sha:
+            return rec
+    return None
+
+
+def executed_work(rec, trace_ms: float):
+    """Executed VALU work of one trace launch from a PMC record, rated at this run's kernel time."""
+    if not rec:
+        return None
+    c = rec["counters"]
+    insts = c["SQ_INSTS_VALU"]
+    util = c["SQ_THREAD_CYCLES_VALU"] / (64.0 * c["SQ_ACTIVE_INST_VALU"]) if c.get("SQ_ACTIVE_INST_VALU") else None
+    lane_ops = insts * 64.0 * util if util else None
+    t = trace_ms * 1e-3
+    out = {"valu_wave_insts_per_launch": int(insts), "valu_lane_util": round(util, 4) if util else None,
+           "valu_issue_frac": round(insts / t / PEAK_VALU_WAVE_INSTS, 4)}
+    if lane_ops:
+        out.update({"valu_lane_ops_per_launch": int(lane_ops), "achieved_T_lane_ops": round(lane_ops / t / 1e12, 2),
+                    "peak_T_lane_ops": round(PEAK_VALU_LANE_OPS / 1e12, 1),
+                    "frac_lane_ops": round(lane_ops / t / PEAK_VALU_LANE_OPS, 4)})
+    out["source"] = rec.get("source", "rocprofv3 --pmc")
+    return out

@@ -40,18 +40,26 @@ class FakeOps:
         self.seen_counts = cnt
         rows = rdist.strip_rows(self.H, self.rb, self.rank, self.world)
         argb = np.ctypeslib.as_array((ctypes.c_int32 * (rows * self.W)).from_address(d_argb)) if rows else None
+        rgb = np.ctypeslib.as_array((ctypes.c_float * (rows * self.W * 3)).from_address(d_img)) if rows else None
         for i in range(rows):
             y = rdist.strip_row_to_y(i, self.rb, self.rank, self.world)
             argb[i * self.W:(i + 1) * self.W] = (self.frame << 24) | (y << 12) | np.arange(self.W)
+            rgb[i * self.W * 3:(i + 1) * self.W * 3] = rgb_pattern(self.frame, y, self.W)
         self.frame += 1
 
 
-def _worker(rank, world, port, W, H, rb, pipeline, q):
+def rgb_pattern(frame, y, W):
+    import numpy as np
+    return (frame * 100000 + y * 100 + np.arange(3 * W) % 3 + 10 * (np.arange(3 * W) // 3)).astype(np.float32)
+
+
+def _worker(rank, world, port, W, H, rb, pipeline, q, gather_rgb=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         ops = FakeOps(W, H, rb, rank, world)
-        sf = rdist.StripFrame(ops, W, H, rb, rank, world, torch.device("cpu"), pipeline=pipeline)
+        sf = rdist.StripFrame(ops, W, H, rb, rank, world, torch.device("cpu"), pipeline=pipeline,
+                              gather_rgb=gather_rgb)
         assert sf.pipeline == pipeline
         expect = [s * 1000 + b for s in range(world) for b in range(ops.bps)]
         ok_counts = ok_frame = True
@@ -61,6 +69,10 @@ def _worker(rank, world, port, W, H, rb, pipeline, q):
             if rank == 0:
                 ys, xs = torch.meshgrid(torch.arange(H), torch.arange(W), indexing="ij")
                 ok_frame &= bool(torch.equal(out, ((frame << 24) | (ys << 12) | xs).to(torch.int32)))
+                if gather_rgb:
+                    import numpy as np
+                    want = np.stack([rgb_pattern(frame, y, W) for y in range(H)]).reshape(H, W, 3)
+                    ok_frame &= bool(np.array_equal(sf.rgb_full.numpy(), want))
             else:
                 ok_frame &= out is None
         q.put((rank, ok_counts, ok_frame))
@@ -76,13 +88,13 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("pipeline", [False, True])
+@pytest.mark.parametrize("pipeline,gather_rgb", [(False, False), (True, False), (False, True), (True, True)])
 @pytest.mark.parametrize("W,H,rb", [(16, 37, 4), (8, 64, 8), (5, 3, 8)])
-def test_strip_frame_world2_gloo(W, H, rb, pipeline):
+def test_strip_frame_world2_gloo(W, H, rb, pipeline, gather_rgb):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, W, H, rb, pipeline, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, W, H, rb, pipeline, q, gather_rgb)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:

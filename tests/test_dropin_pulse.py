@@ -1,0 +1,49 @@
+"""The drop-in boundary against the reference's only real caller, src/common/Pulse.cpp (unmodified).
+
+include/reflaxman/dropin/{Render,Scene}.h replace the reference's Render.h / Scene.h; the caller keeps its
+own value types, asset IO and camera motion (Camera::proceedControl / inMotion, Pulse.cpp:96,108) and links
+librfx.so instead of the renderer's .cpp files (tools/pulse_build.py).  A headless platform
+(tests/native/pulse_headless.cpp) drives Pulse's screenshot flow: F2, 800x600, SSAA 2x2, depth 20.
+
+* CPU (build container, needs /root/reference): Pulse.cpp and the caller's sources compile and link against
+  the drop-in headers -- the compile-only proof a maintainer needs.
+* GPU: the drop-in Pulse binary (built in-tree by __graft_entry__.build()) writes a screenshot whose BMP file
+  equals, byte for byte, the one the reference's own Pulse + CPU renderer wrote (tests/golden/manifest.json
+  pulse_screenshot_800x600_ss2, tools/gen_golden.py).
+"""
+import hashlib
+import os
+import subprocess
+import sys
+
+import pytest
+
+from helpers import manifest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DROPIN = os.path.join(ROOT, "tests", "native", "_build", "pulse_dropin")
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/src/common"), reason="needs the reference sources")
+def test_pulse_compiles_against_dropin_headers(tmp_path):
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import pulse_build
+    exe = pulse_build.build("dropin", str(tmp_path / "pulse_dropin"))
+    assert os.path.getsize(exe) > 0
+
+
+@pytest.mark.gpu
+def test_pulse_screenshot_matches_reference(tmp_path):
+    c = manifest()["cases"]["pulse_screenshot_800x600_ss2"]
+    if not os.path.exists(DROPIN):
+        pytest.fail("tests/native/_build/pulse_dropin missing: run __graft_entry__.build() where /root/reference exists")
+    env = {**os.environ, "RFX_SPHERE_SEED": str(c["RFX_SPHERE_SEED"]), "RFX_JITTER_SEED": str(c["RFX_JITTER_SEED"])}
+    out = str(tmp_path) + "/"
+    r = subprocess.run([DROPIN, out, str(c["res_key"]), str(c["ss_key"])], capture_output=True, text=True, env=env,
+                       timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    path = r.stdout.strip()
+    assert os.path.basename(path) == c["file"]
+    data = open(path, "rb").read()
+    assert len(data) == c["bytes"]
+    assert hashlib.sha256(data).hexdigest() == c["sha_bmp"]

@@ -71,6 +71,8 @@ def build_scene_with(L, desc):
         mt, rgb, refl, tr = ob[-1]
         if ob[0] == "sphere":
             L.rfx_scene_add_sphere(s, fa(ob[1]), ob[2], mt, fa(rgb), refl, tr)
+        elif ob[0] == "plane":
+            L.rfx_scene_add_plane(s, fa(ob[1]), fa(ob[2]), mt, fa(rgb), refl, tr)
         else:
             L.rfx_scene_add_triangle(s, fa(ob[1]), fa(ob[2]), fa(ob[3]), mt, fa(rgb), refl, tr)
     for (oi, ti, uv) in desc.settex:
@@ -82,16 +84,17 @@ def build_scene_with(L, desc):
 
 
 class Runner:
-    def __init__(self, name, path, desc, W, H, depth, seed):
+    def __init__(self, name, path, desc, W, H, depth, seed, tile_order=None):
         self.name = name
         L = self.L = _lib.bind(path)
         self.scene, eye, view, fov = build_scene_with(L, desc)
         self.r = C.c_void_p()
-        _lib.check(L.rfx_renderer_create(C.byref(self.r), 0)) if False else None
         rc = L.rfx_renderer_create(C.byref(self.r), 0)
         assert rc == 0, L.rfx_last_error()
         assert L.rfx_renderer_set_scene(self.r, self.scene) == 0, L.rfx_last_error()
         assert L.rfx_renderer_set_rng(self.r, seed, 0) == 0
+        if tile_order is not None:
+            assert L.rfx_renderer_set_tile_order(self.r, tile_order) == 0
         self.W, self.H = W, H
         self.img, self.argb = C.c_void_p(), C.c_void_p()
         assert L.rfx_device_alloc(self.r, W * H * 12, C.byref(self.img)) == 0
@@ -108,8 +111,15 @@ class Runner:
             rc = self.L.rfx_render_frame(self.r, C.byref(self.frame), self.img, self.argb, None, None)
             assert rc == 0, self.L.rfx_last_error()
 
-    def first_frame_hashes(self):
-        self.render(1)
+    def close(self):
+        self.L.rfx_device_free(self.r, self.img)
+        self.L.rfx_device_free(self.r, self.argb)
+        self.L.rfx_renderer_destroy(self.r)
+        self.L.rfx_scene_destroy(self.scene)
+
+    def frame_hashes(self, n=1):
+        """Render n frames (continuing the random stream); hashes of the last one."""
+        self.render(n)
         assert self.L.rfx_synchronize(self.r) == 0
         rgb = np.empty(self.W * self.H * 3, np.float32)
         argb = np.empty(self.W * self.H, np.uint32)
@@ -146,10 +156,19 @@ def cmd_run(args):
         keep = set(args.only.split(","))
         paths, names = zip(*[(p, n) for p, n in zip(paths, names) if n in keep])
     runners = [Runner(n, p, desc, args.width, args.height, args.depth, 1350490027) for n, p in zip(names, paths)]
+    # parity of every variant: frame 1 against the reference's full-frame hash (when the manifest has one), and
+    # frame 1 + LATER frames (rendered in the learned longest-tile-first order, after the tile sorts) against
+    # the product build rendering the same frames in raster order
+    later = max(2, args.later_frame)
+    ref = Runner("raster", _build.LIB, desc, args.width, args.height, args.depth, 1350490027, tile_order=0)
+    ref_first = ref.frame_hashes(1)
+    ref_later = ref.frame_hashes(later - 1)
+    ref.close()
     parity = {}
     for r in runners:
-        hf, ha = r.first_frame_hashes()
-        parity[r.name] = (key in man and hf == man[key]["sha_f32"] and ha == man[key]["sha_argb"]) if key in man else None
+        first = r.frame_hashes(1)
+        ok = first == ref_first and (key not in man or first == (man[key]["sha_f32"], man[key]["sha_argb"]))
+        parity[r.name] = ok and r.frame_hashes(later - 1) == ref_later
         r.render(args.warmup)
     times = {r.name: [] for r in runners}
     pre = {r.name: [] for r in runners}
@@ -163,6 +182,10 @@ def cmd_run(args):
     base = statistics.median(times[runners[0].name])
     out = []
     for r in runners:
+        if not parity[r.name]:  # a variant that renders other pixels has no timing worth reporting
+            out.append({"variant": r.name, "defines": VARIANTS.get(r.name), "parity_sha_ok": False,
+                        "timings": None})
+            continue
         med = statistics.median(times[r.name])
         out.append({"variant": r.name, "defines": VARIANTS.get(r.name), "parity_sha_ok": parity[r.name],
                     "trace_ms_median": round(med, 4), "trace_ms_min": round(min(times[r.name]), 4),
@@ -186,6 +209,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=12)
     ap.add_argument("--frames", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--later-frame", type=int, default=7, help="frame (1-based) also checked against raster order")
     args = ap.parse_args()
     if args.cmd == "build":
         cmd_build(args.variants.split(","))

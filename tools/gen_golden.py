@@ -326,6 +326,23 @@ def main():
                                       names=sorted(loads))
             print("file fixtures", flush=True)
 
+        # the reference's own application controller (Pulse.cpp, unmodified, headless platform) taking a
+        # screenshot through its menus: 800x600 (key 1), SSAA 2x2 (key 2), depth 20 -- the BMP file's SHA-256
+        if want("pulse"):
+            sys.path.insert(0, os.path.join(ROOT, "tools"))
+            import pulse_build
+            exe = pulse_build.build("reference", os.path.join(tmp, "pulse_ref"))
+            shot = os.path.join(tmp, "shot") + "/"
+            os.makedirs(shot)
+            seeds = {"RFX_SPHERE_SEED": DEFAULT_SEED, "RFX_JITTER_SEED": 424238335}
+            r = subprocess.run([exe, shot, "1", "2"], check=True, capture_output=True, text=True,
+                               env={**os.environ, **{k: str(v) for k, v in seeds.items()}})
+            data = open(r.stdout.strip(), "rb").read()
+            cases["pulse_screenshot_800x600_ss2"] = dict(kind="pulse", res_key=1, ss_key=2, W=800, H=600, ss=2,
+                                                         depth=20, bytes=len(data), sha_bmp=sha(data),
+                                                         file=os.path.basename(r.stdout.strip()), **seeds)
+            print("pulse screenshot", flush=True)
+
         # stress bands (4K width) with stream advance
         for y0 in (0, 1080):
             key = f"band_stress4096_3840x2160_d12_y{y0}_r4"

@@ -20,9 +20,17 @@ REGIONS = ["sphere_loop", "triangle_loop", "winner", "light_loop", "shadow_anyhi
 
 
 def main():
-    path = os.path.join(_build.LIBDIR, "diag", sys.argv[2] if len(sys.argv) > 2 else "librfx_prof.so")
-    scene = sys.argv[1] if len(sys.argv) > 1 else "synth16"
-    r = ab.Runner("prof", path, scenes.get_scene(scene), 3840, 2160, 8, 1350490027)
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scene", default="synth16")
+    ap.add_argument("--width", type=int, default=3840)
+    ap.add_argument("--height", type=int, default=2160)
+    ap.add_argument("--depth", type=int, default=8)
+    ap.add_argument("--lib", default="librfx_prof.so")
+    a = ap.parse_args()
+    path = os.path.join(_build.LIBDIR, "diag", a.lib)
+    scene = a.scene
+    r = ab.Runner("prof", path, scenes.get_scene(scene), a.width, a.height, a.depth, 1350490027)
     r.render(2)
     assert r.L.rfx_synchronize(r.r) == 0
     buf = (C.c_ulonglong * 16)()
@@ -31,15 +39,20 @@ def main():
     assert r.L.rfx_synchronize(r.r) == 0
     assert r.L.rfx_debug_prof_read(buf, 1) == 16
     tot = buf[7]
-    cb = (C.c_ulonglong * 16)()
+    cb = (C.c_ulonglong * 32)()
     cull = {}
-    if hasattr(r.L, "rfx_debug_cull_read") and r.L.rfx_debug_cull_read(cb, 1) == 16:
+    if hasattr(r.L, "rfx_debug_cull_read") and r.L.rfx_debug_cull_read(cb, 1) == 32:
         for k, name in ((0, "closest"), (1, "shadow")):
             v = cb[8 * k: 8 * k + 7]
             n = max(v[0], 1)
             cull[name] = {"bundles": v[0], "usable": round(v[1] / n, 3), "live_lanes": round(v[2] / n, 1),
                           "kept_pairs": round(v[3] / n, 2), "valid_pairs": round(v[5] / n, 2),
                           "kept_tris": round(v[4] / n, 2), "valid_tris": round(v[6] / n, 2)}
+        v = cb[16:22]
+        n = max(v[0], 1)
+        cull["closest_large"] = {"bundles": v[0], "usable": round(v[1] / n, 3), "live_lanes": round(v[2] / n, 1),
+                                 "kept_chunks": round(v[3] / n, 2), "kept_spheres": round(v[4] / n, 1),
+                                 "pair_tests": round(v[5] / n, 1)}
     print(json.dumps({"scene": scene, "lib": os.path.basename(path), "cycles": {k: int(v) for k, v in zip(REGIONS, buf[:8])},
                       "wave_executions": {k: int(v) for k, v in zip(REGIONS, buf[8:])},
                       "share_of_trace": {k: round(v / tot, 4) for k, v in zip(REGIONS, buf[:8])},

@@ -23,7 +23,8 @@ def main():
     if not os.path.exists(path):
         path = _build.build_variant("segs", ["RFX_DEBUG_SEGS"])
     W, H = 3840, 2160
-    r = ab.Runner("segs", path, scenes.get_scene(sys.argv[1] if len(sys.argv) > 1 else "synth16"), W, H, 8,
+    depth = int(sys.argv[2]) if len(sys.argv) > 2 else 8
+    r = ab.Runner("segs", path, scenes.get_scene(sys.argv[1] if len(sys.argv) > 1 else "synth16"), W, H, depth,
                   1350490027)
     r.render(1)
     assert r.L.rfx_synchronize(r.r) == 0
