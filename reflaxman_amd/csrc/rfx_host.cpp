@@ -610,6 +610,54 @@ static int upload(rfx_renderer *r, const std::vector<T> &v, const T **dst)
   return RFX_OK;
 }
 
+// Pair BVH of a large scene: leaves are the device sphere pairs (2j, 2j + 1, Morton-adjacent); internal nodes
+// split their pairs at the median of the pair centres along the longest axis.  Each node stores its two
+// children's boxes (spheres grown by their radii); the kernel widens them by its exact-cull margin per ray.
+// Returns the node index (or ~pair for a leaf) of range [a, b) of `pairs`; depth: internal levels below.
+namespace {
+struct PairBox { double lo[3], hi[3], c[3]; };
+
+int build_pair_bvh(std::vector<BvhNode> &nodes, std::vector<uint32_t> &pairs, size_t a, size_t b,
+                   const std::vector<PairBox> &box, int level, int &depth)
+{
+  if (b - a == 1) return ~(int)pairs[a];
+  depth = std::max(depth, level + 1);
+  const int id = (int)nodes.size();
+  nodes.push_back(BvhNode{});
+  double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (size_t i = a; i < b; ++i)
+    for (int k = 0; k < 3; ++k) { lo[k] = fmin(lo[k], box[pairs[i]].c[k]); hi[k] = fmax(hi[k], box[pairs[i]].c[k]); }
+  int axis = 0;
+  for (int k = 1; k < 3; ++k)
+    if (hi[k] - lo[k] > hi[axis] - lo[axis]) axis = k;
+  const size_t mid = a + (b - a) / 2;
+  std::nth_element(pairs.begin() + a, pairs.begin() + mid, pairs.begin() + b, [&](uint32_t x, uint32_t y) {
+    return box[x].c[axis] < box[y].c[axis] || (box[x].c[axis] == box[y].c[axis] && x < y);
+  });
+  const int kids[2] = {build_pair_bvh(nodes, pairs, a, mid, box, level + 1, depth),
+                       build_pair_bvh(nodes, pairs, mid, b, box, level + 1, depth)};
+  const size_t range[2][2] = {{a, mid}, {mid, b}};
+  BvhNode &n = nodes[id];
+  for (int c = 0; c < 2; ++c)
+  {
+    double l[3] = {INFINITY, INFINITY, INFINITY}, h[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (size_t i = range[c][0]; i < range[c][1]; ++i)
+      for (int k = 0; k < 3; ++k) { l[k] = fmin(l[k], box[pairs[i]].lo[k]); h[k] = fmax(h[k], box[pairs[i]].hi[k]); }
+    // round outwards to float
+    n.lx[c] = nextafterf((float)l[0], -INFINITY); n.ly[c] = nextafterf((float)l[1], -INFINITY);
+    n.lz[c] = nextafterf((float)l[2], -INFINITY);
+    n.hx[c] = nextafterf((float)h[0], INFINITY); n.hy[c] = nextafterf((float)h[1], INFINITY);
+    n.hz[c] = nextafterf((float)h[2], INFINITY);
+    n.child[c] = kids[c];
+  }
+  return id;
+}
+}  // namespace
+
+#ifndef RFX_BVH_STACK
+#define RFX_BVH_STACK 16  // the kernel's per-lane traversal stack (rfx_trace.h kBvhStack)
+#endif
+
 extern "C" int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *s)
 {
   if (!r || !s) return fail(RFX_ERR_ARG, "set_scene: bad args");
@@ -649,9 +697,18 @@ extern "C" int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *s)
       const HostSphere &sp = s->spheres[i];
       const double c[3] = {sp.center.x, sp.center.y, sp.center.z};
       uint32_t q[3];
+      // one cell size for all three axes (the largest extent): cubic cells keep a chunk compact even when
+      // the centres span a thin slab (C5: y over 0.5 units, x over 24) -- per-axis scaling would interleave
+      // the thin axis' bits as if it were as long as the others and cut chunks into wide slivers
+      double cube = 0.0;
+      for (int a = 0; a < 3; ++a) cube = fmax(cube, hi[a] - lo[a]);
       for (int a = 0; a < 3; ++a)
       {
+#ifdef RFX_MORTON_AXIS
         const double ext = hi[a] - lo[a];
+#else
+        const double ext = cube;
+#endif
         const double f = ext > 0.0 && std::isfinite(ext) ? (c[a] - lo[a]) / ext : 0.0;
         q[a] = (uint32_t)fmin(fmax(f * 1023.0, 0.0), 1023.0);
       }
@@ -773,6 +830,31 @@ extern "C" int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *s)
       cull_valid |= 1ull << (32 + i);
     }
   }
+  // pair BVH (large scenes; spheres of a pair whose second slot is padding: r2 = -inf, never hit)
+  std::vector<BvhNode> bvh;
+  int bvh_depth = 0;
+#ifndef RFX_NO_BVH
+  if (nsph > 32)
+  {
+    const size_t npairs = (nsph + 1) / 2;
+    std::vector<PairBox> box(npairs);
+    for (size_t j = 0; j < npairs; ++j)
+    {
+      PairBox &b = box[j];
+      for (int k = 0; k < 3; ++k) { b.lo[k] = INFINITY; b.hi[k] = -INFINITY; }
+      for (size_t q = 2 * j; q < std::min(nsph, 2 * j + 2); ++q)
+      {
+        const double c[3] = {bd[q].x, bd[q].y, bd[q].z}, rr = bd[q].r;
+        for (int k = 0; k < 3; ++k) { b.lo[k] = fmin(b.lo[k], c[k] - rr); b.hi[k] = fmax(b.hi[k], c[k] + rr); }
+      }
+      for (int k = 0; k < 3; ++k) b.c[k] = 0.5 * (b.lo[k] + b.hi[k]);
+    }
+    std::vector<uint32_t> pairs(npairs);
+    for (size_t j = 0; j < npairs; ++j) pairs[j] = (uint32_t)j;
+    build_pair_bvh(bvh, pairs, 0, npairs, box, 0, bvh_depth);
+    if (bvh_depth > RFX_BVH_STACK) { bvh.clear(); bvh_depth = 0; }  // deeper than the kernel's stack: chunk loops
+  }
+#endif
   std::vector<PlaneGeo> pg;
   std::vector<MatRec> pm;
   for (const HostPlane &p : s->planes)
@@ -807,7 +889,8 @@ extern "C" int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *s)
       (rc = upload(r, tg, &d.tri_geo)) || (rc = upload(r, ts, &d.tri_shade)) || (rc = upload(r, tm, &d.tri_mat)) ||
       (rc = upload(r, lr, &d.lights)) || (rc = upload(r, tr, &d.texs)) || (rc = upload(r, pool, &d.texels)) ||
       (rc = upload(r, bd, &d.bound)) || (rc = upload(r, cs, &d.cull_small)) || (rc = upload(r, cb, &d.chunk_bound)) ||
-      (rc = upload(r, pg, &d.pln_geo)) || (rc = upload(r, pm, &d.pln_mat)) || (rc = upload(r, loc, &d.obj_loc)))
+      (rc = upload(r, pg, &d.pln_geo)) || (rc = upload(r, pm, &d.pln_mat)) || (rc = upload(r, loc, &d.obj_loc)) ||
+      (rc = upload(r, bvh, &d.bvh)))
     return rc;
   d.n_sph = (int32_t)sg.size();
   d.n_tri = (int32_t)tg.size();
@@ -815,6 +898,7 @@ extern "C" int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *s)
   d.n_chunk = (int32_t)cb.size();
   d.n_pln = (int32_t)pg.size();
   d.n_tex = (int32_t)tr.size();
+  d.bvh_depth = bvh_depth;
   d.n_obj = (int32_t)loc.size();
   d.cull_valid = cull_valid;
   d.skybox_tex = s->skybox;

@@ -190,6 +190,24 @@ __device__ __forceinline__ void stage_small_scene(const DevScene &S)
   if (t < 64) s_cull[t] = S.cull_small[t];
 }
 
+// 7 waves per SIMD (<= 72 VGPRs, a few spills): the kernel is VALU-issue bound; more waves hide the
+// scene-load and texel latencies better than spills cost (tools/ab.py, C3 trace kernel: 6 -> 7 -2.6%;
+// 8 waves / 64 VGPRs spill enough to lose 4-7%)
+#ifndef RFX_WAVES_PER_EU
+#define RFX_WAVES_PER_EU 7
+#endif
+// waves per workgroup (1, 2 or 4): a wave is an 8x8 pixel tile, a workgroup 8x8 / 16x8 / 16x16 pixels.
+// Two: a workgroup's slots free when its slower wave ends, and the per-workgroup LDS staging stays cheap
+// (tools/ab.py, C3 trace kernel: 4 -> 2 waves -2.5%, 1 wave +3.6%)
+#ifndef RFX_WG_WAVES
+#define RFX_WG_WAVES 2
+#endif
+constexpr uint32_t kWgWaves = RFX_WG_WAVES, kWgThreads = 64 * kWgWaves;
+constexpr uint32_t kTileWavesX = kWgWaves >= 2 ? 2 : 1, kTileWavesY = kWgWaves / kTileWavesX;
+constexpr uint32_t kTileW = 8 * kTileWavesX, kTileH = 8 * kTileWavesY;
+static_assert(kWgWaves == 1 || kWgWaves == 2 || kWgWaves == 4, "RFX_WG_WAVES: 1, 2 or 4");
+#define RFX_TRACE_BOUNDS __launch_bounds__(kWgThreads) __attribute__((amdgpu_waves_per_eu(RFX_WAVES_PER_EU)))
+
 // ------------------------------------------------------------- sampling
 template <bool STATS>
 __device__ __forceinline__ col texel_uv(const DevScene &S, int tex, float u, float v, const float *lut, Cnt &cnt)
@@ -549,6 +567,143 @@ __device__ __forceinline__ bool tri_takes(float sq, float best_sq, int obj, int 
                       : (obj < best_obj && sqrt_rn(sq) == sqrt_rn(best_sq));
 }
 
+// ------------------------------------------------------------- large scenes: per-ray pair BVH
+// Each lane walks the pair BVH (rfx_types.h BvhNode) with its own ray: both children's boxes are tested per
+// step, the nearer one is entered first and the farther one pushed on a per-lane stack in LDS.  The boxes are
+// widened per ray by the exact-cull margin of the wave bundles (a sphere the reference's float test reports as
+// hit lies within r + 8.1e-4 |o - c| of the ray; kCullRel = 4e-3 covers it five times, with |o - c| bounded
+// by the L1 distance to the box centre plus its L1 half-size), so a box the ray misses holds no sphere the
+// reference could report: skipping it changes no result.  Closest hit: a child whose entry distance exceeds
+// the best hit so far (with 0.1% slack over rounding; sphere distances computed by the reference are at least
+// the entry distance into their widened box) cannot win or tie and is skipped too.  Leaves run the exact
+// pair test with the (distance, object index) rule, so the visiting order changes no result.
+constexpr int kBvhStack = 16;  // rfx_host.cpp RFX_BVH_STACK: deeper hierarchies fall back to the chunk loops
+__shared__ int32_t s_bvh_stack[kBvhStack * kWgThreads];
+
+struct RayInv { float ix, iy, iz; };
+__device__ __forceinline__ RayInv ray_inv(v3 ray)
+{
+  return RayInv{__builtin_amdgcn_rcpf(ray.x), __builtin_amdgcn_rcpf(ray.y), __builtin_amdgcn_rcpf(ray.z)};
+}
+
+// child c of node n against the ray: hit (conservative), and the entry parameter t (>= 0) of the widened box.
+// Every decision is a comparison that a NaN fails in the keeping direction.
+__device__ __forceinline__ bool bvh_box(const BvhNode &n, int c, v3 o, const RayInv &ri, float &tn)
+{
+  const float lx = n.lx[c], ly = n.ly[c], lz = n.lz[c], hx = n.hx[c], hy = n.hy[c], hz = n.hz[c];
+  const float cx = 0.5f * (lx + hx), cy = 0.5f * (ly + hy), cz = 0.5f * (lz + hz);
+  const float m = kCullRel * (fabsf(o.x - cx) + fabsf(o.y - cy) + fabsf(o.z - cz) +
+                              0.5f * ((hx - lx) + (hy - ly) + (hz - lz))) + 1e-6f;
+  const float ax = (lx - m - o.x) * ri.ix, bx = (hx + m - o.x) * ri.ix;
+  const float ay = (ly - m - o.y) * ri.iy, by = (hy + m - o.y) * ri.iy;
+  const float az = (lz - m - o.z) * ri.iz, bz = (hz + m - o.z) * ri.iz;
+  // fminf / fmaxf return the other operand for a NaN (0 * inf on an axis-parallel ray): that axis is ignored
+  const float t0 = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), 0.0f));
+  const float t1 = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+  tn = t0;
+  return !(t0 > t1 * 1.00001f + 1e-30f);
+}
+
+// closest sphere hit of one lane's ray over the BVH (Scene.cpp:86-106 restricted to the spheres)
+template <bool STATS>
+__device__ __forceinline__ void closest_spheres_bvh(const DevScene &S, v3 origin, v3 ray, const RayConst &k, Hit &h,
+                                                    Cnt &cnt)
+{
+  const RayInv ri = ray_inv(ray);
+  const float a = 0.5f * k.a2;                // |ray|^2 (exact: a2 = 2a)
+  int32_t *stack = s_bvh_stack + threadIdx.x;
+  int sp = 0, node = 0;
+  for (;;)
+  {
+    if (node >= 0)
+    {
+      const BvhNode n = S.bvh[node];
+      float t0, t1;
+      // a child entered beyond the best hit cannot hold a closer (or tying) sphere
+      const bool h0 = bvh_box(n, 0, origin, ri, t0) && !(t0 * t0 * a > h.sq * 1.001f);
+      const bool h1 = bvh_box(n, 1, origin, ri, t1) && !(t1 * t1 * a > h.sq * 1.001f);
+      if (h0 && h1)
+      {
+        const bool first0 = !(t1 < t0);
+        stack[kWgThreads * sp++] = first0 ? n.child[1] : n.child[0];
+        node = first0 ? n.child[0] : n.child[1];
+        continue;
+      }
+      if (h0 || h1)
+      {
+        node = h0 ? n.child[0] : n.child[1];
+        continue;
+      }
+    }
+    else
+    {
+      const int j = ~node;
+      f2 b, d;
+      pair_bd(S.sph_pair[j], origin, k, b, d);
+      if (pair_may_hit(b, d))
+      {
+        float t, sq;
+        if (sphere_tail<STATS, false>(b.x, d.x, ray, k, t, sq, cnt))
+        {
+          const int obj = S.sph_info[4 * j];
+          if (tri_takes(sq, h.sq, obj, h.obj)) { h.sq = sq; h.obj = obj; h.i = 2 * j; h.t = t; }
+        }
+        if (sphere_tail<STATS, false>(b.y, d.y, ray, k, t, sq, cnt))
+        {
+          const int obj = S.sph_info[4 * j + 2];
+          if (tri_takes(sq, h.sq, obj, h.obj)) { h.sq = sq; h.obj = obj; h.i = 2 * j + 1; h.t = t; }
+        }
+      }
+    }
+    if (sp == 0) break;
+    node = stack[kWgThreads * --sp];
+  }
+}
+
+// any sphere but skip_sph occludes the shadow ray (Scene.cpp:129-141 restricted to the spheres)
+template <bool STATS>
+__device__ __forceinline__ bool occluded_spheres_bvh(const DevScene &S, v3 o, v3 ray, const RayConst &k, int skip_sph,
+                                                     Cnt &cnt)
+{
+  const RayInv ri = ray_inv(ray);
+  int32_t *stack = s_bvh_stack + threadIdx.x;
+  int sp = 0, node = 0;
+  float t, sq;
+  for (;;)
+  {
+    if (node >= 0)
+    {
+      const BvhNode n = S.bvh[node];
+      float t0, t1;
+      const bool h0 = bvh_box(n, 0, o, ri, t0), h1 = bvh_box(n, 1, o, ri, t1);
+      if (h0 && h1)
+      {
+        stack[kWgThreads * sp++] = n.child[1];
+        node = n.child[0];
+        continue;
+      }
+      if (h0 || h1)
+      {
+        node = h0 ? n.child[0] : n.child[1];
+        continue;
+      }
+    }
+    else
+    {
+      const int j = ~node;
+      f2 b, d;
+      pair_bd(S.sph_pair[j], o, k, b, d);
+      // the hit object is filtered out after its test, which does not change the boolean
+      if (pair_may_hit(b, d) &&
+          ((sphere_tail<STATS, true>(b.x, d.x, ray, k, t, sq, cnt) && 2 * j != skip_sph) ||
+           (sphere_tail<STATS, true>(b.y, d.y, ray, k, t, sq, cnt) && 2 * j + 1 != skip_sph)))
+        return true;
+    }
+    if (sp == 0) return false;
+    node = stack[kWgThreads * --sp];
+  }
+}
+
 // The planes (Scene::addPlane extension, Plane.cpp:36-73) for one lane, after the other kinds: every lane that
 // traces tests every plane (an infinite plane has no bounding sphere to cull with).
 template <bool STATS>
@@ -598,7 +753,9 @@ __device__ __forceinline__ void closest_hit(const DevScene &S, v3 origin, v3 ray
   uint32_t st_chunks = 0, st_sph = 0, st_pairs = 0;
 #endif
   RFX_PROF_BEGIN(P_SPH);
-  for (int cfirst = 0; cfirst < S.n_chunk; cfirst += 64)
+  const bool use_bvh = !STATS && S.bvh != nullptr;
+  if (use_bvh && live) closest_spheres_bvh<STATS>(S, origin, ray, k, h, cnt);
+  for (int cfirst = 0; !use_bvh && cfirst < S.n_chunk; cfirst += 64)
   {
     uint64_t cm = cull ? cull_chunk(S.chunk_bound, cfirst, min(64, S.n_chunk - cfirst), *B)
                        : all_bits(min(64, S.n_chunk - cfirst));
@@ -799,7 +956,9 @@ __device__ __forceinline__ bool occluded(const DevScene &S, v3 o, v3 ray, bool l
   const bool cull = B && B->ok;
   bool occ = false;
   float t, sq, u, v;
-  for (int cfirst = 0; cfirst < S.n_chunk; cfirst += 64)
+  const bool use_bvh = !STATS && S.bvh != nullptr;
+  if (use_bvh && live) occ = occluded_spheres_bvh<STATS>(S, o, ray, k, skip_sph, cnt);
+  for (int cfirst = 0; !use_bvh && cfirst < S.n_chunk; cfirst += 64)
   {
     if (__ballot(live && !occ) == 0) return occ;
     uint64_t cm = cull ? cull_chunk(S.chunk_bound, cfirst, min(64, S.n_chunk - cfirst), *B)
@@ -862,6 +1021,7 @@ __device__ __forceinline__ bool occluded(const DevScene &S, v3 o, v3 ray, bool l
     if (live && !occ) occ = occluded_planes<STATS>(S, o, ray, k, skip_pln, cnt);
   return occ;
 }
+
 
 // ------------------------------------------------------------- Scene::trace
 // Scene::trace (Scene.cpp:73-236) for one trace per lane, the bounce loop run wave-wide: every
@@ -1149,23 +1309,6 @@ __device__ __forceinline__ uint32_t clock32()
   return (uint32_t)c;
 }
 
-// 7 waves per SIMD (<= 72 VGPRs, a few spills): the kernel is VALU-issue bound; more waves hide the
-// scene-load and texel latencies better than spills cost (tools/ab.py, C3 trace kernel: 6 -> 7 -2.6%;
-// 8 waves / 64 VGPRs spill enough to lose 4-7%)
-#ifndef RFX_WAVES_PER_EU
-#define RFX_WAVES_PER_EU 7
-#endif
-// waves per workgroup (1, 2 or 4): a wave is an 8x8 pixel tile, a workgroup 8x8 / 16x8 / 16x16 pixels.
-// Two: a workgroup's slots free when its slower wave ends, and the per-workgroup LDS staging stays cheap
-// (tools/ab.py, C3 trace kernel: 4 -> 2 waves -2.5%, 1 wave +3.6%)
-#ifndef RFX_WG_WAVES
-#define RFX_WG_WAVES 2
-#endif
-constexpr uint32_t kWgWaves = RFX_WG_WAVES, kWgThreads = 64 * kWgWaves;
-constexpr uint32_t kTileWavesX = kWgWaves >= 2 ? 2 : 1, kTileWavesY = kWgWaves / kTileWavesX;
-constexpr uint32_t kTileW = 8 * kTileWavesX, kTileH = 8 * kTileWavesY;
-static_assert(kWgWaves == 1 || kWgWaves == 2 || kWgWaves == 4, "RFX_WG_WAVES: 1, 2 or 4");
-#define RFX_TRACE_BOUNDS __launch_bounds__(kWgThreads) __attribute__((amdgpu_waves_per_eu(RFX_WAVES_PER_EU)))
 
 // Pixel loop variants of Render::renderNext: block preview (sampleNum < 0), one plain trace per pixel
 // (sampleNum == 1, no jitter, no accumulation -- the benchmark frame), and the general SSAA / additive

@@ -47,6 +47,10 @@ struct alignas(16) Bound { float x, y, z, r; };
 // shift), lanes 32-63 triangles 0-31.  A triangle record also carries its plane (unit normal n, n . v0);
 // a sphere's or an empty lane's plane is zero.
 struct alignas(16) CullRec { float x, y, z, r, nx, ny, nz, d; };
+// Bounding-volume hierarchy over the sphere pairs of a large scene (rfx_host.cpp build_pair_bvh): an internal
+// node holds its two children's boxes (the spheres grown by their radii) and their indices: c >= 0 an internal
+// node, c < 0 the leaf pair ~c (spheres 2(~c), 2(~c) + 1 of the device arrays, which are in Morton order).
+struct alignas(16) BvhNode { float lx[2], ly[2], lz[2], hx[2], hy[2], hz[2]; int32_t child[2], pad[2]; };
 // Plane(pos, norm, material) (Plane.h:6-14): the normal as given (the reference never normalises it)
 struct alignas(16) PlaneGeo { float px, py, pz, nx, ny, nz; int32_t obj, dielectric; };
 struct alignas(16) LightRec { float ox, oy, oz, radius, r, g, b, power; }; // OmniLight.h
@@ -65,6 +69,7 @@ struct DevScene {
   const uint32_t *texels;     // texel pool, ARGB
   const Bound *bound;         // n_sph + n_tri bounding spheres
   const Bound *chunk_bound;   // n_chunk bounding spheres of 64-sphere chunks (large scenes: Morton order)
+  const BvhNode *bvh;         // large scenes: pair BVH, root 0 (null: the chunk loops)
   const CullRec *cull_small;  // 64 lane records (small scenes only, else null)
   const PlaneGeo *pln_geo;    // n_pln (tested by every ray, never culled)
   const MatRec *pln_mat;      // n_pln
@@ -72,6 +77,7 @@ struct DevScene {
   uint64_t cull_valid;        // lanes of cull_small that hold an object
   int32_t n_sph, n_tri, n_light, skybox_tex;
   int32_t n_pln, n_obj, n_tex;
+  int32_t bvh_depth;          // internal levels of the BVH (<= kBvhStack)
   int32_t n_chunk;            // (n_sph + 63) / 64
   float amb_r, amb_g, amb_b;  // diffLightColor * diffLightPower (Scene.cpp:186, host-folded)
   float env_r, env_g, env_b;  // envColor (Scene.cpp:12,55)

@@ -32,6 +32,8 @@ _HIP = C.CDLL("libamdhip64.so")
 
 VARIANTS = {
     "base": [],
+    "mortonaxis": ["RFX_MORTON_AXIS"],
+    "nobvh": ["RFX_NO_BVH"],
     "wg2": ["RFX_WG_WAVES=2"],
     "wg4": ["RFX_WG_WAVES=4"],
     "wpe8": ["RFX_WAVES_PER_EU=8"],
