@@ -163,6 +163,8 @@ def main():
     ap.add_argument("--height", type=int, default=None)
     ap.add_argument("--depth", type=int, default=None)
     ap.add_argument("--gather-rgb", action="store_true", help="N > 1: gather the float RGB strips to rank 0 too")
+    ap.add_argument("--regroup", type=int, default=None,
+                    help="ray regrouping: park traces after n segments (0 off; default: the library's choice)")
     ap.add_argument("--row-block", type=int, default=8)
     ap.add_argument("--cpu-stride", type=int, default=2, help="cpu_baseline samples every n-th row")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -204,6 +206,8 @@ def main():
     scene, cam = build_scene(desc)
     rr = Renderer(device=local, sphere_seed=SEED)
     rr.set_scene(scene)
+    if args.regroup is not None:
+        rr.set_regroup(args.regroup)
     # one non-default stream, current for torch (collectives, copies) and passed to librfx (a NULL stream
     # would select the renderer's own non-blocking stream, unordered with torch's work)
     stream = torch.cuda.Stream(device=dev)

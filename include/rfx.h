@@ -111,6 +111,11 @@ int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *scene);
  * 0 = raster order, no cost recording; 2 = raster order with cost recording (A/B of the sort's overhead).
  * Block-preview frames (sample_num < 0) always run in raster order. */
 int rfx_renderer_set_tile_order(rfx_renderer *r, int mode);
+/* Ray regrouping of plain one-sample frames (no pixel changes): a trace still alive after park_after bounce
+ * segments is parked in an HBM queue and resumed by a second kernel in packed waves (lanes whose traces ended
+ * no longer idle in their tile's wave).  -1 (default) = after 3 segments on scenes with more than 32 spheres
+ * or triangles, off on small ones; 0 = off; n >= 1 = after n segments on any scene. */
+int rfx_renderer_set_regroup(rfx_renderer *r, int park_after);
 /* The reference's two LCG streams (trace_math.h:34-39): Vector3.cpp's (randomInsideSphere) and
  * Render.cpp's (additive jitter).  Both persist across frames exactly as the reference's would. */
 int rfx_renderer_set_rng(rfx_renderer *r, uint32_t sphere_seed, uint32_t jitter_seed);

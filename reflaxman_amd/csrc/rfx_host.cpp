@@ -37,6 +37,7 @@ hipError_t launch_trace(const DevScene &S, const FrameParams &P, bool stats, hip
 uint32_t trace_tiles(const FrameParams &P);
 size_t tile_order_scratch();
 hipError_t launch_tile_order(const uint32_t *cost, uint32_t n, uint32_t *order, uint32_t *scratch, hipStream_t st);
+void launch_bounce(int cfg, dim3 grid, const DevScene &S, const FrameParams &P, hipStream_t st);
 hipError_t launch_kat(int what, const DevScene &S, int tex, const void *in, const int32_t *objs, uint32_t n, void *out,
                       hipStream_t st);
 }  // namespace rfx
@@ -435,6 +436,9 @@ extern "C" uint32_t rfx_strip_row_to_y(uint32_t r, uint32_t rb, uint32_t rank, u
 #ifndef RFX_WAVE_TILES  // schedule unit: the wave's 8x8 tile (1) or the workgroup's 16x8 (0); tools/ab.py, C3: -2.7% trace
 #define RFX_WAVE_TILES 1
 #endif
+#ifndef RFX_PARK_AFTER
+#define RFX_PARK_AFTER 3  // large-scene plain frames: segments before a live trace is parked for the bounce kernel
+#endif
 #ifndef RFX_TILE_SORT_EVERY
 #define RFX_TILE_SORT_EVERY 4  // tools/ab.py, C3: every launch -7.5% trace time vs raster order, every 4th -9.4%, every 16th -9.8%
 #endif
@@ -470,6 +474,12 @@ struct rfx_renderer {
   bool tile_pending = false;         // a sort has been launched: its order is valid for (tile_n, tile_key)
   hipStream_t tile_waited = nullptr; // the stream that already waits on the last sort (tile_join)
   uint64_t tile_count = 0;           // scheduled launches (costs are recorded every RFX_TILE_SORT_EVERY-th)
+  // ray regrouping of large-scene plain frames (RFX_PARK_AFTER): parked traces, their count and the bounce
+  // kernel's claim counter (d_qctr[0], d_qctr[1])
+  int park_after = -1;  // rfx_renderer_set_regroup: -1 = default (RFX_PARK_AFTER on large scenes), 0 = off
+  QRay *d_queue = nullptr;
+  uint64_t queue_cap = 0;
+  uint32_t *d_qctr = nullptr;
   // per-phase event timing: triples {start, after pre-pass, after trace}
   bool timing = false;
   std::vector<hipEvent_t> events;
@@ -572,6 +582,7 @@ extern "C" void rfx_renderer_destroy(rfx_renderer *r)
   (void)hipFree(r->d_seed); (void)hipFree(r->d_err); (void)hipFree(r->d_rd);
   (void)hipFree(r->d_blk_cnt); (void)hipFree(r->d_jump);
   (void)hipFree(r->d_img); (void)hipFree(r->d_argb); (void)hipFree(r->d_cnt);
+  (void)hipFree(r->d_queue); (void)hipFree(r->d_qctr);
   for (hipEvent_t e : r->events) (void)hipEventDestroy(e);
   if (r->tile_stream) (void)hipStreamSynchronize(r->tile_stream);
   (void)hipFree(r->d_tile_cost); (void)hipFree(r->d_tile_order); (void)hipFree(r->d_tile_scratch);
@@ -588,6 +599,13 @@ extern "C" int rfx_renderer_set_tile_order(rfx_renderer *r, int mode)
 {
   if (!r || mode < 0 || mode > 3) return fail(RFX_ERR_ARG, "renderer_set_tile_order: mode 0, 1, 2 or 3");
   r->tile_mode = mode;
+  return RFX_OK;
+}
+
+extern "C" int rfx_renderer_set_regroup(rfx_renderer *r, int park_after)
+{
+  if (!r || park_after < -1) return fail(RFX_ERR_ARG, "renderer_set_regroup: -1 (default), 0 (off) or segments >= 1");
+  r->park_after = park_after;
   return RFX_OK;
 }
 
@@ -1075,6 +1093,29 @@ static int finish_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *d_counts
   if ((rc = timing_event(r, st)) != RFX_OK) return rc;
   P.img = d_rgb;
   P.argb = d_argb;
+  // ray regrouping: plain pixels of a large scene park their traces after RFX_PARK_AFTER segments; the bounce
+  // kernel resumes them in packed waves (rfx_trace.h bounce_kernel)
+  const bool small = r->dev.n_sph <= 32 && r->dev.n_tri <= 32;
+  const bool plain = P.ss == 1 && !P.additive && !P.accumulate;
+  const int park_after = r->park_after < 0 ? (small ? 0 : RFX_PARK_AFTER) : r->park_after;
+  const bool park = park_after > 0 && plain && !d_counters && P.depth > park_after && P.grid_rows;
+  if (park)
+  {
+    if (pl.traces > r->queue_cap)
+    {
+      (void)hipFree(r->d_queue);
+      r->d_queue = nullptr;
+      r->queue_cap = 0;
+      HIP_CHECK(hipMalloc(&r->d_queue, pl.traces * sizeof(QRay)));
+      r->queue_cap = pl.traces;
+    }
+    if (!r->d_qctr) HIP_CHECK(hipMalloc(&r->d_qctr, 2 * sizeof(uint32_t)));
+    HIP_CHECK(hipMemsetAsync(r->d_qctr, 0, 2 * sizeof(uint32_t), st));
+    P.queue = r->d_queue;
+    P.queue_count = r->d_qctr;
+    P.queue_next = r->d_qctr + 1;
+    P.park_after = park_after;
+  }
   P.rd_state = r->d_rd;
   P.counters = (unsigned long long *)d_counters;
   // mode 1 schedules only launches of at least RFX_TILE_ORDER_MIN_TILES tiles: on shorter ones the sort's
@@ -1085,6 +1126,15 @@ static int finish_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *d_counts
   bool record = false;
   if (sched && (rc = tile_schedule(r, P, st, key, record)) != RFX_OK) return rc;
   if (P.grid_rows) HIP_CHECK(launch_trace(r->dev, P, d_counters != nullptr, st));
+  if (park)
+  {
+    // one pass of packed waves over the queue: enough workgroups to fill the chip, each claiming 64 traces at a time
+    const uint64_t waves = (pl.traces + 63) / 64;
+    const uint32_t groups = (uint32_t)std::min<uint64_t>((waves + 1) / 2, 4096);
+    const int cfg = 1 | (r->dev.n_light > 32 ? 2 : 0) | (small ? 4 : 0) | (r->dev.n_pln ? 8 : 0);  // rfx_trace.h kCfg*
+    launch_bounce(cfg, dim3(groups), r->dev, P, st);
+    HIP_CHECK(hipGetLastError());
+  }
   if (record)
   {
     // sort this launch's tile costs into the next launch's order beside the next frame's pre-pass

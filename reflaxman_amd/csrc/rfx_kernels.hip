@@ -430,7 +430,12 @@ static void launch_mode_cfg(bool stats, int mode, int cfg, dim3 grid, const DevS
                             hipStream_t st)
 {
   if (mode == kModeBlock) (stats ? launch_trace_block_stats : launch_trace_block_fast)(cfg, grid, S, P, st);
-  else if (mode == kModePlain) (stats ? launch_trace_plain_stats : launch_trace_plain_fast)(cfg, grid, S, P, st);
+  else if (mode == kModePlain)
+  {
+    if (stats) launch_trace_plain_stats(cfg, grid, S, P, st);
+    else if (P.park_after > 0) launch_trace_plain_park(cfg, grid, S, P, st);
+    else launch_trace_plain_fast(cfg, grid, S, P, st);
+  }
   else (stats ? launch_trace_ssaa_stats : launch_trace_ssaa_fast)(cfg, grid, S, P, st);
 }
 

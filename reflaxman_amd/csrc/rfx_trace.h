@@ -577,7 +577,11 @@ __device__ __forceinline__ bool tri_takes(float sq, float best_sq, int obj, int 
 // the best hit so far (with 0.1% slack over rounding; sphere distances computed by the reference are at least
 // the entry distance into their widened box) cannot win or tie and is skipped too.  Leaves run the exact
 // pair test with the (distance, object index) rule, so the visiting order changes no result.
-constexpr int kBvhStack = 16;  // rfx_host.cpp RFX_BVH_STACK: deeper hierarchies fall back to the chunk loops
+constexpr int kBvhStack = 16;
+#ifndef RFX_NARROW_BUNDLE_COS
+#define RFX_NARROW_BUNDLE_COS 0.9995f
+#endif
+constexpr float kNarrowBundleCos = RFX_NARROW_BUNDLE_COS;  // rfx_host.cpp RFX_BVH_STACK: deeper hierarchies fall back to the chunk loops
 __shared__ int32_t s_bvh_stack[kBvhStack * kWgThreads];
 
 struct RayInv { float ix, iy, iz; };
@@ -753,7 +757,9 @@ __device__ __forceinline__ void closest_hit(const DevScene &S, v3 origin, v3 ray
   uint32_t st_chunks = 0, st_sph = 0, st_pairs = 0;
 #endif
   RFX_PROF_BEGIN(P_SPH);
-  const bool use_bvh = !STATS && S.bvh != nullptr;
+  // a narrow bundle (the primary rays of a tile: one origin, a cone of ~0.1 degree) culls the Morton chunks and
+  // their spheres for the whole wave at once; wider ones walk the BVH lane by lane
+  const bool use_bvh = !STATS && S.bvh != nullptr && !(cull && B->cosa > kNarrowBundleCos);
   if (use_bvh && live) closest_spheres_bvh<STATS>(S, origin, ray, k, h, cnt);
   for (int cfirst = 0; !use_bvh && cfirst < S.n_chunk; cfirst += 64)
   {
@@ -1031,15 +1037,26 @@ __device__ __forceinline__ bool occluded(const DevScene &S, v3 o, v3 ray, bool l
 // CULL: wave bundles skip objects no live lane can hit (closest hit and shadow rays); MANYL: more than
 // 32 lights (shadow masks and shading in blocks of 32); PLANES: the scene holds planes.  Call with every lane
 // of the wave active; `valid` lanes trace.  Returns the trace's colour (zero for invalid lanes).
-template <bool STATS, bool CULL, bool MANYL, bool SMALL, bool PLANES>
-__device__ __forceinline__ col trace(const DevScene &S, v3 origin, v3 ray, int depth, v3 rd, const float *lut,
-                                     Cnt &cnt, bool valid)
+// Parking (ray regrouping): where the bounce loop would start segment `park` of a trace, the trace's state is
+// appended to the queue instead (one atomic per wave, packed lane order) and the trace ends here; the bounce
+// kernel resumes it from exactly that state, so every float op is the same.
+struct Park {
+  int after;           // segments before parking (<= 0: never)
+  QRay *queue;
+  uint32_t *count;
+  uint32_t trace, out;  // this lane's randDir trace index and output pixel
+};
+
+// Scene::trace from a mid-trace state (mulc, pix after `refl` segments); park: see Park.  *parked: this lane's
+// trace was queued and its returned colour is not final.
+template <bool STATS, bool CULL, bool MANYL, bool SMALL, bool PLANES, bool PARK>
+__device__ __forceinline__ col trace_from(const DevScene &S, v3 origin, v3 ray, col mulc, col pix, int refl, int depth,
+                                          v3 rd, const float *lut, Cnt &cnt, bool valid, const Park &park, bool &parked)
 {
-  if (valid) RFX_CNT(C_RAYS);
+  parked = false;
+  if (valid && refl == 0) RFX_CNT(C_RAYS);
   const Tabs<SMALL> T{S};
-  col mulc = mkc(1.0f, 1.0f, 1.0f), pix = mkc(0.0f, 0.0f, 0.0f);
-  int refl = 0;
-  bool alive = valid && depth > 0;
+  bool alive = valid && refl < depth;
 #ifdef RFX_DEBUG_SEGS
   int nseg = 0;  // diagnostic build only (tools/segstats.py): the trace's segment count replaces its colour
 #endif
@@ -1254,6 +1271,28 @@ __device__ __forceinline__ col trace(const DevScene &S, v3 origin, v3 ray, int d
       RFX_PROF_END(P_SKY);
       alive = false;
     }
+    if constexpr (!STATS && PARK)
+    {
+      if (refl == park.after && __ballot(alive))
+      {
+        // every lane of the wave is here (wave-uniform loop); the live ones append their state
+        const uint64_t pm = __ballot(alive);
+        uint32_t base = 0;
+        if (__lane_id() == (uint32_t)(__ffsll((long long)pm) - 1)) base = atomicAdd(park.count, (uint32_t)__popcll(pm));
+        base = __builtin_amdgcn_readlane(base, __ffsll((long long)pm) - 1);
+        if (alive)
+        {
+          QRay q;
+          q.ox = origin.x; q.oy = origin.y; q.oz = origin.z; q.dx = ray.x;
+          q.dy = ray.y; q.dz = ray.z; q.mr = mulc.r; q.mg = mulc.g;
+          q.mb = mulc.b; q.pr = pix.r; q.pg = pix.g; q.pb = pix.b;
+          q.trace = park.trace; q.out = park.out; q.refl = (uint32_t)refl; q.pad = 0;
+          park.queue[base + (uint32_t)__popcll(pm & ((1ull << __lane_id()) - 1ull))] = q;
+          parked = true;
+          alive = false;
+        }
+      }
+    }
   }
   RFX_PROF_END(P_SEG);
 #ifdef RFX_DEBUG_SEGS
@@ -1261,6 +1300,16 @@ __device__ __forceinline__ col trace(const DevScene &S, v3 origin, v3 ray, int d
 #else
   return pix;
 #endif
+}
+
+template <bool STATS, bool CULL, bool MANYL, bool SMALL, bool PLANES>
+__device__ __forceinline__ col trace(const DevScene &S, v3 origin, v3 ray, int depth, v3 rd, const float *lut,
+                                     Cnt &cnt, bool valid)
+{
+  bool parked;
+  return trace_from<STATS, CULL, MANYL, SMALL, PLANES, false>(S, origin, ray, mkc(1.0f, 1.0f, 1.0f), mkc(0.0f, 0.0f, 0.0f), 0,
+                                                       depth, rd, lut, cnt, valid, Park{0, nullptr, nullptr, 0, 0},
+                                                       parked);
 }
 
 template <bool STATS>
@@ -1316,8 +1365,9 @@ __device__ __forceinline__ uint32_t clock32()
 enum TraceMode { kModeSsaa = 0, kModeBlock = 1, kModePlain = 2 };
 // CFG bits: kCfgCull -- wave-bundle culling (every non-stats launch); kCfgManyLights -- more than 32 lights;
 // kCfgSmall -- at most 32 spheres and 32 triangles (one lane-layout cull mask for the whole scene)
-// kCfgPlanes -- the scene holds planes (Scene::addPlane extension)
-constexpr int kCfgCull = 1, kCfgManyLights = 2, kCfgSmall = 4, kCfgPlanes = 8;
+// kCfgPlanes -- the scene holds planes (Scene::addPlane extension); kCfgPark -- plain pixels park their traces
+// for the bounce kernel (ray regrouping; rfx_trace_plain_park.hip)
+constexpr int kCfgCull = 1, kCfgManyLights = 2, kCfgSmall = 4, kCfgPlanes = 8, kCfgPark = 16;
 
 // one workgroup = kTileW x kTileH output pixels (block mode: block corners), one wave = an 8x8 tile (ray coherence).
 // Every lane of a wave reaches trace() -- lanes outside the frame or the cursor span as invalid -- so the
@@ -1326,7 +1376,7 @@ template <bool STATS, int MODE, int CFG>
 __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
 {
   constexpr bool CULL = (CFG & kCfgCull) != 0, MANYL = (CFG & kCfgManyLights) != 0, SMALL = (CFG & kCfgSmall) != 0;
-  constexpr bool PLANES = (CFG & kCfgPlanes) != 0;
+  constexpr bool PLANES = (CFG & kCfgPlanes) != 0, PARK = MODE == kModePlain && !STATS && (CFG & kCfgPark) != 0;
   __shared__ float lut[256];
   for (uint32_t i = threadIdx.x; i < 256; i += kWgThreads) lut[i] = (float)i / 255.0f;  // Color.cpp:11-13
   stage_powf_tables();
@@ -1409,13 +1459,17 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
     const uint64_t pr = p - P.p_begin;
     const float rx = (float)x - P.wh, ry = (float)y - P.hh;                       // Render.cpp:152-153
     col out;
+    bool parked = false;
     if constexpr (MODE == kModePlain)
     {
       // Render.cpp:183 with ssx = ssy = 0, sampleNum = 1, no jitter: float(0) / 1 == +0, rnd == 0
       const v3 ray = mmul(view, mk(rx + 0.0f + 0.0f, ry + 0.0f + 0.0f, P.rz));
       v3 rd = mk(0.0f, 0.0f, 0.0f);
       if (valid) rd = load_rd(P, pr);
-      const col c = trace<STATS, CULL, MANYL, SMALL, PLANES>(S, eye, ray, P.depth, rd, lut, cnt, valid);
+      const Park park{P.park_after, P.queue, P.queue_count, (uint32_t)pr, (uint32_t)((size_t)orow * P.W + x)};
+      const col c = trace_from<STATS, CULL, MANYL, SMALL, PLANES, PARK>(S, eye, ray, mkc(1.0f, 1.0f, 1.0f),
+                                                                  mkc(0.0f, 0.0f, 0.0f), 0, P.depth, rd, lut, cnt,
+                                                                  valid, park, parked);
       out = cadd(mkc(0.0f, 0.0f, 0.0f), c);                                      // Render.cpp:185 (/ 1.0f exact)
     }
     else
@@ -1448,7 +1502,7 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
       }
       out = fin;
     }
-    if (valid)
+    if (valid && !parked)
     {
       const size_t o = (size_t)orow * P.W + x;
       float *d = P.img + o * 3;
@@ -1466,6 +1520,48 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
   flush_counters<STATS>(P, cnt);
   RFX_PROF_FLUSH();
 
+}
+
+// The parked traces (rfx_types.h QRay) of a plain-pixel launch resumed in packed waves: each wave claims 64
+// queue entries at a time (one atomic), runs the rest of their bounce loops and writes their pixels exactly
+// as the trace kernel would have (Render.cpp:185 and the ARGB epilogue).  Waves exit once the queue is
+// drained; the queue holds traces from all over the frame, so waves no longer idle on lanes whose traces
+// ended (the trace kernel's tail of 1-2 live lanes per wave at depth 3+).
+template <int CFG>
+__global__ RFX_TRACE_BOUNDS void bounce_kernel(DevScene S, FrameParams P)
+{
+  constexpr bool CULL = (CFG & kCfgCull) != 0, MANYL = (CFG & kCfgManyLights) != 0, SMALL = (CFG & kCfgSmall) != 0;
+  constexpr bool PLANES = (CFG & kCfgPlanes) != 0;
+  __shared__ float lut[256];
+  for (uint32_t i = threadIdx.x; i < 256; i += kWgThreads) lut[i] = (float)i / 255.0f;  // Color.cpp:11-13
+  stage_powf_tables();
+  if constexpr (SMALL) stage_small_scene(S);
+  __syncthreads();
+  Cnt cnt;
+  const uint32_t n = *P.queue_count, lane = __lane_id();
+  for (;;)
+  {
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(P.queue_next, 64u);
+    base = __builtin_amdgcn_readfirstlane(base);
+    if (base >= n) break;
+    const uint32_t i = base + lane;
+    const bool valid = i < n;
+    QRay q{};
+    if (valid) q = P.queue[i];
+    const v3 rd = valid ? load_rd(P, q.trace) : mk(0.0f, 0.0f, 0.0f);
+    bool parked;
+    const col c = trace_from<false, CULL, MANYL, SMALL, PLANES, false>(
+        S, mk(q.ox, q.oy, q.oz), mk(q.dx, q.dy, q.dz), mkc(q.mr, q.mg, q.mb), mkc(q.pr, q.pg, q.pb), (int)q.refl, P.depth,
+        rd, lut, cnt, valid, Park{0, nullptr, nullptr, 0, 0}, parked);
+    if (valid)
+    {
+      const col out = cadd(mkc(0.0f, 0.0f, 0.0f), c);                            // Render.cpp:185
+      float *d = P.img + (size_t)q.out * 3;
+      d[0] = out.r; d[1] = out.g; d[2] = out.b;
+      if (P.argb) P.argb[q.out] = argb(out);
+    }
+  }
 }
 
 // ------------------------------------------------------------- launch of one family (the rfx_trace_*.hip TUs)
@@ -1509,5 +1605,7 @@ RFX_DECLARE_TRACE_FAMILY(launch_trace_ssaa_fast);
 RFX_DECLARE_TRACE_FAMILY(launch_trace_ssaa_stats);
 RFX_DECLARE_TRACE_FAMILY(launch_trace_block_fast);
 RFX_DECLARE_TRACE_FAMILY(launch_trace_block_stats);
+RFX_DECLARE_TRACE_FAMILY(launch_trace_plain_park);
+RFX_DECLARE_TRACE_FAMILY(launch_bounce);
 
 }  // namespace rfx

@@ -1,0 +1,53 @@
+// The ray-regrouping family of librfx.so: plain-pixel trace kernels that park their live traces after
+// FrameParams::park_after segments (kCfgPark) and the bounce kernel that resumes the parked traces in packed
+// waves -- its own TU so it compiles in parallel with the other families (reflaxman_amd/_build.py).
+#include "rfx_trace.h"
+
+namespace rfx {
+
+template <int CFG>
+static void launch_park_one(dim3 grid, const DevScene &S, const FrameParams &P, hipStream_t st)
+{
+  hipLaunchKernelGGL((trace_kernel<false, kModePlain, CFG | kCfgPark>), grid, dim3(kWgThreads), 0, st, S, P);
+}
+
+void launch_trace_plain_park(int cfg, dim3 grid, const DevScene &S, const FrameParams &P, hipStream_t st)
+{
+  switch (cfg & ~kCfgPark)
+  {
+    case 1: launch_park_one<1>(grid, S, P, st); break;
+    case 3: launch_park_one<3>(grid, S, P, st); break;
+    case 5: launch_park_one<5>(grid, S, P, st); break;
+    case 7: launch_park_one<7>(grid, S, P, st); break;
+    case 9: launch_park_one<9>(grid, S, P, st); break;
+    case 11: launch_park_one<11>(grid, S, P, st); break;
+    case 13: launch_park_one<13>(grid, S, P, st); break;
+    case 15: launch_park_one<15>(grid, S, P, st); break;
+    default: break;
+  }
+}
+
+// the bounce kernel of the parked traces (rfx_trace.h bounce_kernel)
+template <int CFG>
+static void launch_bounce_one(dim3 grid, const DevScene &S, const FrameParams &P, hipStream_t st)
+{
+  hipLaunchKernelGGL((bounce_kernel<CFG>), grid, dim3(kWgThreads), 0, st, S, P);
+}
+
+void launch_bounce(int cfg, dim3 grid, const DevScene &S, const FrameParams &P, hipStream_t st)
+{
+  switch (cfg)
+  {
+    case 1: launch_bounce_one<1>(grid, S, P, st); break;
+    case 3: launch_bounce_one<3>(grid, S, P, st); break;
+    case 5: launch_bounce_one<5>(grid, S, P, st); break;
+    case 7: launch_bounce_one<7>(grid, S, P, st); break;
+    case 9: launch_bounce_one<9>(grid, S, P, st); break;
+    case 11: launch_bounce_one<11>(grid, S, P, st); break;
+    case 13: launch_bounce_one<13>(grid, S, P, st); break;
+    case 15: launch_bounce_one<15>(grid, S, P, st); break;
+    default: break;
+  }
+}
+
+}  // namespace rfx

@@ -84,6 +84,16 @@ struct DevScene {
   float half_tile_w, half_tile_h;  // Skybox.cpp:21-37
 };
 
+// A trace parked between bounce segments (large scenes, plain pixels): the state Scene::trace carries from
+// one segment to the next (Scene.cpp:80-234: origin, ray, mulColor, pixelColor, refl), the trace index of its
+// randDir and the output pixel.  64 B: one lane stores / loads it with four 16-B accesses.
+struct alignas(16) QRay {
+  float ox, oy, oz, dx;
+  float dy, dz, mr, mg;
+  float mb, pr, pg, pb;
+  uint32_t trace, out, refl, pad;
+};
+
 struct FrameParams {
   float eye_x, eye_y, eye_z;
   float v11, v12, v13, v21, v22, v23, v31, v32, v33;  // Render::renderCameraView
@@ -105,6 +115,12 @@ struct FrameParams {
   const uint32_t *tile_order;   // workgroup i renders tile tile_order[i] (previous frame's LPT order), or null: tile i
   uint32_t *tile_cost;          // per tile: its clock cycles this frame (the next frame's order), or null
   uint32_t tiles_x;             // schedule tiles per grid row (set by launch_trace)
+  // ray regrouping (plain pixels, large scenes): a trace still alive after park_after segments is appended to
+  // queue (queue_count: entries) instead of continuing; the bounce kernel then runs the queue in packed waves,
+  // claiming 64 entries at a time from queue_next.  park_after <= 0: no parking.
+  QRay *queue;
+  uint32_t *queue_count, *queue_next;
+  int32_t park_after;
 };
 
 }  // namespace rfx

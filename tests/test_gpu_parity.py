@@ -388,3 +388,27 @@ def test_textures_loaded_from_tga_files(tmp_path):
     assert np.array_equal(r.copyImage(), g["argb"])
     assert r.imagePixels().tobytes() == g["rgb"].tobytes()
     r.close()
+
+
+@pytest.mark.parametrize("key,park", [("hash_synth16_3840x2160_d8", 1), ("hash_synth16_3840x2160_d8", 2),
+                                      ("hash_default_640x480_d4", 1), ("hash_synth16_7680x4320_d8", 3)])
+def test_regrouped_frame_matches_reference_hash(key, park):
+    """Ray regrouping (traces parked after `park` segments, resumed by the packed bounce kernel) on the small-scene
+    configs, where it is off by default: the full frame still hashes to the reference's."""
+    c = CASES[key]
+    rgb, argb, r = run_case(c, regroup=park)
+    assert sha(argb) == c["sha_argb"], key
+    assert sha(rgb) == c["sha_f32"], key
+    r.close()
+
+
+@pytest.mark.parametrize("key", sorted(k for k, c in CASES.items() if c["kind"] == "band" and c["scene"] == "stress4096"))
+def test_stress_band_without_regrouping(key):
+    """C5 with regrouping off (on by default there): the reference's bands again."""
+    c = CASES[key]
+    rgb, argb, r = gpu_render(scene(c["scene"]), c["W"], c["H"], c["depth"], sphere_seed=c["sphere_seed"], regroup=0)
+    g = np.load(os.path.join(GOLDEN, key + ".npz"))
+    y0, rows = c["y0"], c["rows"]
+    assert np.array_equal(argb[y0:y0 + rows], g["argb"])
+    assert rgb[y0:y0 + rows].tobytes() == g["rgb"].tobytes()
+    r.close()

@@ -34,6 +34,12 @@ VARIANTS = {
     "base": [],
     "mortonaxis": ["RFX_MORTON_AXIS"],
     "nobvh": ["RFX_NO_BVH"],
+    "nopark": ["RFX_PARK_AFTER=0"],
+    "park1": ["RFX_PARK_AFTER=1"],
+    "park3": ["RFX_PARK_AFTER=3"],
+    "bvhall": ["RFX_NARROW_BUNDLE_COS=2.0f"],
+    "narrow99": ["RFX_NARROW_BUNDLE_COS=0.99f"],
+    "narrow9999": ["RFX_NARROW_BUNDLE_COS=0.99999f"],
     "wg2": ["RFX_WG_WAVES=2"],
     "wg4": ["RFX_WG_WAVES=4"],
     "wpe8": ["RFX_WAVES_PER_EU=8"],
