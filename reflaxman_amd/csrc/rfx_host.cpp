@@ -628,7 +628,30 @@ static int upload(rfx_renderer *r, const std::vector<T> &v, const T **dst)
   return RFX_OK;
 }
 
-// Pair BVH of a large scene: leaves are the device sphere pairs (2j, 2j + 1, Morton-adjacent); internal nodes
+// Device order of a large scene's spheres: recursive median splits of the centres along their longest axis,
+// left parts of even size, so pairs (2j, 2j + 1) are neighbours and every aligned run of 2^k spheres is a
+// compact cluster (the 64-sphere chunks of the bundle cull, the leaves of the pair BVH).
+static void spatial_order(std::vector<uint32_t> &idx, size_t a, size_t b, const std::vector<HostSphere> &sp)
+{
+  if (b - a <= 2) return;
+  double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+  for (size_t i = a; i < b; ++i)
+  {
+    const double c[3] = {sp[idx[i]].center.x, sp[idx[i]].center.y, sp[idx[i]].center.z};
+    for (int k = 0; k < 3; ++k) { lo[k] = fmin(lo[k], c[k]); hi[k] = fmax(hi[k], c[k]); }
+  }
+  int axis = 0;
+  for (int k = 1; k < 3; ++k)
+    if (hi[k] - lo[k] > hi[axis] - lo[axis]) axis = k;
+  const size_t mid = a + 2 * ((b - a + 2) / 4);
+  auto key = [&](uint32_t i) { return axis == 0 ? sp[i].center.x : axis == 1 ? sp[i].center.y : sp[i].center.z; };
+  std::nth_element(idx.begin() + a, idx.begin() + mid, idx.begin() + b,
+                   [&](uint32_t x, uint32_t y) { return key(x) < key(y) || (key(x) == key(y) && x < y); });
+  spatial_order(idx, a, mid, sp);
+  spatial_order(idx, mid, b, sp);
+}
+
+// Pair BVH of a large scene: leaves are the device sphere pairs (2j, 2j + 1, neighbours); internal nodes
 // split their pairs at the median of the pair centres along the longest axis.  Each node stores its two
 // children's boxes (spheres grown by their radii); the kernel widens them by its exact-cull margin per ray.
 // Returns the node index (or ~pair for a leaf) of range [a, b) of `pairs`; depth: internal levels below.
@@ -686,54 +709,15 @@ extern "C" int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *s)
   std::vector<SphereGeo> sg;
   std::vector<MatRec> sm, tm;
   std::vector<int32_t> si;
-  // Large scenes (more than 32 spheres): spheres in spatial order -- 30-bit Morton code of the centre in
-  // the centres' bounding box, ties by insertion index -- so each 64-sphere chunk of the device arrays is
-  // compact and its bounding sphere can cull it as a whole.  Every record keeps its object index (sph_info),
+  // Large scenes (more than 32 spheres): spheres in spatial order (spatial_order: recursive median splits),
+  // so each 64-sphere chunk of the device arrays is compact and its bounding sphere can cull it as a whole,
+  // and each pair is a BVH leaf.  Every record keeps its object index (sph_info),
   // and the large-scene kernel path compares (distance, object index), so the order changes no result.
   const size_t nsph = s->spheres.size();
   std::vector<uint32_t> order(nsph);
   for (size_t i = 0; i < nsph; ++i) order[i] = (uint32_t)i;
-  if (nsph > 32)
-  {
-    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-    for (const HostSphere &sp : s->spheres)
-    {
-      const double c[3] = {sp.center.x, sp.center.y, sp.center.z};
-      for (int a = 0; a < 3; ++a) { lo[a] = fmin(lo[a], c[a]); hi[a] = fmax(hi[a], c[a]); }
-    }
-    auto spread = [](uint32_t v) {  // 10 bits -> every third bit
-      v &= 0x3FFu;
-      v = (v | (v << 16)) & 0x030000FFu;
-      v = (v | (v << 8)) & 0x0300F00Fu;
-      v = (v | (v << 4)) & 0x030C30C3u;
-      v = (v | (v << 2)) & 0x09249249u;
-      return v;
-    };
-    std::vector<uint32_t> code(nsph);
-    for (size_t i = 0; i < nsph; ++i)
-    {
-      const HostSphere &sp = s->spheres[i];
-      const double c[3] = {sp.center.x, sp.center.y, sp.center.z};
-      uint32_t q[3];
-      // one cell size for all three axes (the largest extent): cubic cells keep a chunk compact even when
-      // the centres span a thin slab (C5: y over 0.5 units, x over 24) -- per-axis scaling would interleave
-      // the thin axis' bits as if it were as long as the others and cut chunks into wide slivers
-      double cube = 0.0;
-      for (int a = 0; a < 3; ++a) cube = fmax(cube, hi[a] - lo[a]);
-      for (int a = 0; a < 3; ++a)
-      {
-#ifdef RFX_MORTON_AXIS
-        const double ext = hi[a] - lo[a];
-#else
-        const double ext = cube;
-#endif
-        const double f = ext > 0.0 && std::isfinite(ext) ? (c[a] - lo[a]) / ext : 0.0;
-        q[a] = (uint32_t)fmin(fmax(f * 1023.0, 0.0), 1023.0);
-      }
-      code[i] = spread(q[0]) | spread(q[1]) << 1 | spread(q[2]) << 2;
-    }
-    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return code[a] < code[b]; });
-  }
+  if (nsph > 32) spatial_order(order, 0, nsph, s->spheres);
+
   for (uint32_t oi : order)
   {
     const HostSphere &sp = s->spheres[oi];
@@ -880,7 +864,7 @@ extern "C" int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *s)
     pg.push_back({p.pos.x, p.pos.y, p.pos.z, p.norm.x, p.norm.y, p.norm.z, p.obj, p.mat.dielectric});
     pm.push_back({p.mat.r, p.mat.g, p.mat.b, p.mat.refl});
   }
-  // object index -> (kind, index in the device arrays): spheres through the Morton order
+  // object index -> (kind, index in the device arrays): spheres through their spatial order
   std::vector<int32_t> loc(s->obj_kind.size());
   {
     std::vector<int32_t> sph_dev(nsph);
