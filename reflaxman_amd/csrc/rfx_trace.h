@@ -1359,6 +1359,29 @@ __device__ __forceinline__ uint32_t clock32()
 }
 
 
+// A wave's 8x8 pixels (lane = 8 row + column) at output row `row0`, column `x0`: the colours go through the
+// wave's LDS slot and leave as ONE 16-B-per-lane store -- lanes 0-47 write the 8 rows of 8 RGB floats
+// (96 B = 6 x 16 B per row, Render.cpp:185's interleaved Color layout), lanes 48-63 the 8 rows of 8 ARGB words
+// (32 B = 2 x 16 B per row).  Call with every lane valid; needs W % 4 == 0 and 16-B-aligned images.
+__device__ __forceinline__ void store_wave_tile(const FrameParams &P, uint32_t x0, uint32_t row0, col out,
+                                                uint32_t lane, uint32_t wave)
+{
+  __shared__ __attribute__((aligned(16))) uint32_t s_out[kWgWaves][256];  // 192 RGB floats + 64 ARGB words
+  uint32_t *s = s_out[wave];
+  s[3 * lane] = __float_as_uint(out.r);
+  s[3 * lane + 1] = __float_as_uint(out.g);
+  s[3 * lane + 2] = __float_as_uint(out.b);
+  s[192 + lane] = argb(out);
+  __builtin_amdgcn_wave_barrier();
+  const bool rgb = lane < 48;
+  const uint32_t k = rgb ? lane : lane - 48;
+  const uint32_t r = rgb ? k / 6u : k >> 1, c = rgb ? k % 6u : k & 1u;
+  const uint4 v = *reinterpret_cast<const uint4 *>(s + (rgb ? r * 24u + 4u * c : 192u + r * 8u + 4u * c));
+  const size_t pix = (size_t)(row0 + r) * P.W + x0;
+  uint32_t *dst = rgb ? reinterpret_cast<uint32_t *>(P.img) + pix * 3 + 4u * c : P.argb + pix + 4u * c;
+  if (rgb || P.argb) *reinterpret_cast<uint4 *>(dst) = v;
+}
+
 // Pixel loop variants of Render::renderNext: block preview (sampleNum < 0), one plain trace per pixel
 // (sampleNum == 1, no jitter, no accumulation -- the benchmark frame), and the general SSAA / additive
 // loop.  The plain variant drops the sample loops and their live state (no spills before the bounce loop).
@@ -1409,6 +1432,10 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
   const uint32_t t8 = P.tile_order ? P.tile_order[kWgWaves * wid + wv]
                                    : (blockIdx.y * kTileWavesY + wv / kTileWavesX) * w8 + blockIdx.x * kTileWavesX + wv % kTileWavesX;
   const uint32_t gx = (t8 % w8) * 8u + (lane & 7u), gy = (t8 / w8) * 8u + (lane >> 3);
+  // the tile index waits in LDS across the bounce loop: the epilogue re-derives the output coordinates from it
+  // instead of keeping (spilling) them
+  __shared__ uint32_t s_t8[kWgWaves];
+  if (lane == 0) s_t8[wv] = t8;
   (void)tile;
 #else
   const uint32_t lx = (wave % kTileWavesX) * 8u + (lane & 7u), ly = (wave / kTileWavesX) * 8u + (lane >> 3);
@@ -1502,17 +1529,36 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
       }
       out = fin;
     }
-    if (valid && !parked)
+#if RFX_WAVE_TILES
+    // output coordinates again, from the tile index in LDS (volatile: re-read, not kept live)
+    const uint32_t t8e = ((volatile uint32_t *)s_t8)[wv];
+    uint32_t le = lane;
+    asm volatile("" : "+v"(le));  // a fresh lane value: its row/column are recomputed, not kept live
+    const uint32_t x0e = (t8e % w8) * 8u, row0e = (t8e / w8) * 8u + (P.nranks > 1 ? 0u : P.row0);
+    const uint32_t xe = x0e + (le & 7u), rowe = row0e + (le >> 3), wslot = wv;
+#else
+    const uint32_t xe = x, rowe = orow, le = lane, x0e = 0, row0e = 0, wslot = wave;
+#endif
+    if (MODE == kModeSsaa && P.accumulate && valid)                                  // Render.cpp:191-194
     {
-      const size_t o = (size_t)orow * P.W + x;
+      const float *d = P.img + ((size_t)rowe * P.W + xe) * 3;
+      out = mkc(d[0] + out.r, d[1] + out.g, d[2] + out.b);
+    }
+    const bool staged = RFX_WAVE_TILES && (P.W & 3u) == 0 &&
+                        ((reinterpret_cast<uintptr_t>(P.img) | reinterpret_cast<uintptr_t>(P.argb)) & 15u) == 0 &&
+                        __builtin_amdgcn_ballot_w64(valid && !parked) == ~0ull;
+    if (staged)
+      store_wave_tile(P, x0e, row0e, out, le, wslot);  // Render::copyImage too
+    else if (valid && !parked)
+    {
+      const size_t o = (size_t)rowe * P.W + xe;
       float *d = P.img + o * 3;
-      if (MODE == kModeSsaa && P.accumulate) out = mkc(d[0] + out.r, d[1] + out.g, d[2] + out.b);  // Render.cpp:191-194
       d[0] = out.r; d[1] = out.g; d[2] = out.b;
       if (P.argb) P.argb[o] = argb(out);                                           // Render::copyImage
     }
 #if RFX_WAVE_TILES
     if (P.tile_cost && __lane_id() == 0)  // per wave tile, located from the live pixel (x, orow)
-      P.tile_cost[(P.nranks > 1 ? orow : orow - P.row0) / 8u * P.tiles_x + x / 8u] = clock32() - s_clk0;
+      P.tile_cost[(P.nranks > 1 ? rowe : rowe - P.row0) / 8u * P.tiles_x + xe / 8u] = clock32() - s_clk0;
 #else
     if (P.tile_cost && __lane_id() == 0) P.tile_cost[s_tile] = clock32() - s_clk0;  // one lane per wave, the last stays
 #endif

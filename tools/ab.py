@@ -32,7 +32,6 @@ _HIP = C.CDLL("libamdhip64.so")
 
 VARIANTS = {
     "base": [],
-    "mortonaxis": ["RFX_MORTON_AXIS"],
     "nobvh": ["RFX_NO_BVH"],
     "nopark": ["RFX_PARK_AFTER=0"],
     "park1": ["RFX_PARK_AFTER=1"],
