@@ -149,6 +149,25 @@ def cpu_baseline(desc, W, H, depth, gpu_rgb, gpu_argb, stride):
         "f32_ulp_histogram": ulp_hist(g_rgb, rgb), "pixels": int(px)}
 
 
+def cpu_allcore(desc, W, H, depth, gpu_rgb, gpu_argb, rate_1core, seconds=8.0):
+    """Context row (BASELINE.md:59-62, not the speedup denominator): the C restatement (bit-exact port) with
+    its rows interleaved over every host thread this job may use, on a centred band sized from the 1-core
+    rate to take about `seconds`; the band is also compared with the GPU frame's."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as orc
+    threads = max(1, min(64, int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)))
+    rows = int(min(H, max(threads, rate_1core * 1e6 * threads * seconds / W)))
+    y0 = (H - rows) // 2
+    t0 = time.perf_counter()
+    rgb, argb = orc.render_band(desc, W, H, depth, y0, rows, SEED, nthreads=threads)
+    secs = time.perf_counter() - t0
+    g = slice(y0, y0 + rows)
+    same = bool(np.array_equal(gpu_rgb[g].view(np.uint32), rgb.view(np.uint32)) and np.array_equal(gpu_argb[g], argb))
+    return {"value": round(W * rows / secs / 1e6, 4), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"rows {y0}..{y0 + rows - 1} of the first frame, rows interleaved over {threads} threads, "
+                      f"{secs:.1f} s; {cpu_model()}", "bit_exact_vs_gpu": same}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -167,6 +186,7 @@ def main():
                     help="ray regrouping: park traces after n segments (0 off; default: the library's choice)")
     ap.add_argument("--row-block", type=int, default=8)
     ap.add_argument("--cpu-stride", type=int, default=2, help="cpu_baseline samples every n-th row")
+    ap.add_argument("--no-cpu-allcore", action="store_true", help="skip the all-core CPU context row")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (gloo: multi-rank rehearsal)")
     ap.add_argument("--one-device", action="store_true", help="all ranks on cuda:0 (rehearsal on a 1-GPU box)")
@@ -381,6 +401,9 @@ def main():
         out["parity"]["sample_vs_cpu_reference"] = delta
         out["max_abs_delta"] = {"u8": delta["max_u8"], "f32_ulp": delta["max_f32_ulp"]}
         out["speedup_vs_cpu_1core"] = round(mrays / cb["value"], 1)
+        if not args.no_cpu_allcore:
+            log("cpu_allcore: the C restatement on every host thread (context row) ...")
+            out["cpu_allcore"] = cpu_allcore(desc, W, H, depth, first_rgb, first_argb, cb["value"])
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

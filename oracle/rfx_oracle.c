@@ -639,7 +639,7 @@ typedef struct {
   const v3 *rand_dirs;      /* per trace, in the reference's trace order */
   const float *jitter;      /* 2 per pixel (additive) or NULL */
   float *image;
-  uint32_t y_begin, y_end;  /* rows of this worker */
+  uint32_t y_begin, y_end, y_step;  /* rows of this worker: y_begin, y_begin + y_step, .. < y_end */
   uint64_t cnt[ORC_NCOUNTERS];
   int counting;
 } job_t;
@@ -673,7 +673,7 @@ static void *render_rows(void *arg)
   }
   const int ss = j->ss;
   const float sq = (float)(ss * ss);
-  for (uint32_t y = j->y_begin; y < j->y_end; ++y)
+  for (uint32_t y = j->y_begin; y < j->y_end; y += j->y_step)
     for (uint32_t x = 0; x < W; ++x)
     {
       const size_t p = (size_t)y * W + x;
@@ -712,7 +712,11 @@ static int run_jobs(job_t *proto, uint32_t y0, uint32_t y1, int nthreads, uint64
       a = (a + n_blk - 1) / n_blk * n_blk; b = (b + n_blk - 1) / n_blk * n_blk;
       if (t == nthreads - 1) b = y1;
     }
-    jobs[t].y_begin = a; jobs[t].y_end = b > y1 ? y1 : b;
+    jobs[t].y_begin = a; jobs[t].y_end = b > y1 ? y1 : b; jobs[t].y_step = 1;
+    if (proto->ss > 0)
+    { /* pixel rows interleaved over the workers (rows differ in cost: sky vs geometry) */
+      jobs[t].y_begin = y0 + (uint32_t)t; jobs[t].y_end = y1; jobs[t].y_step = (uint32_t)nthreads;
+    }
     memset(jobs[t].cnt, 0, sizeof(jobs[t].cnt));
   }
   if (nthreads == 1) render_rows(&jobs[0]);
