@@ -1,6 +1,6 @@
 """Summarise rocprofv3 --pmc CSVs for one kernel (per-launch means of each counter).
 
-    python tools/pmc_summary.py [--kernel SUBSTR] [--out profiles/pmc_trace_kernel.json
+    python tools/pmc_summary.py [--kernel SUBSTR] [--out profiles/pmc/<name>.json
                                  --config SCENE W H DEPTH NGPUS] CSV...
 
 With --out, also writes the HBM traffic record bench.py reads for `roofline.traffic`:
@@ -13,6 +13,11 @@ import argparse
 import collections
 import csv
 import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from reflaxman_amd import _lib  # noqa: E402
 
 
 def summarise(paths, kernel="trace_kernel<false"):
@@ -29,6 +34,7 @@ def main():
     ap.add_argument("--kernel", default="trace_kernel<false")
     ap.add_argument("--out")
     ap.add_argument("--config", nargs=5)
+    ap.add_argument("--lib-sha256", default=None, help="build the counters came from (default: the in-tree librfx.so)")
     ap.add_argument("csv", nargs="+")
     a = ap.parse_args()
     s = summarise(a.csv, a.kernel)
@@ -39,6 +45,7 @@ def main():
         scene, W, H, depth, n = a.config
         rec = {
             "kernel": a.kernel, "config": [scene, int(W), int(H), int(depth), int(n)],
+            "lib_sha256": a.lib_sha256 or _lib.lib_sha256(),
             "fetch_bytes_per_launch": int(s["FETCH_SIZE"] * 1024), "write_bytes_per_launch": int(s["WRITE_SIZE"] * 1024),
             "hbm_bytes_per_launch": int((s["FETCH_SIZE"] + s["WRITE_SIZE"]) * 1024),
             "note": "rocprofv3 FETCH_SIZE + WRITE_SIZE (KiB) per dispatch, separate --pmc passes; FETCH_SIZE uncorrected "
