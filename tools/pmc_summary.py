@@ -1,6 +1,6 @@
-"""Summarise rocprofv3 --pmc CSVs for one kernel (per-launch means of each counter).
+"""Summarise rocprofv3 --pmc CSVs of the trace kernel (+ its bounce kernel): per-frame means of each counter.
 
-    python tools/pmc_summary.py [--kernel SUBSTR] [--out profiles/pmc/<name>.json
+    python tools/pmc_summary.py [--kernel SUBSTR[,SUBSTR..]] [--out profiles/pmc/<name>.json
                                  --config SCENE W H DEPTH NGPUS] CSV...
 
 With --out, also writes the HBM traffic record bench.py reads for `roofline.traffic`:
@@ -20,18 +20,23 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from reflaxman_amd import _lib  # noqa: E402
 
 
-def summarise(paths, kernel="trace_kernel<false"):
-    agg = collections.defaultdict(list)
+def summarise(paths, kernel="trace_kernel<false,bounce_kernel"):
+    """Per-frame counters: the mean per dispatch of each matching kernel (any of the comma-separated
+    substrings), summed over the kernels -- the trace kernel and, on regrouped frames, its bounce kernel,
+    each launched once per frame."""
+    keys = kernel.split(",")
+    agg = collections.defaultdict(lambda: collections.defaultdict(list))
     for p in paths:
         for r in csv.DictReader(open(p)):
-            if kernel in r["Kernel_Name"]:
-                agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in sorted(agg.items())}
+            name = r["Kernel_Name"]
+            if any(k in name for k in keys):
+                agg[r["Counter_Name"]][name].append(float(r["Counter_Value"]))
+    return {c: sum(sum(v) / len(v) for v in per.values()) for c, per in sorted(agg.items())}
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--kernel", default="trace_kernel<false")
+    ap.add_argument("--kernel", default="trace_kernel<false,bounce_kernel")
     ap.add_argument("--out")
     ap.add_argument("--config", nargs=5)
     ap.add_argument("--lib-sha256", default=None, help="build the counters came from (default: the in-tree librfx.so)")
