@@ -652,9 +652,17 @@ static void spatial_order(std::vector<uint32_t> &idx, size_t a, size_t b, const 
 }
 
 // Pair BVH of a large scene: leaves are the device sphere pairs (2j, 2j + 1, neighbours); internal nodes
-// split their pairs at the median of the pair centres along the longest axis.  Each node stores its two
+// split their pairs where the surface-area heuristic is lowest (every position of the pair centres sorted
+// along each axis), as long as the split keeps the tree within the kernel's stack depth, else at the
+// median of the pair centres along the longest axis.  Each node stores its two
 // children's boxes (spheres grown by their radii); the kernel widens them by its exact-cull margin per ray.
 // Returns the node index (or ~pair for a leaf) of range [a, b) of `pairs`; depth: internal levels below.
+#ifndef RFX_BVH_SAH  // pair BVH splits: surface-area heuristic (1) or median (0); tools/ab.py, C5: -0.8%
+#define RFX_BVH_SAH 1
+#endif
+#ifndef RFX_BVH_STACK
+#define RFX_BVH_STACK 16  // the kernel's per-lane traversal stack (rfx_trace.h kBvhStack)
+#endif
 namespace {
 struct PairBox { double lo[3], hi[3], c[3]; };
 
@@ -671,7 +679,50 @@ int build_pair_bvh(std::vector<BvhNode> &nodes, std::vector<uint32_t> &pairs, si
   int axis = 0;
   for (int k = 1; k < 3; ++k)
     if (hi[k] - lo[k] > hi[axis] - lo[axis]) axis = k;
-  const size_t mid = a + (b - a) / 2;
+  size_t mid = a + (b - a) / 2;
+#if RFX_BVH_SAH
+  // surface-area heuristic over sorted pair centres (all three axes, every split position), while the depth
+  // budget allows an unbalanced split: the subtree of n leaves must still fit RFX_BVH_STACK levels
+  const size_t cnt = b - a;
+  int need = 0;
+  while (((size_t)1 << need) < cnt) ++need;
+  if (level + need + 2 <= RFX_BVH_STACK && cnt > 2)
+  {
+    double best = INFINITY;
+    int best_axis = axis;
+    size_t best_mid = mid;
+    std::vector<uint32_t> tmp(pairs.begin() + a, pairs.begin() + b);
+    std::vector<double> right(cnt + 1);
+    auto area = [](const double *l, const double *h) {
+      const double dx = h[0] - l[0], dy = h[1] - l[1], dz = h[2] - l[2];
+      return dx * dy + dy * dz + dz * dx;
+    };
+    for (int ax = 0; ax < 3; ++ax)
+    {
+      std::sort(tmp.begin(), tmp.end(), [&](uint32_t x, uint32_t y) {
+        return box[x].c[ax] < box[y].c[ax] || (box[x].c[ax] == box[y].c[ax] && x < y);
+      });
+      double l[3] = {INFINITY, INFINITY, INFINITY}, h[3] = {-INFINITY, -INFINITY, -INFINITY};
+      for (size_t i = cnt; i-- > 0;)
+      {
+        for (int k = 0; k < 3; ++k) { l[k] = fmin(l[k], box[tmp[i]].lo[k]); h[k] = fmax(h[k], box[tmp[i]].hi[k]); }
+        right[i] = area(l, h) * (double)(cnt - i);
+      }
+      for (int k = 0; k < 3; ++k) { l[k] = INFINITY; h[k] = -INFINITY; }
+      // a split leaving at most 2^(budget - 1) leaves on each side keeps the depth bound
+      const size_t cap = (size_t)1 << std::min(30, RFX_BVH_STACK - level - 2);
+      for (size_t i = 1; i < cnt; ++i)
+      {
+        for (int k = 0; k < 3; ++k) { l[k] = fmin(l[k], box[tmp[i - 1]].lo[k]); h[k] = fmax(h[k], box[tmp[i - 1]].hi[k]); }
+        if (i > cap || cnt - i > cap) continue;
+        const double cost = area(l, h) * (double)i + right[i];
+        if (cost < best) { best = cost; best_axis = ax; best_mid = a + i; }
+      }
+    }
+    axis = best_axis;
+    mid = best_mid;
+  }
+#endif
   std::nth_element(pairs.begin() + a, pairs.begin() + mid, pairs.begin() + b, [&](uint32_t x, uint32_t y) {
     return box[x].c[axis] < box[y].c[axis] || (box[x].c[axis] == box[y].c[axis] && x < y);
   });
@@ -697,6 +748,9 @@ int build_pair_bvh(std::vector<BvhNode> &nodes, std::vector<uint32_t> &pairs, si
 
 #ifndef RFX_BVH_STACK
 #define RFX_BVH_STACK 16  // the kernel's per-lane traversal stack (rfx_trace.h kBvhStack)
+#endif
+#ifndef RFX_BVH_STACK16
+#define RFX_BVH_STACK16 1  // the kernel's stack slots are int16 (rfx_trace.h BvhSlot)
 #endif
 
 extern "C" int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *s)
@@ -855,6 +909,9 @@ extern "C" int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *s)
     for (size_t j = 0; j < npairs; ++j) pairs[j] = (uint32_t)j;
     build_pair_bvh(bvh, pairs, 0, npairs, box, 0, bvh_depth);
     if (bvh_depth > RFX_BVH_STACK) { bvh.clear(); bvh_depth = 0; }  // deeper than the kernel's stack: chunk loops
+#if RFX_BVH_STACK16
+    if (bvh.size() > 32767 || npairs > 32768) { bvh.clear(); bvh_depth = 0; }  // int16 stack slots
+#endif
   }
 #endif
   std::vector<PlaneGeo> pg;

@@ -582,7 +582,18 @@ constexpr int kBvhStack = 16;
 #define RFX_NARROW_BUNDLE_COS 0.9995f
 #endif
 constexpr float kNarrowBundleCos = RFX_NARROW_BUNDLE_COS;  // rfx_host.cpp RFX_BVH_STACK: deeper hierarchies fall back to the chunk loops
-__shared__ int32_t s_bvh_stack[kBvhStack * kWgThreads];
+// Stack slots: int16 node / ~pair indices (1; the host builds no BVH for 32768 or more nodes or pairs) or int32
+// (0).  Halving the stack's LDS (8 -> 4 KB per workgroup) makes C5 6.3% faster (tools/ab.py): workgroups
+// holding less LDS fit the CU's LDS with more slack as they finish out of order.
+#ifndef RFX_BVH_STACK16
+#define RFX_BVH_STACK16 1
+#endif
+#if RFX_BVH_STACK16
+typedef int16_t BvhSlot;
+#else
+typedef int32_t BvhSlot;
+#endif
+__shared__ BvhSlot s_bvh_stack[kBvhStack * kWgThreads];
 
 struct RayInv { float ix, iy, iz; };
 __device__ __forceinline__ RayInv ray_inv(v3 ray)
@@ -615,7 +626,7 @@ __device__ __forceinline__ void closest_spheres_bvh(const DevScene &S, v3 origin
 {
   const RayInv ri = ray_inv(ray);
   const float a = 0.5f * k.a2;                // |ray|^2 (exact: a2 = 2a)
-  int32_t *stack = s_bvh_stack + threadIdx.x;
+  BvhSlot *stack = s_bvh_stack + threadIdx.x;
   int sp = 0, node = 0;
   for (;;)
   {
@@ -670,7 +681,7 @@ __device__ __forceinline__ bool occluded_spheres_bvh(const DevScene &S, v3 o, v3
                                                      Cnt &cnt)
 {
   const RayInv ri = ray_inv(ray);
-  int32_t *stack = s_bvh_stack + threadIdx.x;
+  BvhSlot *stack = s_bvh_stack + threadIdx.x;
   int sp = 0, node = 0;
   float t, sq;
   for (;;)

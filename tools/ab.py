@@ -53,6 +53,8 @@ VARIANTS = {
     "every8": ["RFX_TILE_SORT_EVERY=8"],
     "wgtiles": ["RFX_WAVE_TILES=0"],
     "every16": ["RFX_TILE_SORT_EVERY=16"],
+    "stack32": ["RFX_BVH_STACK16=0"],
+    "median": ["RFX_BVH_SAH=0"],
 }
 
 
