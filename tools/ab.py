@@ -93,7 +93,7 @@ def build_scene_with(L, desc):
 
 
 class Runner:
-    def __init__(self, name, path, desc, W, H, depth, seed, tile_order=None):
+    def __init__(self, name, path, desc, W, H, depth, seed, tile_order=None, regroup=None):
         self.name = name
         L = self.L = _lib.bind(path)
         self.scene, eye, view, fov = build_scene_with(L, desc)
@@ -104,6 +104,8 @@ class Runner:
         assert L.rfx_renderer_set_rng(self.r, seed, 0) == 0
         if tile_order is not None:
             assert L.rfx_renderer_set_tile_order(self.r, tile_order) == 0
+        if regroup is not None:
+            assert L.rfx_renderer_set_regroup(self.r, regroup) == 0
         self.W, self.H = W, H
         self.img, self.argb = C.c_void_p(), C.c_void_p()
         assert L.rfx_device_alloc(self.r, W * H * 12, C.byref(self.img)) == 0
@@ -164,7 +166,10 @@ def cmd_run(args):
     if args.only:
         keep = set(args.only.split(","))
         paths, names = zip(*[(p, n) for p, n in zip(paths, names) if n in keep])
-    runners = [Runner(n, p, desc, args.width, args.height, args.depth, 1350490027) for n, p in zip(names, paths)]
+    # runtime variants: every build once per --regroup setting (rfx_renderer_set_regroup), named build@parkN
+    regroups = [None] if not args.regroup else [int(v) for v in args.regroup.split(",")]
+    runners = [Runner(n if g is None else f"{n}@park{g}", p, desc, args.width, args.height, args.depth, 1350490027,
+                      regroup=g) for n, p in zip(names, paths) for g in regroups]
     # parity of every variant: frame 1 against the reference's full-frame hash (when the manifest has one), and
     # frame 1 + LATER frames (rendered in the learned longest-tile-first order, after the tile sorts) against
     # the product build rendering the same frames in raster order
@@ -192,11 +197,11 @@ def cmd_run(args):
     out = []
     for r in runners:
         if not parity[r.name]:  # a variant that renders other pixels has no timing worth reporting
-            out.append({"variant": r.name, "defines": VARIANTS.get(r.name), "parity_sha_ok": False,
+            out.append({"variant": r.name, "defines": VARIANTS.get(r.name.split("@")[0]), "parity_sha_ok": False,
                         "timings": None})
             continue
         med = statistics.median(times[r.name])
-        out.append({"variant": r.name, "defines": VARIANTS.get(r.name), "parity_sha_ok": parity[r.name],
+        out.append({"variant": r.name, "defines": VARIANTS.get(r.name.split("@")[0]), "parity_sha_ok": parity[r.name],
                     "trace_ms_median": round(med, 4), "trace_ms_min": round(min(times[r.name]), 4),
                     "prepass_ms_median": round(statistics.median(pre[r.name]), 4),
                     "frame_ms_median": round(statistics.median(wall[r.name]), 4),
@@ -219,6 +224,7 @@ def main():
     ap.add_argument("--frames", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--later-frame", type=int, default=7, help="frame (1-based) also checked against raster order")
+    ap.add_argument("--regroup", default="", help="comma list of park_after settings to run each build with (0 = off)")
     args = ap.parse_args()
     if args.cmd == "build":
         cmd_build(args.variants.split(","))
