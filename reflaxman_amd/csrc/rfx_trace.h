@@ -1056,13 +1056,14 @@ struct Park {
   QRay *queue;
   uint32_t *count;
   uint32_t trace, out;  // this lane's randDir trace index and output pixel
+  __device__ __forceinline__ void ids(uint32_t &t, uint32_t &o) const { t = trace; o = out; }
 };
 
 // Scene::trace from a mid-trace state (mulc, pix after `refl` segments); park: see Park.  *parked: this lane's
 // trace was queued and its returned colour is not final.
-template <bool STATS, bool CULL, bool MANYL, bool SMALL, bool PLANES, bool PARK>
+template <bool STATS, bool CULL, bool MANYL, bool SMALL, bool PLANES, bool PARK, class PK>
 __device__ __forceinline__ col trace_from(const DevScene &S, v3 origin, v3 ray, col mulc, col pix, int refl, int depth,
-                                          v3 rd, const float *lut, Cnt &cnt, bool valid, const Park &park, bool &parked)
+                                          v3 rd, const float *lut, Cnt &cnt, bool valid, const PK &park, bool &parked)
 {
   parked = false;
   if (valid && refl == 0) RFX_CNT(C_RAYS);
@@ -1297,7 +1298,9 @@ __device__ __forceinline__ col trace_from(const DevScene &S, v3 origin, v3 ray, 
           q.ox = origin.x; q.oy = origin.y; q.oz = origin.z; q.dx = ray.x;
           q.dy = ray.y; q.dz = ray.z; q.mr = mulc.r; q.mg = mulc.g;
           q.mb = mulc.b; q.pr = pix.r; q.pg = pix.g; q.pb = pix.b;
-          q.trace = park.trace; q.out = park.out; q.refl = (uint32_t)refl; q.pad = 0;
+          uint32_t qt, qo;
+          park.ids(qt, qo);
+          q.trace = qt; q.out = qo; q.refl = (uint32_t)refl; q.pad = 0;
           park.queue[base + (uint32_t)__popcll(pm & ((1ull << __lane_id()) - 1ull))] = q;
           parked = true;
           alive = false;
@@ -1345,6 +1348,31 @@ __device__ __forceinline__ uint32_t strip_row_to_y(uint32_t r, const FrameParams
   const uint32_t blk = r / P.row_block, w = r % P.row_block;
   return (blk * P.nranks + P.rank) * P.row_block + w;
 }
+
+// the wave's schedule tile (index into the wave-tile grid), kept in LDS across the bounce loop
+__shared__ uint32_t s_tile8[kWgWaves];
+
+// Park info of a plain-pixel trace-kernel lane: its randDir trace index and output pixel are re-derived from the
+// wave's tile index in LDS when the trace parks (a fresh lane id through an empty asm), instead of being kept
+// live across the bounce loop (C3 park instantiation: 13 -> 2 VGPR spills)
+struct ParkTile {
+  int after;
+  QRay *queue;
+  uint32_t *count;
+  const FrameParams &P;
+  uint32_t wv, w8;
+  __device__ __forceinline__ void ids(uint32_t &t, uint32_t &o) const
+  {
+    const uint32_t t8 = ((volatile uint32_t *)s_tile8)[wv];
+    uint32_t le = __lane_id();
+    asm volatile("" : "+v"(le));
+    const uint32_t gx = (t8 % w8) * 8u + (le & 7u), gy = (t8 / w8) * 8u + (le >> 3);
+    const uint32_t y = P.nranks > 1 ? strip_row_to_y(gy, P) : gy + P.row0;
+    const uint32_t orow = P.nranks > 1 ? gy : y;
+    t = (uint32_t)((uint64_t)y * P.W + gx - P.p_begin);
+    o = (uint32_t)((size_t)orow * P.W + gx);
+  }
+};
 
 // trace i's randomInsideSphere draw (Vector3.cpp:176-188) from the LCG state before its accepted triple
 __device__ __forceinline__ v3 rd_from_state(uint32_t s)
@@ -1445,8 +1473,7 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
   const uint32_t gx = (t8 % w8) * 8u + (lane & 7u), gy = (t8 / w8) * 8u + (lane >> 3);
   // the tile index waits in LDS across the bounce loop: the epilogue re-derives the output coordinates from it
   // instead of keeping (spilling) them
-  __shared__ uint32_t s_t8[kWgWaves];
-  if (lane == 0) s_t8[wv] = t8;
+  if (lane == 0) s_tile8[wv] = t8;
   (void)tile;
 #else
   const uint32_t lx = (wave % kTileWavesX) * 8u + (lane & 7u), ly = (wave / kTileWavesX) * 8u + (lane >> 3);
@@ -1504,7 +1531,11 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
       const v3 ray = mmul(view, mk(rx + 0.0f + 0.0f, ry + 0.0f + 0.0f, P.rz));
       v3 rd = mk(0.0f, 0.0f, 0.0f);
       if (valid) rd = load_rd(P, pr);
+#if RFX_WAVE_TILES
+      const ParkTile park{P.park_after, P.queue, P.queue_count, P, wv, w8};
+#else
       const Park park{P.park_after, P.queue, P.queue_count, (uint32_t)pr, (uint32_t)((size_t)orow * P.W + x)};
+#endif
       const col c = trace_from<STATS, CULL, MANYL, SMALL, PLANES, PARK>(S, eye, ray, mkc(1.0f, 1.0f, 1.0f),
                                                                   mkc(0.0f, 0.0f, 0.0f), 0, P.depth, rd, lut, cnt,
                                                                   valid, park, parked);
@@ -1542,7 +1573,7 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
     }
 #if RFX_WAVE_TILES
     // output coordinates again, from the tile index in LDS (volatile: re-read, not kept live)
-    const uint32_t t8e = ((volatile uint32_t *)s_t8)[wv];
+    const uint32_t t8e = ((volatile uint32_t *)s_tile8)[wv];
     uint32_t le = lane;
     asm volatile("" : "+v"(le));  // a fresh lane value: its row/column are recomputed, not kept live
     const uint32_t x0e = (t8e % w8) * 8u, row0e = (t8e / w8) * 8u + (P.nranks > 1 ? 0u : P.row0);
