@@ -667,7 +667,7 @@ namespace {
 struct PairBox { double lo[3], hi[3], c[3]; };
 
 int build_pair_bvh(std::vector<BvhNode> &nodes, std::vector<uint32_t> &pairs, size_t a, size_t b,
-                   const std::vector<PairBox> &box, int level, int &depth)
+                   const std::vector<PairBox> &box, const double *ref, int level, int &depth)
 {
   if (b - a == 1) return ~(int)pairs[a];
   depth = std::max(depth, level + 1);
@@ -726,8 +726,8 @@ int build_pair_bvh(std::vector<BvhNode> &nodes, std::vector<uint32_t> &pairs, si
   std::nth_element(pairs.begin() + a, pairs.begin() + mid, pairs.begin() + b, [&](uint32_t x, uint32_t y) {
     return box[x].c[axis] < box[y].c[axis] || (box[x].c[axis] == box[y].c[axis] && x < y);
   });
-  const int kids[2] = {build_pair_bvh(nodes, pairs, a, mid, box, level + 1, depth),
-                       build_pair_bvh(nodes, pairs, mid, b, box, level + 1, depth)};
+  const int kids[2] = {build_pair_bvh(nodes, pairs, a, mid, box, ref, level + 1, depth),
+                       build_pair_bvh(nodes, pairs, mid, b, box, ref, level + 1, depth)};
   const size_t range[2][2] = {{a, mid}, {mid, b}};
   BvhNode &n = nodes[id];
   for (int c = 0; c < 2; ++c)
@@ -741,6 +741,10 @@ int build_pair_bvh(std::vector<BvhNode> &nodes, std::vector<uint32_t> &pairs, si
     n.hx[c] = nextafterf((float)h[0], INFINITY); n.hy[c] = nextafterf((float)h[1], INFINITY);
     n.hz[c] = nextafterf((float)h[2], INFINITY);
     n.child[c] = kids[c];
+    // margin term of the child against the reference point ref (the root box centre), rounded up
+    double mt = 0.0;
+    for (int k = 0; k < 3; ++k) mt += fabs(ref[k] - 0.5 * (l[k] + h[k])) + 0.5 * (h[k] - l[k]);
+    n.mt[c] = nextafterf((float)(mt * 1.0001), INFINITY);
   }
   return id;
 }
@@ -889,6 +893,7 @@ extern "C" int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *s)
   // pair BVH (large scenes; spheres of a pair whose second slot is padding: r2 = -inf, never hit)
   std::vector<BvhNode> bvh;
   int bvh_depth = 0;
+  double bvh_ref[3] = {0.0, 0.0, 0.0};
 #ifndef RFX_NO_BVH
   if (nsph > 32)
   {
@@ -907,7 +912,13 @@ extern "C" int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *s)
     }
     std::vector<uint32_t> pairs(npairs);
     for (size_t j = 0; j < npairs; ++j) pairs[j] = (uint32_t)j;
-    build_pair_bvh(bvh, pairs, 0, npairs, box, 0, bvh_depth);
+    for (int k = 0; k < 3; ++k)
+    {
+      double lo = INFINITY, hi = -INFINITY;
+      for (const PairBox &pb : box) { lo = fmin(lo, pb.lo[k]); hi = fmax(hi, pb.hi[k]); }
+      bvh_ref[k] = (double)(float)(0.5 * (lo + hi));  // the float the kernel measures from
+    }
+    build_pair_bvh(bvh, pairs, 0, npairs, box, bvh_ref, 0, bvh_depth);
     if (bvh_depth > RFX_BVH_STACK) { bvh.clear(); bvh_depth = 0; }  // deeper than the kernel's stack: chunk loops
 #if RFX_BVH_STACK16
     if (bvh.size() > 32767 || npairs > 32768) { bvh.clear(); bvh_depth = 0; }  // int16 stack slots
@@ -958,6 +969,7 @@ extern "C" int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *s)
   d.n_pln = (int32_t)pg.size();
   d.n_tex = (int32_t)tr.size();
   d.bvh_depth = bvh_depth;
+  d.bvh_rx = (float)bvh_ref[0]; d.bvh_ry = (float)bvh_ref[1]; d.bvh_rz = (float)bvh_ref[2];
   d.n_obj = (int32_t)loc.size();
   d.cull_valid = cull_valid;
   d.skybox_tex = s->skybox;

@@ -595,10 +595,14 @@ typedef int32_t BvhSlot;
 #endif
 __shared__ BvhSlot s_bvh_stack[kBvhStack * kWgThreads];
 
-struct RayInv { float ix, iy, iz; };
-__device__ __forceinline__ RayInv ray_inv(v3 ray)
+#ifndef RFX_BVH_NODE_MARGIN  // box margins from the node's stored term and one per-ray distance (1) or per box (0)
+#define RFX_BVH_NODE_MARGIN 1
+#endif
+struct RayInv { float ix, iy, iz, dm; };  // dm: kCullRel |o - bvh_ref|_1 + 1e-6 (RFX_BVH_NODE_MARGIN)
+__device__ __forceinline__ RayInv ray_inv(const DevScene &S, v3 o, v3 ray)
 {
-  return RayInv{__builtin_amdgcn_rcpf(ray.x), __builtin_amdgcn_rcpf(ray.y), __builtin_amdgcn_rcpf(ray.z)};
+  const float dm = kCullRel * (fabsf(o.x - S.bvh_rx) + fabsf(o.y - S.bvh_ry) + fabsf(o.z - S.bvh_rz)) + 1e-6f;
+  return RayInv{__builtin_amdgcn_rcpf(ray.x), __builtin_amdgcn_rcpf(ray.y), __builtin_amdgcn_rcpf(ray.z), dm};
 }
 
 // child c of node n against the ray: hit (conservative), and the entry parameter t (>= 0) of the widened box.
@@ -606,9 +610,14 @@ __device__ __forceinline__ RayInv ray_inv(v3 ray)
 __device__ __forceinline__ bool bvh_box(const BvhNode &n, int c, v3 o, const RayInv &ri, float &tn)
 {
   const float lx = n.lx[c], ly = n.ly[c], lz = n.lz[c], hx = n.hx[c], hy = n.hy[c], hz = n.hz[c];
+#if RFX_BVH_NODE_MARGIN
+  // |o - c|_1 + half-size_1 <= |o - ref|_1 + mt[c]: a margin at least the per-box one below
+  const float m = ri.dm + kCullRel * n.mt[c];
+#else
   const float cx = 0.5f * (lx + hx), cy = 0.5f * (ly + hy), cz = 0.5f * (lz + hz);
   const float m = kCullRel * (fabsf(o.x - cx) + fabsf(o.y - cy) + fabsf(o.z - cz) +
                               0.5f * ((hx - lx) + (hy - ly) + (hz - lz))) + 1e-6f;
+#endif
   const float ax = (lx - m - o.x) * ri.ix, bx = (hx + m - o.x) * ri.ix;
   const float ay = (ly - m - o.y) * ri.iy, by = (hy + m - o.y) * ri.iy;
   const float az = (lz - m - o.z) * ri.iz, bz = (hz + m - o.z) * ri.iz;
@@ -624,7 +633,7 @@ template <bool STATS>
 __device__ __forceinline__ void closest_spheres_bvh(const DevScene &S, v3 origin, v3 ray, const RayConst &k, Hit &h,
                                                     Cnt &cnt)
 {
-  const RayInv ri = ray_inv(ray);
+  const RayInv ri = ray_inv(S, origin, ray);
   const float a = 0.5f * k.a2;                // |ray|^2 (exact: a2 = 2a)
   BvhSlot *stack = s_bvh_stack + threadIdx.x;
   int sp = 0, node = 0;
@@ -680,7 +689,7 @@ template <bool STATS>
 __device__ __forceinline__ bool occluded_spheres_bvh(const DevScene &S, v3 o, v3 ray, const RayConst &k, int skip_sph,
                                                      Cnt &cnt)
 {
-  const RayInv ri = ray_inv(ray);
+  const RayInv ri = ray_inv(S, o, ray);
   BvhSlot *stack = s_bvh_stack + threadIdx.x;
   int sp = 0, node = 0;
   float t, sq;

@@ -50,7 +50,9 @@ struct alignas(16) CullRec { float x, y, z, r, nx, ny, nz, d; };
 // Bounding-volume hierarchy over the sphere pairs of a large scene (rfx_host.cpp build_pair_bvh): an internal
 // node holds its two children's boxes (the spheres grown by their radii) and their indices: c >= 0 an internal
 // node, c < 0 the leaf pair ~c (spheres 2(~c), 2(~c) + 1 of the device arrays, which are in Morton order).
-struct alignas(16) BvhNode { float lx[2], ly[2], lz[2], hx[2], hy[2], hz[2]; int32_t child[2], pad[2]; };
+// mt[c]: |ref - centre of child c|_1 + its L1 half-size (ref: DevScene::bvh_ref), so that kCullRel (|o - ref|_1 + mt[c])
+// bounds the kernel's per-ray box margin from above with one add per child (triangle inequality)
+struct alignas(16) BvhNode { float lx[2], ly[2], lz[2], hx[2], hy[2], hz[2]; int32_t child[2]; float mt[2]; };
 // Plane(pos, norm, material) (Plane.h:6-14): the normal as given (the reference never normalises it)
 struct alignas(16) PlaneGeo { float px, py, pz, nx, ny, nz; int32_t obj, dielectric; };
 struct alignas(16) LightRec { float ox, oy, oz, radius, r, g, b, power; }; // OmniLight.h
@@ -78,6 +80,7 @@ struct DevScene {
   int32_t n_sph, n_tri, n_light, skybox_tex;
   int32_t n_pln, n_obj, n_tex;
   int32_t bvh_depth;          // internal levels of the BVH (<= kBvhStack)
+  float bvh_rx, bvh_ry, bvh_rz;  // the BVH's margin reference point (its root box centre)
   int32_t n_chunk;            // (n_sph + 63) / 64
   float amb_r, amb_g, amb_b;  // diffLightColor * diffLightPower (Scene.cpp:186, host-folded)
   float env_r, env_g, env_b;  // envColor (Scene.cpp:12,55)

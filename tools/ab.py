@@ -54,6 +54,7 @@ VARIANTS = {
     "wgtiles": ["RFX_WAVE_TILES=0"],
     "every16": ["RFX_TILE_SORT_EVERY=16"],
     "stack32": ["RFX_BVH_STACK16=0"],
+    "boxmargin": ["RFX_BVH_NODE_MARGIN=0"],
     "median": ["RFX_BVH_SAH=0"],
 }
 
