@@ -27,10 +27,12 @@ def main():
     ap.add_argument("--height", type=int, default=2160)
     ap.add_argument("--depth", type=int, default=8)
     ap.add_argument("--lib", default="librfx_prof.so")
+    ap.add_argument("--regroup", type=int, default=None,
+                    help="rfx_renderer_set_regroup setting (large scenes: 0, since only the plain kernel is instrumented)")
     a = ap.parse_args()
     path = os.path.join(_build.LIBDIR, "diag", a.lib)
     scene = a.scene
-    r = ab.Runner("prof", path, scenes.get_scene(scene), a.width, a.height, a.depth, 1350490027)
+    r = ab.Runner("prof", path, scenes.get_scene(scene), a.width, a.height, a.depth, 1350490027, regroup=a.regroup)
     r.render(2)
     assert r.L.rfx_synchronize(r.r) == 0
     buf = (C.c_ulonglong * 16)()
