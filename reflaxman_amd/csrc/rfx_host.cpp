@@ -28,10 +28,10 @@ namespace rfx {
 uint64_t rng_blocks_for(uint64_t traces);
 void rng_jump_table(uint64_t nblk, uint32_t *out);
 hipError_t launch_rng_count(const uint32_t *d_seed, const uint32_t *d_jump, uint32_t *d_blk_cnt, uint64_t blk0,
-                            uint64_t nblk_slice, hipStream_t st);
+                            uint64_t nblk_slice, uint16_t *d_masks, hipStream_t st);
 hipError_t launch_rng_finish(const uint32_t *d_seed, const uint32_t *d_jump, uint32_t *d_next_seed,
-                             const uint32_t *d_blk_cnt, uint64_t nblk, uint64_t traces, uint32_t *d_rd_state,
-                             int *d_err, uint64_t ss2, uint64_t W, uint32_t row_block,
+                             const uint32_t *d_blk_cnt, const uint16_t *d_masks, uint64_t nblk, uint64_t traces,
+                             uint32_t *d_rd_state, int *d_err, uint64_t ss2, uint64_t W, uint32_t row_block,
                              uint32_t rank, uint32_t nranks, hipStream_t st);
 hipError_t launch_trace(const DevScene &S, const FrameParams &P, bool stats, hipStream_t st);
 uint32_t trace_tiles(const FrameParams &P);
@@ -459,6 +459,7 @@ struct rfx_renderer {
   // workspaces
   uint32_t *d_rd = nullptr; uint64_t rd_cap = 0;  // per-trace LCG states (rng_emit)
   uint32_t *d_blk_cnt = nullptr; uint64_t blk_cap = 0;
+  uint16_t *d_rng_masks = nullptr;  // one device's accept flags per pre-pass thread (rng_count -> rng_emit)
   uint32_t *d_jump = nullptr;  // LCG jump table for blk_cap blocks (rng_jump_table)
   // host staging for rfx_render_frame_host
   float *d_img = nullptr; uint32_t *d_argb = nullptr; uint64_t *d_cnt = nullptr; size_t img_cap = 0;
@@ -580,7 +581,7 @@ extern "C" void rfx_renderer_destroy(rfx_renderer *r)
   (void)hipStreamSynchronize(r->stream);
   free_scene(r);
   (void)hipFree(r->d_seed); (void)hipFree(r->d_err); (void)hipFree(r->d_rd);
-  (void)hipFree(r->d_blk_cnt); (void)hipFree(r->d_jump);
+  (void)hipFree(r->d_blk_cnt); (void)hipFree(r->d_jump); (void)hipFree(r->d_rng_masks);
   (void)hipFree(r->d_img); (void)hipFree(r->d_argb); (void)hipFree(r->d_cnt);
   (void)hipFree(r->d_queue); (void)hipFree(r->d_qctr);
   for (hipEvent_t e : r->events) (void)hipEventDestroy(e);
@@ -1031,9 +1032,10 @@ static int ensure_rng_workspace(rfx_renderer *r, uint64_t traces, uint64_t nblk)
   }
   if (nblk > r->blk_cap)
   {
-    (void)hipFree(r->d_blk_cnt); (void)hipFree(r->d_jump);
-    r->d_blk_cnt = nullptr; r->d_jump = nullptr; r->blk_cap = 0;
+    (void)hipFree(r->d_blk_cnt); (void)hipFree(r->d_jump); (void)hipFree(r->d_rng_masks);
+    r->d_blk_cnt = nullptr; r->d_jump = nullptr; r->d_rng_masks = nullptr; r->blk_cap = 0;
     HIP_CHECK(hipMalloc(&r->d_blk_cnt, nblk * sizeof(uint32_t)));
+    HIP_CHECK(hipMalloc(&r->d_rng_masks, nblk * 256 * sizeof(uint16_t)));
     std::vector<uint32_t> jump(2 * (256 + nblk));
     rng_jump_table(nblk, jump.data());
     HIP_CHECK(hipMalloc(&r->d_jump, jump.size() * sizeof(uint32_t)));
@@ -1050,9 +1052,9 @@ static int enqueue_rng(rfx_renderer *r, uint64_t traces, hipStream_t st)
   int rc;
   const uint64_t nblk = rng_layout(traces, 1, nullptr);
   if ((rc = ensure_rng_workspace(r, traces, nblk)) != RFX_OK) return rc;
-  HIP_CHECK(launch_rng_count(seed_cur(r), r->d_jump, r->d_blk_cnt, 0, nblk, st));
-  HIP_CHECK(launch_rng_finish(seed_cur(r), r->d_jump, seed_next(r), r->d_blk_cnt, nblk, traces, r->d_rd,
-                              r->d_err, 1, 1, 1, 0, 1, st));
+  HIP_CHECK(launch_rng_count(seed_cur(r), r->d_jump, r->d_blk_cnt, 0, nblk, r->d_rng_masks, st));
+  HIP_CHECK(launch_rng_finish(seed_cur(r), r->d_jump, seed_next(r), r->d_blk_cnt, r->d_rng_masks, nblk, traces,
+                              r->d_rd, r->d_err, 1, 1, 1, 0, 1, st));
   r->seed_idx ^= 1u;
   return RFX_OK;
 }
@@ -1086,7 +1088,7 @@ extern "C" int rfx_frame_rng_count(rfx_renderer *r, const rfx_frame *f, uint32_t
   uint64_t bps = 0;
   const uint64_t nblk = rng_layout(pl.traces, nslices, &bps);
   if ((rc = ensure_rng_workspace(r, pl.traces, nblk)) != RFX_OK) return rc;
-  HIP_CHECK(launch_rng_count(seed_cur(r), r->d_jump, d_blk_counts, (uint64_t)slice * bps, bps, pl.st));
+  HIP_CHECK(launch_rng_count(seed_cur(r), r->d_jump, d_blk_counts, (uint64_t)slice * bps, bps, nullptr, pl.st));
   return RFX_OK;
 }
 
@@ -1133,14 +1135,14 @@ static int tile_schedule(rfx_renderer *r, FrameParams &P, hipStream_t st, uint64
   return RFX_OK;
 }
 
-static int finish_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *d_counts, uint64_t nblk, float *d_rgb,
-                        uint32_t *d_argb, uint64_t *d_counters)
+static int finish_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *d_counts, const uint16_t *d_masks,
+                        uint64_t nblk, float *d_rgb, uint32_t *d_argb, uint64_t *d_counters)
 {
   int rc;
   FrameParams &P = pl.P;
   const hipStream_t st = pl.st;
   const uint64_t ss2 = P.ss > 0 ? (uint64_t)(P.ss * P.ss) : 1;
-  HIP_CHECK(launch_rng_finish(seed_cur(r), r->d_jump, seed_next(r), d_counts, nblk, pl.traces, r->d_rd,
+  HIP_CHECK(launch_rng_finish(seed_cur(r), r->d_jump, seed_next(r), d_counts, d_masks, nblk, pl.traces, r->d_rd,
                               r->d_err, ss2, P.W, P.row_block, P.rank, P.nranks, st));
   r->seed_idx ^= 1u;
   if ((rc = timing_event(r, st)) != RFX_OK) return rc;
@@ -1218,7 +1220,7 @@ extern "C" int rfx_render_frame_counted(rfx_renderer *r, const rfx_frame *f, uin
   const uint64_t nblk = rng_layout(pl.traces, nslices, nullptr);
   if ((rc = ensure_rng_workspace(r, pl.traces, nblk)) != RFX_OK) return rc;
   if ((rc = timing_event(r, pl.st)) != RFX_OK) return rc;
-  return finish_frame(r, pl, d_blk_counts, nblk, d_rgb, d_argb, d_counters);
+  return finish_frame(r, pl, d_blk_counts, nullptr, nblk, d_rgb, d_argb, d_counters);
 }
 
 extern "C" int rfx_render_frame(rfx_renderer *r, const rfx_frame *f, float *d_rgb, uint32_t *d_argb,
@@ -1232,8 +1234,9 @@ extern "C" int rfx_render_frame(rfx_renderer *r, const rfx_frame *f, float *d_rg
   const uint64_t nblk = rng_layout(pl.traces, 1, nullptr);
   if ((rc = ensure_rng_workspace(r, pl.traces, nblk)) != RFX_OK) return rc;
   if ((rc = timing_event(r, pl.st)) != RFX_OK) return rc;
-  HIP_CHECK(launch_rng_count(seed_cur(r), r->d_jump, r->d_blk_cnt, 0, nblk, pl.st));
-  return finish_frame(r, pl, r->d_blk_cnt, nblk, d_rgb, d_argb, d_counters);
+  // one device counts every block, so the emit can take its accept flags instead of regenerating them
+  HIP_CHECK(launch_rng_count(seed_cur(r), r->d_jump, r->d_blk_cnt, 0, nblk, r->d_rng_masks, pl.st));
+  return finish_frame(r, pl, r->d_blk_cnt, r->d_rng_masks, nblk, d_rgb, d_argb, d_counters);
 }
 
 static int plan_frame(rfx_renderer *r, const rfx_frame *f, void *stream, FramePlan &plan)

@@ -124,20 +124,23 @@ constexpr LcgJump lcg_jump_const(int draws)
 constexpr LcgJump kHalfJump = lcg_jump_const(3 * kHalfRun);
 
 // accepted-triple count of blocks [blk0, blk0 + gridDim.x): one slice of the stream (multi-GPU: one per rank)
+// masks (optional, one device): each thread's 16 accept flags, so that rng_emit regenerates only the LCG states
 __global__ __launch_bounds__(kRngBlock) void rng_count(const uint32_t *seed, const uint32_t *jump, uint32_t *blk_cnt,
-                                                       uint64_t blk0)
+                                                       uint64_t blk0, uint16_t *masks)
 {
   const uint64_t b = blk0 + blockIdx.x;
   uint32_t s = thread_state(*seed, jump, b, threadIdx.x);
   uint32_t s2 = kHalfJump.a * s + kHalfJump.c;
-  uint32_t c = 0;
+  uint32_t c = 0, acc = 0;
   float x, y, z;
 #pragma unroll
   for (int j = 0; j < kHalfRun; ++j)
   {
-    c += triple(s, x, y, z) ? 1u : 0u;
-    c += triple(s2, x, y, z) ? 1u : 0u;
+    const bool a = triple(s, x, y, z), a2 = triple(s2, x, y, z);
+    acc |= (a ? 1u : 0u) << j | (a2 ? 1u : 0u) << (j + kHalfRun);
+    c += (a ? 1u : 0u) + (a2 ? 1u : 0u);
   }
+  if (masks) masks[b * kRngBlock + threadIdx.x] = (uint16_t)acc;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
   __shared__ uint32_t wsum[kRngBlock / 64];
@@ -171,8 +174,8 @@ __device__ __forceinline__ bool owned(uint64_t idx, const EmitFilter &f)
 // coalesced 4-byte stores.  Trace i then re-derives its randDir from that state (rd_from_state): three
 // LCG steps and three exact conversions.
 __global__ __launch_bounds__(kRngBlock) void rng_emit(const uint32_t *seed, const uint32_t *jump, const uint32_t *blk_cnt,
-                                                      uint64_t need, uint32_t *rd_state, uint32_t *next_seed, int *err,
-                                                      EmitFilter flt)
+                                                      const uint16_t *masks, uint64_t need, uint32_t *rd_state,
+                                                      uint32_t *next_seed, int *err, EmitFilter flt)
 {
   __shared__ uint32_t sst[kTriplesPerBlock];
   __shared__ uint32_t wsum[kRngBlock / 64];
@@ -206,15 +209,32 @@ __global__ __launch_bounds__(kRngBlock) void rng_emit(const uint32_t *seed, cons
   uint32_t s2 = kHalfJump.a * s + kHalfJump.c;
   uint32_t st[kTriplesPerThread];
   uint32_t acc = 0, c = 0;
-  float x, y, z;
-#pragma unroll
-  for (int j = 0; j < kHalfRun; ++j)
+  if (masks)
   {
-    st[j] = s;
-    st[j + kHalfRun] = s2;
-    const bool a = triple(s, x, y, z), a2 = triple(s2, x, y, z);
-    acc |= (a ? 1u : 0u) << j | (a2 ? 1u : 0u) << (j + kHalfRun);
-    c += (a ? 1u : 0u) + (a2 ? 1u : 0u);
+    // the accept flags rng_count recorded: only the LCG states are regenerated (3 steps per triple)
+    acc = masks[(uint64_t)blockIdx.x * kRngBlock + threadIdx.x];
+    c = (uint32_t)__popc(acc);
+#pragma unroll
+    for (int j = 0; j < kHalfRun; ++j)
+    {
+      st[j] = s;
+      st[j + kHalfRun] = s2;
+      s = lcg_step(lcg_step(lcg_step(s)));
+      s2 = lcg_step(lcg_step(lcg_step(s2)));
+    }
+  }
+  else
+  {
+    float x, y, z;
+#pragma unroll
+    for (int j = 0; j < kHalfRun; ++j)
+    {
+      st[j] = s;
+      st[j + kHalfRun] = s2;
+      const bool a = triple(s, x, y, z), a2 = triple(s2, x, y, z);
+      acc |= (a ? 1u : 0u) << j | (a2 ? 1u : 0u) << (j + kHalfRun);
+      c += (a ? 1u : 0u) + (a2 ? 1u : 0u);
+    }
   }
   // exclusive scan of c across the workgroup
   const uint32_t lane = threadIdx.x & 63;
@@ -407,22 +427,23 @@ void rng_jump_table(uint64_t nblk, uint32_t *out)
 
 // first half of the pre-pass: accept counts of blocks [blk0, blk0 + nblk_slice)
 hipError_t launch_rng_count(const uint32_t *d_seed, const uint32_t *d_jump, uint32_t *d_blk_cnt, uint64_t blk0,
-                            uint64_t nblk_slice, hipStream_t st)
+                            uint64_t nblk_slice, uint16_t *d_masks, hipStream_t st)
 {
   if (nblk_slice)
-    hipLaunchKernelGGL(rng_count, dim3((uint32_t)nblk_slice), dim3(kRngBlock), 0, st, d_seed, d_jump, d_blk_cnt, blk0);
+    hipLaunchKernelGGL(rng_count, dim3((uint32_t)nblk_slice), dim3(kRngBlock), 0, st, d_seed, d_jump, d_blk_cnt, blk0,
+                       d_masks);
   return hipGetLastError();
 }
 
 // second half: scan all nblk counts, scatter the randDirs this rank needs, carry the stream state
 hipError_t launch_rng_finish(const uint32_t *d_seed, const uint32_t *d_jump, uint32_t *d_next_seed,
-                             const uint32_t *d_blk_cnt, uint64_t nblk, uint64_t traces, uint32_t *d_rd_state,
-                             int *d_err, uint64_t ss2, uint64_t W, uint32_t row_block,
+                             const uint32_t *d_blk_cnt, const uint16_t *d_masks, uint64_t nblk, uint64_t traces,
+                             uint32_t *d_rd_state, int *d_err, uint64_t ss2, uint64_t W, uint32_t row_block,
                              uint32_t rank, uint32_t nranks, hipStream_t st)
 {
   const EmitFilter flt{ss2 ? ss2 : 1, W ? W : 1, row_block ? row_block : 1, rank, nranks ? nranks : 1};
-  hipLaunchKernelGGL(rng_emit, dim3((uint32_t)nblk), dim3(kRngBlock), 0, st, d_seed, d_jump, d_blk_cnt, traces,
-                     d_rd_state, d_next_seed, d_err, flt);
+  hipLaunchKernelGGL(rng_emit, dim3((uint32_t)nblk), dim3(kRngBlock), 0, st, d_seed, d_jump, d_blk_cnt, d_masks,
+                     traces, d_rd_state, d_next_seed, d_err, flt);
   return hipGetLastError();
 }
 
