@@ -762,7 +762,7 @@ __device__ __forceinline__ bool occluded_planes(const DevScene &S, v3 o, v3 ray,
 }
 
 // Call with every lane of the wave active; `live` lanes trace (origin, ray).  B: the bundle, or null.
-// Large scenes: the spheres are stored in spatial (Morton) order, 64 to a chunk with a bounding sphere;
+// Large scenes: the spheres are stored in spatial order (recursive median splits), 64 to a chunk with a bounding sphere;
 // the bundle culls whole chunks (one lane per chunk), then the spheres of the surviving chunks.  The
 // visiting order is then not the insertion order, so spheres take the general (distance, object) rule.
 template <bool STATS, bool PLANES>
@@ -777,7 +777,7 @@ __device__ __forceinline__ void closest_hit(const DevScene &S, v3 origin, v3 ray
   uint32_t st_chunks = 0, st_sph = 0, st_pairs = 0;
 #endif
   RFX_PROF_BEGIN(P_SPH);
-  // a narrow bundle (the primary rays of a tile: one origin, a cone of ~0.1 degree) culls the Morton chunks and
+  // a narrow bundle (the primary rays of a tile: one origin, a cone of ~0.1 degree) culls the spatial chunks and
   // their spheres for the whole wave at once; wider ones walk the BVH lane by lane
   const bool use_bvh = !STATS && S.bvh != nullptr && !(cull && B->cosa > kNarrowBundleCos);
   if (use_bvh && live) closest_spheres_bvh<STATS>(S, origin, ray, k, h, cnt);

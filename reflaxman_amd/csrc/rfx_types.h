@@ -1,5 +1,5 @@
 // POD layouts shared by the host C-ABI (rfx_host.cpp) and the gfx950 kernels
-// (rfx_kernels.hip).  All device arrays are structure-of-arrays, 16-B aligned,
+// (rfx_trace.h, rfx_kernels.hip).  All device arrays are structure-of-arrays, 16-B aligned,
 // and walked in wave-uniform order by the trace kernel, so the compiler serves
 // them through the scalar cache (s_load_dwordx4) rather than per-lane loads.
 #pragma once
@@ -39,7 +39,7 @@ struct alignas(16) TriShade {                                        // Triangle
   float t11, t12, t21, t22;   // tuvTrans _11 _12 _21 _22 (_13 = _23 = 0 by construction)
   float tv0; int32_t tex; int32_t dielectric; int32_t obj;
 };
-// Bounding sphere of an object for the wave-bundle cull (rfx_kernels.hip): spheres first, then triangles.
+// Bounding sphere of an object for the wave-bundle cull (rfx_trace.h): spheres first, then triangles.
 // r = +inf marks an object that is never culled (an ill-conditioned triangle, see rfx_host.cpp).
 struct alignas(16) Bound { float x, y, z, r; };
 // Small scenes (<= 32 spheres, <= 32 triangles): one cull record per lane of a wave.  Lanes 0-15 hold
@@ -49,7 +49,7 @@ struct alignas(16) Bound { float x, y, z, r; };
 struct alignas(16) CullRec { float x, y, z, r, nx, ny, nz, d; };
 // Bounding-volume hierarchy over the sphere pairs of a large scene (rfx_host.cpp build_pair_bvh): an internal
 // node holds its two children's boxes (the spheres grown by their radii) and their indices: c >= 0 an internal
-// node, c < 0 the leaf pair ~c (spheres 2(~c), 2(~c) + 1 of the device arrays, which are in Morton order).
+// node, c < 0 the leaf pair ~c (spheres 2(~c), 2(~c) + 1 of the device arrays, which are in spatial order).
 // mt[c]: |ref - centre of child c|_1 + its L1 half-size (ref: DevScene::bvh_ref), so that kCullRel (|o - ref|_1 + mt[c])
 // bounds the kernel's per-ray box margin from above with one add per child (triangle inequality)
 struct alignas(16) BvhNode { float lx[2], ly[2], lz[2], hx[2], hy[2], hz[2]; int32_t child[2]; float mt[2]; };
@@ -70,7 +70,7 @@ struct DevScene {
   const TexRec *texs;         // n_tex
   const uint32_t *texels;     // texel pool, ARGB
   const Bound *bound;         // n_sph + n_tri bounding spheres
-  const Bound *chunk_bound;   // n_chunk bounding spheres of 64-sphere chunks (large scenes: Morton order)
+  const Bound *chunk_bound;   // n_chunk bounding spheres of 64-sphere chunks (large scenes: spatial order)
   const BvhNode *bvh;         // large scenes: pair BVH, root 0 (null: the chunk loops)
   const CullRec *cull_small;  // 64 lane records (small scenes only, else null)
   const PlaneGeo *pln_geo;    // n_pln (tested by every ray, never culled)

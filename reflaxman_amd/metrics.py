@@ -4,7 +4,7 @@ Counting rule: every f32 + - x / sqrt is 1 FLOP, compares,
 abs, clamps, selects and negations are 0, each powf is 1.  The weights are the
 operations the trace loop *needs* per event in our formulation (closest-hit
 candidates stop at their distance; drop/normal/reflection/texel are derived
-once, for the winner) -- read off reflaxman_amd/csrc/rfx_kernels.hip, which
+once, for the winner) -- read off reflaxman_amd/csrc/rfx_trace.h, which
 follows Scene.cpp:73-236 operation for operation.  The event counts come from
 the stats build of the same kernel (``trace_kernel<true>``) and are tested
 equal to the CPU restatement's (tests/test_gpu_parity.py).
