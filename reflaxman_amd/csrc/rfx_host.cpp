@@ -34,6 +34,7 @@ hipError_t launch_rng_finish(const uint32_t *d_seed, const uint32_t *d_jump, uin
                              uint32_t *d_rd_state, int *d_err, uint64_t ss2, uint64_t W, uint32_t row_block,
                              uint32_t rank, uint32_t nranks, hipStream_t st);
 hipError_t launch_trace(const DevScene &S, const FrameParams &P, bool stats, hipStream_t st);
+hipError_t launch_prim_cull(const DevScene &S, const FrameParams &P, uint64_t *masks, hipStream_t st);
 uint32_t trace_tiles(const FrameParams &P);
 size_t tile_order_scratch();
 hipError_t launch_tile_order(const uint32_t *cost, uint32_t n, uint32_t *order, uint32_t *scratch, hipStream_t st);
@@ -436,6 +437,9 @@ extern "C" uint32_t rfx_strip_row_to_y(uint32_t r, uint32_t rb, uint32_t rank, u
 #ifndef RFX_WAVE_TILES  // schedule unit: the wave's 8x8 tile (1) or the workgroup's 16x8 (0); tools/ab.py, C3: -2.7% trace
 #define RFX_WAVE_TILES 1
 #endif
+#ifndef RFX_PRIM_MASK  // small scenes: precomputed primary-bundle cull masks (1) or per-launch bundles (0)
+#define RFX_PRIM_MASK 1
+#endif
 #ifndef RFX_PARK_AFTER
 #define RFX_PARK_AFTER 3  // large-scene plain frames: segments before a live trace is parked for the bounce kernel
 #endif
@@ -478,6 +482,11 @@ struct rfx_renderer {
   // ray regrouping of large-scene plain frames (RFX_PARK_AFTER): parked traces, their count and the bounce
   // kernel's claim counter (d_qctr[0], d_qctr[1])
   int park_after = -1;  // rfx_renderer_set_regroup: -1 = default (RFX_PARK_AFTER on large scenes), 0 = off
+  // primary-bundle cull masks (small scenes, plain frames): one u64 per wave tile, valid for prim_key
+  uint64_t *d_prim_mask = nullptr;
+  size_t prim_cap = 0;
+  std::vector<uint8_t> prim_key;
+  uint64_t scene_gen = 0;  // bumped by every set_scene
   QRay *d_queue = nullptr;
   uint64_t queue_cap = 0;
   uint32_t *d_qctr = nullptr;
@@ -583,7 +592,7 @@ extern "C" void rfx_renderer_destroy(rfx_renderer *r)
   (void)hipFree(r->d_seed); (void)hipFree(r->d_err); (void)hipFree(r->d_rd);
   (void)hipFree(r->d_blk_cnt); (void)hipFree(r->d_jump); (void)hipFree(r->d_rng_masks);
   (void)hipFree(r->d_img); (void)hipFree(r->d_argb); (void)hipFree(r->d_cnt);
-  (void)hipFree(r->d_queue); (void)hipFree(r->d_qctr);
+  (void)hipFree(r->d_queue); (void)hipFree(r->d_qctr); (void)hipFree(r->d_prim_mask);
   for (hipEvent_t e : r->events) (void)hipEventDestroy(e);
   if (r->tile_stream) (void)hipStreamSynchronize(r->tile_stream);
   (void)hipFree(r->d_tile_cost); (void)hipFree(r->d_tile_order); (void)hipFree(r->d_tile_scratch);
@@ -853,11 +862,13 @@ extern "C" int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *s)
   }
   // small-scene lane table (rfx_types.h CullRec)
   std::vector<CullRec> cs;
+  std::vector<CullTri> ct;
   uint64_t cull_valid = 0;
   const bool small = s->spheres.size() <= 32 && s->tris.size() <= 32;
   if (small)
   {
     cs.assign(64, CullRec{});
+    ct.assign(32, CullTri{});
     for (size_t i = 0; i < s->spheres.size(); ++i)
     {
       const int lane = (int)(i & 1u) * 16 + (int)(i >> 1);
@@ -889,6 +900,36 @@ extern "C" int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *s)
       }
       cs[32 + i] = c;
       cull_valid |= 1ull << (32 + i);
+      // footprint record (primary-bundle masks): the dual rows of the basis (A, B, C) = (v2 - v0, v1 - v0, n) in
+      // double (the float inverse the reference computes differs by a relative ~cond eps, inside the test's
+      // margins); only for well-conditioned triangles (cond < 100)
+      CullTri q{};
+      q.v0x = t.v0.x; q.v0y = t.v0.y; q.v0z = t.v0.z;
+      q.nu = q.nv = q.nuv = INFINITY;
+      if (t.cond < 100.0 && c.nx * c.nx + c.ny * c.ny + c.nz * c.nz > 0.5f)
+      {
+        const double A[3] = {(double)t.v2.x - t.v0.x, (double)t.v2.y - t.v0.y, (double)t.v2.z - t.v0.z};
+        const double Bv[3] = {(double)t.v1.x - t.v0.x, (double)t.v1.y - t.v0.y, (double)t.v1.z - t.v0.z};
+        const double Cv[3] = {c.nx, c.ny, c.nz};
+        auto cross = [](const double *a, const double *b, double *o) {
+          o[0] = a[1] * b[2] - a[2] * b[1]; o[1] = a[2] * b[0] - a[0] * b[2]; o[2] = a[0] * b[1] - a[1] * b[0];
+        };
+        double bc[3], ca[3];
+        cross(Bv, Cv, bc);
+        cross(Cv, A, ca);
+        const double det = A[0] * bc[0] + A[1] * bc[1] + A[2] * bc[2];
+        if (fabs(det) > 0.0)
+        {
+          const double gu[3] = {bc[0] / det, bc[1] / det, bc[2] / det}, gv[3] = {ca[0] / det, ca[1] / det, ca[2] / det};
+          q.gux = (float)gu[0]; q.guy = (float)gu[1]; q.guz = (float)gu[2];
+          q.gvx = (float)gv[0]; q.gvy = (float)gv[1]; q.gvz = (float)gv[2];
+          q.nu = (float)(sqrt(gu[0] * gu[0] + gu[1] * gu[1] + gu[2] * gu[2]) * 1.001);
+          q.nv = (float)(sqrt(gv[0] * gv[0] + gv[1] * gv[1] + gv[2] * gv[2]) * 1.001);
+          const double s0 = gu[0] + gv[0], s1 = gu[1] + gv[1], s2 = gu[2] + gv[2];
+          q.nuv = (float)(sqrt(s0 * s0 + s1 * s1 + s2 * s2) * 1.001);
+        }
+      }
+      ct[i] = q;
     }
   }
   // pair BVH (large scenes; spheres of a pair whose second slot is padding: r2 = -inf, never hit)
@@ -959,7 +1000,7 @@ extern "C" int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *s)
       (rc = upload(r, si, &d.sph_info)) ||
       (rc = upload(r, tg, &d.tri_geo)) || (rc = upload(r, ts, &d.tri_shade)) || (rc = upload(r, tm, &d.tri_mat)) ||
       (rc = upload(r, lr, &d.lights)) || (rc = upload(r, tr, &d.texs)) || (rc = upload(r, pool, &d.texels)) ||
-      (rc = upload(r, bd, &d.bound)) || (rc = upload(r, cs, &d.cull_small)) || (rc = upload(r, cb, &d.chunk_bound)) ||
+      (rc = upload(r, bd, &d.bound)) || (rc = upload(r, cs, &d.cull_small)) || (rc = upload(r, ct, &d.cull_tri)) || (rc = upload(r, cb, &d.chunk_bound)) ||
       (rc = upload(r, pg, &d.pln_geo)) || (rc = upload(r, pm, &d.pln_mat)) || (rc = upload(r, loc, &d.obj_loc)) ||
       (rc = upload(r, bvh, &d.bvh)))
     return rc;
@@ -981,6 +1022,8 @@ extern "C" int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *s)
   d.half_tile_h = s->half_tile_h;
   r->dev = d;
   r->has_scene = true;
+  ++r->scene_gen;
+  r->prim_key.clear();
   return RFX_OK;
 }
 
@@ -1180,6 +1223,36 @@ static int finish_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *d_counts
   uint64_t key = 0;
   bool record = false;
   if (sched && (rc = tile_schedule(r, P, st, key, record)) != RFX_OK) return rc;
+  // primary-bundle cull masks: small scenes, plain frames, culling launches; recomputed only when the camera,
+  // the frame geometry or the scene changed (the bench's frames all reuse one set)
+  if (small && plain && !d_counters && !park && P.grid_rows && RFX_WAVE_TILES && RFX_PRIM_MASK)
+  {
+    struct Key { float cam[15]; uint32_t W, H, grid_rows, row0, row_block, rank, nranks; int32_t depth;
+                 uint64_t p_begin, p_end, gen; } k;
+    memset(&k, 0, sizeof(k));  // padding bytes too: the key is compared bytewise
+    const float cam[15] = {P.eye_x, P.eye_y, P.eye_z, P.v11, P.v12, P.v13, P.v21, P.v22, P.v23,
+                           P.v31, P.v32, P.v33, P.rz, P.wh, P.hh};
+    memcpy(k.cam, cam, sizeof(cam));
+    k.W = P.W; k.H = P.H; k.grid_rows = P.grid_rows; k.row0 = P.row0; k.row_block = P.row_block; k.rank = P.rank;
+    k.nranks = P.nranks; k.depth = P.depth > 0 ? 1 : 0; k.p_begin = P.p_begin; k.p_end = P.p_end; k.gen = r->scene_gen;
+    const size_t ntiles = trace_tiles(P);
+    std::vector<uint8_t> kb((const uint8_t *)&k, (const uint8_t *)&k + sizeof(k));
+    if (ntiles > r->prim_cap)
+    {
+      (void)hipFree(r->d_prim_mask);
+      r->d_prim_mask = nullptr;
+      r->prim_cap = 0;
+      HIP_CHECK(hipMalloc(&r->d_prim_mask, ntiles * sizeof(uint64_t)));
+      r->prim_cap = ntiles;
+      r->prim_key.clear();
+    }
+    if (kb != r->prim_key)
+    {
+      HIP_CHECK(launch_prim_cull(r->dev, P, r->d_prim_mask, st));
+      r->prim_key = kb;
+    }
+    P.prim_mask = r->d_prim_mask;
+  }
   if (P.grid_rows) HIP_CHECK(launch_trace(r->dev, P, d_counters != nullptr, st));
   if (park)
   {

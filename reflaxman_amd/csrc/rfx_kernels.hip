@@ -489,6 +489,14 @@ uint32_t trace_tiles(const FrameParams &P)
   return (RFX_WAVE_TILES ? kWgWaves : 1u) * g.x * g.y;
 }
 
+// the primary-bundle cull masks of a small scene's plain frame (prim_cull_kernel), one per wave tile
+hipError_t launch_prim_cull(const DevScene &S, const FrameParams &P, uint64_t *masks, hipStream_t st)
+{
+  const dim3 grid = trace_grid(P);
+  hipLaunchKernelGGL(prim_cull_kernel<0>, grid, dim3(kWgThreads), 0, st, S, P, masks);
+  return hipGetLastError();
+}
+
 hipError_t launch_trace(const DevScene &S, const FrameParams &P, bool stats, hipStream_t st)
 {
   const dim3 grid = trace_grid(P);

@@ -503,13 +503,47 @@ __device__ __forceinline__ uint64_t cull_chunk(const Bound *bound, int first, in
   return __ballot(keep);
 }
 
+// Triangle footprint (primary bundles, prim_cull_kernel): when every origin lies more than rw (plus a margin) on
+// one side of the plane and every direction heads into it (the cone's least cosine to the normal, ndmin, at
+// least 0.1), the crossing points lie in a disk around the axis ray's crossing P0 of radius
+//   R = h chord (1 + 1 / an) / ndmin + rw (1 + 1 / ndmin)
+// (h: the bundle centre's height over the plane, an: the axis's cosine to the normal, chord = |dir - axis| <=
+// sqrt(2 - 2 cosa): |dir / (n.dir) - a / (n.a)| <= |dir - a| (1 + 1 / n.a) / n.dir, and an origin offset d moves
+// a crossing by at most |d| (1 + 1 / n.dir)).  If that disk lies outside the triangle in (u, v) -- u or v below
+// 0, or u + v above 1, by more than R |gu|, R |gv|, R |gu + gv| -- no ray of the bundle can hit it.  Margins
+// cover the reference's float (u, v): its inverse basis and its t differ from the exact ones by a relative
+// ~150 eps for cond < 100, amplified at most 10x by 1 / ndmin; the margins are 1e-2 of |g| times the
+// distances involved (|o - v0| plus the travel to the plane).
+__device__ __forceinline__ bool tri_footprint_misses(const CullTri &q, float side, float an, const Bundle &B)
+{
+  const float h = fabsf(side), anp = side > 0.0f ? -an : an;  // height, cosine of the axis into the plane
+  const float snp = __builtin_amdgcn_sqrtf(fmaxf(1.0f - anp * anp, 0.0f));
+  const float ndmin = anp * B.cosa - snp * B.sina;
+  if (!(h > B.rw * 1.01f + 1e-4f && ndmin > 0.1f)) return false;
+  const float ind = __builtin_amdgcn_rcpf(ndmin) * 1.001f, ian = __builtin_amdgcn_rcpf(anp) * 1.001f;
+  const float tp = h * ian * (1.0f / 1.001f);                 // travel of the axis ray to the plane (approximate)
+  const float px = B.cx + tp * B.ax - q.v0x, py = B.cy + tp * B.ay - q.v0y, pz = B.cz + tp * B.az - q.v0z;
+  const float chord = __builtin_amdgcn_sqrtf(fmaxf(2.0f - 2.0f * B.cosa, 0.0f)) * 1.001f;
+  const float R = (h * chord * (1.0f + ian) * ind + B.rw * (1.0f + ind) + 1e-4f * tp) * 1.001f + 1e-6f;
+  // distances the reference's rounding scales with: |o - v0| <= |c - v0| + rw, travel <= (h + rw) / ndmin
+  const float cvx = B.cx - q.v0x, cvy = B.cy - q.v0y, cvz = B.cz - q.v0z;
+  const float mag = __builtin_amdgcn_sqrtf(cvx * cvx + cvy * cvy + cvz * cvz) * 1.001f + B.rw + (h + B.rw) * ind;
+  const float m = 1e-2f * mag + 1e-6f;
+  const float u0 = q.gux * px + q.guy * py + q.guz * pz, v0 = q.gvx * px + q.gvy * py + q.gvz * pz;
+  return u0 + (R + m) * q.nu < 0.0f || v0 + (R + m) * q.nv < 0.0f ||
+         u0 + v0 - R * q.nuv - m * (q.nu + q.nv) > 1.0f;
+}
+
 // Small scenes: lane l tests cull record l (rfx_types.h CullRec) -- the cone test of cull_chunk, and
 // for a triangle also its plane: when every origin lies more than rw (plus a margin) on one side and
 // every direction leaves that side (axis . n beyond sin of the cone's half-angle, plus a margin), every
 // ray has t <= 0 for the plane.  The reference's float test then sees -ao.z and ar.z of opposite signs
 // too: for a basis with cond <= 1000 their rounding error stays below 2e-4 of |o - v0| and |ray|, inside
-// the 1e-3 margins.  Bits of lanes without an object are cleared.
-__device__ __forceinline__ uint64_t cull_small(const CullRec *tab, uint64_t valid, const Bundle &B)
+// the 1e-3 margins.  FOOT (the precomputed primary masks only): triangles also take the footprint test above.
+// Bits of lanes without an object are cleared.
+template <bool FOOT = false>
+__device__ __forceinline__ uint64_t cull_small(const CullRec *tab, uint64_t valid, const Bundle &B,
+                                               const CullTri *ttab = nullptr)
 {
   const CullRec g = tab[threadIdx.x & 63u];
   const float vx = g.x - B.cx, vy = g.y - B.cy, vz = g.z - B.cz;
@@ -522,7 +556,9 @@ __device__ __forceinline__ uint64_t cull_small(const CullRec *tab, uint64_t vali
   const float an = g.nx * B.ax + g.ny * B.ay + g.nz * B.az;
   const float ms = B.rw + 1e-3f * (L + g.r + B.rw) + 1e-6f, ma = B.sina + 1e-3f;
   const bool away = (side > ms && an > ma) || (side < -ms && an < -ma);
-  const bool keep = !(L > rp && va < lim) && !away;
+  bool keep = !(L > rp && va < lim) && !away;
+  if constexpr (FOOT)
+    if ((threadIdx.x & 63u) >= 32u && keep) keep = !tri_footprint_misses(ttab[(threadIdx.x & 63u) - 32u], side, an, B);
   return __ballot(keep) & valid;
 }
 
@@ -1072,7 +1108,8 @@ struct Park {
 // trace was queued and its returned colour is not final.
 template <bool STATS, bool CULL, bool MANYL, bool SMALL, bool PLANES, bool PARK, class PK>
 __device__ __forceinline__ col trace_from(const DevScene &S, v3 origin, v3 ray, col mulc, col pix, int refl, int depth,
-                                          v3 rd, const float *lut, Cnt &cnt, bool valid, const PK &park, bool &parked)
+                                          v3 rd, const float *lut, Cnt &cnt, bool valid, const PK &park, bool &parked,
+                                          bool use_first = false, uint64_t first_om = 0)
 {
   parked = false;
   if (valid && refl == 0) RFX_CNT(C_RAYS);
@@ -1093,9 +1130,17 @@ __device__ __forceinline__ col trace_from(const DevScene &S, v3 origin, v3 ray, 
       uint64_t om = S.cull_valid;
       if constexpr (CULL)
       {
-        const Bundle B = make_bundle(origin, ray, alive);
-        if (B.ok) om = cull_small(T.cull(), S.cull_valid, B);
-        RFX_CULL_STAT(0, B.ok, __ballot(alive), om, S.cull_valid);
+        if (use_first)
+        {
+          om = first_om;  // the primary bundle's mask, precomputed for this tile (prim_cull_kernel)
+          use_first = false;
+        }
+        else
+        {
+          const Bundle B = make_bundle(origin, ray, alive);
+          if (B.ok) om = cull_small(T.cull(), S.cull_valid, B);
+          RFX_CULL_STAT(0, B.ok, __ballot(alive), om, S.cull_valid);
+        }
       }
       if (alive) closest_hit_small<STATS, PLANES>(S, origin, ray, om, h, cnt);
       else h.obj = -1;
@@ -1545,9 +1590,16 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
 #else
       const Park park{P.park_after, P.queue, P.queue_count, (uint32_t)pr, (uint32_t)((size_t)orow * P.W + x)};
 #endif
+#if RFX_WAVE_TILES
+      const bool use_pm = SMALL && CULL && !STATS && P.prim_mask != nullptr;
+      const uint64_t pm = use_pm ? P.prim_mask[t8] : 0ull;
+#else
+      const bool use_pm = false;
+      const uint64_t pm = 0ull;
+#endif
       const col c = trace_from<STATS, CULL, MANYL, SMALL, PLANES, PARK>(S, eye, ray, mkc(1.0f, 1.0f, 1.0f),
                                                                   mkc(0.0f, 0.0f, 0.0f), 0, P.depth, rd, lut, cnt,
-                                                                  valid, park, parked);
+                                                                  valid, park, parked, use_pm, pm);
       out = cadd(mkc(0.0f, 0.0f, 0.0f), c);                                      // Render.cpp:185 (/ 1.0f exact)
     }
     else
@@ -1617,6 +1669,39 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
   flush_counters<STATS>(P, cnt);
   RFX_PROF_FLUSH();
 
+}
+
+// Primary-bundle cull masks of a small scene's plain frame, one per wave tile (FrameParams::prim_mask): wave t8
+// builds its tile's primary rays exactly as trace_kernel does (same tile mapping, same validity), their bundle
+// (one origin: the eye) and its cull mask -- with the triangle footprint test, which the trace kernel could not
+// afford per segment.  The masks depend only on the camera, the frame and the scene, so the host recomputes
+// them only when those change.
+template <int UNUSED>  // a template: the header is compiled into several TUs, rfx_kernels.hip instantiates it
+__global__ RFX_TRACE_BOUNDS void prim_cull_kernel(DevScene S, FrameParams P, uint64_t *masks)
+{
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(wave);
+  const uint32_t w8 = kTileWavesX * gridDim.x;
+  const uint32_t t8 = (blockIdx.y * kTileWavesY + wv / kTileWavesX) * w8 + blockIdx.x * kTileWavesX + wv % kTileWavesX;
+  const uint32_t gx = (t8 % w8) * 8u + (lane & 7u), gy = (t8 / w8) * 8u + (lane >> 3);
+  const uint32_t x = gx;
+  const uint32_t y = P.nranks > 1 ? strip_row_to_y(gy, P) : gy + P.row0;
+  const uint64_t p = (uint64_t)y * P.W + x;
+  const bool valid = gx < P.W && gy < P.grid_rows && p >= P.p_begin && p < P.p_end && P.depth > 0;
+  m33 view;
+  view.m11 = P.v11; view.m12 = P.v12; view.m13 = P.v13;
+  view.m21 = P.v21; view.m22 = P.v22; view.m23 = P.v23;
+  view.m31 = P.v31; view.m32 = P.v32; view.m33 = P.v33;
+  const v3 eye = mk(P.eye_x, P.eye_y, P.eye_z);
+  const float rx = (float)x - P.wh, ry = (float)y - P.hh;                       // Render.cpp:152-153
+  const v3 ray = mmul(view, mk(rx + 0.0f + 0.0f, ry + 0.0f + 0.0f, P.rz));     // as trace_kernel (plain)
+  uint64_t om = 0;
+  if (__ballot(valid))
+  {
+    const Bundle B = make_bundle(eye, ray, valid);
+    om = B.ok ? cull_small<true>(S.cull_small, S.cull_valid, B, S.cull_tri) : S.cull_valid;
+  }
+  if (lane == 0) masks[t8] = om;
 }
 
 // The parked traces (rfx_types.h QRay) of a plain-pixel launch resumed in packed waves: each wave claims 64

@@ -47,6 +47,11 @@ struct alignas(16) Bound { float x, y, z, r; };
 // shift), lanes 32-63 triangles 0-31.  A triangle record also carries its plane (unit normal n, n . v0);
 // a sphere's or an empty lane's plane is zero.
 struct alignas(16) CullRec { float x, y, z, r, nx, ny, nz, d; };
+// Footprint record of small-scene triangle i (for the primary-bundle masks, prim_cull_kernel): vertex v0 and the
+// rows gu, gv of the inverse of the reference's basis [v2 - v0 | v1 - v0 | -norm] (Triangle.cpp:17-18), so that
+// u = gu . (P - v0) and v = gv . (P - v0) for P in the plane; nu = |gu|, nv = |gv|, nuv = |gu + gv| (+inf: the
+// footprint test must not touch the triangle -- ill-conditioned or degenerate).
+struct alignas(16) CullTri { float v0x, v0y, v0z, nu, gux, guy, guz, nv, gvx, gvy, gvz, nuv; };
 // Bounding-volume hierarchy over the sphere pairs of a large scene (rfx_host.cpp build_pair_bvh): an internal
 // node holds its two children's boxes (the spheres grown by their radii) and their indices: c >= 0 an internal
 // node, c < 0 the leaf pair ~c (spheres 2(~c), 2(~c) + 1 of the device arrays, which are in spatial order).
@@ -73,6 +78,7 @@ struct DevScene {
   const Bound *chunk_bound;   // n_chunk bounding spheres of 64-sphere chunks (large scenes: spatial order)
   const BvhNode *bvh;         // large scenes: pair BVH, root 0 (null: the chunk loops)
   const CullRec *cull_small;  // 64 lane records (small scenes only, else null)
+  const CullTri *cull_tri;    // 32 triangle footprint records (small scenes only, else null)
   const PlaneGeo *pln_geo;    // n_pln (tested by every ray, never culled)
   const MatRec *pln_mat;      // n_pln
   const int32_t *obj_loc;     // n_obj: object index -> kind << 28 | index within its kind's device arrays
@@ -124,6 +130,8 @@ struct FrameParams {
   QRay *queue;
   uint32_t *queue_count, *queue_next;
   int32_t park_after;
+  // small scenes, plain pixels: per wave tile, the cull mask of its primary bundle (prim_cull_kernel), or null
+  const uint64_t *prim_mask;
 };
 
 }  // namespace rfx

@@ -55,6 +55,7 @@ VARIANTS = {
     "every16": ["RFX_TILE_SORT_EVERY=16"],
     "stack32": ["RFX_BVH_STACK16=0"],
     "boxmargin": ["RFX_BVH_NODE_MARGIN=0"],
+    "noprim": ["RFX_PRIM_MASK=0"],
     "median": ["RFX_BVH_SAH=0"],
 }
 
