@@ -116,6 +116,11 @@ int rfx_renderer_set_tile_order(rfx_renderer *r, int mode);
  * no longer idle in their tile's wave).  -1 (default) = after 3 segments on scenes with more than 32 spheres
  * or triangles, off on small ones; 0 = off; n >= 1 = after n segments on any scene. */
 int rfx_renderer_set_regroup(rfx_renderer *r, int park_after);
+/* Primary-bundle cull masks of small-scene plain frames (no pixel changes): the first segment's cull mask of every
+ * 8x8 wave tile, computed by one extra launch for a view (camera, frame geometry, scene) and reused while the
+ * view stays.  1 (default) = built when a view repeats (the second frame of a still camera on), so a camera that
+ * moves every frame never pays for them; 2 = built before every launch; 0 = off (per-launch bundles). */
+int rfx_renderer_set_prim_masks(rfx_renderer *r, int mode);
 /* The reference's two LCG streams (trace_math.h:34-39): Vector3.cpp's (randomInsideSphere) and
  * Render.cpp's (additive jitter).  Both persist across frames exactly as the reference's would. */
 int rfx_renderer_set_rng(rfx_renderer *r, uint32_t sphere_seed, uint32_t jitter_seed);

@@ -440,6 +440,7 @@ extern "C" uint32_t rfx_strip_row_to_y(uint32_t r, uint32_t rb, uint32_t rank, u
 #ifndef RFX_PRIM_MASK  // small scenes: precomputed primary-bundle cull masks (1) or per-launch bundles (0)
 #define RFX_PRIM_MASK 1
 #endif
+
 #ifndef RFX_PARK_AFTER
 #define RFX_PARK_AFTER 3  // large-scene plain frames: segments before a live trace is parked for the bounce kernel
 #endif
@@ -485,8 +486,10 @@ struct rfx_renderer {
   // primary-bundle cull masks (small scenes, plain frames): one u64 per wave tile, valid for prim_key
   uint64_t *d_prim_mask = nullptr;
   size_t prim_cap = 0;
-  std::vector<uint8_t> prim_key;
+  std::vector<uint8_t> prim_key;   // the view the masks hold (empty: none)
+  std::vector<uint8_t> prim_seen;  // the view of the last plain small-scene launch
   uint64_t scene_gen = 0;  // bumped by every set_scene
+  int prim_mode = 1;       // rfx_renderer_set_prim_masks
   QRay *d_queue = nullptr;
   uint64_t queue_cap = 0;
   uint32_t *d_qctr = nullptr;
@@ -609,6 +612,15 @@ extern "C" int rfx_renderer_set_tile_order(rfx_renderer *r, int mode)
 {
   if (!r || mode < 0 || mode > 3) return fail(RFX_ERR_ARG, "renderer_set_tile_order: mode 0, 1, 2 or 3");
   r->tile_mode = mode;
+  return RFX_OK;
+}
+
+extern "C" int rfx_renderer_set_prim_masks(rfx_renderer *r, int mode)
+{
+  if (!r || mode < 0 || mode > 2) return fail(RFX_ERR_ARG, "renderer_set_prim_masks: mode 0, 1 or 2");
+  r->prim_mode = mode;
+  r->prim_key.clear();
+  r->prim_seen.clear();
   return RFX_OK;
 }
 
@@ -1024,6 +1036,7 @@ extern "C" int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *s)
   r->has_scene = true;
   ++r->scene_gen;
   r->prim_key.clear();
+  r->prim_seen.clear();
   return RFX_OK;
 }
 
@@ -1225,7 +1238,7 @@ static int finish_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *d_counts
   if (sched && (rc = tile_schedule(r, P, st, key, record)) != RFX_OK) return rc;
   // primary-bundle cull masks: small scenes, plain frames, culling launches; recomputed only when the camera,
   // the frame geometry or the scene changed (the bench's frames all reuse one set)
-  if (small && plain && !d_counters && !park && P.grid_rows && RFX_WAVE_TILES && RFX_PRIM_MASK)
+  if (small && plain && !d_counters && !park && P.grid_rows && RFX_WAVE_TILES && RFX_PRIM_MASK && r->prim_mode)
   {
     struct Key { float cam[15]; uint32_t W, H, grid_rows, row0, row_block, rank, nranks; int32_t depth;
                  uint64_t p_begin, p_end, gen; } k;
@@ -1245,13 +1258,22 @@ static int finish_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *d_counts
       HIP_CHECK(hipMalloc(&r->d_prim_mask, ntiles * sizeof(uint64_t)));
       r->prim_cap = ntiles;
       r->prim_key.clear();
+      r->prim_seen.clear();
     }
-    if (kb != r->prim_key)
+    // a view seen for the first time renders with per-launch bundles (a camera that moves every frame never pays
+    // for masks); the masks are built when the same view comes again, and kept while it stays
+    if (r->prim_mode == 2 || kb != r->prim_key)
     {
-      HIP_CHECK(launch_prim_cull(r->dev, P, r->d_prim_mask, st));
-      r->prim_key = kb;
+      const bool repeat = kb == r->prim_seen;
+      r->prim_seen = kb;
+      r->prim_key.clear();
+      if (repeat || r->prim_mode == 2)
+      {
+        HIP_CHECK(launch_prim_cull(r->dev, P, r->d_prim_mask, st));
+        r->prim_key = kb;
+      }
     }
-    P.prim_mask = r->d_prim_mask;
+    if (!r->prim_key.empty()) P.prim_mask = r->d_prim_mask;
   }
   if (P.grid_rows) HIP_CHECK(launch_trace(r->dev, P, d_counters != nullptr, st));
   if (park)

@@ -306,6 +306,11 @@ class Renderer:
         2 raster order with cost recording.  No pixel changes."""
         check(_lib.load().rfx_renderer_set_tile_order(self._h, int(mode)), "set_tile_order")
 
+    def set_prim_masks(self, mode: int):
+        """Primary-bundle cull masks of small-scene plain frames (rfx.h rfx_renderer_set_prim_masks): 1 built when
+        a view repeats (default), 2 before every launch, 0 off.  No pixel changes."""
+        check(_lib.load().rfx_renderer_set_prim_masks(self._h, int(mode)), "set_prim_masks")
+
     def set_regroup(self, park_after: int):
         """Ray regrouping (rfx.h rfx_renderer_set_regroup): -1 default (large scenes, after 3 segments), 0 off,
         n >= 1 park traces alive after n segments for the packed bounce kernel.  No pixel changes."""

@@ -412,3 +412,42 @@ def test_stress_band_without_regrouping(key):
     assert np.array_equal(argb[y0:y0 + rows], g["argb"])
     assert rgb[y0:y0 + rows].tobytes() == g["rgb"].tobytes()
     r.close()
+
+
+@pytest.mark.parametrize("key", ["hash_synth16_3840x2160_d8", "hash_default_640x480_d4", "hash_synth16_7680x4320_d8"])
+def test_primary_masks_match_reference_hash(key):
+    """Precomputed primary-bundle cull masks (rfx_renderer_set_prim_masks 2: built before the launch, so the
+    very first frame uses them): the full frame still hashes to the reference's."""
+    c = CASES[key]
+    rgb, argb, r = run_case(c, prim_masks=2)
+    assert sha(argb) == c["sha_argb"], key
+    assert sha(rgb) == c["sha_f32"], key
+    r.close()
+
+
+@pytest.mark.parametrize("key", sorted(k for k, c in CASES.items()
+                                       if c["kind"] == "render" and c.get("stored") and c["ss"] == 1
+                                       and not c["additive"] and c["W"] * c["H"] > 1))
+def test_primary_masks_on_goldens(key):
+    """Every stored one-sample golden with the masks built before the launch."""
+    c = CASES[key]
+    rgb, argb, r = run_case(c, prim_masks=2)
+    g = np.load(os.path.join(GOLDEN, key + ".npz"))
+    assert np.array_equal(argb, g["argb"]), key
+    assert rgb.tobytes() == g["rgb"].tobytes(), key
+    r.close()
+
+
+def test_primary_masks_over_repeated_views():
+    """A still camera over 4 frames (masks built on the second and reused) and a camera that alternates between
+    two views: every frame equals the frame rendered without masks."""
+    desc = scene("synth16")
+    W, H, depth = 640, 360, 8
+    frames = {}
+    for mode in (0, 1):
+        out = []
+        _, _, r = gpu_render(desc, W, H, depth, frames=4, prim_masks=mode,
+                             each_frame=lambda rgb, argb: out.append((rgb.tobytes(), argb.tobytes())))
+        r.close()
+        frames[mode] = out
+    assert frames[0] == frames[1]

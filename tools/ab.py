@@ -55,7 +55,6 @@ VARIANTS = {
     "every16": ["RFX_TILE_SORT_EVERY=16"],
     "stack32": ["RFX_BVH_STACK16=0"],
     "boxmargin": ["RFX_BVH_NODE_MARGIN=0"],
-    "noprim": ["RFX_PRIM_MASK=0"],
     "median": ["RFX_BVH_SAH=0"],
 }
 
@@ -95,7 +94,7 @@ def build_scene_with(L, desc):
 
 
 class Runner:
-    def __init__(self, name, path, desc, W, H, depth, seed, tile_order=None, regroup=None):
+    def __init__(self, name, path, desc, W, H, depth, seed, tile_order=None, regroup=None, prim=None):
         self.name = name
         L = self.L = _lib.bind(path)
         self.scene, eye, view, fov = build_scene_with(L, desc)
@@ -108,6 +107,8 @@ class Runner:
             assert L.rfx_renderer_set_tile_order(self.r, tile_order) == 0
         if regroup is not None:
             assert L.rfx_renderer_set_regroup(self.r, regroup) == 0
+        if prim is not None:
+            assert L.rfx_renderer_set_prim_masks(self.r, prim) == 0
         self.W, self.H = W, H
         self.img, self.argb = C.c_void_p(), C.c_void_p()
         assert L.rfx_device_alloc(self.r, W * H * 12, C.byref(self.img)) == 0
@@ -170,8 +171,10 @@ def cmd_run(args):
         paths, names = zip(*[(p, n) for p, n in zip(paths, names) if n in keep])
     # runtime variants: every build once per --regroup setting (rfx_renderer_set_regroup), named build@parkN
     regroups = [None] if not args.regroup else [int(v) for v in args.regroup.split(",")]
-    runners = [Runner(n if g is None else f"{n}@park{g}", p, desc, args.width, args.height, args.depth, 1350490027,
-                      regroup=g) for n, p in zip(names, paths) for g in regroups]
+    prims = [None] if not args.prim else [int(v) for v in args.prim.split(",")]
+    runners = [Runner(n + ("" if g is None else f"@park{g}") + ("" if q is None else f"@prim{q}"), p, desc, args.width,
+                      args.height, args.depth, 1350490027, regroup=g, prim=q)
+               for n, p in zip(names, paths) for g in regroups for q in prims]
     # parity of every variant: frame 1 against the reference's full-frame hash (when the manifest has one), and
     # frame 1 + LATER frames (rendered in the learned longest-tile-first order, after the tile sorts) against
     # the product build rendering the same frames in raster order
@@ -227,6 +230,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--later-frame", type=int, default=7, help="frame (1-based) also checked against raster order")
     ap.add_argument("--regroup", default="", help="comma list of park_after settings to run each build with (0 = off)")
+    ap.add_argument("--prim", default="", help="comma list of rfx_renderer_set_prim_masks modes to run each build with")
     args = ap.parse_args()
     if args.cmd == "build":
         cmd_build(args.variants.split(","))
