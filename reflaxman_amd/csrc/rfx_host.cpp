@@ -440,6 +440,7 @@ extern "C" uint32_t rfx_strip_row_to_y(uint32_t r, uint32_t rb, uint32_t rank, u
 #ifndef RFX_PRIM_MASK  // small scenes: precomputed primary-bundle cull masks (1) or per-launch bundles (0)
 #define RFX_PRIM_MASK 1
 #endif
+constexpr size_t kPrimWords = 5;  // per wave tile (rfx_trace.h kPrimStride)
 
 #ifndef RFX_PARK_AFTER
 #define RFX_PARK_AFTER 3  // large-scene plain frames: segments before a live trace is parked for the bounce kernel
@@ -1255,7 +1256,7 @@ static int finish_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *d_counts
       (void)hipFree(r->d_prim_mask);
       r->d_prim_mask = nullptr;
       r->prim_cap = 0;
-      HIP_CHECK(hipMalloc(&r->d_prim_mask, ntiles * sizeof(uint64_t)));
+      HIP_CHECK(hipMalloc(&r->d_prim_mask, ntiles * kPrimWords * sizeof(uint64_t)));
       r->prim_cap = ntiles;
       r->prim_key.clear();
       r->prim_seen.clear();

@@ -489,11 +489,14 @@ uint32_t trace_tiles(const FrameParams &P)
   return (RFX_WAVE_TILES ? kWgWaves : 1u) * g.x * g.y;
 }
 
-// the primary-bundle cull masks of a small scene's plain frame (prim_cull_kernel), one per wave tile
+// the per-view masks of a small scene's plain frame (prim_cull_kernel), kPrimStride words per wave tile
 hipError_t launch_prim_cull(const DevScene &S, const FrameParams &P, uint64_t *masks, hipStream_t st)
 {
   const dim3 grid = trace_grid(P);
-  hipLaunchKernelGGL(prim_cull_kernel<0>, grid, dim3(kWgThreads), 0, st, S, P, masks);
+  if (S.n_pln > 0)
+    hipLaunchKernelGGL(prim_cull_kernel<true>, grid, dim3(kWgThreads), 0, st, S, P, masks);
+  else
+    hipLaunchKernelGGL(prim_cull_kernel<false>, grid, dim3(kWgThreads), 0, st, S, P, masks);
   return hipGetLastError();
 }
 

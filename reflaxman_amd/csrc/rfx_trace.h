@@ -429,6 +429,10 @@ __device__ __forceinline__ bool plane_hit(const PlaneGeo &g, v3 o, v3 ray, float
 // decision is a conjunction of comparisons, so a NaN anywhere keeps the object.
 constexpr float kCullRel = 4e-3f;
 
+// per-view primary masks (prim_cull_kernel): per wave tile, the closest hit's mask and the shadow masks of the
+// first kPrimLights lights
+constexpr int kPrimLights = 4, kPrimStride = 1 + kPrimLights;
+
 struct Bundle {
   float cx, cy, cz, rw;
   float ax, ay, az, cosa, sina;
@@ -472,6 +476,37 @@ __device__ __forceinline__ Bundle make_bundle(v3 o, v3 d, bool live)
   const float dev = 1.0f - cosl;
   // a live lane with a non-finite or degenerate ray disables the bound for the whole wave
   const bool bad = live && !(e2 <= 1.0e30f && dev >= -0.5f && dev <= 2.5f);
+  const float e2m = wave_max_nonneg(live ? e2 : 0.0f);
+  const float devm = wave_max_nonneg(live ? fmaxf(dev, 0.0f) : 0.0f);
+  B.rw = __builtin_amdgcn_sqrtf(e2m) * 1.0001f;
+  B.cosa = 1.0f - devm - 4e-6f;                                                // approximate cosines: widen
+  B.sina = __builtin_amdgcn_sqrtf(fmaxf(1.0f - B.cosa * B.cosa, 0.0f) + 1e-7f) * 1.001f;
+  B.ok = __ballot(bad) == 0 && B.cosa > 0.1f && B.rw <= 1.0e15f;
+  return B;
+}
+
+// Bundle of every ray (o, d + rd R) with |rd| <= 1 of the `live` lanes (the shadow rays toward a light of radius R
+// for any randDir, Scene.cpp:128-129): make_bundle's cone widened per lane by the angular radius asin(R / |d|) of
+// the direction ball, cos(alpha + beta) = cos a cos b - sin a sin b.  A lane whose ball reaches its own origin's
+// side (R >= |d| / 2) disables the bound.  For the per-view primary shadow masks (prim_cull_kernel).
+__device__ __forceinline__ Bundle make_bundle_ball(v3 o, v3 d, float R, bool live)
+{
+  Bundle B;
+  const int ref = __ffsll((long long)__ballot(live)) - 1;
+  B.cx = lane_bcast(o.x, ref); B.cy = lane_bcast(o.y, ref); B.cz = lane_bcast(o.z, ref);
+  const float dx = lane_bcast(d.x, ref), dy = lane_bcast(d.y, ref), dz = lane_bcast(d.z, ref);
+  const float inv = __builtin_amdgcn_rsqf(dx * dx + dy * dy + dz * dz);
+  B.ax = dx * inv; B.ay = dy * inv; B.az = dz * inv;
+  const float ex = o.x - B.cx, ey = o.y - B.cy, ez = o.z - B.cz;
+  const float e2 = ex * ex + ey * ey + ez * ez;
+  const float d2 = d.x * d.x + d.y * d.y + d.z * d.z;
+  const float id = __builtin_amdgcn_rsqf(d2);
+  const float ca = fminf((d.x * B.ax + d.y * B.ay + d.z * B.az) * id, 1.0f);      // cos alpha (approximate)
+  const float sa = __builtin_amdgcn_sqrtf(fmaxf(1.0f - ca * ca, 0.0f));
+  const float sb = fminf(R * id * 1.001f, 1.0f), cb = __builtin_amdgcn_sqrtf(fmaxf(1.0f - sb * sb, 0.0f));
+  const float cosl = ca * cb - sa * sb;
+  const float dev = 1.0f - cosl;
+  const bool bad = live && !(e2 <= 1.0e30f && dev >= -0.5f && dev <= 2.5f && sb < 0.5f);
   const float e2m = wave_max_nonneg(live ? e2 : 0.0f);
   const float devm = wave_max_nonneg(live ? fmaxf(dev, 0.0f) : 0.0f);
   B.rw = __builtin_amdgcn_sqrtf(e2m) * 1.0001f;
@@ -1109,8 +1144,11 @@ struct Park {
 template <bool STATS, bool CULL, bool MANYL, bool SMALL, bool PLANES, bool PARK, class PK>
 __device__ __forceinline__ col trace_from(const DevScene &S, v3 origin, v3 ray, col mulc, col pix, int refl, int depth,
                                           v3 rd, const float *lut, Cnt &cnt, bool valid, const PK &park, bool &parked,
-                                          bool use_first = false, uint64_t first_om = 0)
+                                          const uint64_t *pm_tile = nullptr)
 {
+  // the first segment of a plain small-scene trace: this tile's per-view masks (prim_cull_kernel) -- the closest
+  // hit's, then one per light for its shadow rays
+  bool seg0 = pm_tile != nullptr;
   parked = false;
   if (valid && refl == 0) RFX_CNT(C_RAYS);
   const Tabs<SMALL> T{S};
@@ -1130,11 +1168,8 @@ __device__ __forceinline__ col trace_from(const DevScene &S, v3 origin, v3 ray, 
       uint64_t om = S.cull_valid;
       if constexpr (CULL)
       {
-        if (use_first)
-        {
-          om = first_om;  // the primary bundle's mask, precomputed for this tile (prim_cull_kernel)
-          use_first = false;
-        }
+        if (seg0)
+          om = pm_tile[0];  // the primary bundle's mask, precomputed for this tile's view (prim_cull_kernel)
         else
         {
           const Bundle B = make_bundle(origin, ray, alive);
@@ -1213,9 +1248,14 @@ __device__ __forceinline__ col trace_from(const DevScene &S, v3 origin, v3 ray, 
             uint64_t om = S.cull_valid;
             if constexpr (CULL)
             {
-              const Bundle SB = make_bundle(drop, sray, facing);
-              if (SB.ok) om = cull_small(T.cull(), S.cull_valid, SB);
-              RFX_CULL_STAT(1, SB.ok, __ballot(facing), om, S.cull_valid);
+              if (!MANYL && seg0 && q < kPrimLights)
+                om = pm_tile[1 + q];  // the primary hits' shadow mask for light q, precomputed for the view
+              else
+              {
+                const Bundle SB = make_bundle(drop, sray, facing);
+                if (SB.ok) om = cull_small(T.cull(), S.cull_valid, SB);
+                RFX_CULL_STAT(1, SB.ok, __ballot(facing), om, S.cull_valid);
+              }
             }
             if (facing && !occluded_small<STATS, PLANES>(S, drop, sray, skip_sph, skip_tri, skip_pln, om, cnt))
               lit |= 1u << q;
@@ -1337,6 +1377,7 @@ __device__ __forceinline__ col trace_from(const DevScene &S, v3 origin, v3 ray, 
       RFX_PROF_END(P_SKY);
       alive = false;
     }
+    seg0 = false;
     if constexpr (!STATS && PARK)
     {
       if (refl == park.after && __ballot(alive))
@@ -1591,15 +1632,13 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
       const Park park{P.park_after, P.queue, P.queue_count, (uint32_t)pr, (uint32_t)((size_t)orow * P.W + x)};
 #endif
 #if RFX_WAVE_TILES
-      const bool use_pm = SMALL && CULL && !STATS && P.prim_mask != nullptr;
-      const uint64_t pm = use_pm ? P.prim_mask[t8] : 0ull;
+      const uint64_t *pm_tile = SMALL && CULL && !STATS && P.prim_mask ? P.prim_mask + (size_t)kPrimStride * t8 : nullptr;
 #else
-      const bool use_pm = false;
-      const uint64_t pm = 0ull;
+      const uint64_t *pm_tile = nullptr;
 #endif
       const col c = trace_from<STATS, CULL, MANYL, SMALL, PLANES, PARK>(S, eye, ray, mkc(1.0f, 1.0f, 1.0f),
                                                                   mkc(0.0f, 0.0f, 0.0f), 0, P.depth, rd, lut, cnt,
-                                                                  valid, park, parked, use_pm, pm);
+                                                                  valid, park, parked, pm_tile);
       out = cadd(mkc(0.0f, 0.0f, 0.0f), c);                                      // Render.cpp:185 (/ 1.0f exact)
     }
     else
@@ -1671,14 +1710,19 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
 
 }
 
-// Primary-bundle cull masks of a small scene's plain frame, one per wave tile (FrameParams::prim_mask): wave t8
-// builds its tile's primary rays exactly as trace_kernel does (same tile mapping, same validity), their bundle
-// (one origin: the eye) and its cull mask -- with the triangle footprint test, which the trace kernel could not
-// afford per segment.  The masks depend only on the camera, the frame and the scene, so the host recomputes
-// them only when those change.
-template <int UNUSED>  // a template: the header is compiled into several TUs, rfx_kernels.hip instantiates it
+// Per-view masks of a small scene's plain frame (FrameParams::prim_mask), kPrimStride words per wave tile t8:
+// [0] the cull mask of the tile's primary bundle, [1 + q] that of its primary hits' shadow rays toward light q
+// for every randDir (q < kPrimLights).  Wave t8 builds its tile's primary rays exactly as trace_kernel does (same
+// tile mapping, same validity), their bundle (one origin: the eye) and cull mask -- with the triangle footprint
+// test, which the trace kernel could not afford per segment -- then the primary hits with the same closest-hit
+// code and that mask, and per light the bundle of all shadow rays of the facing lanes (make_bundle_ball).  The
+// masks depend only on the view (camera, frame geometry, scene), so the host builds them once per view.
+template <bool PLANES>
 __global__ RFX_TRACE_BOUNDS void prim_cull_kernel(DevScene S, FrameParams P, uint64_t *masks)
 {
+  stage_small_scene(S);
+  __syncthreads();
+  const Tabs<true> T{S};
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(wave);
   const uint32_t w8 = kTileWavesX * gridDim.x;
@@ -1695,13 +1739,54 @@ __global__ RFX_TRACE_BOUNDS void prim_cull_kernel(DevScene S, FrameParams P, uin
   const v3 eye = mk(P.eye_x, P.eye_y, P.eye_z);
   const float rx = (float)x - P.wh, ry = (float)y - P.hh;                       // Render.cpp:152-153
   const v3 ray = mmul(view, mk(rx + 0.0f + 0.0f, ry + 0.0f + 0.0f, P.rz));     // as trace_kernel (plain)
+  uint64_t *out = masks + (size_t)kPrimStride * t8;
   uint64_t om = 0;
   if (__ballot(valid))
   {
     const Bundle B = make_bundle(eye, ray, valid);
-    om = B.ok ? cull_small<true>(S.cull_small, S.cull_valid, B, S.cull_tri) : S.cull_valid;
+    om = B.ok ? cull_small<true>(T.cull(), S.cull_valid, B, S.cull_tri) : S.cull_valid;
   }
-  if (lane == 0) masks[t8] = om;
+  if (lane == 0) out[0] = om;
+  // the primary hits, as trace_from's first segment finds them with this mask (Scene.cpp:86-106)
+  Cnt cnt;
+  Hit h;
+  if (valid) closest_hit_small<false, PLANES>(S, eye, ray, om, h, cnt);
+  else h.obj = -1;
+  const bool hit = valid && h.obj >= 0;
+  v3 drop = eye, norm = mk(0.0f, 0.0f, 0.0f);
+  if (hit)
+  {
+    drop = add(eye, mul(ray, h.t));
+    if (h.kind == 0)
+    {
+      const SphereGeo g = T.sph_geo(h.i);
+      norm = sub(drop, mk(g.cx, g.cy, g.cz));                                    // Sphere.cpp:67
+    }
+    else if (!PLANES || h.kind == 1)
+    {
+      const TriShade sh = T.tri_shade(h.i);
+      norm = mk(sh.nx, sh.ny, sh.nz);
+    }
+    else
+    {
+      const PlaneGeo g = S.pln_geo[h.i];
+      norm = mk(g.nx, g.ny, g.nz);                                               // Plane.cpp:58-59
+    }
+  }
+  const int nl = min(S.n_light, kPrimLights);
+  for (int q = 0; q < nl; ++q)
+  {
+    const LightRec L = S.lights[q];
+    const v3 dtl = sub(mk(L.ox, L.oy, L.oz), drop);
+    const bool facing = hit && dot(dtl, norm) > kVerySmall;                      // Scene.cpp:125
+    uint64_t sm = 0;
+    if (__ballot(facing))
+    {
+      const Bundle SB = make_bundle_ball(drop, dtl, L.radius, facing);
+      sm = SB.ok ? cull_small(T.cull(), S.cull_valid, SB) : S.cull_valid;
+    }
+    if (lane == 0) out[1 + q] = sm;
+  }
 }
 
 // The parked traces (rfx_types.h QRay) of a plain-pixel launch resumed in packed waves: each wave claims 64

@@ -451,3 +451,19 @@ def test_primary_masks_over_repeated_views():
         r.close()
         frames[mode] = out
     assert frames[0] == frames[1]
+
+
+def test_primary_masks_full_size_frames():
+    """C3 at full size over 6 frames (masks built on the second frame and reused): every frame equals the frame
+    rendered without masks (the first also equals the reference's hash)."""
+    c = CASES["hash_synth16_3840x2160_d8"]
+    hashes = {}
+    for mode in (0, 1):
+        out = []
+        _, _, r = gpu_render(scene(c["scene"]), c["W"], c["H"], c["depth"], frames=6, prim_masks=mode,
+                             sphere_seed=c["sphere_seed"],
+                             each_frame=lambda rgb, argb: out.append((sha(rgb), sha(argb))))
+        r.close()
+        hashes[mode] = out
+    assert hashes[0][0] == (c["sha_f32"], c["sha_argb"])
+    assert hashes[0] == hashes[1]
