@@ -193,6 +193,8 @@ def main():
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (gloo: multi-rank rehearsal)")
     ap.add_argument("--one-device", action="store_true", help="all ranks on cuda:0 (rehearsal on a 1-GPU box)")
     ap.add_argument("--no-pipeline", action="store_true", help="N > 1: gather each frame's strips before the next frame")
+    ap.add_argument("--no-count-ahead", action="store_true",
+                    help="N > 1: count and all-gather each frame's RNG blocks on its critical path, not during the last trace")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -243,7 +245,8 @@ def main():
         # the own strips, ARGB8 strip gather to rank 0 + device un-interleave (reflaxman_amd/dist.py)
         from reflaxman_amd.dist import RfxStripOps, StripFrame
         sf = StripFrame(RfxStripOps(rr, frame, stream.cuda_stream), W, H, rb, rank, world, dev,
-                        pipeline=False if args.no_pipeline else None, gather_rgb=args.gather_rgb)
+                        pipeline=False if args.no_pipeline else None, gather_rgb=args.gather_rgb,
+                        count_ahead=False if args.no_count_ahead else None)
         rows, img, argb = sf.rows, sf.img, sf.argb
     else:
         rows = H
@@ -296,6 +299,8 @@ def main():
             ok_a = sha(first_argb.tobytes()) == man[key]["sha_argb"]
             parity["full_frame_vs_reference_sha256"] = {"f32": ok_f, "argb8": ok_a, "case": key}
     counters = torch.zeros(_lib.RFX_NCOUNTERS, dtype=torch.int64, device=dev)
+    if world > 1:
+        sf.drop_lookahead()  # the counted frame below advances the random stream itself (every rank)
     rr.render_frame(frame, img.data_ptr(), argb.data_ptr(), counters.data_ptr(), stream.cuda_stream)
     torch.cuda.synchronize()
     cnt = counters.cpu().numpy().astype(np.uint64)
@@ -379,7 +384,7 @@ def main():
     # HBM traffic and executed VALU work of the trace kernel: rocprofv3 --pmc passes of this very workload
     # and library build (tools/prof_round.sh -> profiles/pmc/), per launch; null when no such record exists
     pmc = metrics.pmc_record(os.path.join(ROOT, "profiles", "pmc"), [args.scene, W, H, depth, world],
-                             _lib.lib_sha256())
+                             _lib.lib_sha256(), _lib.device_sha256())
     traffic = pmc["hbm_bytes_per_launch"] if pmc else None
     workload = (c_desc if not custom else f"{args.scene} scene") + f", {W}x{H}, depth {depth}, 1 spp"
     if world > 1:
@@ -392,7 +397,7 @@ def main():
         "config": {"workload": workload, "name": None if custom else cfg_name.upper(),
                    "scene": args.scene, "width": W, "height": H, "depth": depth, "spp": 1,
                    "parallelism": (f"row-strips{rb}x{world}" + ("+pipelined-gather" if sf.pipeline else ""))
-                                  if world > 1 else "single-gpu"},
+                                  + ("+count-ahead" if sf.count_ahead else "") if world > 1 else "single-gpu"},
         "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": metrics.PEAK_FP32_VALU_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved / metrics.PEAK_FP32_VALU_TFLOPS, 4),
                      "traffic": traffic, "kernel": "rfx::trace_kernel (plain pixel mode, wave-bundle culling)",

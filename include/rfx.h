@@ -171,6 +171,13 @@ int rfx_frame_rng_count(rfx_renderer *r, const rfx_frame *frame, uint32_t slice,
                         uint32_t *d_blk_counts, void *stream);
 int rfx_render_frame_counted(rfx_renderer *r, const rfx_frame *frame, uint32_t nslices, const uint32_t *d_blk_counts,
                              float *d_rgb, uint32_t *d_argb, uint64_t *d_counters, void *stream);
+/* The same, recording the caller's hipEvent_t `emitted_event` on `stream` once the randDirs are emitted, before the
+ * trace: from then on the next frame's stream state is on the device, so the next frame's rfx_frame_rng_count and
+ * all-gather may run on another stream while this frame traces (reflaxman_amd/dist.py count-ahead).  The renderer's
+ * RNG stream must not advance in between (no other render call on this renderer). */
+int rfx_render_frame_counted_ev(rfx_renderer *r, const rfx_frame *frame, uint32_t nslices,
+                                const uint32_t *d_blk_counts, float *d_rgb, uint32_t *d_argb, uint64_t *d_counters,
+                                void *stream, void *emitted_event);
 
 /* Optional per-phase timing of rfx_render_frame with HIP events recorded on the launch stream:
  * enable, render, then read the summed device time (ms) of the RNG pre-pass and of the trace kernel

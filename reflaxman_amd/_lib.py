@@ -75,6 +75,8 @@ SIGNATURES = [
     ("rfx_frame_rng_count", C.c_int, [C.c_void_p, C.POINTER(Frame), C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p]),
     ("rfx_render_frame_counted", C.c_int, [C.c_void_p, C.POINTER(Frame), C.c_uint32, C.c_void_p, C.c_void_p,
                                            C.c_void_p, C.c_void_p, C.c_void_p]),
+    ("rfx_render_frame_counted_ev", C.c_int, [C.c_void_p, C.POINTER(Frame), C.c_uint32, C.c_void_p, C.c_void_p,
+                                              C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     ("rfx_renderer_set_timing", C.c_int, [C.c_void_p, C.c_int]),
     ("rfx_renderer_set_tile_order", C.c_int, [C.c_void_p, C.c_int]),
     ("rfx_renderer_set_prim_masks", C.c_int, [C.c_void_p, C.c_int]),
@@ -139,6 +141,24 @@ def lib_sha256(path: str = None) -> str:
     import hashlib
     with open(path or _build.LIB, "rb") as f:
         return hashlib.sha256(f.read()).hexdigest()
+
+
+def device_sha256(path: str = None) -> str:
+    """SHA-256 of the library's device code (its .hip_fatbin ELF section: every kernel's code object).  Host-only
+    changes leave it alone (the build is deterministic), so it keys the PMC records of profiles/pmc to the
+    kernels they measured; None if the section is absent."""
+    import hashlib
+    import struct
+    with open(path or _build.LIB, "rb") as f:
+        b = f.read()
+    shoff = struct.unpack_from("<Q", b, 0x28)[0]
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", b, 0x3A)
+    secs = [struct.unpack_from("<IIQQQQIIQQ", b, shoff + i * shentsize) for i in range(shnum)]
+    names = secs[shstrndx][4]
+    for name_off, _, _, _, off, size, *_ in secs:
+        if b[names + name_off:b.index(b"\0", names + name_off)] == b".hip_fatbin":
+            return hashlib.sha256(b[off:off + size]).hexdigest()
+    return None
 
 
 def check(rc: int, what: str = "") -> int:

@@ -1193,7 +1193,8 @@ static int tile_schedule(rfx_renderer *r, FrameParams &P, hipStream_t st, uint64
 }
 
 static int finish_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *d_counts, const uint16_t *d_masks,
-                        uint64_t nblk, float *d_rgb, uint32_t *d_argb, uint64_t *d_counters)
+                        uint64_t nblk, float *d_rgb, uint32_t *d_argb, uint64_t *d_counters,
+                        hipEvent_t emitted = nullptr)
 {
   int rc;
   FrameParams &P = pl.P;
@@ -1202,6 +1203,9 @@ static int finish_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *d_counts
   HIP_CHECK(launch_rng_finish(seed_cur(r), r->d_jump, seed_next(r), d_counts, d_masks, nblk, pl.traces, r->d_rd,
                               r->d_err, ss2, P.W, P.row_block, P.rank, P.nranks, st));
   r->seed_idx ^= 1u;
+  // the caller's event: the randDirs are written and the next frame's stream state is known (the next frame's
+  // RNG count may start on another stream while this frame traces)
+  if (emitted) HIP_CHECK(hipEventRecord(emitted, st));
   if ((rc = timing_event(r, st)) != RFX_OK) return rc;
   P.img = d_rgb;
   P.argb = d_argb;
@@ -1308,6 +1312,13 @@ extern "C" int rfx_render_frame_counted(rfx_renderer *r, const rfx_frame *f, uin
                                         const uint32_t *d_blk_counts, float *d_rgb, uint32_t *d_argb,
                                         uint64_t *d_counters, void *stream)
 {
+  return rfx_render_frame_counted_ev(r, f, nslices, d_blk_counts, d_rgb, d_argb, d_counters, stream, nullptr);
+}
+
+extern "C" int rfx_render_frame_counted_ev(rfx_renderer *r, const rfx_frame *f, uint32_t nslices,
+                                           const uint32_t *d_blk_counts, float *d_rgb, uint32_t *d_argb,
+                                           uint64_t *d_counters, void *stream, void *emitted_event)
+{
   FramePlan pl;
   int rc;
   if ((rc = plan_frame(r, f, stream, pl)) != RFX_OK) return rc;
@@ -1316,7 +1327,7 @@ extern "C" int rfx_render_frame_counted(rfx_renderer *r, const rfx_frame *f, uin
   const uint64_t nblk = rng_layout(pl.traces, nslices, nullptr);
   if ((rc = ensure_rng_workspace(r, pl.traces, nblk)) != RFX_OK) return rc;
   if ((rc = timing_event(r, pl.st)) != RFX_OK) return rc;
-  return finish_frame(r, pl, d_blk_counts, nullptr, nblk, d_rgb, d_argb, d_counters);
+  return finish_frame(r, pl, d_blk_counts, nullptr, nblk, d_rgb, d_argb, d_counters, (hipEvent_t)emitted_event);
 }
 
 extern "C" int rfx_render_frame(rfx_renderer *r, const rfx_frame *f, float *d_rgb, uint32_t *d_argb,

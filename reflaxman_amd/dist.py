@@ -43,15 +43,38 @@ class RfxStripOps:
         _lib.check(self.L.rfx_frame_rng_blocks(self.r._h, C.byref(self.frame), nslices, C.byref(bps)), "rng_blocks")
         return bps.value
 
-    def rng_count(self, slice_: int, nslices: int, d_counts: int):
+    def rng_count(self, slice_: int, nslices: int, d_counts: int, stream: int = 0):
+        """Count the accepted triples of slice `slice_` of the NEXT frame's stream (from the state the last emit
+        left), on `stream` (default: the ops' stream)."""
         _lib.check(self.L.rfx_frame_rng_count(self.r._h, C.byref(self.frame), slice_, nslices, C.c_void_p(d_counts),
-                                              C.c_void_p(self.stream or None)), "rng_count")
+                                              C.c_void_p(stream or self.stream)), "rng_count")
 
-    def render_counted(self, nslices: int, d_counts: int, d_img: int, d_argb: int, d_counters: int = 0):
-        _lib.check(self.L.rfx_render_frame_counted(self.r._h, C.byref(self.frame), nslices, C.c_void_p(d_counts),
-                                                   C.c_void_p(d_img), C.c_void_p(d_argb or None),
-                                                   C.c_void_p(d_counters or None), C.c_void_p(self.stream or None)),
+    def render_counted(self, nslices: int, d_counts: int, d_img: int, d_argb: int, d_counters: int = 0,
+                       emitted_event: int = 0):
+        """Scan the all-gathered counts, emit this rank's randDirs (then record `emitted_event`, a hipEvent_t,
+        if given) and trace its strips."""
+        _lib.check(self.L.rfx_render_frame_counted_ev(self.r._h, C.byref(self.frame), nslices, C.c_void_p(d_counts),
+                                                      C.c_void_p(d_img), C.c_void_p(d_argb or None),
+                                                      C.c_void_p(d_counters or None), C.c_void_p(self.stream or None),
+                                                      C.c_void_p(emitted_event or None)),
                    "render_frame_counted")
+
+
+class _Done:
+    """An exchange that already completed (gloo on CPU)."""
+
+    def wait(self):
+        pass
+
+
+class _EventWork:
+    """A completed-on-device step as a work object: wait() orders the current stream after it."""
+
+    def __init__(self, ev):
+        self.ev = ev
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.ev)
 
 
 def strip_rows(H: int, row_block: int, rank: int, world: int) -> int:
@@ -82,10 +105,17 @@ class StripFrame:
     all-gather) while frame i+1 renders; strip and gather buffers are double-buffered, and rank 0
     un-interleaves on a side stream.  A frame's assembled image is complete once the device is
     synchronised (every step's work, gathers included, is on the device's streams).
+
+    count_ahead (default: on for the nccl backend): frame i+1's RNG count and its all-gather (a third
+    communicator, on a side stream) start as soon as frame i's randDirs are emitted -- the next frame's
+    stream state is then on the device -- and run while frame i traces, so the exchange step leaves the
+    per-frame critical path (count, all-gather, emit, trace becomes emit, trace).  The renderer's random
+    stream must not advance between steps by any other call (drop_lookahead() first, on every rank).
     """
 
     def __init__(self, ops, W: int, H: int, row_block: int, rank: int, world: int, device: torch.device,
-                 gather_to_root: bool = True, pipeline: Optional[bool] = None, gather_rgb: bool = False):
+                 gather_to_root: bool = True, pipeline: Optional[bool] = None, gather_rgb: bool = False,
+                 count_ahead: Optional[bool] = None):
         self.ops, self.W, self.H, self.rb = ops, W, H, row_block
         self.rank, self.world, self.device = rank, world, device
         self.gather_to_root = gather_to_root
@@ -126,15 +156,52 @@ class StripFrame:
         self.works: List[list] = [[] for _ in range(nbuf)]
         self.done: List[Optional[torch.cuda.Event]] = [None] * nbuf
         self.frame = 0
+        if count_ahead is None:
+            count_ahead = world > 1 and dist.get_backend() == "nccl"
+        # (asked for explicitly it also runs at world 1: the device-side ordering test, tests/test_gpu_multirank.py)
+        self.count_ahead = bool(count_ahead) and not self._host_staged()
+        self.count_group = dist.new_group(list(range(world))) if self.count_ahead else None
+        self.count_stream = torch.cuda.Stream(device=device) if self.count_ahead and cuda else None
+        self.emitted = torch.cuda.Event() if self.count_ahead and cuda else None
+        if self.emitted is not None:
+            self.emitted.record(torch.cuda.current_stream(device))  # torch creates the hipEvent_t at its first record
+        self.ahead = None  # the next frame's count all-gather in flight (its work object), once one is
+
+    def _count_next(self):
+        """Count the next frame's slice and start its all-gather, ordered after this frame's emit only."""
+        if self.count_stream is None:  # CPU (gloo orchestration tests): the ops are synchronous
+            self.ops.rng_count(self.rank, self.world, self.counts.data_ptr())
+            self.ahead = self._all_gather_counts(group=self.count_group, async_op=True) or _Done()
+            return
+        with torch.cuda.stream(self.count_stream):
+            self.count_stream.wait_event(self.emitted)
+            self.ops.rng_count(self.rank, self.world, self.counts.data_ptr(), stream=self.count_stream.cuda_stream)
+            self.ahead = self._all_gather_counts(group=self.count_group, async_op=True)
+        if self.ahead is None:  # completed on the side stream: order the next emit after it
+            ev = torch.cuda.Event()
+            ev.record(self.count_stream)
+            self.ahead = _EventWork(ev)
+
+    def drop_lookahead(self):
+        """Complete and discard the next frame's counts (call on every rank before anything else advances the
+        renderer's random stream); the next step counts afresh."""
+        if self.ahead is not None:
+            self.ahead.wait()
+            if self.count_stream is not None:
+                torch.cuda.current_stream(self.device).wait_stream(self.count_stream)
+        self.ahead = None
 
     def _host_staged(self) -> bool:
         # gloo on device tensors (a multi-rank rehearsal on one GPU): stage the collectives through host memory
         return self.device.type == "cuda" and dist.get_backend() != "nccl"
 
-    def _all_gather_counts(self):
+    def _all_gather_counts(self, group=None, async_op: bool = False):
         mine = self.counts[self.rank * self.bps:(self.rank + 1) * self.bps]
         if dist.get_backend() == "nccl":
-            dist.all_gather_into_tensor(self.counts, mine.clone())
+            return dist.all_gather_into_tensor(self.counts, mine.clone(), group=group, async_op=async_op)
+        if async_op:  # gloo on CPU (the orchestration tests): the exchange completes here
+            dist.all_gather(list(self.counts.split(self.bps)), mine.clone(), group=group)
+            return None
         elif self._host_staged():
             h = self.counts.cpu()
             dist.all_gather(list(h.split(self.bps)), h[self.rank * self.bps:(self.rank + 1) * self.bps].clone())
@@ -184,10 +251,18 @@ class StripFrame:
         argb = self.argb_bufs[k]
         img = self.img_bufs[k % len(self.img_bufs)]
         self.argb, self.img = argb, img
-        self.ops.rng_count(self.rank, self.world, self.counts.data_ptr())
-        if self.world > 1:
-            self._all_gather_counts()
-        self.ops.render_counted(self.world, self.counts.data_ptr(), img.data_ptr(), argb.data_ptr(), d_counters)
+        if self.ahead is not None:
+            # this frame's counts were all-gathered while the last frame traced: order this stream after them
+            self.ahead.wait()
+        else:
+            self.ops.rng_count(self.rank, self.world, self.counts.data_ptr())
+            if self.world > 1:
+                self._all_gather_counts()
+        self.ahead = None
+        self.ops.render_counted(self.world, self.counts.data_ptr(), img.data_ptr(), argb.data_ptr(), d_counters,
+                                self.emitted.cuda_event if self.emitted is not None else 0)
+        if self.count_ahead:
+            self._count_next()
         if self.world == 1 or not self.gather_to_root:
             return argb[: self.rows * self.W].view(self.rows, self.W) if self.world == 1 else None
         if not self.pipeline:

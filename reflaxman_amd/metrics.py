@@ -113,15 +113,18 @@ def summary(counts) -> dict:
     }
 
 
-def pmc_record(directory: str, config, lib_sha: str):
-    """The rocprofv3 --pmc record (tools/pmc_summary.py --out) of this workload and library build, or None."""
+def pmc_record(directory: str, config, lib_sha: str, device_sha: str = None):
+    """The rocprofv3 --pmc record (tools/pmc_summary.py --out) of this workload and of this library build -- the
+    same library file, or the same device code (its .hip_fatbin section, _lib.device_sha256) -- or None."""
     if not os.path.isdir(directory):
         return None
     for name in sorted(os.listdir(directory)):
         if not name.endswith(".json"):
             continue
         rec = json.load(open(os.path.join(directory, name)))
-        if rec.get("config") == list(config) and rec.get("lib_sha256") == lib_sha:
+        if rec.get("config") != list(config):
+            continue
+        if rec.get("lib_sha256") == lib_sha or (device_sha and rec.get("device_sha256") == device_sha):
             return rec
     return None
 

@@ -17,23 +17,26 @@ from reflaxman_amd import _lib
 
 
 class FakeOps:
-    """Slice counts = slice * 1000 + block; strip pixels = (frame row << 12) | x."""
+    """Slice counts of the n-th count call = slice * 1000 + 100 * n + block (so a frame that traced with another
+    frame's counts shows); strip pixels = (frame row << 12) | x."""
 
     def __init__(self, W, H, rb, rank, world, bps=5):
         self.W, self.H, self.rb, self.rank, self.world, self.bps = W, H, rb, rank, world, bps
         self.seen_counts = None
         self.frame = 0
+        self.ncount = 0
 
     def blocks_per_slice(self, nslices):
         return self.bps
 
-    def rng_count(self, slice_, nslices, d_counts):
+    def rng_count(self, slice_, nslices, d_counts, stream=0):
         t = torch.from_numpy(__import__("numpy").ctypeslib.as_array(
             (__import__("ctypes").c_int32 * (nslices * self.bps)).from_address(d_counts)))
         for b in range(self.bps):
-            t[slice_ * self.bps + b] = slice_ * 1000 + b
+            t[slice_ * self.bps + b] = slice_ * 1000 + 100 * self.ncount + b
+        self.ncount += 1
 
-    def render_counted(self, nslices, d_counts, d_img, d_argb, d_counters=0):
+    def render_counted(self, nslices, d_counts, d_img, d_argb, d_counters=0, emitted_event=0):
         import ctypes
         import numpy as np
         cnt = np.ctypeslib.as_array((ctypes.c_int32 * (nslices * self.bps)).from_address(d_counts)).copy()
@@ -53,18 +56,21 @@ def rgb_pattern(frame, y, W):
     return (frame * 100000 + y * 100 + np.arange(3 * W) % 3 + 10 * (np.arange(3 * W) // 3)).astype(np.float32)
 
 
-def _worker(rank, world, port, W, H, rb, pipeline, q, gather_rgb=False):
+def _worker(rank, world, port, W, H, rb, pipeline, q, gather_rgb=False, count_ahead=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         ops = FakeOps(W, H, rb, rank, world)
         sf = rdist.StripFrame(ops, W, H, rb, rank, world, torch.device("cpu"), pipeline=pipeline,
-                              gather_rgb=gather_rgb)
-        assert sf.pipeline == pipeline
-        expect = [s * 1000 + b for s in range(world) for b in range(ops.bps)]
+                              gather_rgb=gather_rgb, count_ahead=count_ahead)
+        assert sf.pipeline == pipeline and sf.count_ahead == count_ahead
         ok_counts = ok_frame = True
-        for frame in range(3):  # three frames: both buffer sets of the pipeline, one of them reused
+        for frame in range(4):  # four frames: both buffer sets of the pipeline, each reused
+            if frame == 2:
+                sf.drop_lookahead()  # the counts of a look-ahead are discarded: frame 2 counts afresh
             out = sf.step()
+            n = frame + 1 if count_ahead and frame >= 2 else frame  # the count call whose counts frame uses
+            expect = [s * 1000 + 100 * n + b for s in range(world) for b in range(ops.bps)]
             ok_counts &= ops.seen_counts.tolist() == expect
             if rank == 0:
                 ys, xs = torch.meshgrid(torch.arange(H), torch.arange(W), indexing="ij")
@@ -88,13 +94,16 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("pipeline,gather_rgb", [(False, False), (True, False), (False, True), (True, True)])
+@pytest.mark.parametrize("pipeline,gather_rgb,count_ahead", [(False, False, False), (True, False, False),
+                                                              (False, True, False), (True, True, False),
+                                                              (False, False, True), (True, True, True)])
 @pytest.mark.parametrize("W,H,rb", [(16, 37, 4), (8, 64, 8), (5, 3, 8)])
-def test_strip_frame_world2_gloo(W, H, rb, pipeline, gather_rgb):
+def test_strip_frame_world2_gloo(W, H, rb, pipeline, gather_rgb, count_ahead):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, W, H, rb, pipeline, q, gather_rgb)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, W, H, rb, pipeline, q, gather_rgb, count_ahead))
+             for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:

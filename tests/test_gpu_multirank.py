@@ -34,3 +34,58 @@ def test_bench_multirank_frame_matches_single_gpu(world):
     assert out["n_gpus"] == world
     assert out["parity"]["multi_rank_frame_equals_single_gpu"] is True
     assert out["value"] > 0
+
+
+def _count_ahead_worker():
+    """Rank 0 of 1 over RCCL: StripFrame with count-ahead (the next frame's RNG count and its all-gather on a side
+    stream after the emit event) over 6 frames, against the same frames from rfx_render_frame."""
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    from reflaxman_amd import scenes
+    from reflaxman_amd.dist import RfxStripOps, StripFrame
+    from reflaxman_amd.render import Renderer, build_scene, make_frame
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        scene, cam = build_scene(scenes.get_scene("synth16"))
+        W, H, D, seed = 640, 360, 8, 1350490027
+        stream = torch.cuda.Stream(device=dev)
+        torch.cuda.set_stream(stream)
+        ra, rb = Renderer(device=0, sphere_seed=seed), Renderer(device=0, sphere_seed=seed)
+        for r in (ra, rb):
+            r.set_scene(scene)
+            r.set_stream(stream.cuda_stream)
+        sf = StripFrame(RfxStripOps(ra, make_frame(cam, W, H, D, 1), stream.cuda_stream), W, H, 8, 0, 1, dev,
+                        count_ahead=True)
+        assert sf.count_ahead and sf.ahead is None
+        fb = make_frame(cam, W, H, D, 1)
+        img = torch.zeros(H * W * 3, dtype=torch.float32, device=dev)
+        argb = torch.zeros(H * W, dtype=torch.int32, device=dev)
+        ok = []
+        for i in range(6):
+            if i == 4:
+                sf.drop_lookahead()  # frame 4 counts afresh on the main stream
+            out = sf.step().clone()
+            rb.render_frame(fb, img.data_ptr(), argb.data_ptr(), 0, stream.cuda_stream)
+            ok.append(bool(torch.equal(out.reshape(-1), argb)) and bool(torch.equal(sf.img[: H * W * 3], img)))
+        torch.cuda.synchronize()
+        print(json.dumps({"frames_equal": ok}))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_count_ahead_rccl_frames_equal_plain_frames():
+    env = {**os.environ, "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(_port())}
+    r = subprocess.run([sys.executable, os.path.abspath(__file__), "count_ahead"], capture_output=True, text=True,
+                       timeout=300, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["frames_equal"] == [True] * 6, out
+
+
+if __name__ == "__main__" and sys.argv[1:] == ["count_ahead"]:
+    _count_ahead_worker()

@@ -51,6 +51,7 @@ def main():
         rec = {
             "kernel": a.kernel, "config": [scene, int(W), int(H), int(depth), int(n)],
             "lib_sha256": a.lib_sha256 or _lib.lib_sha256(),
+            "device_sha256": None if a.lib_sha256 else _lib.device_sha256(),
             "fetch_bytes_per_launch": int(s["FETCH_SIZE"] * 1024), "write_bytes_per_launch": int(s["WRITE_SIZE"] * 1024),
             "hbm_bytes_per_launch": int((s["FETCH_SIZE"] + s["WRITE_SIZE"]) * 1024),
             "note": "rocprofv3 FETCH_SIZE + WRITE_SIZE (KiB) per dispatch, separate --pmc passes; FETCH_SIZE uncorrected "
