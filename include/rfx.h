@@ -116,6 +116,10 @@ int rfx_renderer_set_tile_order(rfx_renderer *r, int mode);
  * no longer idle in their tile's wave).  -1 (default) = after 3 segments on scenes with more than 32 spheres
  * or triangles, off on small ones; 0 = off; n >= 1 = after n segments on any scene. */
 int rfx_renderer_set_regroup(rfx_renderer *r, int park_after);
+/* regrouped frames: 1 = the parked traces are counting-sorted by direction octant and origin cell before the bounce
+ * kernel takes them, 0 (default) = taken in park order (a tile's survivors together: faster on C5).
+ * Changes the schedule, never a value. */
+int rfx_renderer_set_regroup_sort(rfx_renderer *r, int on);
 /* Primary-bundle cull masks of small-scene plain frames (no pixel changes): the first segment's cull mask of every
  * 8x8 wave tile, computed by one extra launch for a view (camera, frame geometry, scene) and reused while the
  * view stays.  1 (default) = built when a view repeats (the second frame of a still camera on), so a camera that

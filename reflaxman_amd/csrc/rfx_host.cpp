@@ -35,6 +35,7 @@ hipError_t launch_rng_finish(const uint32_t *d_seed, const uint32_t *d_jump, uin
                              uint32_t rank, uint32_t nranks, hipStream_t st);
 hipError_t launch_trace(const DevScene &S, const FrameParams &P, bool stats, hipStream_t st);
 hipError_t launch_prim_cull(const DevScene &S, const FrameParams &P, uint64_t *masks, hipStream_t st);
+hipError_t launch_queue_sort(const uint32_t *count, const uint32_t *key, uint32_t *hist, uint32_t *order, hipStream_t st);
 uint32_t trace_tiles(const FrameParams &P);
 size_t tile_order_scratch();
 hipError_t launch_tile_order(const uint32_t *cost, uint32_t n, uint32_t *order, uint32_t *scratch, hipStream_t st);
@@ -442,6 +443,12 @@ extern "C" uint32_t rfx_strip_row_to_y(uint32_t r, uint32_t rb, uint32_t rank, u
 #endif
 constexpr size_t kPrimWords = 5;  // per wave tile (rfx_trace.h kPrimStride)
 
+#ifndef RFX_QUEUE_SORT
+// regrouped frames: the bounce kernel takes the parked traces bucket by bucket (1) or in park order (0).  tools/ab.py,
+// C5 trace + bounce: park after 3 sorted 3.48 vs 3.40 ms unsorted (+2.3%); after 2: 3.53 vs 3.69 (-4.2%, still
+// above park-3 unsorted).  Park order keeps a tile's survivors together, which a coarse cell key cannot beat.
+#define RFX_QUEUE_SORT 0
+#endif
 #ifndef RFX_PARK_AFTER
 #define RFX_PARK_AFTER 3  // large-scene plain frames: segments before a live trace is parked for the bounce kernel
 #endif
@@ -493,7 +500,9 @@ struct rfx_renderer {
   int prim_mode = 1;       // rfx_renderer_set_prim_masks
   QRay *d_queue = nullptr;
   uint64_t queue_cap = 0;
-  uint32_t *d_qctr = nullptr;
+  uint32_t *d_qctr = nullptr;   // count, claim counter, then the sort's kQueueBuckets histogram words
+  uint32_t *d_qkey = nullptr, *d_qorder = nullptr;  // regroup sort: per entry its bucket; entries in bucket order
+  int queue_sort = RFX_QUEUE_SORT;  // rfx_renderer_set_regroup_sort
   // per-phase event timing: triples {start, after pre-pass, after trace}
   bool timing = false;
   std::vector<hipEvent_t> events;
@@ -597,6 +606,7 @@ extern "C" void rfx_renderer_destroy(rfx_renderer *r)
   (void)hipFree(r->d_blk_cnt); (void)hipFree(r->d_jump); (void)hipFree(r->d_rng_masks);
   (void)hipFree(r->d_img); (void)hipFree(r->d_argb); (void)hipFree(r->d_cnt);
   (void)hipFree(r->d_queue); (void)hipFree(r->d_qctr); (void)hipFree(r->d_prim_mask);
+  (void)hipFree(r->d_qkey); (void)hipFree(r->d_qorder);
   for (hipEvent_t e : r->events) (void)hipEventDestroy(e);
   if (r->tile_stream) (void)hipStreamSynchronize(r->tile_stream);
   (void)hipFree(r->d_tile_cost); (void)hipFree(r->d_tile_order); (void)hipFree(r->d_tile_scratch);
@@ -629,6 +639,13 @@ extern "C" int rfx_renderer_set_regroup(rfx_renderer *r, int park_after)
 {
   if (!r || park_after < -1) return fail(RFX_ERR_ARG, "renderer_set_regroup: -1 (default), 0 (off) or segments >= 1");
   r->park_after = park_after;
+  return RFX_OK;
+}
+
+extern "C" int rfx_renderer_set_regroup_sort(rfx_renderer *r, int on)
+{
+  if (!r || on < 0 || on > 1) return fail(RFX_ERR_ARG, "renderer_set_regroup_sort: 0 or 1");
+  r->queue_sort = on;
   return RFX_OK;
 }
 
@@ -1025,6 +1042,16 @@ extern "C" int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *s)
   d.n_tex = (int32_t)tr.size();
   d.bvh_depth = bvh_depth;
   d.bvh_rx = (float)bvh_ref[0]; d.bvh_ry = (float)bvh_ref[1]; d.bvh_rz = (float)bvh_ref[2];
+  if (!bvh.empty())  // regroup sort keys: 8 origin cells per axis over the root box
+  {
+    const BvhNode &root = bvh[0];
+    const float lo[3] = {fminf(root.lx[0], root.lx[1]), fminf(root.ly[0], root.ly[1]), fminf(root.lz[0], root.lz[1])};
+    const float hi[3] = {fmaxf(root.hx[0], root.hx[1]), fmaxf(root.hy[0], root.hy[1]), fmaxf(root.hz[0], root.hz[1])};
+    float s[3];
+    for (int k = 0; k < 3; ++k) s[k] = hi[k] > lo[k] ? 8.0f / (hi[k] - lo[k]) : 0.0f;
+    d.key_lx = lo[0]; d.key_ly = lo[1]; d.key_lz = lo[2];
+    d.key_sx = s[0]; d.key_sy = s[1]; d.key_sz = s[2];
+  }
   d.n_obj = (int32_t)loc.size();
   d.cull_valid = cull_valid;
   d.skybox_tex = s->skybox;
@@ -1215,22 +1242,32 @@ static int finish_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *d_counts
   const bool plain = P.ss == 1 && !P.additive && !P.accumulate;
   const int park_after = r->park_after < 0 ? (small ? 0 : RFX_PARK_AFTER) : r->park_after;
   const bool park = park_after > 0 && plain && !d_counters && P.depth > park_after && P.grid_rows;
+  const bool sort_queue = park && r->queue_sort && RFX_WAVE_TILES;  // keys are written by the wave-tile kernel
   if (park)
   {
     if (pl.traces > r->queue_cap)
     {
-      (void)hipFree(r->d_queue);
+      (void)hipFree(r->d_queue); (void)hipFree(r->d_qkey); (void)hipFree(r->d_qorder);
       r->d_queue = nullptr;
+      r->d_qkey = r->d_qorder = nullptr;
       r->queue_cap = 0;
       HIP_CHECK(hipMalloc(&r->d_queue, pl.traces * sizeof(QRay)));
+      HIP_CHECK(hipMalloc(&r->d_qkey, pl.traces * sizeof(uint32_t)));
+      HIP_CHECK(hipMalloc(&r->d_qorder, pl.traces * sizeof(uint32_t)));
       r->queue_cap = pl.traces;
     }
-    if (!r->d_qctr) HIP_CHECK(hipMalloc(&r->d_qctr, 2 * sizeof(uint32_t)));
-    HIP_CHECK(hipMemsetAsync(r->d_qctr, 0, 2 * sizeof(uint32_t), st));
+    const size_t qwords = 2 + kQueueBuckets;
+    if (!r->d_qctr) HIP_CHECK(hipMalloc(&r->d_qctr, qwords * sizeof(uint32_t)));
+    HIP_CHECK(hipMemsetAsync(r->d_qctr, 0, (sort_queue ? qwords : 2) * sizeof(uint32_t), st));
     P.queue = r->d_queue;
     P.queue_count = r->d_qctr;
     P.queue_next = r->d_qctr + 1;
     P.park_after = park_after;
+    if (sort_queue)
+    {
+      P.queue_key = r->d_qkey;
+      P.queue_order = r->d_qorder;
+    }
   }
   P.rd_state = r->d_rd;
   P.counters = (unsigned long long *)d_counters;
@@ -1287,6 +1324,7 @@ static int finish_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *d_counts
     const uint64_t waves = (pl.traces + 63) / 64;
     const uint32_t groups = (uint32_t)std::min<uint64_t>((waves + 1) / 2, 4096);
     const int cfg = 1 | (r->dev.n_light > 32 ? 2 : 0) | (small ? 4 : 0) | (r->dev.n_pln ? 8 : 0);  // rfx_trace.h kCfg*
+    if (sort_queue) HIP_CHECK(launch_queue_sort(r->d_qctr, r->d_qkey, r->d_qctr + 2, r->d_qorder, st));
     launch_bounce(cfg, dim3(groups), r->dev, P, st);
     HIP_CHECK(hipGetLastError());
   }

@@ -2,6 +2,7 @@
 //   rng_count / rng_emit : the reference's serial LCG stream (trace_math.h:34-39, Vector3.cpp:176-188) as a
 //       parallel pre-pass;
 //   lpt_hist / lpt_scan / lpt_scatter : the longest-tile-first schedule of the trace launch;
+//   qs_hist / qs_scan / qs_scatter : the regroup queue's bucket order (ray regrouping of large scenes);
 //   kat_* : the trace kernel's primitive code on known-answer inputs (rfx.h rfx_kat_*);
 // and the library-internal launchers.
 #include "rfx_trace.h"
@@ -83,6 +84,73 @@ hipError_t launch_tile_order(const uint32_t *cost, uint32_t n, uint32_t *order, 
   hipLaunchKernelGGL(lpt_hist, dim3(kLptGroups), dim3(kLptThreads), 0, st, cost, n, chunk, scratch);
   hipLaunchKernelGGL(lpt_scan, dim3(1), dim3(kLptBuckets), 0, st, scratch);
   hipLaunchKernelGGL(lpt_scatter, dim3(kLptGroups), dim3(kLptThreads), 0, st, cost, n, chunk, scratch, order);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------- regroup queue sort
+// The parked traces of a frame (QRay queue, count on the device) listed bucket by bucket (rfx_trace.h queue_key:
+// direction octant, origin cell), so that the bounce kernel's packed waves take traces that walk similar BVH paths.
+// A counting sort over kQsGroups workgroups: per-group LDS histograms added into a global one, one scan, then each
+// group reserves its range of every bucket with one atomic and ranks its entries in LDS.  The order within a bucket
+// is whatever the atomics give: it changes which wave resumes a trace, never a value.
+constexpr int kQsThreads = 1024, kQsGroups = 256;
+
+__global__ __launch_bounds__(kQsThreads) void qs_hist(const uint32_t *count, const uint32_t *key, uint32_t *hist)
+{
+  __shared__ uint32_t h[kQueueBuckets];
+  for (uint32_t b = threadIdx.x; b < kQueueBuckets; b += kQsThreads) h[b] = 0;
+  __syncthreads();
+  const uint32_t n = *count, chunk = (n + kQsGroups - 1) / kQsGroups;
+  const uint32_t i0 = blockIdx.x * chunk, i1 = min(n, i0 + chunk);
+  for (uint32_t i = i0 + threadIdx.x; i < i1; i += kQsThreads) atomicAdd(&h[key[i]], 1u);
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < kQueueBuckets; b += kQsThreads)
+    if (h[b]) atomicAdd(&hist[b], h[b]);
+}
+
+// hist <- exclusive prefix sums (the first slot of each bucket); 4 buckets per thread
+__global__ __launch_bounds__(kQsThreads) void qs_scan(uint32_t *hist)
+{
+  static_assert(kQueueBuckets == 4 * kQsThreads, "qs_scan: 4 buckets per thread");
+  __shared__ uint32_t s[kQsThreads];
+  const uint32_t t = threadIdx.x;
+  const uint4 v = reinterpret_cast<const uint4 *>(hist)[t];
+  const uint32_t sum = v.x + v.y + v.z + v.w;
+  s[t] = sum;
+  __syncthreads();
+  for (uint32_t off = 1; off < kQsThreads; off <<= 1)
+  {
+    const uint32_t x = t >= off ? s[t - off] : 0u;
+    __syncthreads();
+    s[t] += x;
+    __syncthreads();
+  }
+  const uint32_t e = s[t] - sum;
+  reinterpret_cast<uint4 *>(hist)[t] = make_uint4(e, e + v.x, e + v.x + v.y, e + v.x + v.y + v.z);
+}
+
+__global__ __launch_bounds__(kQsThreads) void qs_scatter(const uint32_t *count, const uint32_t *key, uint32_t *cursor,
+                                                         uint32_t *order)
+{
+  __shared__ uint32_t h[kQueueBuckets];
+  for (uint32_t b = threadIdx.x; b < kQueueBuckets; b += kQsThreads) h[b] = 0;
+  __syncthreads();
+  const uint32_t n = *count, chunk = (n + kQsGroups - 1) / kQsGroups;
+  const uint32_t i0 = blockIdx.x * chunk, i1 = min(n, i0 + chunk);
+  for (uint32_t i = i0 + threadIdx.x; i < i1; i += kQsThreads) atomicAdd(&h[key[i]], 1u);
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < kQueueBuckets; b += kQsThreads)
+    if (h[b]) h[b] = atomicAdd(&cursor[b], h[b]);  // this group's first slot of bucket b
+  __syncthreads();
+  for (uint32_t i = i0 + threadIdx.x; i < i1; i += kQsThreads) order[atomicAdd(&h[key[i]], 1u)] = i;
+}
+
+// hist: kQueueBuckets zeroed words (the frame's queue counter memset clears them)
+hipError_t launch_queue_sort(const uint32_t *count, const uint32_t *key, uint32_t *hist, uint32_t *order, hipStream_t st)
+{
+  hipLaunchKernelGGL(qs_hist, dim3(kQsGroups), dim3(kQsThreads), 0, st, count, key, hist);
+  hipLaunchKernelGGL(qs_scan, dim3(1), dim3(kQsThreads), 0, st, hist);
+  hipLaunchKernelGGL(qs_scatter, dim3(kQsGroups), dim3(kQsThreads), 0, st, count, key, hist, order);
   return hipGetLastError();
 }
 

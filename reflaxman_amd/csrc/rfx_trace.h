@@ -1137,7 +1137,25 @@ struct Park {
   uint32_t *count;
   uint32_t trace, out;  // this lane's randDir trace index and output pixel
   __device__ __forceinline__ void ids(uint32_t &t, uint32_t &o) const { t = trace; o = out; }
+  __device__ __forceinline__ uint32_t *keys() const { return nullptr; }
 };
+
+// Regroup sort key of a parked trace (RFX_QUEUE_SORT): its direction octant and the Morton index of its origin's cell
+// in an 8 x 8 x 8 grid over the BVH root box -- traces of one bucket walk similar BVH paths.  Only the order in which
+// the bounce kernel takes the traces depends on it, never a value (every trace resumes from its own state).
+__device__ __forceinline__ uint32_t queue_key(const DevScene &S, v3 o, v3 d)
+{
+  const auto cell = [](float v, float lo, float s) -> uint32_t {
+    return (uint32_t)fminf(fmaxf((v - lo) * s, 0.0f), 7.0f);  // NaN: fmaxf takes the 0
+  };
+  const uint32_t cx = cell(o.x, S.key_lx, S.key_sx), cy = cell(o.y, S.key_ly, S.key_sy), cz = cell(o.z, S.key_lz, S.key_sz);
+  uint32_t m = 0;
+#pragma unroll
+  for (int b = 0; b < 3; ++b)
+    m |= (((cx >> b) & 1u) << (3 * b)) | (((cy >> b) & 1u) << (3 * b + 1)) | (((cz >> b) & 1u) << (3 * b + 2));
+  const uint32_t oct = (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u);
+  return oct << 9 | m;
+}
 
 // Scene::trace from a mid-trace state (mulc, pix after `refl` segments); park: see Park.  *parked: this lane's
 // trace was queued and its returned colour is not final.
@@ -1396,7 +1414,9 @@ __device__ __forceinline__ col trace_from(const DevScene &S, v3 origin, v3 ray, 
           uint32_t qt, qo;
           park.ids(qt, qo);
           q.trace = qt; q.out = qo; q.refl = (uint32_t)refl; q.pad = 0;
-          park.queue[base + (uint32_t)__popcll(pm & ((1ull << __lane_id()) - 1ull))] = q;
+          const uint32_t slot = base + (uint32_t)__popcll(pm & ((1ull << __lane_id()) - 1ull));
+          park.queue[slot] = q;
+          if (uint32_t *keys = park.keys()) keys[slot] = queue_key(S, origin, ray);
           parked = true;
           alive = false;
         }
@@ -1467,6 +1487,7 @@ struct ParkTile {
     t = (uint32_t)((uint64_t)y * P.W + gx - P.p_begin);
     o = (uint32_t)((size_t)orow * P.W + gx);
   }
+  __device__ __forceinline__ uint32_t *keys() const { return P.queue_key; }
 };
 
 // trace i's randomInsideSphere draw (Vector3.cpp:176-188) from the LCG state before its accepted triple
@@ -1815,7 +1836,7 @@ __global__ RFX_TRACE_BOUNDS void bounce_kernel(DevScene S, FrameParams P)
     const uint32_t i = base + lane;
     const bool valid = i < n;
     QRay q{};
-    if (valid) q = P.queue[i];
+    if (valid) q = P.queue[P.queue_order ? P.queue_order[i] : i];
     const v3 rd = valid ? load_rd(P, q.trace) : mk(0.0f, 0.0f, 0.0f);
     bool parked;
     const col c = trace_from<false, CULL, MANYL, SMALL, PLANES, false>(

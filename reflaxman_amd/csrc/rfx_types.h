@@ -87,6 +87,8 @@ struct DevScene {
   int32_t n_pln, n_obj, n_tex;
   int32_t bvh_depth;          // internal levels of the BVH (<= kBvhStack)
   float bvh_rx, bvh_ry, bvh_rz;  // the BVH's margin reference point (its root box centre)
+  float key_lx, key_ly, key_lz;  // regroup sort keys: origin cell = (o - key_l) * key_s in [0, 8) per axis (the BVH
+  float key_sx, key_sy, key_sz;  // root box; 0 scale without a BVH: one cell)
   int32_t n_chunk;            // (n_sph + 63) / 64
   float amb_r, amb_g, amb_b;  // diffLightColor * diffLightPower (Scene.cpp:186, host-folded)
   float env_r, env_g, env_b;  // envColor (Scene.cpp:12,55)
@@ -96,6 +98,7 @@ struct DevScene {
 // A trace parked between bounce segments (large scenes, plain pixels): the state Scene::trace carries from
 // one segment to the next (Scene.cpp:80-234: origin, ray, mulColor, pixelColor, refl), the trace index of its
 // randDir and the output pixel.  64 B: one lane stores / loads it with four 16-B accesses.
+constexpr uint32_t kQueueBuckets = 4096;  // regroup sort buckets (rfx_trace.h queue_key)
 struct alignas(16) QRay {
   float ox, oy, oz, dx;
   float dy, dz, mr, mg;
@@ -130,6 +133,10 @@ struct FrameParams {
   QRay *queue;
   uint32_t *queue_count, *queue_next;
   int32_t park_after;
+  // regroup sort (RFX_QUEUE_SORT): queue_key[i] is entry i's bucket (direction octant, origin cell), written at park
+  // time; queue_order lists the entries bucket by bucket, and the bounce kernel claims them in that order
+  uint32_t *queue_key;
+  const uint32_t *queue_order;
   // small scenes, plain pixels: per wave tile, the cull mask of its primary bundle (prim_cull_kernel), or null
   const uint64_t *prim_mask;
 };

@@ -316,6 +316,11 @@ class Renderer:
         n >= 1 park traces alive after n segments for the packed bounce kernel.  No pixel changes."""
         check(_lib.load().rfx_renderer_set_regroup(self._h, int(park_after)), "set_regroup")
 
+    def set_regroup_sort(self, on: bool):
+        """Regrouped frames (rfx.h rfx_renderer_set_regroup_sort): the bounce kernel takes the parked traces sorted
+        by direction octant and origin cell, or in park order (default).  No pixel changes."""
+        check(_lib.load().rfx_renderer_set_regroup_sort(self._h, int(bool(on))), "set_regroup_sort")
+
     def set_timing(self, enable: bool):
         check(_lib.load().rfx_renderer_set_timing(self._h, int(bool(enable))), "set_timing")
 

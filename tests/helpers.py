@@ -19,7 +19,8 @@ def sha(a) -> str:
 
 
 def gpu_render(desc, W, H, depth, ss=1, additive=False, frames=1, sphere_seed=1350490027, jitter_seed=0,
-               chunks=None, device=0, tile_order=None, each_frame=None, regroup=None, prim_masks=None):
+               chunks=None, device=0, tile_order=None, each_frame=None, regroup=None, prim_masks=None,
+               regroup_sort=None):
     """Render through the Python mirror of Render (reflaxman_amd.render.Render) on the GPU.
 
     chunks: None -> one renderNext(W*H) per frame; else a list of renderNext sizes cycled until done.
@@ -32,6 +33,8 @@ def gpu_render(desc, W, H, depth, ss=1, additive=False, frames=1, sphere_seed=13
         r._r.set_tile_order(tile_order)
     if regroup is not None:
         r._r.set_regroup(regroup)
+    if regroup_sort is not None:
+        r._r.set_regroup_sort(regroup_sort)
     if prim_masks is not None:
         r._r.set_prim_masks(prim_masks)
     for _ in range(frames):

@@ -390,23 +390,28 @@ def test_textures_loaded_from_tga_files(tmp_path):
     r.close()
 
 
-@pytest.mark.parametrize("key,park", [("hash_synth16_3840x2160_d8", 1), ("hash_synth16_3840x2160_d8", 2),
-                                      ("hash_default_640x480_d4", 1), ("hash_synth16_7680x4320_d8", 3)])
-def test_regrouped_frame_matches_reference_hash(key, park):
-    """Ray regrouping (traces parked after `park` segments, resumed by the packed bounce kernel) on the small-scene
-    configs, where it is off by default: the full frame still hashes to the reference's."""
+@pytest.mark.parametrize("key,park,qsort", [("hash_synth16_3840x2160_d8", 1, 1), ("hash_synth16_3840x2160_d8", 2, 1),
+                                            ("hash_default_640x480_d4", 1, 1), ("hash_synth16_7680x4320_d8", 3, 1),
+                                            ("hash_synth16_3840x2160_d8", 1, 0), ("hash_default_640x480_d4", 2, 0)])
+def test_regrouped_frame_matches_reference_hash(key, park, qsort):
+    """Ray regrouping (traces parked after `park` segments, resumed by the packed bounce kernel -- in bucket order or
+    in park order) on the small-scene configs, where it is off by default: the full frame still hashes to the
+    reference's."""
     c = CASES[key]
-    rgb, argb, r = run_case(c, regroup=park)
+    rgb, argb, r = run_case(c, regroup=park, regroup_sort=qsort)
     assert sha(argb) == c["sha_argb"], key
     assert sha(rgb) == c["sha_f32"], key
     r.close()
 
 
 @pytest.mark.parametrize("key", sorted(k for k, c in CASES.items() if c["kind"] == "band" and c["scene"] == "stress4096"))
-def test_stress_band_without_regrouping(key):
-    """C5 with regrouping off (on by default there): the reference's bands again."""
+@pytest.mark.parametrize("regroup,qsort", [(0, None), (3, 1), (2, 1)])
+def test_stress_band_other_regrouping(key, regroup, qsort):
+    """C5 with regrouping off, and with the parked traces sorted into buckets (the default takes them in park
+    order): the reference's bands again."""
     c = CASES[key]
-    rgb, argb, r = gpu_render(scene(c["scene"]), c["W"], c["H"], c["depth"], sphere_seed=c["sphere_seed"], regroup=0)
+    rgb, argb, r = gpu_render(scene(c["scene"]), c["W"], c["H"], c["depth"], sphere_seed=c["sphere_seed"],
+                              regroup=regroup, regroup_sort=qsort)
     g = np.load(os.path.join(GOLDEN, key + ".npz"))
     y0, rows = c["y0"], c["rows"]
     assert np.array_equal(argb[y0:y0 + rows], g["argb"])

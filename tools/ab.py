@@ -56,6 +56,7 @@ VARIANTS = {
     "stack32": ["RFX_BVH_STACK16=0"],
     "boxmargin": ["RFX_BVH_NODE_MARGIN=0"],
     "median": ["RFX_BVH_SAH=0"],
+    "qsort": ["RFX_QUEUE_SORT=1"],
 }
 
 
