@@ -364,7 +364,7 @@ __global__ __launch_bounds__(kKatThreads) void kat_objects(DevScene S, const flo
   const int32_t loc = S.obj_loc[objs[i]];
   const int kind = loc >> 28, idx = loc & 0x0FFFFFFF;
   const RayConst k = ray_const(ray);
-  bool hit = false, any = false;
+  bool hit = false, any = false, pre_bad = false;
   float t = 0.0f, sq = 0.0f, t2, sq2, u = 0.0f, v = 0.0f, u2, v2;
   v3 norm = mk(0.0f, 0.0f, 0.0f), drop = o;
   col c = mkc(0.0f, 0.0f, 0.0f);
@@ -390,6 +390,8 @@ __global__ __launch_bounds__(kKatThreads) void kat_objects(DevScene S, const flo
   {
     hit = tri_hit<false, false>(S.tri_geo[idx], o, ray, t, u, v, sq, cnt, k);
     any = tri_hit<false, true>(S.tri_geo[idx], o, ray, t2, u2, v2, sq2, cnt, k);
+    // the large-scene shadow form (reject before the divide) must decide alike: a disagreement reads as NaN
+    if (tri_hit<false, true, true>(S.tri_geo[idx], o, ray, t2, u2, v2, sq2, cnt, k) != any) pre_bad = true;
     if (hit)
     {
       drop = add(o, mul(ray, t));
@@ -424,7 +426,7 @@ __global__ __launch_bounds__(kKatThreads) void kat_objects(DevScene S, const flo
     w[10] = sqrt_rn(sq);
     w[11] = c.r; w[12] = c.g; w[13] = c.b;
   }
-  w[14] = any ? 1.0f : 0.0f;
+  w[14] = pre_bad ? __builtin_nanf("") : any ? 1.0f : 0.0f;
 }
 
 // tex >= 0: Texture::getTexelColor(u, v) of texture tex (in: n x 2); tex < 0: Skybox::getTexelColor(ray)

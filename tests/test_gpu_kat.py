@@ -141,3 +141,40 @@ def test_kat_argb():
     out = r.kat_argb(g["inp"])
     r.close()
     assert np.array_equal(out, g["out"])
+
+
+def test_triangle_reject_before_divide_decides_like_the_divide():
+    """Large-scene shadow rays reject plane crossings outside a triangle before the correctly rounded divide
+    (rfx_trace.h tri_hit PRE); the KAT kernel evaluates both forms and writes NaN where they disagree.  2^20 rays
+    aimed within a few ulp of the edges u = 0, v = 0, u + v = 1 (and at random points), from random origins and
+    ray lengths: no disagreement."""
+    rng = np.random.default_rng(7)
+    n = 1 << 20
+    s = Scene()
+    quads = [((-5.0, 0.0, -5.0), (5.0, 0.0, -5.0), (5.0, 0.0, 5.0)), ((-5.0, 0.0, -5.0), (5.0, 0.0, 5.0), (-5.0, 0.0, 5.0)),
+             ((-3.0, -2.0, 7.0), (4.0, 1.5, 7.5), (0.5, 6.0, 8.0))]
+    for a, b, c in quads:
+        s.addTriangle(Vector3(*a), Vector3(*b), Vector3(*c), KAT_MAT)
+    obj = rng.integers(0, len(quads), n).astype(np.int32)
+    v0 = np.array([q[0] for q in quads], np.float64)[obj]
+    e1 = (np.array([q[1] for q in quads], np.float64) - np.array([q[0] for q in quads]))[obj]
+    e2 = (np.array([q[2] for q in quads], np.float64) - np.array([q[0] for q in quads]))[obj]
+    u = rng.random(n)
+    v = rng.random(n) * (1 - u)
+    eps = rng.normal(0, 1e-6, n)
+    edge = rng.integers(0, 4, n)
+    u = np.where(edge == 0, eps, u)
+    v = np.where(edge == 1, eps, v)
+    v = np.where(edge == 2, 1 - u + eps, v)
+    p = v0 + u[:, None] * e1 + v[:, None] * e2
+    d = rng.normal(size=(n, 3))
+    d /= np.linalg.norm(d, axis=1)[:, None]
+    o = p + d * rng.uniform(0.01, 50.0, n)[:, None]
+    ray = (p - o) * rng.uniform(0.05, 20.0, n)[:, None]
+    rays = np.concatenate([o, ray], axis=1).astype(np.float32)
+    r = Renderer()
+    r.set_scene(s)
+    out = r.kat_objects(rays, obj)
+    r.close()
+    assert not np.isnan(out[:, 14]).any(), int(np.isnan(out[:, 14]).sum())
+    assert 0.2 * n < out[:, 14].sum() < 0.9 * n  # both outcomes well represented
