@@ -62,6 +62,9 @@ CONFIGS = {
     "c4": ("synth16", 7680, 4320, 8, "C4 synth16 (the C3 scene: 16 spheres + 4 textured triangles + sun)"),
     "c5": ("stress4096", 3840, 2160, 12, "C5 stress4096: 4096 spheres + ground quad + sun"),
 }
+# cpu_baseline row strides: about 5 s of the reference's single-core trace time per config (C5's CPU rate is
+# 0.0064 Mrays/s: every 270th row)
+CPU_STRIDE = {"c1": 1, "c2": 4, "c3": 2, "c4": 16, "c5": 270}
 
 
 def frame_size(n: int, w0: int, h0: int, scaling: str):
@@ -187,7 +190,8 @@ def main():
     ap.add_argument("--regroup", type=int, default=None,
                     help="ray regrouping: park traces after n segments (0 off; default: the library's choice)")
     ap.add_argument("--row-block", type=int, default=8)
-    ap.add_argument("--cpu-stride", type=int, default=2, help="cpu_baseline samples every n-th row")
+    ap.add_argument("--cpu-stride", type=int, default=None,
+                    help="cpu_baseline samples every n-th row (default per config: a ~5 s single-core sample)")
     ap.add_argument("--no-cpu-allcore", action="store_true", help="skip the all-core CPU context row")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (gloo: multi-rank rehearsal)")
@@ -420,7 +424,8 @@ def main():
     }
     if world == 1 and not args.no_cpu_baseline:
         log("cpu_baseline: reference CPU path on a row sample of the same frame ...")
-        cb, delta = cpu_baseline(desc, W, H, depth, first_rgb, first_argb, args.cpu_stride)
+        stride = args.cpu_stride or (2 if custom else CPU_STRIDE[cfg_name])
+        cb, delta = cpu_baseline(desc, W, H, depth, first_rgb, first_argb, stride)
         out["cpu_baseline"] = cb
         out["parity"]["sample_vs_cpu_reference"] = delta
         out["max_abs_delta"] = {"u8": delta["max_u8"], "f32_ulp": delta["max_f32_ulp"]}
