@@ -197,6 +197,9 @@ def main():
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (gloo: multi-rank rehearsal)")
     ap.add_argument("--one-device", action="store_true", help="all ranks on cuda:0 (rehearsal on a 1-GPU box)")
     ap.add_argument("--no-pipeline", action="store_true", help="N > 1: gather each frame's strips before the next frame")
+    ap.add_argument("--partition", choices=["bands", "strips"], default="bands",
+                    help="N > 1: load-balanced contiguous bands received in place on rank 0 (default), or block-cyclic "
+                         "row strips gathered and un-interleaved")
     ap.add_argument("--no-count-ahead", action="store_true",
                     help="N > 1: count and all-gather each frame's RNG blocks on its critical path, not during the last trace")
     args = ap.parse_args()
@@ -242,15 +245,18 @@ def main():
     torch.cuda.set_stream(stream)
     rr.set_stream(stream.cuda_stream)
 
-    frame = make_frame(cam, W, H, depth, 1, row_block=rb if world > 1 else 0, rank=rank, nranks=world)
+    bands = world > 1 and args.partition == "bands"
+    frame = make_frame(cam, W, H, depth, 1, row_block=rb if world > 1 and not bands else 0, rank=rank, nranks=world)
     traces = W * H
     if world > 1:
         # sliced RNG pre-pass (count own slice -> all-gather block counts -> emit own strips), trace of
         # the own strips, ARGB8 strip gather to rank 0 + device un-interleave (reflaxman_amd/dist.py)
-        from reflaxman_amd.dist import RfxStripOps, StripFrame
-        sf = StripFrame(RfxStripOps(rr, frame, stream.cuda_stream), W, H, rb, rank, world, dev,
-                        pipeline=False if args.no_pipeline else None, gather_rgb=args.gather_rgb,
-                        count_ahead=False if args.no_count_ahead else None)
+        from reflaxman_amd.dist import BandFrame, RfxStripOps, StripFrame
+        ops = RfxStripOps(rr, frame, stream.cuda_stream)
+        common = dict(pipeline=False if args.no_pipeline else None, gather_rgb=args.gather_rgb,
+                      count_ahead=False if args.no_count_ahead else None)
+        sf = BandFrame(ops, W, H, rank, world, dev, **common) if bands else \
+            StripFrame(ops, W, H, rb, rank, world, dev, **common)
         rows, img, argb = sf.rows, sf.img, sf.argb
     else:
         rows = H
@@ -332,6 +338,10 @@ def main():
             prewarm = int(pw.item())
         for _ in range(prewarm):
             step()
+    if bands:
+        # cut the bands from measured per-rank render times (rank 0's receive included), then keep them
+        sf.balance(rounds=3, frames=8)
+        log(f"rank {rank}: bands {sf.bounds}")
     # ---- warmup, then K timed steps (barrier + synchronize on both sides)
     for _ in range(args.warmup):
         step()
@@ -382,7 +392,10 @@ def main():
     ms_step = elapsed / args.steps * 1e3
     mrays = traces * args.steps / elapsed / 1e6
     # the trace kernel of one rank processes its strip: per-launch FLOPs = frame FLOPs / world (balanced strips)
-    flops_launch = flops_frame / world
+    # (bands: the rank's share of the frame's rows -- rows differ in cost, so this is approximate)
+    if world > 1:
+        rows = sf.rows
+    flops_launch = flops_frame / world if world == 1 or not bands else flops_frame * rows / H
     achieved = flops_launch / (trace_avg * 1e-3) / 1e12
     px_launch = rows * W
     # HBM traffic and executed VALU work of the trace kernel: rocprofv3 --pmc passes of this very workload
@@ -400,8 +413,9 @@ def main():
         "scaling": args.scaling if world > 1 else "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {"workload": workload, "name": None if custom else cfg_name.upper(),
                    "scene": args.scene, "width": W, "height": H, "depth": depth, "spp": 1,
-                   "parallelism": (f"row-strips{rb}x{world}" + ("+pipelined-gather" if sf.pipeline else ""))
-                                  + ("+count-ahead" if sf.count_ahead else "") if world > 1 else "single-gpu"},
+                   "parallelism": ((f"balanced-bands-x{world}" if bands else f"row-strips{rb}x{world}")
+                                   + ("+pipelined-gather" if sf.pipeline else "")
+                                   + ("+count-ahead" if sf.count_ahead else "")) if world > 1 else "single-gpu"},
         "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": metrics.PEAK_FP32_VALU_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved / metrics.PEAK_FP32_VALU_TFLOPS, 4),
                      "traffic": traffic, "kernel": "rfx::trace_kernel (plain pixel mode, wave-bundle culling)",
@@ -421,6 +435,7 @@ def main():
                                            * args.steps / elapsed / 1e6, 1),
         "end_to_end_incl_d2h": e2e,
         "parity": parity,
+        **({"band_bounds": sf.bounds} if bands else {}),
     }
     if world == 1 and not args.no_cpu_baseline:
         log("cpu_baseline: reference CPU path on a row sample of the same frame ...")

@@ -142,7 +142,11 @@ typedef struct {
   uint32_t row_block;       /* strip partition: rows are dealt in blocks of row_block ...   */
   uint32_t rank, nranks;    /* ... block b belongs to rank b % nranks (nranks == 1: whole frame) */
   uint64_t pixel_begin;     /* raster span [pixel_begin, pixel_end) of this call: the Render::renderNext */
-  uint64_t pixel_end;       /* cursor span (Render.cpp:136-215); 0, 0 = the whole frame.  nranks == 1 only */
+  uint64_t pixel_end;       /* cursor span (Render.cpp:136-215); 0, 0 = the whole frame.  nranks == 1, or a band */
+  /* Band partition: nranks > 1 with row_block == 0 -- this rank traces the whole rows [pixel_begin, pixel_end) / W of
+   * the W x H frame into whole-frame buffers (d_rgb W*H*3, d_argb W*H; only the band's rows are written), with the
+   * frame's random stream sliced nranks ways as for strips (rfx_frame_rng_count / rfx_render_frame_counted).  Rank 0
+   * can then receive each band straight into its rows of the frame (reflaxman_amd/dist.py BandFrame). */
 } rfx_frame;
 
 /* rows of `frame` that `rank` owns under the block-cyclic strip partition */

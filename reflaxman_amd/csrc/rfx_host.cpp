@@ -32,7 +32,8 @@ hipError_t launch_rng_count(const uint32_t *d_seed, const uint32_t *d_jump, uint
 hipError_t launch_rng_finish(const uint32_t *d_seed, const uint32_t *d_jump, uint32_t *d_next_seed,
                              const uint32_t *d_blk_cnt, const uint16_t *d_masks, uint64_t nblk, uint64_t traces,
                              uint32_t *d_rd_state, int *d_err, uint64_t ss2, uint64_t W, uint32_t row_block,
-                             uint32_t rank, uint32_t nranks, hipStream_t st);
+                             uint32_t rank, uint32_t nranks, uint64_t *d_blk_off, uint64_t lo, uint64_t hi,
+                             hipStream_t st);
 hipError_t launch_trace(const DevScene &S, const FrameParams &P, bool stats, hipStream_t st);
 hipError_t launch_prim_cull(const DevScene &S, const FrameParams &P, uint64_t *masks, hipStream_t st);
 hipError_t launch_queue_sort(const uint32_t *count, const uint32_t *key, uint32_t *hist, uint32_t *order, hipStream_t st);
@@ -433,7 +434,9 @@ extern "C" uint32_t rfx_strip_row_to_y(uint32_t r, uint32_t rb, uint32_t rank, u
 #define RFX_TILE_ORDER_DEFAULT 1
 #endif
 #ifndef RFX_TILE_ORDER_MIN_TILES
-#define RFX_TILE_ORDER_MIN_TILES 65536  // 8x8 wave tiles: C3 (3840x2160) has 129,600, C2 (1920x1080) 32,400
+// 8x8 wave tiles: C3 (3840x2160) has 129,600, C2 (1920x1080) 32,400, a C4 rank's strips at N = 8 65,280 (their
+// trace 0.41 ms unsorted vs 0.34 at N = 4 per eighth of the frame, tools/root_overhead.py)
+#define RFX_TILE_ORDER_MIN_TILES 49152
 #endif
 #ifndef RFX_WAVE_TILES  // schedule unit: the wave's 8x8 tile (1) or the workgroup's 16x8 (0); tools/ab.py, C3: -2.7% trace
 #define RFX_WAVE_TILES 1
@@ -472,6 +475,7 @@ struct rfx_renderer {
   // workspaces
   uint32_t *d_rd = nullptr; uint64_t rd_cap = 0;  // per-trace LCG states (rng_emit)
   uint32_t *d_blk_cnt = nullptr; uint64_t blk_cap = 0;
+  uint64_t *d_blk_off = nullptr;  // the emit's scanned block offsets (rng_scan)
   uint16_t *d_rng_masks = nullptr;  // one device's accept flags per pre-pass thread (rng_count -> rng_emit)
   uint32_t *d_jump = nullptr;  // LCG jump table for blk_cap blocks (rng_jump_table)
   // host staging for rfx_render_frame_host
@@ -603,7 +607,7 @@ extern "C" void rfx_renderer_destroy(rfx_renderer *r)
   (void)hipStreamSynchronize(r->stream);
   free_scene(r);
   (void)hipFree(r->d_seed); (void)hipFree(r->d_err); (void)hipFree(r->d_rd);
-  (void)hipFree(r->d_blk_cnt); (void)hipFree(r->d_jump); (void)hipFree(r->d_rng_masks);
+  (void)hipFree(r->d_blk_cnt); (void)hipFree(r->d_jump); (void)hipFree(r->d_rng_masks); (void)hipFree(r->d_blk_off);
   (void)hipFree(r->d_img); (void)hipFree(r->d_argb); (void)hipFree(r->d_cnt);
   (void)hipFree(r->d_queue); (void)hipFree(r->d_qctr); (void)hipFree(r->d_prim_mask);
   (void)hipFree(r->d_qkey); (void)hipFree(r->d_qorder);
@@ -1116,9 +1120,10 @@ static int ensure_rng_workspace(rfx_renderer *r, uint64_t traces, uint64_t nblk)
   }
   if (nblk > r->blk_cap)
   {
-    (void)hipFree(r->d_blk_cnt); (void)hipFree(r->d_jump); (void)hipFree(r->d_rng_masks);
-    r->d_blk_cnt = nullptr; r->d_jump = nullptr; r->d_rng_masks = nullptr; r->blk_cap = 0;
+    (void)hipFree(r->d_blk_cnt); (void)hipFree(r->d_jump); (void)hipFree(r->d_rng_masks); (void)hipFree(r->d_blk_off);
+    r->d_blk_cnt = nullptr; r->d_jump = nullptr; r->d_rng_masks = nullptr; r->d_blk_off = nullptr; r->blk_cap = 0;
     HIP_CHECK(hipMalloc(&r->d_blk_cnt, nblk * sizeof(uint32_t)));
+    HIP_CHECK(hipMalloc(&r->d_blk_off, nblk * sizeof(uint64_t)));
     HIP_CHECK(hipMalloc(&r->d_rng_masks, nblk * 256 * sizeof(uint16_t)));
     std::vector<uint32_t> jump(2 * (256 + nblk));
     rng_jump_table(nblk, jump.data());
@@ -1127,6 +1132,16 @@ static int ensure_rng_workspace(rfx_renderer *r, uint64_t traces, uint64_t nblk)
     r->blk_cap = nblk;
   }
   return RFX_OK;
+}
+
+// Block offsets of the emit from a scan launch (multi-GPU strips: the emit skips most blocks, so their own prefix
+// sums would be nearly all of its work; many blocks: those sums grow quadratically), else summed by each block
+#ifndef RFX_RNG_SCAN_MIN_BLOCKS
+#define RFX_RNG_SCAN_MIN_BLOCKS 8192  // C3: 3.9K blocks, C4 frame: 15.5K
+#endif
+static uint64_t *rng_scan(rfx_renderer *r, uint64_t nblk, uint32_t nranks)
+{
+  return (nranks > 1 || nblk >= RFX_RNG_SCAN_MIN_BLOCKS) ? r->d_blk_off : nullptr;
 }
 
 // Whole pre-pass on one device: every block counted here (the 1-GPU path, and the redundant form of the
@@ -1138,7 +1153,7 @@ static int enqueue_rng(rfx_renderer *r, uint64_t traces, hipStream_t st)
   if ((rc = ensure_rng_workspace(r, traces, nblk)) != RFX_OK) return rc;
   HIP_CHECK(launch_rng_count(seed_cur(r), r->d_jump, r->d_blk_cnt, 0, nblk, r->d_rng_masks, st));
   HIP_CHECK(launch_rng_finish(seed_cur(r), r->d_jump, seed_next(r), r->d_blk_cnt, r->d_rng_masks, nblk, traces,
-                              r->d_rd, r->d_err, 1, 1, 1, 0, 1, st));
+                              r->d_rd, r->d_err, 1, 1, 1, 0, 1, rng_scan(r, nblk, 1), 0, UINT64_MAX, st));
   r->seed_idx ^= 1u;
   return RFX_OK;
 }
@@ -1148,6 +1163,9 @@ struct FramePlan {
   FrameParams P;
   uint64_t traces = 0;
   hipStream_t st = nullptr;
+  // band partition (rfx.h: nranks > 1, row_block 0): the emit writes the randDirs of traces [band_lo, band_hi) only
+  bool band = false;
+  uint64_t band_lo = 0, band_hi = UINT64_MAX;
 };
 
 static int plan_frame(rfx_renderer *r, const rfx_frame *f, void *stream, FramePlan &plan);
@@ -1228,7 +1246,8 @@ static int finish_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *d_counts
   const hipStream_t st = pl.st;
   const uint64_t ss2 = P.ss > 0 ? (uint64_t)(P.ss * P.ss) : 1;
   HIP_CHECK(launch_rng_finish(seed_cur(r), r->d_jump, seed_next(r), d_counts, d_masks, nblk, pl.traces, r->d_rd,
-                              r->d_err, ss2, P.W, P.row_block, P.rank, P.nranks, st));
+                              r->d_err, ss2, P.W, P.row_block, P.rank, P.nranks,
+                              rng_scan(r, nblk, pl.band ? 2 : P.nranks), pl.band_lo, pl.band_hi, st));
   r->seed_idx ^= 1u;
   // the caller's event: the randDirs are written and the next frame's stream state is known (the next frame's
   // RNG count may start on another stream while this frame traces)
@@ -1392,8 +1411,9 @@ static int plan_frame(rfx_renderer *r, const rfx_frame *f, void *stream, FramePl
     return fail(RFX_ERR_ARG, "render_frame: W=%u H=%u reflect_num=%d sample_num=%d", f->width, f->height,
                 f->reflect_num, f->sample_num);
   const uint32_t nranks = f->nranks ? f->nranks : 1;
-  if (nranks > 1 && (f->sample_num < 0 || !f->row_block || f->rank >= nranks))
-    return fail(RFX_ERR_ARG, "render_frame: strip partition needs sample_num > 0, row_block > 0, rank < nranks");
+  const bool band = nranks > 1 && !f->row_block;  // band partition: this rank's rows [pixel_begin, pixel_end) / W
+  if (nranks > 1 && (f->sample_num < 0 || f->rank >= nranks))
+    return fail(RFX_ERR_ARG, "render_frame: a partition needs sample_num > 0, rank < nranks");
   if (f->sample_num > 256 || f->sample_num < -4096) return fail(RFX_ERR_ARG, "render_frame: sample_num out of range");
   int rc;
   if ((rc = set_dev(r)) != RFX_OK) return rc;
@@ -1402,6 +1422,17 @@ static int plan_frame(rfx_renderer *r, const rfx_frame *f, void *stream, FramePl
   const uint32_t W = f->width, H = f->height;
   const uint64_t npx = (uint64_t)W * H;
   uint64_t p0 = f->pixel_begin, p1 = f->pixel_end;
+  if (band)
+  {
+    // the band's rows; the frame (random stream, trace indices, output rows) stays the whole W x H frame
+    if (p0 >= p1 || p1 > npx || p0 % W || p1 % W)
+      return fail(RFX_ERR_ARG, "render_frame: a band is whole rows [pixel_begin, pixel_end) / W of the frame");
+    plan.band = true;
+    plan.band_lo = p0 * (uint64_t)(f->sample_num * f->sample_num);
+    plan.band_hi = p1 * (uint64_t)(f->sample_num * f->sample_num);
+    p0 = 0;
+    p1 = npx;
+  }
   if (p0 == 0 && p1 == 0) p1 = npx;
   if (p0 >= p1 || p1 > npx) return fail(RFX_ERR_ARG, "render_frame: pixel span [%llu, %llu) outside frame",
                                         (unsigned long long)p0, (unsigned long long)p1);
@@ -1428,6 +1459,11 @@ static int plan_frame(rfx_renderer *r, const rfx_frame *f, void *stream, FramePl
     traces = (p1 - p0) * (uint64_t)(f->sample_num * f->sample_num);
     row0 = nranks > 1 ? 0 : y0;
     grid_rows = nranks > 1 ? rfx_strip_rows(H, f->row_block, f->rank, nranks) : y1 - y0 + 1;
+    if (band)
+    {
+      row0 = (uint32_t)(f->pixel_begin / W);
+      grid_rows = (uint32_t)((f->pixel_end - f->pixel_begin) / W);
+    }
   }
   if (traces >= (1ull << 32)) return fail(RFX_ERR_ARG, "render_frame: %llu traces exceed 2^32", (unsigned long long)traces);
   plan.traces = traces;
@@ -1448,8 +1484,8 @@ static int plan_frame(rfx_renderer *r, const rfx_frame *f, void *stream, FramePl
   P.additive = f->sample_num > 0 && f->additive;
   P.jitter_seed = r->jitter_seed;
   P.row_block = f->row_block ? f->row_block : 1;
-  P.rank = nranks > 1 ? f->rank : 0;
-  P.nranks = nranks;
+  P.rank = nranks > 1 && !band ? f->rank : 0;
+  P.nranks = band ? 1 : nranks;  // a band traces like a 1-GPU span of rows: absolute rows, whole-frame buffers
   P.grid_rows = grid_rows;
   P.row0 = row0;
   P.p_begin = p0;

@@ -223,15 +223,17 @@ __global__ __launch_bounds__(kRngBlock) void rng_count(const uint32_t *seed, con
 }
 
 // Which traces a rank needs randDirs for: trace i -> pixel i / ss2 -> row -> strip (row / row_block)
-// -> owner strip % nranks (rfx_strip_row_to_y).  nranks <= 1: every trace.
+// -> owner strip % nranks (rfx_strip_row_to_y); nranks <= 1: the traces [lo, hi) (a band of rows, or every trace).
 struct EmitFilter {
   uint64_t ss2;       // traces per pixel (ss^2), 1 in block mode
   uint64_t W;         // pixels per row of the trace index space
   uint32_t row_block, rank, nranks;
+  uint64_t lo, hi;    // nranks <= 1: trace range written
 };
 
 __device__ __forceinline__ bool owned(uint64_t idx, const EmitFilter &f)
 {
+  if (f.nranks <= 1) return idx >= f.lo && idx < f.hi;
   return ((idx / f.ss2 / f.W / f.row_block) % f.nranks) == f.rank;
 }
 
@@ -241,24 +243,58 @@ __device__ __forceinline__ bool owned(uint64_t idx, const EmitFilter &f)
 // places the accepted triples' states in LDS at their block-local rank, and writes the range out with
 // coalesced 4-byte stores.  Trace i then re-derives its randDir from that state (rd_from_state): three
 // LCG steps and three exact conversions.
+// Exclusive prefix sums of the nblk block counts (one workgroup, a contiguous run of counts per thread): the emit's
+// block offsets when there are many blocks or the emit skips most of them (multi-GPU), where every block summing its
+// predecessors itself (quadratic in nblk) would cost more than this launch.
+constexpr int kScanThreads = 1024;
+__global__ __launch_bounds__(kScanThreads) void rng_offsets(const uint32_t *blk_cnt, uint64_t nblk, uint64_t *off)
+{
+  __shared__ uint64_t s[kScanThreads];
+  const uint64_t per = (nblk + kScanThreads - 1) / kScanThreads;
+  const uint64_t b0 = min(nblk, (uint64_t)threadIdx.x * per), b1 = min(nblk, b0 + per);
+  uint64_t sum = 0;
+  for (uint64_t b = b0; b < b1; ++b) sum += blk_cnt[b];
+  s[threadIdx.x] = sum;
+  __syncthreads();
+  for (uint32_t o = 1; o < kScanThreads; o <<= 1)
+  {
+    const uint64_t x = threadIdx.x >= o ? s[threadIdx.x - o] : 0ull;
+    __syncthreads();
+    s[threadIdx.x] += x;
+    __syncthreads();
+  }
+  uint64_t run = s[threadIdx.x] - sum;
+  for (uint64_t b = b0; b < b1; ++b)
+  {
+    off[b] = run;
+    run += blk_cnt[b];
+  }
+}
+
 __global__ __launch_bounds__(kRngBlock) void rng_emit(const uint32_t *seed, const uint32_t *jump, const uint32_t *blk_cnt,
-                                                      const uint16_t *masks, uint64_t need, uint32_t *rd_state,
-                                                      uint32_t *next_seed, int *err, EmitFilter flt)
+                                                      const uint64_t *blk_off, const uint16_t *masks, uint64_t need,
+                                                      uint32_t *rd_state, uint32_t *next_seed, int *err, EmitFilter flt)
 {
   __shared__ uint32_t sst[kTriplesPerBlock];
   __shared__ uint32_t wsum[kRngBlock / 64];
-  // this block's first trace: the accept counts of the blocks before it, summed by the block (the count
-  // array is a few KB and L2-resident, so no separate scan pass)
-  uint32_t part = 0;
-  for (uint32_t k = threadIdx.x; k < blockIdx.x; k += kRngBlock) part += blk_cnt[k];
+  // this block's first trace: from the scanned offsets, or the accept counts of the blocks before it summed by the
+  // block (few blocks: the count array is a few KB and L2-resident, and no separate scan launch is needed)
+  uint64_t off;
+  if (blk_off)
+    off = blk_off[blockIdx.x];
+  else
+  {
+    uint32_t part = 0;
+    for (uint32_t k = threadIdx.x; k < blockIdx.x; k += kRngBlock) part += blk_cnt[k];
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
-  __shared__ uint64_t s_off;
-  if (threadIdx.x == 0) s_off = 0;
-  __syncthreads();
-  if ((threadIdx.x & 63) == 0) atomicAdd((unsigned long long *)&s_off, (unsigned long long)part);
-  __syncthreads();
-  const uint64_t off = s_off;
+    for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+    __shared__ uint64_t s_off;
+    if (threadIdx.x == 0) s_off = 0;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) atomicAdd((unsigned long long *)&s_off, (unsigned long long)part);
+    __syncthreads();
+    off = s_off;
+  }
   // the last block flags a stream too short for the frame (host: RFX_ERR_RNG)
   if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0 && off + blk_cnt[blockIdx.x] < need) *err = 1;
   if (off >= need) return;
@@ -266,6 +302,7 @@ __global__ __launch_bounds__(kRngBlock) void rng_emit(const uint32_t *seed, cons
   const uint64_t last = off + cnt - 1;
   // block-uniform skip: a block whose accepted indices all belong to other ranks' strips (and do not
   // include the frame's last trace, whose stream state every rank carries forward) writes nothing
+  if (flt.nranks <= 1 && last != need - 1 && (last < flt.lo || off >= flt.hi)) return;  // outside the band
   if (flt.nranks > 1 && last != need - 1)
   {
     const uint64_t s_lo = off / flt.ss2 / flt.W / flt.row_block, s_hi = last / flt.ss2 / flt.W / flt.row_block;
@@ -331,7 +368,7 @@ __global__ __launch_bounds__(kRngBlock) void rng_emit(const uint32_t *seed, cons
   for (uint32_t i = threadIdx.x; i < cnt; i += kRngBlock)
   {
     const uint64_t idx = off + i;
-    if (flt.nranks <= 1 || owned(idx, flt)) rd_state[idx] = sst[i];
+    if (owned(idx, flt)) rd_state[idx] = sst[i];
   }
 }
 
@@ -506,14 +543,17 @@ hipError_t launch_rng_count(const uint32_t *d_seed, const uint32_t *d_jump, uint
 }
 
 // second half: scan all nblk counts, scatter the randDirs this rank needs, carry the stream state
+// d_blk_off: nblk words of scratch for the scanned offsets, or null (every emit block sums its predecessors)
 hipError_t launch_rng_finish(const uint32_t *d_seed, const uint32_t *d_jump, uint32_t *d_next_seed,
                              const uint32_t *d_blk_cnt, const uint16_t *d_masks, uint64_t nblk, uint64_t traces,
                              uint32_t *d_rd_state, int *d_err, uint64_t ss2, uint64_t W, uint32_t row_block,
-                             uint32_t rank, uint32_t nranks, hipStream_t st)
+                             uint32_t rank, uint32_t nranks, uint64_t *d_blk_off, uint64_t lo, uint64_t hi,
+                             hipStream_t st)
 {
-  const EmitFilter flt{ss2 ? ss2 : 1, W ? W : 1, row_block ? row_block : 1, rank, nranks ? nranks : 1};
-  hipLaunchKernelGGL(rng_emit, dim3((uint32_t)nblk), dim3(kRngBlock), 0, st, d_seed, d_jump, d_blk_cnt, d_masks,
-                     traces, d_rd_state, d_next_seed, d_err, flt);
+  const EmitFilter flt{ss2 ? ss2 : 1, W ? W : 1, row_block ? row_block : 1, rank, nranks ? nranks : 1, lo, hi};
+  if (d_blk_off) hipLaunchKernelGGL(rng_offsets, dim3(1), dim3(kScanThreads), 0, st, d_blk_cnt, nblk, d_blk_off);
+  hipLaunchKernelGGL(rng_emit, dim3((uint32_t)nblk), dim3(kRngBlock), 0, st, d_seed, d_jump, d_blk_cnt,
+                     (const uint64_t *)d_blk_off, d_masks, traces, d_rd_state, d_next_seed, d_err, flt);
   return hipGetLastError();
 }
 

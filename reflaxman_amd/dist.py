@@ -38,6 +38,11 @@ class RfxStripOps:
         self.stream = stream_ptr
         self.L = _lib.load()
 
+    def set_rows(self, y0: int, y1: int):
+        """Band partition: this rank traces rows [y0, y1) (rfx.h: row_block 0, pixel span of whole rows)."""
+        self.frame.row_block = 0
+        self.frame.pixel_begin, self.frame.pixel_end = y0 * self.frame.width, y1 * self.frame.width
+
     def blocks_per_slice(self, nslices: int) -> int:
         bps = C.c_uint64()
         _lib.check(self.L.rfx_frame_rng_blocks(self.r._h, C.byref(self.frame), nslices, C.byref(bps)), "rng_blocks")
@@ -95,67 +100,23 @@ def strip_row_to_y(i: int, row_block: int, rank: int, world: int) -> int:
     return (i // row_block * world + rank) * row_block + i % row_block
 
 
-class StripFrame:
-    """Rank `rank`'s part of a W x H frame rendered by `world` ranks; rank 0 ends with the ARGB8 frame and,
-    with gather_rgb, the float RGB frame too (the reference's std::vector<Color> image, Render.h:10, that
-    Render::imagePixel reads, Render.cpp:103-114).
+class _CountedFrame:
+    """The per-frame RNG exchange of a partitioned frame (strips or bands): every rank counts its slice of the
+    frame's random stream, the slice counts are all-gathered, and the emit scans them (rfx.h
+    rfx_frame_rng_count / rfx_render_frame_counted).
 
-    pipeline (default: on for the nccl backend): the strip gathers of frame i run on their own communicator
-    (a second process group, so their RCCL stream does not serialise with the next frame's count
-    all-gather) while frame i+1 renders; strip and gather buffers are double-buffered, and rank 0
-    un-interleaves on a side stream.  A frame's assembled image is complete once the device is
-    synchronised (every step's work, gathers included, is on the device's streams).
-
-    count_ahead (default: on for the nccl backend): frame i+1's RNG count and its all-gather (a third
+    count_ahead (default: on for the nccl backend): frame i+1's RNG count and its all-gather (their own
     communicator, on a side stream) start as soon as frame i's randDirs are emitted -- the next frame's
     stream state is then on the device -- and run while frame i traces, so the exchange step leaves the
     per-frame critical path (count, all-gather, emit, trace becomes emit, trace).  The renderer's random
     stream must not advance between steps by any other call (drop_lookahead() first, on every rank).
     """
 
-    def __init__(self, ops, W: int, H: int, row_block: int, rank: int, world: int, device: torch.device,
-                 gather_to_root: bool = True, pipeline: Optional[bool] = None, gather_rgb: bool = False,
-                 count_ahead: Optional[bool] = None):
-        self.ops, self.W, self.H, self.rb = ops, W, H, row_block
-        self.rank, self.world, self.device = rank, world, device
-        self.gather_to_root = gather_to_root
-        self.gather_rgb = bool(gather_rgb) and gather_to_root and world > 1
-        self.rows = strip_rows(H, row_block, rank, world)
-        self.max_rows = max(strip_rows(H, row_block, r, world) for r in range(world))
+    def _init_counts(self, ops, rank: int, world: int, device: torch.device, count_ahead: Optional[bool]):
+        self.ops, self.rank, self.world, self.device = ops, rank, world, device
         self.bps = ops.blocks_per_slice(world)
         self.counts = torch.zeros(world * self.bps, dtype=torch.int32, device=device)
-        if pipeline is None:
-            pipeline = world > 1 and gather_to_root and dist.get_backend() == "nccl"
-        self.pipeline = bool(pipeline) and world > 1 and gather_to_root and not self._host_staged()
-        nbuf = 2 if self.pipeline else 1
-        # per-rank strip buffers (every rank the same size for the gather): ARGB8, float RGB
-        self.argb_bufs = [torch.zeros(self.max_rows * W, dtype=torch.int32, device=device) for _ in range(nbuf)]
-        self.img_bufs = [torch.zeros(max(self.max_rows, 1) * W * 3, dtype=torch.float32, device=device)
-                         for _ in range(nbuf if self.gather_rgb else 1)]
-        self.argb, self.img = self.argb_bufs[0], self.img_bufs[0]
-        # what rank 0 gathers: (strip buffers, values per frame row, dtype)
-        self.planes = [(self.argb_bufs, W, torch.int32)]
-        if self.gather_rgb:
-            self.planes.append((self.img_bufs, 3 * W, torch.float32))
-        self.fulls: List[List[torch.Tensor]] = []         # [plane][k]: H x per_row frame on rank 0
-        self.gather_lists: List[List[List[torch.Tensor]]] = []  # [plane][k][rank]
-        self.row_index: List[torch.Tensor] = []
-        if gather_to_root and rank == 0:
-            for bufs, per_row, dt in self.planes:
-                self.fulls.append([torch.zeros(H * per_row, dtype=dt, device=device) for _ in range(nbuf)])
-                self.gather_lists.append([[torch.empty_like(bufs[0]) for _ in range(world)] for _ in range(nbuf)])
-            for r in range(world):
-                n = strip_rows(H, row_block, r, world)
-                self.row_index.append(torch.tensor([strip_row_to_y(i, row_block, r, world) for i in range(n)],
-                                                   dtype=torch.int64, device=device))
-        self.full: Optional[torch.Tensor] = self.fulls[0][0] if self.fulls else None
-        self.rgb_full: Optional[torch.Tensor] = self.fulls[1][0] if self.gather_rgb and self.fulls else None
-        self.group = dist.new_group(list(range(world))) if self.pipeline else None
         cuda = device.type == "cuda"
-        self.side = torch.cuda.Stream(device=device) if self.pipeline and cuda and rank == 0 else None
-        self.works: List[list] = [[] for _ in range(nbuf)]
-        self.done: List[Optional[torch.cuda.Event]] = [None] * nbuf
-        self.frame = 0
         if count_ahead is None:
             count_ahead = world > 1 and dist.get_backend() == "nccl"
         # (asked for explicitly it also runs at world 1: the device-side ordering test, tests/test_gpu_multirank.py)
@@ -166,6 +127,23 @@ class StripFrame:
         if self.emitted is not None:
             self.emitted.record(torch.cuda.current_stream(device))  # torch creates the hipEvent_t at its first record
         self.ahead = None  # the next frame's count all-gather in flight (its work object), once one is
+
+    def _frame_counts(self):
+        """This frame's all-gathered slice counts in self.counts, ordered before the emit on this stream."""
+        if self.ahead is not None:
+            # counted and all-gathered while the last frame traced: order this stream after them
+            self.ahead.wait()
+        else:
+            self.ops.rng_count(self.rank, self.world, self.counts.data_ptr())
+            if self.world > 1:
+                self._all_gather_counts()
+        self.ahead = None
+
+    def _render(self, img: torch.Tensor, argb: torch.Tensor, d_counters: int):
+        self.ops.render_counted(self.world, self.counts.data_ptr(), img.data_ptr(), argb.data_ptr(), d_counters,
+                                self.emitted.cuda_event if self.emitted is not None else 0)
+        if self.count_ahead:
+            self._count_next()
 
     def _count_next(self):
         """Count the next frame's slice and start its all-gather, ordered after this frame's emit only."""
@@ -209,6 +187,62 @@ class StripFrame:
         else:
             dist.all_gather(list(self.counts.split(self.bps)), mine.clone())
 
+
+class StripFrame(_CountedFrame):
+    """Rank `rank`'s part of a W x H frame rendered by `world` ranks; rank 0 ends with the ARGB8 frame and,
+    with gather_rgb, the float RGB frame too (the reference's std::vector<Color> image, Render.h:10, that
+    Render::imagePixel reads, Render.cpp:103-114).
+
+    pipeline (default: on for the nccl backend): the strip gathers of frame i run on their own communicator
+    (a second process group, so their RCCL stream does not serialise with the next frame's count
+    all-gather) while frame i+1 renders; strip and gather buffers are double-buffered, and rank 0
+    un-interleaves on a side stream.  A frame's assembled image is complete once the device is
+    synchronised (every step's work, gathers included, is on the device's streams).  count_ahead: see
+    _CountedFrame.
+    """
+
+    def __init__(self, ops, W: int, H: int, row_block: int, rank: int, world: int, device: torch.device,
+                 gather_to_root: bool = True, pipeline: Optional[bool] = None, gather_rgb: bool = False,
+                 count_ahead: Optional[bool] = None):
+        self.W, self.H, self.rb = W, H, row_block
+        self._init_counts(ops, rank, world, device, count_ahead)
+        self.gather_to_root = gather_to_root
+        self.gather_rgb = bool(gather_rgb) and gather_to_root and world > 1
+        self.rows = strip_rows(H, row_block, rank, world)
+        self.max_rows = max(strip_rows(H, row_block, r, world) for r in range(world))
+        if pipeline is None:
+            pipeline = world > 1 and gather_to_root and dist.get_backend() == "nccl"
+        self.pipeline = bool(pipeline) and world > 1 and gather_to_root and not self._host_staged()
+        nbuf = 2 if self.pipeline else 1
+        # per-rank strip buffers (every rank the same size for the gather): ARGB8, float RGB
+        self.argb_bufs = [torch.zeros(self.max_rows * W, dtype=torch.int32, device=device) for _ in range(nbuf)]
+        self.img_bufs = [torch.zeros(max(self.max_rows, 1) * W * 3, dtype=torch.float32, device=device)
+                         for _ in range(nbuf if self.gather_rgb else 1)]
+        self.argb, self.img = self.argb_bufs[0], self.img_bufs[0]
+        # what rank 0 gathers: (strip buffers, values per frame row, dtype)
+        self.planes = [(self.argb_bufs, W, torch.int32)]
+        if self.gather_rgb:
+            self.planes.append((self.img_bufs, 3 * W, torch.float32))
+        self.fulls: List[List[torch.Tensor]] = []         # [plane][k]: H x per_row frame on rank 0
+        self.gather_lists: List[List[List[torch.Tensor]]] = []  # [plane][k][rank]
+        self.row_index: List[torch.Tensor] = []
+        if gather_to_root and rank == 0:
+            for bufs, per_row, dt in self.planes:
+                self.fulls.append([torch.zeros(H * per_row, dtype=dt, device=device) for _ in range(nbuf)])
+                self.gather_lists.append([[torch.empty_like(bufs[0]) for _ in range(world)] for _ in range(nbuf)])
+            for r in range(world):
+                n = strip_rows(H, row_block, r, world)
+                self.row_index.append(torch.tensor([strip_row_to_y(i, row_block, r, world) for i in range(n)],
+                                                   dtype=torch.int64, device=device))
+        self.full: Optional[torch.Tensor] = self.fulls[0][0] if self.fulls else None
+        self.rgb_full: Optional[torch.Tensor] = self.fulls[1][0] if self.gather_rgb and self.fulls else None
+        self.group = dist.new_group(list(range(world))) if self.pipeline else None
+        cuda = device.type == "cuda"
+        self.side = torch.cuda.Stream(device=device) if self.pipeline and cuda and rank == 0 else None
+        self.works: List[list] = [[] for _ in range(nbuf)]
+        self.done: List[Optional[torch.cuda.Event]] = [None] * nbuf
+        self.frame = 0
+
     def _gather_strips(self, k: int):
         for pi, (bufs, _, _) in enumerate(self.planes):
             lst = self.gather_lists[pi][k] if self.rank == 0 else None
@@ -251,18 +285,8 @@ class StripFrame:
         argb = self.argb_bufs[k]
         img = self.img_bufs[k % len(self.img_bufs)]
         self.argb, self.img = argb, img
-        if self.ahead is not None:
-            # this frame's counts were all-gathered while the last frame traced: order this stream after them
-            self.ahead.wait()
-        else:
-            self.ops.rng_count(self.rank, self.world, self.counts.data_ptr())
-            if self.world > 1:
-                self._all_gather_counts()
-        self.ahead = None
-        self.ops.render_counted(self.world, self.counts.data_ptr(), img.data_ptr(), argb.data_ptr(), d_counters,
-                                self.emitted.cuda_event if self.emitted is not None else 0)
-        if self.count_ahead:
-            self._count_next()
+        self._frame_counts()
+        self._render(img, argb, d_counters)
         if self.world == 1 or not self.gather_to_root:
             return argb[: self.rows * self.W].view(self.rows, self.W) if self.world == 1 else None
         if not self.pipeline:
@@ -286,3 +310,179 @@ class StripFrame:
             ev.record(self.side)
             self.done[k] = ev
         return fv
+
+
+def equal_bounds(H: int, world: int, grain: int = 8) -> List[int]:
+    """Band bounds (world + 1 rows, 0 .. H) of about H / world rows each, on multiples of `grain`."""
+    b = [0] + [min(H, max(0, int(round(H * r / world / grain)) * grain)) for r in range(1, world)] + [H]
+    return _fix_bounds(b, H, grain)
+
+
+def _fix_bounds(b: List[int], H: int, grain: int) -> List[int]:
+    """Strictly increasing bounds, each band at least `grain` rows where the frame allows it."""
+    world = len(b) - 1
+    g = grain if H >= grain * world else 1
+    out = [0]
+    for r in range(1, world):
+        out.append(min(max(b[r], out[-1] + g), H - g * (world - r)))
+    out.append(H)
+    return out
+
+
+def balanced_bounds(bounds: List[int], times: List[float], H: int, grain: int = 8) -> List[int]:
+    """New band bounds from each band's measured time per frame: the cost density of band r (time / rows) is taken
+    as uniform over its rows, and the frame's cumulative cost is cut into `world` equal parts on multiples of
+    `grain`.  Deterministic in its inputs, so ranks that all-gathered the same times agree on the result."""
+    world = len(bounds) - 1
+    rows = [bounds[r + 1] - bounds[r] for r in range(world)]
+    known = [t / n for t, n in zip(times, rows) if n > 0 and t > 0]
+    mean = sum(known) / len(known) if known else 1.0
+    dens = [(t / n if n > 0 and t > 0 else mean) for t, n in zip(times, rows)]
+    total = sum(d * n for d, n in zip(dens, rows))
+    out = [0]
+    r, acc = 0, 0.0  # acc: cost of the rows before band r's start
+    for k in range(1, world):
+        target = total * k / world
+        while r < world - 1 and acc + dens[r] * rows[r] < target:
+            acc += dens[r] * rows[r]
+            r += 1
+        y = bounds[r] + (target - acc) / dens[r]
+        out.append(int(round(y / grain)) * grain)
+    out.append(H)
+    return _fix_bounds(out, H, grain)
+
+
+class BandFrame(_CountedFrame):
+    """Rank `rank`'s band of a W x H frame rendered by `world` ranks: contiguous rows [bounds[rank],
+    bounds[rank + 1]), traced into whole-frame buffers (rfx.h band partition), so that rank 0 receives every band
+    straight into its rows of the frame -- its own band is rendered there in place -- with no strip
+    un-interleave: rank 0's work beyond the other ranks' is the RCCL receive alone.  Bands are load-balanced from
+    measured per-rank frame times (balance(): a few rounds before timing starts), which also shrinks rank 0's
+    band by what the receive costs it.  Rank 0 ends with the ARGB8 frame (and with gather_rgb the float RGB frame,
+    the reference's image that Render::imagePixel reads, Render.cpp:103-114).
+
+    pipeline (default: on for the nccl backend): frame i's band sends / receives run on their own communicator
+    while frame i + 1 renders into the other of two buffer sets.  count_ahead: see _CountedFrame.
+    """
+
+    def __init__(self, ops, W: int, H: int, rank: int, world: int, device: torch.device, gather_to_root: bool = True,
+                 pipeline: Optional[bool] = None, gather_rgb: bool = False, count_ahead: Optional[bool] = None,
+                 bounds: Optional[List[int]] = None, grain: int = 8):
+        self.W, self.H, self.grain = W, H, grain
+        self._init_counts(ops, rank, world, device, count_ahead)
+        self.gather_to_root = gather_to_root and world > 1
+        self.gather_rgb = bool(gather_rgb) and self.gather_to_root
+        if pipeline is None:
+            pipeline = world > 1 and gather_to_root and dist.get_backend() == "nccl"
+        self.pipeline = bool(pipeline) and self.gather_to_root and not self._host_staged()
+        nbuf = 2 if self.pipeline else 1
+        # whole-frame buffers: ARGB8 and float RGB (rank 0's are the assembled frames)
+        self.argb_bufs = [torch.zeros(H * W, dtype=torch.int32, device=device) for _ in range(nbuf)]
+        self.img_bufs = [torch.zeros(H * W * 3, dtype=torch.float32, device=device)
+                         for _ in range(nbuf if self.gather_rgb else 1)]
+        self.argb, self.img = self.argb_bufs[0], self.img_bufs[0]
+        self.group = dist.new_group(list(range(world))) if self.pipeline else None
+        self.works: List[list] = [[] for _ in range(nbuf)]
+        self.frame = 0
+        self._events: Optional[list] = None  # (start, end) HIP events around each frame's render while balancing
+        self.set_bounds(bounds or equal_bounds(H, world, grain))
+        self.full: Optional[torch.Tensor] = self.argb.view(H, W) if rank == 0 else None
+        self.rgb_full: Optional[torch.Tensor] = self.img.view(H, W, 3) if rank == 0 and self.gather_rgb else None
+
+    def set_bounds(self, bounds: List[int]):
+        """Band bounds for the next frames (the same list on every rank)."""
+        assert len(bounds) == self.world + 1 and bounds[0] == 0 and bounds[-1] == self.H, bounds
+        assert all(bounds[r] < bounds[r + 1] for r in range(self.world)), bounds
+        self.bounds = list(bounds)
+        self.y0, self.y1 = bounds[self.rank], bounds[self.rank + 1]
+        self.rows = self.y1 - self.y0
+        self.ops.set_rows(self.y0, self.y1)
+
+    def _sends(self, k: int):
+        """(tensor, peer, is_send) of frame buffer set k: every band to rank 0."""
+        W, ops = self.W, []
+        planes = [(self.argb_bufs[k], 1)]
+        if self.gather_rgb:
+            planes.append((self.img_bufs[k], 3))
+        for buf, per in planes:
+            if self.rank == 0:
+                for r in range(1, self.world):
+                    ops.append((buf[self.bounds[r] * W * per:self.bounds[r + 1] * W * per], r, False))
+            else:
+                ops.append((buf[self.y0 * W * per:self.y1 * W * per], 0, True))
+        return ops
+
+    def _exchange(self, k: int):
+        todo = self._sends(k)
+        if self._host_staged():  # gloo on device tensors (one-GPU rehearsal): through host memory, in order
+            for t, peer, send in todo:
+                if send:
+                    dist.send(t.cpu(), peer)
+                else:
+                    h = torch.empty(t.shape, dtype=t.dtype)
+                    dist.recv(h, peer)
+                    t.copy_(h)
+            return []
+        if dist.get_backend() == "nccl":
+            p2p = [dist.P2POp(dist.isend if send else dist.irecv, t, peer, group=self.group) for t, peer, send in todo]
+            return dist.batch_isend_irecv(p2p) if p2p else []
+        return [dist.isend(t, peer, group=self.group) if send else dist.irecv(t, peer, group=self.group)
+                for t, peer, send in todo]
+
+    def step(self, d_counters: int = 0) -> Optional[torch.Tensor]:
+        """Render this rank's band of one frame; rank 0 returns the (H, W) int32 ARGB frame (with pipeline:
+        complete once the device is synchronised; with gather_rgb also in self.rgb_full)."""
+        k = self.frame % len(self.argb_bufs)
+        self.frame += 1
+        for w in self.works[k]:  # buffer set k's sends / receives of two frames ago
+            w.wait()
+        self.works[k] = []
+        argb = self.argb_bufs[k]
+        img = self.img_bufs[k % len(self.img_bufs)]
+        self.argb, self.img = argb, img
+        self._frame_counts()
+        if self._events is not None:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
+        self._render(img, argb, d_counters)
+        if self._events is not None:
+            ev[1].record()
+            self._events.append(ev)
+        if self.world == 1 or not self.gather_to_root:
+            return argb.view(self.H, self.W) if self.world == 1 else None
+        works = self._exchange(k)
+        if self.pipeline and self.device.type == "cuda":
+            self.works[k] = works
+        else:
+            for w in works:
+                w.wait()
+        if self.rank != 0:
+            return None
+        self.full = argb.view(self.H, self.W)
+        if self.gather_rgb:
+            self.rgb_full = img.view(self.H, self.W, 3)
+        return self.full
+
+    def balance(self, rounds: int = 3, frames: int = 8, timer=None) -> List[int]:
+        """Re-cut the bands `rounds` times from each rank's measured render time over `frames` frames (HIP events
+        on the render stream, or `timer(step)` -> seconds per frame); returns the final bounds."""
+        for _ in range(rounds):
+            t = timer(self.step) if timer else self._time_render(frames)
+            times = torch.tensor([t], dtype=torch.float64)
+            if dist.get_backend() == "nccl":
+                times = times.to(self.device)
+            allt = [torch.zeros_like(times) for _ in range(self.world)]
+            dist.all_gather(allt, times)
+            self.set_bounds(balanced_bounds(self.bounds, [float(x.item()) for x in allt], self.H, self.grain))
+        return self.bounds
+
+    def _time_render(self, frames: int) -> float:
+        """Seconds per frame of this rank's emit + trace: HIP events around the render on its stream (after the
+        wait for the counts, so other ranks' progress is not counted; what concurrent sends / receives take from
+        the render on this device is)."""
+        self._events = []
+        for _ in range(frames):
+            self.step()
+        torch.cuda.synchronize(self.device)
+        ev, self._events = self._events, None
+        return sum(s.elapsed_time(e) for s, e in ev) * 1e-3 / max(len(ev), 1)

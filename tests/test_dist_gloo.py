@@ -25,6 +25,10 @@ class FakeOps:
         self.seen_counts = None
         self.frame = 0
         self.ncount = 0
+        self.band = None  # (y0, y1): band partition (whole-frame buffers, absolute rows)
+
+    def set_rows(self, y0, y1):
+        self.band = (y0, y1)
 
     def blocks_per_slice(self, nslices):
         return self.bps
@@ -41,11 +45,15 @@ class FakeOps:
         import numpy as np
         cnt = np.ctypeslib.as_array((ctypes.c_int32 * (nslices * self.bps)).from_address(d_counts)).copy()
         self.seen_counts = cnt
-        rows = rdist.strip_rows(self.H, self.rb, self.rank, self.world)
+        if self.band:  # whole-frame buffers, the band's rows written in place
+            rows = self.H
+            ys = [(y, y) for y in range(*self.band)]
+        else:
+            rows = rdist.strip_rows(self.H, self.rb, self.rank, self.world)
+            ys = [(i, rdist.strip_row_to_y(i, self.rb, self.rank, self.world)) for i in range(rows)]
         argb = np.ctypeslib.as_array((ctypes.c_int32 * (rows * self.W)).from_address(d_argb)) if rows else None
         rgb = np.ctypeslib.as_array((ctypes.c_float * (rows * self.W * 3)).from_address(d_img)) if rows else None
-        for i in range(rows):
-            y = rdist.strip_row_to_y(i, self.rb, self.rank, self.world)
+        for i, y in ys:
             argb[i * self.W:(i + 1) * self.W] = (self.frame << 24) | (y << 12) | np.arange(self.W)
             rgb[i * self.W * 3:(i + 1) * self.W * 3] = rgb_pattern(self.frame, y, self.W)
         self.frame += 1
@@ -123,3 +131,64 @@ def test_strip_helpers_match_library():
                     n = rdist.strip_rows(H, rb, r, world)
                     for i in (0, n // 2, n - 1) if n else ():
                         assert rdist.strip_row_to_y(i, rb, r, world) == L.rfx_strip_row_to_y(i, rb, r, world)
+
+
+def _band_worker(rank, world, port, W, H, pipeline, q, gather_rgb, count_ahead):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import numpy as np
+        ops = FakeOps(W, H, 0, rank, world)
+        sf = rdist.BandFrame(ops, W, H, rank, world, torch.device("cpu"), pipeline=pipeline, gather_rgb=gather_rgb,
+                             count_ahead=count_ahead, grain=2)
+        ok_frame = True
+        bounds = []
+        for frame in range(5):
+            if frame == 2:
+                # re-cut the bands from fake per-rank times (rank r's rows cost r + 1 each): the frames stay whole
+                nb = sf.balance(rounds=2, timer=lambda step: (step(), sf.rows * (sf.rank + 1))[1])
+                bounds.append(nb)
+            out = sf.step()
+            fno = ops.frame - 1
+            if rank == 0:
+                ys, xs = torch.meshgrid(torch.arange(H), torch.arange(W), indexing="ij")
+                ok_frame &= bool(torch.equal(out, ((fno << 24) | (ys << 12) | xs).to(torch.int32)))
+                if gather_rgb:
+                    want = np.stack([rgb_pattern(fno, y, W) for y in range(H)]).reshape(H, W, 3)
+                    ok_frame &= bool(np.array_equal(sf.rgb_full.numpy(), want))
+            else:
+                ok_frame &= out is None
+        q.put((rank, ok_frame, bounds[0]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("pipeline,gather_rgb,count_ahead", [(False, False, False), (True, True, True)])
+@pytest.mark.parametrize("world,W,H", [(2, 16, 37), (3, 8, 64)])
+def test_band_frame_gloo(world, W, H, pipeline, gather_rgb, count_ahead):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_band_worker, args=(r, world, port, W, H, pipeline, q, gather_rgb, count_ahead))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    res = sorted(q.get(timeout=10) for _ in range(world))
+    assert [r[1] for r in res] == [True] * world, res
+    b = res[0][2]
+    assert all(r[2] == b for r in res)  # every rank cut the same bands
+    assert b[0] == 0 and b[-1] == H and all(b[i] < b[i + 1] for i in range(world))
+    assert b[1] - b[0] > b[world] - b[world - 1]  # the cheap rank 0 took more rows than the dearest
+
+
+def test_balanced_bounds():
+    # uniform cost: equal bands; a band twice as dear per row: cut where the cumulative cost halves
+    assert rdist.balanced_bounds([0, 50, 100], [1.0, 1.0], 100, 1) == [0, 50, 100]
+    assert rdist.balanced_bounds([0, 50, 100], [1.0, 3.0], 100, 1) == [0, 67, 100]
+    b = rdist.balanced_bounds(rdist.equal_bounds(4320, 8), [1, 1, 1, 1, 2, 2, 2, 2], 4320)
+    assert b[0] == 0 and b[-1] == 4320 and all(x % 8 == 0 for x in b) and b == sorted(set(b))
+    # degenerate inputs keep valid bands
+    assert rdist.balanced_bounds([0, 8, 16, 24], [0.0, 1.0, 1e9], 24, 8) == [0, 8, 16, 24]

@@ -21,12 +21,12 @@ def _port():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 3])
-def test_bench_multirank_frame_matches_single_gpu(world):
+@pytest.mark.parametrize("world,partition", [(2, "bands"), (3, "bands"), (2, "strips"), (3, "strips")])
+def test_bench_multirank_frame_matches_single_gpu(world, partition):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
            "--master-addr", "127.0.0.1", f"--master-port={_port()}", os.path.join(ROOT, "bench.py"),
            "--gpus", str(world), "--steps", "2", "--warmup", "1", "--width", "640", "--height", "360",
-           "--backend", "gloo", "--one-device", "--no-cpu-baseline"]
+           "--backend", "gloo", "--one-device", "--no-cpu-baseline", "--partition", partition]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-3000:]
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
@@ -34,6 +34,9 @@ def test_bench_multirank_frame_matches_single_gpu(world):
     assert out["n_gpus"] == world
     assert out["parity"]["multi_rank_frame_equals_single_gpu"] is True
     assert out["value"] > 0
+    if partition == "bands":
+        b = out["band_bounds"]
+        assert len(b) == world + 1 and b[0] == 0 and b[-1] == 360
 
 
 def _count_ahead_worker():

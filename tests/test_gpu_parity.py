@@ -370,6 +370,51 @@ def test_c4_strips_assemble_to_reference_hash(nranks):
     assert sha(img) == c["sha_f32"]
 
 
+@pytest.mark.parametrize("bounds", [[0, 2000, 4320], [0, 1000, 2200, 2208, 4320],
+                                    [0, 600, 1096, 1600, 2160, 2704, 3240, 3800, 4320]])
+def test_c4_bands_assemble_to_reference_hash(bounds):
+    """C4 under the band partition (rfx.h: nranks > 1, row_block 0), with uneven bands as the balancer cuts them
+    (one of them 8 rows): each rank counts its slice of the random stream (the exchange emulated: every rank counts
+    every slice), emits and traces only its rows into a whole-frame buffer, and the bands are copied into one
+    frame, as rank 0 receives them: SHA-256 of the f32 frame and of the ARGB8 frame equal the reference's."""
+    import ctypes as C
+    from reflaxman_amd import _lib
+    from reflaxman_amd.render import Renderer, build_scene, make_frame
+    c = CASES["hash_synth16_7680x4320_d8"]
+    W, H, depth = c["W"], c["H"], c["depth"]
+    nranks = len(bounds) - 1
+    s, cam = build_scene(scene("synth16"))
+    L = _lib.load()
+    img = np.zeros((H, W, 3), np.float32)
+    argb = np.zeros((H, W), np.uint32)
+    for rank in range(nranks):
+        y0, y1 = bounds[rank], bounds[rank + 1]
+        rr = Renderer(sphere_seed=c["sphere_seed"])
+        rr.set_scene(s)
+        f = make_frame(cam, W, H, depth, 1, row_block=0, rank=rank, nranks=nranks, pixel_begin=y0 * W,
+                       pixel_end=y1 * W)
+        bps = C.c_uint64()
+        _lib.check(L.rfx_frame_rng_blocks(rr._h, C.byref(f), nranks, C.byref(bps)))
+        d_cnt, p_img, p_argb = C.c_void_p(), C.c_void_p(), C.c_void_p()
+        _lib.check(L.rfx_device_alloc(rr._h, nranks * bps.value * 4, C.byref(d_cnt)))
+        for sl in range(nranks):
+            _lib.check(L.rfx_frame_rng_count(rr._h, C.byref(f), sl, nranks, d_cnt, None))
+        _lib.check(L.rfx_device_alloc(rr._h, H * W * 12, C.byref(p_img)))
+        _lib.check(L.rfx_device_alloc(rr._h, H * W * 4, C.byref(p_argb)))
+        _lib.check(L.rfx_render_frame_counted(rr._h, C.byref(f), nranks, d_cnt, p_img, p_argb, None, None))
+        part = np.empty((H, W, 3), np.float32)
+        part_argb = np.empty((H, W), np.uint32)
+        _lib.check(L.rfx_memcpy_d2h(rr._h, part.ctypes.data_as(C.c_void_p), p_img, part.nbytes))
+        _lib.check(L.rfx_memcpy_d2h(rr._h, part_argb.ctypes.data_as(C.c_void_p), p_argb, part_argb.nbytes))
+        img[y0:y1] = part[y0:y1]
+        argb[y0:y1] = part_argb[y0:y1]
+        for p in (d_cnt, p_img, p_argb):
+            L.rfx_device_free(rr._h, p)
+        rr.close()
+    assert sha(argb) == c["sha_argb"]
+    assert sha(img) == c["sha_f32"]
+
+
 def test_textures_loaded_from_tga_files(tmp_path):
     """The scene's textures read from TGA files by the library's loader (Scene.addTexture /
     setSkyboxTexture, Texture.cpp:34-108) -- the files the reference read for the same golden."""

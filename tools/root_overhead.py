@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--width", type=int, default=7680)
     ap.add_argument("--height", type=int, default=4320)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--partition", choices=["strips", "bands"], default="strips",
+                    help="bands: rank 0 traces rows [0, H / N) into the whole frame and receives the other bands in place")
     a = ap.parse_args()
     N, W, H, rb = a.nranks, a.width, a.height, 8
     L = _lib.load()
@@ -46,12 +48,15 @@ def main():
     rr = Renderer(device=0, sphere_seed=1350490027)
     rr.set_scene(scene)
     rr.set_stream(st.cuda_stream)
-    f = make_frame(cam, W, H, 8, 1, row_block=rb, rank=0, nranks=N)
+    bands = a.partition == "bands"
+    band = (H // N) // 8 * 8
+    f = make_frame(cam, W, H, 8, 1, row_block=0 if bands else rb, rank=0, nranks=N,
+                   pixel_begin=0, pixel_end=band * W if bands else 0)
     bps = C.c_uint64()
     _lib.check(L.rfx_frame_rng_blocks(rr._h, C.byref(f), N, C.byref(bps)))
     counts = torch.zeros(N * bps.value, dtype=torch.int32, device=dev)
-    rows = strip_rows(H, rb, 0, N)
-    maxr = max(strip_rows(H, rb, r, N) for r in range(N))
+    rows = band if bands else strip_rows(H, rb, 0, N)
+    maxr = H if bands else max(strip_rows(H, rb, r, N) for r in range(N))
     img = torch.zeros(maxr * W * 3, dtype=torch.float32, device=dev)
     argb = [torch.zeros(maxr * W, dtype=torch.int32, device=dev) for _ in range(2)]
     src = [torch.randint(0, 1 << 24, (maxr * W,), dtype=torch.int32, device=dev) for _ in range(N)]
@@ -77,6 +82,12 @@ def main():
         ev.record(st)
         with torch.cuda.stream(side):
             side.wait_event(ev)
+            if bands:  # the other bands land in their rows of rank 0's frame: no un-interleave
+                argb[b][band * W:].copy_(src[1][band * W:])
+                e2 = torch.cuda.Event()
+                e2.record(side)
+                done[b] = e2
+                return
             gl[b][0].copy_(argb[b])  # rank 0's own strip: a local copy in the gather
             for r in range(1, N):
                 gl[b][r].copy_(src[r])  # the received strips landing in HBM
@@ -91,6 +102,23 @@ def main():
     for _ in range(5):
         frame(0, True)
     torch.cuda.synchronize()
+    # phases of rank 0's own frame (HIP events: the emit of the counted pre-pass, the trace), and the N counts
+    rr.get_timing()
+    rr.set_timing(True)
+    for k in range(a.frames):
+        frame(k, False)
+    pre_ms, trace_ms, nfr = rr.get_timing()
+    rr.set_timing(False)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record(st)
+    for k in range(a.frames):
+        for s in range(N):
+            _lib.check(L.rfx_frame_rng_count(rr._h, C.byref(f), s, N, C.c_void_p(counts.data_ptr()),
+                                             C.c_void_p(st.cuda_stream)))
+    ev1.record(st)
+    torch.cuda.synchronize()
+    phases = {"emit_ms": pre_ms / max(nfr, 1), "trace_ms": trace_ms / max(nfr, 1),
+              "counts_all_slices_ms": ev0.elapsed_time(ev1) / a.frames}
     for _ in range(a.rounds):
         for mode, asm in (("alone", False), ("with_assembly", True)):
             torch.cuda.synchronize()
@@ -99,8 +127,9 @@ def main():
                 frame(k, asm)
             torch.cuda.synchronize()
             res[mode].append((time.perf_counter() - t0) / a.frames * 1e3)
-    out = {"nranks": N, "frame": [W, H], "rank0_rows": rows, "ms_per_frame": {k: sorted(v)[len(v) // 2] for k, v in res.items()}}
+    out = {"nranks": N, "partition": a.partition, "frame": [W, H], "rank0_rows": rows, "ms_per_frame": {k: sorted(v)[len(v) // 2] for k, v in res.items()}}
     out["root_extra_frac"] = round(out["ms_per_frame"]["with_assembly"] / out["ms_per_frame"]["alone"] - 1, 4)
+    out["phases_alone"] = {k: round(v, 4) for k, v in phases.items()}
     print(json.dumps(out))
 
 
