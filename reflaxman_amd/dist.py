@@ -369,6 +369,8 @@ class BandFrame(_CountedFrame):
                  pipeline: Optional[bool] = None, gather_rgb: bool = False, count_ahead: Optional[bool] = None,
                  bounds: Optional[List[int]] = None, grain: int = 8):
         self.W, self.H, self.grain = W, H, grain
+        b0 = bounds or equal_bounds(H, world, grain)
+        ops.set_rows(b0[rank], b0[rank + 1])  # the frame is a band frame from here on (the RNG layout below reads it)
         self._init_counts(ops, rank, world, device, count_ahead)
         self.gather_to_root = gather_to_root and world > 1
         self.gather_rgb = bool(gather_rgb) and self.gather_to_root
@@ -385,7 +387,7 @@ class BandFrame(_CountedFrame):
         self.works: List[list] = [[] for _ in range(nbuf)]
         self.frame = 0
         self._events: Optional[list] = None  # (start, end) HIP events around each frame's render while balancing
-        self.set_bounds(bounds or equal_bounds(H, world, grain))
+        self.set_bounds(b0)
         self.full: Optional[torch.Tensor] = self.argb.view(H, W) if rank == 0 else None
         self.rgb_full: Optional[torch.Tensor] = self.img.view(H, W, 3) if rank == 0 and self.gather_rgb else None
 
