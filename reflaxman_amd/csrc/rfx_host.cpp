@@ -32,8 +32,11 @@ hipError_t launch_rng_count(const uint32_t *d_seed, const uint32_t *d_jump, uint
 hipError_t launch_rng_finish(const uint32_t *d_seed, const uint32_t *d_jump, uint32_t *d_next_seed,
                              const uint32_t *d_blk_cnt, const uint16_t *d_masks, uint64_t nblk, uint64_t traces,
                              uint32_t *d_rd_state, int *d_err, uint64_t ss2, uint64_t W, uint32_t row_block,
-                             uint32_t rank, uint32_t nranks, uint64_t *d_blk_off, uint64_t lo, uint64_t hi,
-                             hipStream_t st);
+                             uint32_t rank, uint32_t nranks, hipStream_t st);
+hipError_t launch_rng_finish_band(const uint32_t *d_seed, const uint32_t *d_jump, uint32_t *d_next_seed,
+                                  const uint32_t *d_blk_cnt, uint64_t nblk, uint64_t traces, uint32_t *d_rd_state,
+                                  int *d_err, uint64_t lo, uint64_t hi, uint64_t *d_off, uint32_t *d_range,
+                                  hipStream_t st);
 hipError_t launch_trace(const DevScene &S, const FrameParams &P, bool stats, hipStream_t st);
 hipError_t launch_prim_cull(const DevScene &S, const FrameParams &P, uint64_t *masks, hipStream_t st);
 hipError_t launch_queue_sort(const uint32_t *count, const uint32_t *key, uint32_t *hist, uint32_t *order, hipStream_t st);
@@ -475,7 +478,8 @@ struct rfx_renderer {
   // workspaces
   uint32_t *d_rd = nullptr; uint64_t rd_cap = 0;  // per-trace LCG states (rng_emit)
   uint32_t *d_blk_cnt = nullptr; uint64_t blk_cap = 0;
-  uint64_t *d_blk_off = nullptr;  // the emit's scanned block offsets (rng_scan)
+  uint64_t *d_blk_off = nullptr;     // band emits: the scanned block offsets ...
+  uint32_t *d_rng_range = nullptr;   // ... and the band's first / last / final block
   uint16_t *d_rng_masks = nullptr;  // one device's accept flags per pre-pass thread (rng_count -> rng_emit)
   uint32_t *d_jump = nullptr;  // LCG jump table for blk_cap blocks (rng_jump_table)
   // host staging for rfx_render_frame_host
@@ -608,6 +612,7 @@ extern "C" void rfx_renderer_destroy(rfx_renderer *r)
   free_scene(r);
   (void)hipFree(r->d_seed); (void)hipFree(r->d_err); (void)hipFree(r->d_rd);
   (void)hipFree(r->d_blk_cnt); (void)hipFree(r->d_jump); (void)hipFree(r->d_rng_masks); (void)hipFree(r->d_blk_off);
+  (void)hipFree(r->d_rng_range);
   (void)hipFree(r->d_img); (void)hipFree(r->d_argb); (void)hipFree(r->d_cnt);
   (void)hipFree(r->d_queue); (void)hipFree(r->d_qctr); (void)hipFree(r->d_prim_mask);
   (void)hipFree(r->d_qkey); (void)hipFree(r->d_qorder);
@@ -1124,6 +1129,7 @@ static int ensure_rng_workspace(rfx_renderer *r, uint64_t traces, uint64_t nblk)
     r->d_blk_cnt = nullptr; r->d_jump = nullptr; r->d_rng_masks = nullptr; r->d_blk_off = nullptr; r->blk_cap = 0;
     HIP_CHECK(hipMalloc(&r->d_blk_cnt, nblk * sizeof(uint32_t)));
     HIP_CHECK(hipMalloc(&r->d_blk_off, nblk * sizeof(uint64_t)));
+    if (!r->d_rng_range) HIP_CHECK(hipMalloc(&r->d_rng_range, 4 * sizeof(uint32_t)));
     HIP_CHECK(hipMalloc(&r->d_rng_masks, nblk * 256 * sizeof(uint16_t)));
     std::vector<uint32_t> jump(2 * (256 + nblk));
     rng_jump_table(nblk, jump.data());
@@ -1132,16 +1138,6 @@ static int ensure_rng_workspace(rfx_renderer *r, uint64_t traces, uint64_t nblk)
     r->blk_cap = nblk;
   }
   return RFX_OK;
-}
-
-// Block offsets of the emit from a scan launch (multi-GPU strips: the emit skips most blocks, so their own prefix
-// sums would be nearly all of its work; many blocks: those sums grow quadratically), else summed by each block
-#ifndef RFX_RNG_SCAN_MIN_BLOCKS
-#define RFX_RNG_SCAN_MIN_BLOCKS 8192  // C3: 3.9K blocks, C4 frame: 15.5K
-#endif
-static uint64_t *rng_scan(rfx_renderer *r, uint64_t nblk, uint32_t nranks)
-{
-  return (nranks > 1 || nblk >= RFX_RNG_SCAN_MIN_BLOCKS) ? r->d_blk_off : nullptr;
 }
 
 // Whole pre-pass on one device: every block counted here (the 1-GPU path, and the redundant form of the
@@ -1153,7 +1149,7 @@ static int enqueue_rng(rfx_renderer *r, uint64_t traces, hipStream_t st)
   if ((rc = ensure_rng_workspace(r, traces, nblk)) != RFX_OK) return rc;
   HIP_CHECK(launch_rng_count(seed_cur(r), r->d_jump, r->d_blk_cnt, 0, nblk, r->d_rng_masks, st));
   HIP_CHECK(launch_rng_finish(seed_cur(r), r->d_jump, seed_next(r), r->d_blk_cnt, r->d_rng_masks, nblk, traces,
-                              r->d_rd, r->d_err, 1, 1, 1, 0, 1, rng_scan(r, nblk, 1), 0, UINT64_MAX, st));
+                              r->d_rd, r->d_err, 1, 1, 1, 0, 1, st));
   r->seed_idx ^= 1u;
   return RFX_OK;
 }
@@ -1245,9 +1241,12 @@ static int finish_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *d_counts
   FrameParams &P = pl.P;
   const hipStream_t st = pl.st;
   const uint64_t ss2 = P.ss > 0 ? (uint64_t)(P.ss * P.ss) : 1;
-  HIP_CHECK(launch_rng_finish(seed_cur(r), r->d_jump, seed_next(r), d_counts, d_masks, nblk, pl.traces, r->d_rd,
-                              r->d_err, ss2, P.W, P.row_block, P.rank, P.nranks,
-                              rng_scan(r, nblk, pl.band ? 2 : P.nranks), pl.band_lo, pl.band_hi, st));
+  if (pl.band)
+    HIP_CHECK(launch_rng_finish_band(seed_cur(r), r->d_jump, seed_next(r), d_counts, nblk, pl.traces, r->d_rd, r->d_err,
+                                     pl.band_lo, pl.band_hi, r->d_blk_off, r->d_rng_range, st));
+  else
+    HIP_CHECK(launch_rng_finish(seed_cur(r), r->d_jump, seed_next(r), d_counts, d_masks, nblk, pl.traces, r->d_rd,
+                                r->d_err, ss2, P.W, P.row_block, P.rank, P.nranks, st));
   r->seed_idx ^= 1u;
   // the caller's event: the randDirs are written and the next frame's stream state is known (the next frame's
   // RNG count may start on another stream while this frame traces)

@@ -243,62 +243,17 @@ __device__ __forceinline__ bool owned(uint64_t idx, const EmitFilter &f)
 // places the accepted triples' states in LDS at their block-local rank, and writes the range out with
 // coalesced 4-byte stores.  Trace i then re-derives its randDir from that state (rd_from_state): three
 // LCG steps and three exact conversions.
-// Exclusive prefix sums of the nblk block counts (one workgroup, a contiguous run of counts per thread): the emit's
-// block offsets when there are many blocks or the emit skips most of them (multi-GPU), where every block summing its
-// predecessors itself (quadratic in nblk) would cost more than this launch.
 constexpr int kScanThreads = 1024;
-__global__ __launch_bounds__(kScanThreads) void rng_offsets(const uint32_t *blk_cnt, uint64_t nblk, uint64_t *off)
-{
-  __shared__ uint64_t s[kScanThreads];
-  const uint64_t per = (nblk + kScanThreads - 1) / kScanThreads;
-  const uint64_t b0 = min(nblk, (uint64_t)threadIdx.x * per), b1 = min(nblk, b0 + per);
-  uint64_t sum = 0;
-  for (uint64_t b = b0; b < b1; ++b) sum += blk_cnt[b];
-  s[threadIdx.x] = sum;
-  __syncthreads();
-  for (uint32_t o = 1; o < kScanThreads; o <<= 1)
-  {
-    const uint64_t x = threadIdx.x >= o ? s[threadIdx.x - o] : 0ull;
-    __syncthreads();
-    s[threadIdx.x] += x;
-    __syncthreads();
-  }
-  uint64_t run = s[threadIdx.x] - sum;
-  for (uint64_t b = b0; b < b1; ++b)
-  {
-    off[b] = run;
-    run += blk_cnt[b];
-  }
-}
 
-__global__ __launch_bounds__(kRngBlock) void rng_emit(const uint32_t *seed, const uint32_t *jump, const uint32_t *blk_cnt,
-                                                      const uint64_t *blk_off, const uint16_t *masks, uint64_t need,
-                                                      uint32_t *rd_state, uint32_t *next_seed, int *err, EmitFilter flt)
+// One block of the emit: block b's accepted triples are the traces [off, off + blk_cnt[b]).  Every thread of the
+// workgroup calls it with the same b and off.
+__device__ __forceinline__ void emit_block(uint32_t b, uint64_t off, const uint32_t *seed, const uint32_t *jump,
+                                           const uint32_t *blk_cnt, const uint16_t *masks, uint64_t need,
+                                           uint32_t *rd_state, uint32_t *next_seed, const EmitFilter &flt,
+                                           uint32_t *sst, uint32_t *wsum)
 {
-  __shared__ uint32_t sst[kTriplesPerBlock];
-  __shared__ uint32_t wsum[kRngBlock / 64];
-  // this block's first trace: from the scanned offsets, or the accept counts of the blocks before it summed by the
-  // block (few blocks: the count array is a few KB and L2-resident, and no separate scan launch is needed)
-  uint64_t off;
-  if (blk_off)
-    off = blk_off[blockIdx.x];
-  else
-  {
-    uint32_t part = 0;
-    for (uint32_t k = threadIdx.x; k < blockIdx.x; k += kRngBlock) part += blk_cnt[k];
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
-    __shared__ uint64_t s_off;
-    if (threadIdx.x == 0) s_off = 0;
-    __syncthreads();
-    if ((threadIdx.x & 63) == 0) atomicAdd((unsigned long long *)&s_off, (unsigned long long)part);
-    __syncthreads();
-    off = s_off;
-  }
-  // the last block flags a stream too short for the frame (host: RFX_ERR_RNG)
-  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0 && off + blk_cnt[blockIdx.x] < need) *err = 1;
   if (off >= need) return;
-  const uint32_t cnt = (uint32_t)min((uint64_t)blk_cnt[blockIdx.x], need - off);  // triples this block emits
+  const uint32_t cnt = (uint32_t)min((uint64_t)blk_cnt[b], need - off);  // triples this block emits
   const uint64_t last = off + cnt - 1;
   // block-uniform skip: a block whose accepted indices all belong to other ranks' strips (and do not
   // include the frame's last trace, whose stream state every rank carries forward) writes nothing
@@ -310,14 +265,14 @@ __global__ __launch_bounds__(kRngBlock) void rng_emit(const uint32_t *seed, cons
     for (uint64_t st = s_lo; st <= s_hi && !any; ++st) any = (st % flt.nranks) == flt.rank;
     if (!any) return;
   }
-  uint32_t s = thread_state(*seed, jump, blockIdx.x, threadIdx.x);
+  uint32_t s = thread_state(*seed, jump, b, threadIdx.x);
   uint32_t s2 = kHalfJump.a * s + kHalfJump.c;
   uint32_t st[kTriplesPerThread];
   uint32_t acc = 0, c = 0;
   if (masks)
   {
     // the accept flags rng_count recorded: only the LCG states are regenerated (3 steps per triple)
-    acc = masks[(uint64_t)blockIdx.x * kRngBlock + threadIdx.x];
+    acc = masks[(uint64_t)b * kRngBlock + threadIdx.x];
     c = (uint32_t)__popc(acc);
 #pragma unroll
     for (int j = 0; j < kHalfRun; ++j)
@@ -369,6 +324,84 @@ __global__ __launch_bounds__(kRngBlock) void rng_emit(const uint32_t *seed, cons
   {
     const uint64_t idx = off + i;
     if (owned(idx, flt)) rd_state[idx] = sst[i];
+  }
+}
+
+__global__ __launch_bounds__(kRngBlock) void rng_emit(const uint32_t *seed, const uint32_t *jump, const uint32_t *blk_cnt,
+                                                      const uint16_t *masks, uint64_t need, uint32_t *rd_state,
+                                                      uint32_t *next_seed, int *err, EmitFilter flt)
+{
+  __shared__ uint32_t sst[kTriplesPerBlock];
+  __shared__ uint32_t wsum[kRngBlock / 64];
+  // this block's first trace: the accept counts of the blocks before it, summed by the block (the count
+  // array is a few KB and L2-resident, so no separate scan pass)
+  uint32_t part = 0;
+  for (uint32_t k = threadIdx.x; k < blockIdx.x; k += kRngBlock) part += blk_cnt[k];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+  __shared__ uint64_t s_off;
+  if (threadIdx.x == 0) s_off = 0;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) atomicAdd((unsigned long long *)&s_off, (unsigned long long)part);
+  __syncthreads();
+  const uint64_t off = s_off;
+  // the last block flags a stream too short for the frame (host: RFX_ERR_RNG)
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0 && off + blk_cnt[blockIdx.x] < need) *err = 1;
+  emit_block(blockIdx.x, off, seed, jump, blk_cnt, masks, need, rd_state, next_seed, flt, sst, wsum);
+}
+
+// Band emit (multi-GPU band partition): only the blocks holding the band's traces [flt.lo, flt.hi), and the block of
+// the frame's last trace (every rank carries the stream state past it), run -- a rank of N emits about 1/N of the
+// blocks instead of launching all of them.  One workgroup scans the counts into offsets and finds those blocks
+// (range: first, last, final); the emit's workgroups then loop over them.
+__global__ __launch_bounds__(kScanThreads) void rng_band_range(const uint32_t *blk_cnt, uint64_t nblk, uint64_t need,
+                                                               uint64_t lo, uint64_t hi, uint64_t *off, uint32_t *range,
+                                                               int *err)
+{
+  __shared__ uint64_t s[kScanThreads];
+  const uint64_t per = (nblk + kScanThreads - 1) / kScanThreads;
+  const uint64_t b0 = min(nblk, (uint64_t)threadIdx.x * per), b1 = min(nblk, b0 + per);
+  uint64_t sum = 0;
+  for (uint64_t b = b0; b < b1; ++b) sum += blk_cnt[b];
+  s[threadIdx.x] = sum;
+  __syncthreads();
+  for (uint32_t o = 1; o < kScanThreads; o <<= 1)
+  {
+    const uint64_t x = threadIdx.x >= o ? s[threadIdx.x - o] : 0ull;
+    __syncthreads();
+    s[threadIdx.x] += x;
+    __syncthreads();
+  }
+  if (threadIdx.x == kScanThreads - 1 && s[threadIdx.x] < need) *err = 1;  // stream too short for the frame
+  uint64_t run = s[threadIdx.x] - sum;
+  // block b holds traces [run, run + cnt_b): first = the block holding lo, last = the one holding hi - 1,
+  // final = the one holding need - 1 (each is exactly one block: the ranges tile [0, total))
+  for (uint64_t b = b0; b < b1; ++b)
+  {
+    const uint64_t c = blk_cnt[b], e = run + c;
+    off[b] = run;
+    if (c && run <= lo && lo < e) range[0] = (uint32_t)b;
+    if (c && run <= hi - 1 && hi - 1 < e) range[1] = (uint32_t)b;
+    if (c && run <= need - 1 && need - 1 < e) range[2] = (uint32_t)b;
+    run = e;
+  }
+}
+
+__global__ __launch_bounds__(kRngBlock) void rng_emit_band(const uint32_t *seed, const uint32_t *jump,
+                                                           const uint32_t *blk_cnt, const uint64_t *off,
+                                                           const uint32_t *range, uint64_t nblk, uint64_t need,
+                                                           uint32_t *rd_state, uint32_t *next_seed, EmitFilter flt)
+{
+  __shared__ uint32_t sst[kTriplesPerBlock];
+  __shared__ uint32_t wsum[kRngBlock / 64];
+  const uint32_t first = range[0], last = range[1], fin = range[2];
+  const uint32_t n = last - first + 1 + (fin > last || fin < first ? 1u : 0u);  // the band's blocks, then the final one
+  for (uint32_t j = blockIdx.x; j < n; j += gridDim.x)
+  {
+    const uint32_t b = j <= last - first ? first + j : fin;
+    if (b >= nblk) break;  // (a stream too short for the frame leaves the range unset: the error flag is raised)
+    emit_block(b, off[b], seed, jump, blk_cnt, nullptr, need, rd_state, next_seed, flt, sst, wsum);
+    __syncthreads();  // sst / wsum are reused by the next block
   }
 }
 
@@ -543,17 +576,33 @@ hipError_t launch_rng_count(const uint32_t *d_seed, const uint32_t *d_jump, uint
 }
 
 // second half: scan all nblk counts, scatter the randDirs this rank needs, carry the stream state
-// d_blk_off: nblk words of scratch for the scanned offsets, or null (every emit block sums its predecessors)
 hipError_t launch_rng_finish(const uint32_t *d_seed, const uint32_t *d_jump, uint32_t *d_next_seed,
                              const uint32_t *d_blk_cnt, const uint16_t *d_masks, uint64_t nblk, uint64_t traces,
                              uint32_t *d_rd_state, int *d_err, uint64_t ss2, uint64_t W, uint32_t row_block,
-                             uint32_t rank, uint32_t nranks, uint64_t *d_blk_off, uint64_t lo, uint64_t hi,
-                             hipStream_t st)
+                             uint32_t rank, uint32_t nranks, hipStream_t st)
 {
-  const EmitFilter flt{ss2 ? ss2 : 1, W ? W : 1, row_block ? row_block : 1, rank, nranks ? nranks : 1, lo, hi};
-  if (d_blk_off) hipLaunchKernelGGL(rng_offsets, dim3(1), dim3(kScanThreads), 0, st, d_blk_cnt, nblk, d_blk_off);
-  hipLaunchKernelGGL(rng_emit, dim3((uint32_t)nblk), dim3(kRngBlock), 0, st, d_seed, d_jump, d_blk_cnt,
-                     (const uint64_t *)d_blk_off, d_masks, traces, d_rd_state, d_next_seed, d_err, flt);
+  const EmitFilter flt{ss2 ? ss2 : 1, W ? W : 1, row_block ? row_block : 1, rank, nranks ? nranks : 1, 0, UINT64_MAX};
+  hipLaunchKernelGGL(rng_emit, dim3((uint32_t)nblk), dim3(kRngBlock), 0, st, d_seed, d_jump, d_blk_cnt, d_masks,
+                     traces, d_rd_state, d_next_seed, d_err, flt);
+  return hipGetLastError();
+}
+
+// the band partition's emit: traces [lo, hi) (and the frame's last trace's stream state); scratch: nblk offsets and
+// 3 range words
+hipError_t launch_rng_finish_band(const uint32_t *d_seed, const uint32_t *d_jump, uint32_t *d_next_seed,
+                                  const uint32_t *d_blk_cnt, uint64_t nblk, uint64_t traces, uint32_t *d_rd_state,
+                                  int *d_err, uint64_t lo, uint64_t hi, uint64_t *d_off, uint32_t *d_range,
+                                  hipStream_t st)
+{
+  const EmitFilter flt{1, 1, 1, 0, 1, lo, hi};
+  (void)hipMemsetAsync(d_range, 0, 3 * sizeof(uint32_t), st);
+  hipLaunchKernelGGL(rng_band_range, dim3(1), dim3(kScanThreads), 0, st, d_blk_cnt, nblk, traces, lo, hi, d_off, d_range,
+                     d_err);
+  // about (hi - lo) / (accept rate pi/6 x 4096) blocks hold the band; the workgroups loop over however many there are
+  const uint64_t est = (hi - lo) / 2048 + 4;
+  hipLaunchKernelGGL(rng_emit_band, dim3((uint32_t)std::min<uint64_t>(est, nblk)), dim3(kRngBlock), 0, st, d_seed, d_jump,
+                     d_blk_cnt, (const uint64_t *)d_off, (const uint32_t *)d_range, nblk, traces, d_rd_state, d_next_seed,
+                     flt);
   return hipGetLastError();
 }
 
