@@ -354,37 +354,72 @@ __global__ __launch_bounds__(kRngBlock) void rng_emit(const uint32_t *seed, cons
 // the frame's last trace (every rank carries the stream state past it), run -- a rank of N emits about 1/N of the
 // blocks instead of launching all of them.  One workgroup scans the counts into offsets and finds those blocks
 // (range: first, last, final); the emit's workgroups then loop over them.
+// One workgroup, tiles of kScanTile counts staged in LDS with coalesced loads (the counts are L2-resident, so
+// per-thread serial loads would leave it latency-bound): each thread scans 16 contiguous counts from LDS, the 1024
+// partial sums are scanned with wave shuffles, and the offsets leave with coalesced stores.  Offsets fit 32 bits
+// (a frame has fewer than 2^32 traces).
+constexpr uint32_t kScanTile = 16 * kScanThreads;
 __global__ __launch_bounds__(kScanThreads) void rng_band_range(const uint32_t *blk_cnt, uint64_t nblk, uint64_t need,
                                                                uint64_t lo, uint64_t hi, uint64_t *off, uint32_t *range,
                                                                int *err)
 {
-  __shared__ uint64_t s[kScanThreads];
-  const uint64_t per = (nblk + kScanThreads - 1) / kScanThreads;
-  const uint64_t b0 = min(nblk, (uint64_t)threadIdx.x * per), b1 = min(nblk, b0 + per);
-  uint64_t sum = 0;
-  for (uint64_t b = b0; b < b1; ++b) sum += blk_cnt[b];
-  s[threadIdx.x] = sum;
-  __syncthreads();
-  for (uint32_t o = 1; o < kScanThreads; o <<= 1)
+  __shared__ uint32_t t[kScanTile];
+  __shared__ uint32_t wsum[kScanThreads / 64];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+  if (tid == 0) { range[0] = 0; range[1] = 0; range[2] = 0; }
+  uint64_t carry = 0;
+  for (uint64_t base = 0; base < nblk; base += kScanTile)
   {
-    const uint64_t x = threadIdx.x >= o ? s[threadIdx.x - o] : 0ull;
+    const uint32_t n = (uint32_t)min((uint64_t)kScanTile, nblk - base);
+#pragma unroll
+    for (uint32_t k = 0; k < 16; ++k)
+    {
+      const uint32_t i = k * kScanThreads + tid;
+      t[i] = i < n ? blk_cnt[base + i] : 0u;
+    }
     __syncthreads();
-    s[threadIdx.x] += x;
+    uint32_t c[16], sum = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 16; ++k) { c[k] = t[16 * tid + k]; sum += c[k]; }
+    // exclusive scan of the 1024 thread sums: within each wave by shuffles, then over the 16 wave totals
+    uint32_t inc = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1)
+    {
+      const uint32_t v = __shfl_up(inc, o, 64);
+      if (lane >= (uint32_t)o) inc += v;
+    }
+    if (lane == 63) wsum[wv] = inc;
+    __syncthreads();
+    uint32_t wb = 0, tot = 0;
+    for (uint32_t w = 0; w < kScanThreads / 64; ++w)
+    {
+      wb += w < wv ? wsum[w] : 0u;
+      tot += wsum[w];
+    }
+    uint64_t run = carry + wb + (inc - sum);
+#pragma unroll
+    for (uint32_t k = 0; k < 16; ++k)
+    {
+      // block base + 16 tid + k holds traces [run, run + c): the band's first / last block and the frame's final one
+      const uint64_t b = base + 16 * tid + k, e = run + c[k];
+      if (c[k] && run <= lo && lo < e) range[0] = (uint32_t)b;
+      if (c[k] && run <= hi - 1 && hi - 1 < e) range[1] = (uint32_t)b;
+      if (c[k] && run <= need - 1 && need - 1 < e) range[2] = (uint32_t)b;
+      t[16 * tid + k] = (uint32_t)run;
+      run = e;
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < 16; ++k)
+    {
+      const uint32_t i = k * kScanThreads + tid;
+      if (i < n) off[base + i] = t[i];
+    }
+    carry += tot;
     __syncthreads();
   }
-  if (threadIdx.x == kScanThreads - 1 && s[threadIdx.x] < need) *err = 1;  // stream too short for the frame
-  uint64_t run = s[threadIdx.x] - sum;
-  // block b holds traces [run, run + cnt_b): first = the block holding lo, last = the one holding hi - 1,
-  // final = the one holding need - 1 (each is exactly one block: the ranges tile [0, total))
-  for (uint64_t b = b0; b < b1; ++b)
-  {
-    const uint64_t c = blk_cnt[b], e = run + c;
-    off[b] = run;
-    if (c && run <= lo && lo < e) range[0] = (uint32_t)b;
-    if (c && run <= hi - 1 && hi - 1 < e) range[1] = (uint32_t)b;
-    if (c && run <= need - 1 && need - 1 < e) range[2] = (uint32_t)b;
-    run = e;
-  }
+  if (tid == 0 && carry < need) *err = 1;  // stream too short for the frame
 }
 
 __global__ __launch_bounds__(kRngBlock) void rng_emit_band(const uint32_t *seed, const uint32_t *jump,
@@ -595,7 +630,6 @@ hipError_t launch_rng_finish_band(const uint32_t *d_seed, const uint32_t *d_jump
                                   hipStream_t st)
 {
   const EmitFilter flt{1, 1, 1, 0, 1, lo, hi};
-  (void)hipMemsetAsync(d_range, 0, 3 * sizeof(uint32_t), st);
   hipLaunchKernelGGL(rng_band_range, dim3(1), dim3(kScanThreads), 0, st, d_blk_cnt, nblk, traces, lo, hi, d_off, d_range,
                      d_err);
   // about (hi - lo) / (accept rate pi/6 x 4096) blocks hold the band; the workgroups loop over however many there are
