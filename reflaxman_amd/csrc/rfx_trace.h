@@ -373,12 +373,18 @@ __device__ __forceinline__ bool tri_hit(const TriGeo &g, v3 o, v3 ray, float &t_
   // exact reject before the division: with opposite signs or a zero (or NaN) numerator, t <= 0 or NaN,
   // which `t > VERY_SMALL_NUMBER` rejects anyway; the divide is skipped when no lane of the wave needs it
   if (!same_sign) return false;
-  if constexpr (!SHADOW && !STATS)
+  if constexpr (!STATS)
   {
-    // exact reject of a plane hit beyond the current closest hit: |ray t|^2 = a nz^2 / arz^2 (real), and
-    // a 2^-16 margin over the float rounding of both sides leaves |ray t| strictly above the best
-    // distance after rounding, so the reference could neither take it nor tie (a2 = 2a exactly)
-    if (nz * nz * k.a2 > best_sq * (arz * arz) * 2.0000305f) return false;
+    // |ray t|^2 = a nz^2 / arz^2 (real, a2 = 2a exactly).  Within DELTA of the origin (a shadow ray or a reflected
+    // ray leaving the triangle it starts on, or its coplanar neighbour: nz ~ 0): the reference's sqDistance, within
+    // ~10 ulp of it, is at most DELTA^2 under the 2^-15 margin, so `sqDistance > DELTA * DELTA` fails -- exact reject
+    // before the divide (tools/ab.py trace ms: C3 -1.1%, C2 d4 -3.4%, C5 -0.4%).
+    const float n2a = nz * nz * k.a2, r2 = arz * arz;
+    if (n2a < (2.0f * (kDelta * kDelta)) * r2 * 0.99997f) return false;
+    // beyond the current closest hit (closest hit only): a 2^-16 margin over the rounding of both sides leaves
+    // |ray t| strictly above the best distance after rounding, so the reference could neither take it nor tie
+    if constexpr (!SHADOW)
+      if (n2a > best_sq * r2 * 2.0000305f) return false;
   }
   const f2 c1{g.a11, g.a21}, c2{g.a12, g.a22}, c3{g.a13, g.a23};
   f2 ao, ar;
