@@ -200,6 +200,8 @@ def main():
     ap.add_argument("--partition", choices=["bands", "strips"], default="bands",
                     help="N > 1: load-balanced contiguous bands received in place on rank 0 (default), or block-cyclic "
                          "row strips gathered and un-interleaved")
+    ap.add_argument("--no-emit-ahead", action="store_true",
+                    help="N > 1: emit each frame's randDirs on its critical path, not during the last trace")
     ap.add_argument("--no-count-ahead", action="store_true",
                     help="N > 1: count and all-gather each frame's RNG blocks on its critical path, not during the last trace")
     args = ap.parse_args()
@@ -254,7 +256,8 @@ def main():
         from reflaxman_amd.dist import BandFrame, RfxStripOps, StripFrame
         ops = RfxStripOps(rr, frame, stream.cuda_stream)
         common = dict(pipeline=False if args.no_pipeline else None, gather_rgb=args.gather_rgb,
-                      count_ahead=False if args.no_count_ahead else None)
+                      count_ahead=False if args.no_count_ahead else None,
+                      emit_ahead=False if args.no_emit_ahead else None)
         sf = BandFrame(ops, W, H, rank, world, dev, **common) if bands else \
             StripFrame(ops, W, H, rb, rank, world, dev, **common)
         rows, img, argb = sf.rows, sf.img, sf.argb
@@ -415,7 +418,8 @@ def main():
                    "scene": args.scene, "width": W, "height": H, "depth": depth, "spp": 1,
                    "parallelism": ((f"balanced-bands-x{world}" if bands else f"row-strips{rb}x{world}")
                                    + ("+pipelined-gather" if sf.pipeline else "")
-                                   + ("+count-ahead" if sf.count_ahead else "")) if world > 1 else "single-gpu"},
+                                   + ("+count-ahead" if sf.count_ahead else "")
+                                   + ("+emit-ahead" if sf.emit_ahead else "")) if world > 1 else "single-gpu"},
         "roofline": {"bound": "valu", "achieved": round(achieved, 3), "peak": metrics.PEAK_FP32_VALU_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved / metrics.PEAK_FP32_VALU_TFLOPS, 4),
                      "traffic": traffic, "kernel": "rfx::trace_kernel (plain pixel mode, wave-bundle culling)",

@@ -187,6 +187,18 @@ int rfx_render_frame_counted_ev(rfx_renderer *r, const rfx_frame *frame, uint32_
                                 const uint32_t *d_blk_counts, float *d_rgb, uint32_t *d_argb, uint64_t *d_counters,
                                 void *stream, void *emitted_event);
 
+/* Emit-ahead (multi-GPU, reflaxman_amd/dist.py): the counted frame split in two, so the next frame's emit can run on
+ * another stream while this frame traces.  rfx_frame_rng_emit scans the all-gathered counts and writes the frame's
+ * randDirs into the renderer's second randDir buffer (the one the last enqueued trace does not read; order it after
+ * the trace before that), records emitted_event, and moves the stream state past the frame;
+ * rfx_render_frame_emitted traces that frame.  One emitted frame at a time; rfx_frame_rng_discard forgets it and
+ * restores the stream state.  Other render calls fail while a frame is pending. */
+int rfx_frame_rng_emit(rfx_renderer *r, const rfx_frame *frame, uint32_t nslices, const uint32_t *d_blk_counts,
+                       void *stream, void *emitted_event);
+int rfx_render_frame_emitted(rfx_renderer *r, const rfx_frame *frame, float *d_rgb, uint32_t *d_argb,
+                             uint64_t *d_counters, void *stream);
+int rfx_frame_rng_discard(rfx_renderer *r);
+
 /* Optional per-phase timing of rfx_render_frame with HIP events recorded on the launch stream:
  * enable, render, then read the summed device time (ms) of the RNG pre-pass and of the trace kernel
  * over the frames since the last read (synchronises; resets the sums). */

@@ -77,6 +77,10 @@ SIGNATURES = [
                                            C.c_void_p, C.c_void_p, C.c_void_p]),
     ("rfx_render_frame_counted_ev", C.c_int, [C.c_void_p, C.POINTER(Frame), C.c_uint32, C.c_void_p, C.c_void_p,
                                               C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    ("rfx_frame_rng_emit", C.c_int, [C.c_void_p, C.POINTER(Frame), C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]),
+    ("rfx_render_frame_emitted", C.c_int, [C.c_void_p, C.POINTER(Frame), C.c_void_p, C.c_void_p, C.c_void_p,
+                                           C.c_void_p]),
+    ("rfx_frame_rng_discard", C.c_int, [C.c_void_p]),
     ("rfx_renderer_set_timing", C.c_int, [C.c_void_p, C.c_int]),
     ("rfx_renderer_set_tile_order", C.c_int, [C.c_void_p, C.c_int]),
     ("rfx_renderer_set_prim_masks", C.c_int, [C.c_void_p, C.c_int]),

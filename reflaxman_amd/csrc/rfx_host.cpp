@@ -477,6 +477,9 @@ struct rfx_renderer {
   uint32_t jitter_seed = 0;
   // workspaces
   uint32_t *d_rd = nullptr; uint64_t rd_cap = 0;  // per-trace LCG states (rng_emit)
+  uint32_t *d_rd_alt = nullptr; uint64_t rd_alt_cap = 0;  // emit-ahead: the second randDir buffer
+  int emit_pending = -1;  // emit-ahead: buffer (0 d_rd, 1 d_rd_alt) of an emitted, untraced frame, or -1
+  int trace_buf = 0;      // buffer the last enqueued trace read
   uint32_t *d_blk_cnt = nullptr; uint64_t blk_cap = 0;
   uint64_t *d_blk_off = nullptr;     // band emits: the scanned block offsets ...
   uint32_t *d_rng_range = nullptr;   // ... and the band's first / last / final block
@@ -610,7 +613,7 @@ extern "C" void rfx_renderer_destroy(rfx_renderer *r)
   (void)hipSetDevice(r->device);
   (void)hipStreamSynchronize(r->stream);
   free_scene(r);
-  (void)hipFree(r->d_seed); (void)hipFree(r->d_err); (void)hipFree(r->d_rd);
+  (void)hipFree(r->d_seed); (void)hipFree(r->d_err); (void)hipFree(r->d_rd); (void)hipFree(r->d_rd_alt);
   (void)hipFree(r->d_blk_cnt); (void)hipFree(r->d_jump); (void)hipFree(r->d_rng_masks); (void)hipFree(r->d_blk_off);
   (void)hipFree(r->d_rng_range);
   (void)hipFree(r->d_img); (void)hipFree(r->d_argb); (void)hipFree(r->d_cnt);
@@ -1233,25 +1236,50 @@ static int tile_schedule(rfx_renderer *r, FrameParams &P, hipStream_t st, uint64
   return RFX_OK;
 }
 
-static int finish_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *d_counts, const uint16_t *d_masks,
-                        uint64_t nblk, float *d_rgb, uint32_t *d_argb, uint64_t *d_counters,
-                        hipEvent_t emitted = nullptr)
+// The randDirs of a planned frame into rd (the scan of the counts and the scatter; the stream state moves past the
+// frame), then the caller's event, if any.
+static int emit_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *d_counts, const uint16_t *d_masks, uint64_t nblk,
+                      uint32_t *rd, hipEvent_t emitted)
 {
-  int rc;
-  FrameParams &P = pl.P;
+  const FrameParams &P = pl.P;
   const hipStream_t st = pl.st;
   const uint64_t ss2 = P.ss > 0 ? (uint64_t)(P.ss * P.ss) : 1;
   if (pl.band)
-    HIP_CHECK(launch_rng_finish_band(seed_cur(r), r->d_jump, seed_next(r), d_counts, nblk, pl.traces, r->d_rd, r->d_err,
+    HIP_CHECK(launch_rng_finish_band(seed_cur(r), r->d_jump, seed_next(r), d_counts, nblk, pl.traces, rd, r->d_err,
                                      pl.band_lo, pl.band_hi, r->d_blk_off, r->d_rng_range, st));
   else
-    HIP_CHECK(launch_rng_finish(seed_cur(r), r->d_jump, seed_next(r), d_counts, d_masks, nblk, pl.traces, r->d_rd,
+    HIP_CHECK(launch_rng_finish(seed_cur(r), r->d_jump, seed_next(r), d_counts, d_masks, nblk, pl.traces, rd,
                                 r->d_err, ss2, P.W, P.row_block, P.rank, P.nranks, st));
   r->seed_idx ^= 1u;
   // the caller's event: the randDirs are written and the next frame's stream state is known (the next frame's
   // RNG count may start on another stream while this frame traces)
   if (emitted) HIP_CHECK(hipEventRecord(emitted, st));
-  if ((rc = timing_event(r, st)) != RFX_OK) return rc;
+  return RFX_OK;
+}
+
+static int trace_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *rd, float *d_rgb, uint32_t *d_argb,
+                       uint64_t *d_counters);
+
+static int finish_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *d_counts, const uint16_t *d_masks,
+                        uint64_t nblk, float *d_rgb, uint32_t *d_argb, uint64_t *d_counters,
+                        hipEvent_t emitted = nullptr)
+{
+  int rc;
+  if (r->emit_pending >= 0)
+    return fail(RFX_ERR_STATE, "render_frame: an emitted frame awaits rfx_render_frame_emitted (or rfx_frame_rng_discard)");
+  if ((rc = emit_frame(r, pl, d_counts, d_masks, nblk, r->d_rd, emitted)) != RFX_OK) return rc;
+  r->trace_buf = 0;
+  if ((rc = timing_event(r, pl.st)) != RFX_OK) return rc;
+  return trace_frame(r, pl, r->d_rd, d_rgb, d_argb, d_counters);
+}
+
+// The trace launch(es) of a planned frame whose randDirs are in rd, and the end-of-frame bookkeeping.
+static int trace_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *rd, float *d_rgb, uint32_t *d_argb,
+                       uint64_t *d_counters)
+{
+  int rc;
+  FrameParams &P = pl.P;
+  const hipStream_t st = pl.st;
   P.img = d_rgb;
   P.argb = d_argb;
   // ray regrouping: plain pixels of a large scene park their traces after RFX_PARK_AFTER segments; the bounce
@@ -1287,7 +1315,7 @@ static int finish_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *d_counts
       P.queue_order = r->d_qorder;
     }
   }
-  P.rd_state = r->d_rd;
+  P.rd_state = rd;
   P.counters = (unsigned long long *)d_counters;
   // mode 1 schedules only launches of at least RFX_TILE_ORDER_MIN_TILES tiles: on shorter ones the sort's
   // latency (three small launches and a cross-stream wait, ~15 us) is not hidden by the RNG pre-pass
@@ -1386,6 +1414,65 @@ extern "C" int rfx_render_frame_counted_ev(rfx_renderer *r, const rfx_frame *f, 
   return finish_frame(r, pl, d_blk_counts, nullptr, nblk, d_rgb, d_argb, d_counters, (hipEvent_t)emitted_event);
 }
 
+// Emit-ahead (multi-GPU): the emit of frame i + 1 on a side stream while frame i traces.  Two randDir buffers: an emit
+// writes the one the last enqueued trace does not read, and the next rfx_render_frame_emitted traces from it.
+extern "C" int rfx_frame_rng_emit(rfx_renderer *r, const rfx_frame *f, uint32_t nslices, const uint32_t *d_blk_counts,
+                                  void *stream, void *emitted_event)
+{
+  FramePlan pl;
+  int rc;
+  if ((rc = plan_frame(r, f, stream, pl)) != RFX_OK) return rc;
+  if (!d_blk_counts || !nslices) return fail(RFX_ERR_ARG, "frame_rng_emit: bad args");
+  if (r->emit_pending >= 0) return fail(RFX_ERR_STATE, "frame_rng_emit: the last emitted frame has not been traced");
+  if (pl.traces == 0) return RFX_OK;
+  const uint64_t nblk = rng_layout(pl.traces, nslices, nullptr);
+  if ((rc = ensure_rng_workspace(r, pl.traces, nblk)) != RFX_OK) return rc;
+  if (r->rd_alt_cap < pl.traces)
+  {
+    (void)hipFree(r->d_rd_alt);
+    r->d_rd_alt = nullptr;
+    r->rd_alt_cap = 0;
+    HIP_CHECK(hipMalloc(&r->d_rd_alt, pl.traces * sizeof(uint32_t)));
+    r->rd_alt_cap = pl.traces;
+  }
+  const int buf = r->trace_buf == 0 ? 1 : 0;  // not the buffer of the last enqueued trace
+  if ((rc = emit_frame(r, pl, d_blk_counts, nullptr, nblk, buf ? r->d_rd_alt : r->d_rd,
+                       (hipEvent_t)emitted_event)) != RFX_OK)
+    return rc;
+  r->emit_pending = buf;
+  return RFX_OK;
+}
+
+extern "C" int rfx_render_frame_emitted(rfx_renderer *r, const rfx_frame *f, float *d_rgb, uint32_t *d_argb,
+                                        uint64_t *d_counters, void *stream)
+{
+  FramePlan pl;
+  int rc;
+  if ((rc = plan_frame(r, f, stream, pl)) != RFX_OK) return rc;
+  if (!d_rgb) return fail(RFX_ERR_ARG, "render_frame_emitted: null framebuffer");
+  if (pl.traces == 0) return RFX_OK;
+  if (r->emit_pending < 0) return fail(RFX_ERR_STATE, "render_frame_emitted: no emitted frame (rfx_frame_rng_emit)");
+  const int buf = r->emit_pending;
+  r->emit_pending = -1;
+  r->trace_buf = buf;
+  if ((rc = timing_event(r, pl.st)) != RFX_OK) return rc;  // (the emit ran on its own stream: no pre-pass time)
+  if ((rc = timing_event(r, pl.st)) != RFX_OK) return rc;
+  return trace_frame(r, pl, buf ? r->d_rd_alt : r->d_rd, d_rgb, d_argb, d_counters);
+}
+
+// Forget an emitted, untraced frame: the stream state returns to before it (the emit read one state word and wrote
+// the other, so flipping back restores it).
+extern "C" int rfx_frame_rng_discard(rfx_renderer *r)
+{
+  if (!r) return fail(RFX_ERR_ARG, "frame_rng_discard: null renderer");
+  if (r->emit_pending >= 0)
+  {
+    r->seed_idx ^= 1u;
+    r->emit_pending = -1;
+  }
+  return RFX_OK;
+}
+
 extern "C" int rfx_render_frame(rfx_renderer *r, const rfx_frame *f, float *d_rgb, uint32_t *d_argb,
                                 uint64_t *d_counters, void *stream)
 {
@@ -1397,6 +1484,8 @@ extern "C" int rfx_render_frame(rfx_renderer *r, const rfx_frame *f, float *d_rg
   const uint64_t nblk = rng_layout(pl.traces, 1, nullptr);
   if ((rc = ensure_rng_workspace(r, pl.traces, nblk)) != RFX_OK) return rc;
   if ((rc = timing_event(r, pl.st)) != RFX_OK) return rc;
+  if (r->emit_pending >= 0)
+    return fail(RFX_ERR_STATE, "render_frame: an emitted frame awaits rfx_render_frame_emitted (or rfx_frame_rng_discard)");
   // one device counts every block, so the emit can take its accept flags instead of regenerating them
   HIP_CHECK(launch_rng_count(seed_cur(r), r->d_jump, r->d_blk_cnt, 0, nblk, r->d_rng_masks, pl.st));
   return finish_frame(r, pl, r->d_blk_cnt, r->d_rng_masks, nblk, d_rgb, d_argb, d_counters);

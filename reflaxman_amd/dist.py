@@ -38,6 +38,21 @@ class RfxStripOps:
         self.stream = stream_ptr
         self.L = _lib.load()
 
+    def rng_emit(self, nslices: int, d_counts: int, stream: int = 0, emitted_event: int = 0):
+        """Emit-ahead: the next frame's randDirs from the all-gathered counts, on `stream` (rfx_frame_rng_emit)."""
+        _lib.check(self.L.rfx_frame_rng_emit(self.r._h, C.byref(self.frame), nslices, C.c_void_p(d_counts),
+                                             C.c_void_p(stream or self.stream), C.c_void_p(emitted_event or None)),
+                   "frame_rng_emit")
+
+    def render_emitted(self, d_img: int, d_argb: int, d_counters: int = 0):
+        """Emit-ahead: trace the emitted frame on the ops' stream (rfx_render_frame_emitted)."""
+        _lib.check(self.L.rfx_render_frame_emitted(self.r._h, C.byref(self.frame), C.c_void_p(d_img),
+                                                   C.c_void_p(d_argb or None), C.c_void_p(d_counters or None),
+                                                   C.c_void_p(self.stream or None)), "render_frame_emitted")
+
+    def rng_discard(self):
+        _lib.check(self.L.rfx_frame_rng_discard(self.r._h), "frame_rng_discard")
+
     def set_rows(self, y0: int, y1: int):
         """Band partition: this rank traces rows [y0, y1) (rfx.h: row_block 0, pixel span of whole rows)."""
         self.frame.row_block = 0
@@ -110,9 +125,15 @@ class _CountedFrame:
     stream state is then on the device -- and run while frame i traces, so the exchange step leaves the
     per-frame critical path (count, all-gather, emit, trace becomes emit, trace).  The renderer's random
     stream must not advance between steps by any other call (drop_lookahead() first, on every rank).
+
+    emit_ahead (default: with count_ahead on a device): frame i+1's emit too runs on the side stream, into the
+    renderer's second randDir buffer, while frame i traces (rfx_frame_rng_emit / rfx_render_frame_emitted): the
+    critical path becomes the trace alone.  The emit waits for the trace before frame i, the last reader of the
+    buffer it overwrites.
     """
 
-    def _init_counts(self, ops, rank: int, world: int, device: torch.device, count_ahead: Optional[bool]):
+    def _init_counts(self, ops, rank: int, world: int, device: torch.device, count_ahead: Optional[bool],
+                     emit_ahead: Optional[bool] = None):
         self.ops, self.rank, self.world, self.device = ops, rank, world, device
         self.bps = ops.blocks_per_slice(world)
         self.counts = torch.zeros(world * self.bps, dtype=torch.int32, device=device)
@@ -127,9 +148,19 @@ class _CountedFrame:
         if self.emitted is not None:
             self.emitted.record(torch.cuda.current_stream(device))  # torch creates the hipEvent_t at its first record
         self.ahead = None  # the next frame's count all-gather in flight (its work object), once one is
+        if emit_ahead is None:
+            emit_ahead = self.count_ahead
+        self.emit_ahead = bool(emit_ahead) and self.count_ahead and cuda and hasattr(ops, "rng_emit")
+        self.emit_ready = False  # emit-ahead: the next frame's randDirs are emitted (self.emitted marks when)
+        self.trace_done = [torch.cuda.Event(), torch.cuda.Event()] if self.emit_ahead else []
+        for e in self.trace_done:
+            e.record(torch.cuda.current_stream(device))
+        self._n = 0  # frames rendered (emit-ahead bookkeeping)
 
     def _frame_counts(self):
         """This frame's all-gathered slice counts in self.counts, ordered before the emit on this stream."""
+        if self.emit_ahead and self.emit_ready:
+            return  # counted, all-gathered and emitted on the side stream
         if self.ahead is not None:
             # counted and all-gathered while the last frame traced: order this stream after them
             self.ahead.wait()
@@ -139,11 +170,44 @@ class _CountedFrame:
                 self._all_gather_counts()
         self.ahead = None
 
-    def _render(self, img: torch.Tensor, argb: torch.Tensor, d_counters: int):
-        self.ops.render_counted(self.world, self.counts.data_ptr(), img.data_ptr(), argb.data_ptr(), d_counters,
-                                self.emitted.cuda_event if self.emitted is not None else 0)
-        if self.count_ahead:
-            self._count_next()
+    def _render(self, img: torch.Tensor, argb: torch.Tensor, d_counters: int, events: Optional[list] = None):
+        """This frame's emit (unless emitted ahead) and trace, and the next frame's look-ahead.  events: a (start,
+        end) pair of timing events to record around the trace."""
+        if not self.emit_ahead:
+            if events:
+                events[0].record()
+            self.ops.render_counted(self.world, self.counts.data_ptr(), img.data_ptr(), argb.data_ptr(), d_counters,
+                                    self.emitted.cuda_event if self.emitted is not None else 0)
+            if events:
+                events[1].record()
+            if self.count_ahead:
+                self._count_next()
+            return
+        main = torch.cuda.current_stream(self.device)
+        if not self.emit_ready:  # nothing emitted ahead: this frame's counts are in self.counts
+            self.ops.rng_emit(self.world, self.counts.data_ptr(), stream=main.cuda_stream,
+                              emitted_event=self.emitted.cuda_event)
+        else:
+            main.wait_event(self.emitted)
+        self.emit_ready = False
+        if events:
+            events[0].record()
+        self.ops.render_emitted(img.data_ptr(), argb.data_ptr(), d_counters)
+        if events:
+            events[1].record()
+        self._n += 1
+        self.trace_done[self._n % 2].record(main)
+        # the next frame: count its slice, all-gather, and emit it -- all on the side stream
+        with torch.cuda.stream(self.count_stream):
+            self.count_stream.wait_event(self.emitted)  # the stream state past this frame
+            self.ops.rng_count(self.rank, self.world, self.counts.data_ptr(), stream=self.count_stream.cuda_stream)
+            w = self._all_gather_counts(group=self.count_group, async_op=True)
+            if w is not None:
+                w.wait()  # the side stream waits for the all-gather
+            self.count_stream.wait_event(self.trace_done[(self._n - 1) % 2])  # the last reader of the emit's buffer
+            self.ops.rng_emit(self.world, self.counts.data_ptr(), stream=self.count_stream.cuda_stream,
+                              emitted_event=self.emitted.cuda_event)
+        self.emit_ready = True
 
     def _count_next(self):
         """Count the next frame's slice and start its all-gather, ordered after this frame's emit only."""
@@ -161,12 +225,15 @@ class _CountedFrame:
             self.ahead = _EventWork(ev)
 
     def drop_lookahead(self):
-        """Complete and discard the next frame's counts (call on every rank before anything else advances the
-        renderer's random stream); the next step counts afresh."""
+        """Complete and discard the next frame's counts (and emitted randDirs, restoring the stream state) -- call
+        on every rank before anything else advances the renderer's random stream; the next step counts afresh."""
         if self.ahead is not None:
             self.ahead.wait()
-            if self.count_stream is not None:
-                torch.cuda.current_stream(self.device).wait_stream(self.count_stream)
+        if self.count_stream is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self.count_stream)
+        if self.emit_ready:
+            self.ops.rng_discard()
+            self.emit_ready = False
         self.ahead = None
 
     def _host_staged(self) -> bool:
@@ -203,9 +270,9 @@ class StripFrame(_CountedFrame):
 
     def __init__(self, ops, W: int, H: int, row_block: int, rank: int, world: int, device: torch.device,
                  gather_to_root: bool = True, pipeline: Optional[bool] = None, gather_rgb: bool = False,
-                 count_ahead: Optional[bool] = None):
+                 count_ahead: Optional[bool] = None, emit_ahead: Optional[bool] = None):
         self.W, self.H, self.rb = W, H, row_block
-        self._init_counts(ops, rank, world, device, count_ahead)
+        self._init_counts(ops, rank, world, device, count_ahead, emit_ahead)
         self.gather_to_root = gather_to_root
         self.gather_rgb = bool(gather_rgb) and gather_to_root and world > 1
         self.rows = strip_rows(H, row_block, rank, world)
@@ -367,11 +434,11 @@ class BandFrame(_CountedFrame):
 
     def __init__(self, ops, W: int, H: int, rank: int, world: int, device: torch.device, gather_to_root: bool = True,
                  pipeline: Optional[bool] = None, gather_rgb: bool = False, count_ahead: Optional[bool] = None,
-                 bounds: Optional[List[int]] = None, grain: int = 8):
+                 bounds: Optional[List[int]] = None, grain: int = 8, emit_ahead: Optional[bool] = None):
         self.W, self.H, self.grain = W, H, grain
         b0 = bounds or equal_bounds(H, world, grain)
         ops.set_rows(b0[rank], b0[rank + 1])  # the frame is a band frame from here on (the RNG layout below reads it)
-        self._init_counts(ops, rank, world, device, count_ahead)
+        self._init_counts(ops, rank, world, device, count_ahead, emit_ahead)
         self.gather_to_root = gather_to_root and world > 1
         self.gather_rgb = bool(gather_rgb) and self.gather_to_root
         if pipeline is None:
@@ -395,6 +462,8 @@ class BandFrame(_CountedFrame):
         """Band bounds for the next frames (the same list on every rank)."""
         assert len(bounds) == self.world + 1 and bounds[0] == 0 and bounds[-1] == self.H, bounds
         assert all(bounds[r] < bounds[r + 1] for r in range(self.world)), bounds
+        if getattr(self, "emit_ready", False) and list(bounds) != self.bounds:
+            self.drop_lookahead()  # the frame emitted ahead holds the old band's randDirs only
         self.bounds = list(bounds)
         self.y0, self.y1 = bounds[self.rank], bounds[self.rank + 1]
         self.rows = self.y1 - self.y0
@@ -443,13 +512,11 @@ class BandFrame(_CountedFrame):
         img = self.img_bufs[k % len(self.img_bufs)]
         self.argb, self.img = argb, img
         self._frame_counts()
+        ev = None
         if self._events is not None:
-            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-            ev[0].record()
-        self._render(img, argb, d_counters)
-        if self._events is not None:
-            ev[1].record()
+            ev = [torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)]
             self._events.append(ev)
+        self._render(img, argb, d_counters, ev)
         if self.world == 1 or not self.gather_to_root:
             return argb.view(self.H, self.W) if self.world == 1 else None
         works = self._exchange(k)

@@ -39,9 +39,10 @@ def test_bench_multirank_frame_matches_single_gpu(world, partition):
         assert len(b) == world + 1 and b[0] == 0 and b[-1] == 360
 
 
-def _count_ahead_worker():
+def _count_ahead_worker(emit_ahead):
     """Rank 0 of 1 over RCCL: StripFrame with count-ahead (the next frame's RNG count and its all-gather on a side
-    stream after the emit event) over 6 frames, against the same frames from rfx_render_frame."""
+    stream after the emit event) -- and with emit-ahead, the next frame's emit there too, into the second randDir
+    buffer -- over 6 frames, against the same frames from rfx_render_frame."""
     sys.path.insert(0, ROOT)
     import torch
     import torch.distributed as dist
@@ -62,8 +63,8 @@ def _count_ahead_worker():
             r.set_scene(scene)
             r.set_stream(stream.cuda_stream)
         sf = StripFrame(RfxStripOps(ra, make_frame(cam, W, H, D, 1), stream.cuda_stream), W, H, 8, 0, 1, dev,
-                        count_ahead=True)
-        assert sf.count_ahead and sf.ahead is None
+                        count_ahead=True, emit_ahead=emit_ahead)
+        assert sf.count_ahead and sf.ahead is None and sf.emit_ahead == emit_ahead
         fb = make_frame(cam, W, H, D, 1)
         img = torch.zeros(H * W * 3, dtype=torch.float32, device=dev)
         argb = torch.zeros(H * W, dtype=torch.int32, device=dev)
@@ -81,14 +82,15 @@ def _count_ahead_worker():
 
 
 @pytest.mark.gpu
-def test_count_ahead_rccl_frames_equal_plain_frames():
+@pytest.mark.parametrize("emit_ahead", [0, 1])
+def test_count_ahead_rccl_frames_equal_plain_frames(emit_ahead):
     env = {**os.environ, "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(_port())}
-    r = subprocess.run([sys.executable, os.path.abspath(__file__), "count_ahead"], capture_output=True, text=True,
-                       timeout=300, cwd=ROOT, env=env)
+    r = subprocess.run([sys.executable, os.path.abspath(__file__), "count_ahead", str(emit_ahead)], capture_output=True,
+                       text=True, timeout=300, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert out["frames_equal"] == [True] * 6, out
 
 
-if __name__ == "__main__" and sys.argv[1:] == ["count_ahead"]:
-    _count_ahead_worker()
+if __name__ == "__main__" and sys.argv[1:2] == ["count_ahead"]:
+    _count_ahead_worker(bool(int(sys.argv[2])))
