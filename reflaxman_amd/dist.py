@@ -1,4 +1,5 @@
-"""Multi-GPU frames: block-cyclic row strips, one RCCL exchange in the RNG pre-pass, strip gather.
+"""Multi-GPU frames: row bands (or block-cyclic strips), one RCCL exchange in the RNG pre-pass, frame assembly on
+rank 0.
 
 One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI).  Per
 frame, rank r:
@@ -6,14 +7,17 @@ frame, rank r:
 1. counts the accepted LCG triples of its 1/N slice of the random stream
    (``rfx_frame_rng_count``) into its slice of a device array;
 2. all-gathers that array -- the only exchange the path needs, N x ~1K uint32;
-3. scans it, emits the randDirs of *its* strips and traces them
-   (``rfx_render_frame_counted``) -- pre-pass and trace work are both 1/N;
-4. gathers its ARGB8 strip to rank 0, which un-interleaves the strips into
-   the frame with one device ``index_copy_`` (rfx_strip_row_to_y).
+3. scans it, emits the randDirs of *its* rows and traces them
+   (``rfx_render_frame_counted``, or ``rfx_frame_rng_emit`` + ``rfx_render_frame_emitted``
+   when steps 1-3a run a frame ahead on a side stream) -- pre-pass and trace work are both 1/N;
+4. BandFrame: sends its band to rank 0, received in place in the frame (RCCL p2p);
+   StripFrame: gathers its ARGB8 strip to rank 0, which un-interleaves the strips
+   with one device ``index_copy_`` (rfx_strip_row_to_y).
 
 The assembled frame equals the 1-GPU frame bit-exactly (tests/test_gpu_parity.py
 emulates the ranks in one process; tests/test_dist_gloo.py runs this module's
-collectives with world_size 2 over gloo on CPU).
+collectives with world_size 2 and 3 over gloo on CPU; tests/test_gpu_multirank.py
+runs bench.py with gloo ranks on one GPU and the look-aheads over RCCL).
 """
 from __future__ import annotations
 
