@@ -311,11 +311,19 @@ def main():
             ok_f = sha(first_rgb.tobytes()) == man[key]["sha_f32"]
             ok_a = sha(first_argb.tobytes()) == man[key]["sha_argb"]
             parity["full_frame_vs_reference_sha256"] = {"f32": ok_f, "argb8": ok_a, "case": key}
-    counters = torch.zeros(_lib.RFX_NCOUNTERS, dtype=torch.int64, device=dev)
-    if world > 1:
-        sf.drop_lookahead()  # the counted frame below advances the random stream itself (every rank)
-    rr.render_frame(frame, img.data_ptr(), argb.data_ptr(), counters.data_ptr(), stream.cuda_stream)
-    torch.cuda.synchronize()
+    # counted frames (the stats kernel) into scratch buffers at N > 1 (the step buffers may still be in pipelined
+    # sends); each advances the random stream itself, on every rank
+    cimg, cargb = (torch.empty_like(img), torch.empty_like(argb)) if world > 1 else (img, argb)
+
+    def counted_frame():
+        c = torch.zeros(_lib.RFX_NCOUNTERS, dtype=torch.int64, device=dev)
+        if world > 1:
+            sf.drop_lookahead()
+        rr.render_frame(frame, cimg.data_ptr(), cargb.data_ptr(), c.data_ptr(), stream.cuda_stream)
+        torch.cuda.synchronize()
+        return c
+
+    counters = counted_frame()
     cnt = counters.cpu().numpy().astype(np.uint64)
     if world > 1:
         c = torch.tensor(cnt.astype(np.int64), device=dev)
@@ -341,10 +349,13 @@ def main():
             prewarm = int(pw.item())
         for _ in range(prewarm):
             step()
+    flops_local = None
     if bands:
         # cut the bands from measured per-rank render times (rank 0's receive included), then keep them
         sf.balance(rounds=3, frames=8)
         log(f"rank {rank}: bands {sf.bounds}")
+        # this rank's work in its final band, for the per-launch roofline
+        flops_local = metrics.summary(counted_frame().cpu().numpy().astype(np.uint64))["flops"]
     # ---- warmup, then K timed steps (barrier + synchronize on both sides)
     for _ in range(args.warmup):
         step()
@@ -395,10 +406,10 @@ def main():
     ms_step = elapsed / args.steps * 1e3
     mrays = traces * args.steps / elapsed / 1e6
     # the trace kernel of one rank processes its strip: per-launch FLOPs = frame FLOPs / world (balanced strips)
-    # (bands: the rank's share of the frame's rows -- rows differ in cost, so this is approximate)
+    # (bands: rank 0's counted work in its final band; strips: an equal share, the strips being balanced)
     if world > 1:
         rows = sf.rows
-    flops_launch = flops_frame / world if world == 1 or not bands else flops_frame * rows / H
+    flops_launch = flops_local if flops_local is not None else flops_frame / world
     achieved = flops_launch / (trace_avg * 1e-3) / 1e12
     px_launch = rows * W
     # HBM traffic and executed VALU work of the trace kernel: rocprofv3 --pmc passes of this very workload
