@@ -171,6 +171,26 @@ def cpu_allcore(desc, W, H, depth, gpu_rgb, gpu_argb, rate_1core, seconds=8.0):
                       f"{secs:.1f} s; {cpu_model()}", "bit_exact_vs_gpu": same}
 
 
+def one_gpu_line(cfg_name, W, H, depth):
+    """The committed 1-GPU bench line of the same frame (profiles/r02/configs/), the denominator of a strong-scaling
+    efficiency at N > 1 (this run does not re-measure it), or None."""
+    d = os.path.join(ROOT, "profiles", "r02", "configs")
+    if not os.path.isdir(d):
+        return None
+    for name in sorted(os.listdir(d)):
+        if not name.startswith(cfg_name + "_") or not name.endswith(".json"):
+            continue
+        try:
+            rec = json.loads(open(os.path.join(d, name)).read().strip().splitlines()[-1])
+        except (OSError, ValueError, IndexError):
+            continue
+        c = rec.get("config", {})
+        if rec.get("n_gpus") == 1 and (c.get("width"), c.get("height"), c.get("depth")) == (W, H, depth):
+            return {"value": rec["value"], "unit": rec["unit"], "ms_per_step": rec["ms_per_step"],
+                    "source": os.path.join("profiles", "r02", "configs", name)}
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -451,6 +471,7 @@ def main():
         "end_to_end_incl_d2h": e2e,
         "parity": parity,
         **({"band_bounds": sf.bounds} if bands else {}),
+        **({"strong_scaling_baseline": one_gpu_line(cfg_name, W, H, depth)} if world > 1 else {}),
     }
     if world == 1 and not args.no_cpu_baseline:
         log("cpu_baseline: reference CPU path on a row sample of the same frame ...")
