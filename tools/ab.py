@@ -57,6 +57,8 @@ VARIANTS = {
     "boxmargin": ["RFX_BVH_NODE_MARGIN=0"],
     "median": ["RFX_BVH_SAH=0"],
     "qsort": ["RFX_QUEUE_SORT=1"],
+    "lpt16k": ["RFX_TILE_ORDER_MIN_TILES=16384"],
+    "lpt4k": ["RFX_TILE_ORDER_MIN_TILES=4096"],
 }
 
 
