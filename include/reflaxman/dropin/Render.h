@@ -4,9 +4,16 @@
 // through the C-ABI (../../rfx.h) instead of the CPU loop of Render.cpp:136-215:
 //   * public camera (the caller's own Camera, Camera.h -- proceedControl/inMotion keep working), scene
 //     (./Scene.h), imageWidth, imageHeight, additiveCounter, inProgress;
-//   * renderBegin snapshots camera.view / camera.eye (Render.cpp:116-134); renderNext(pixels) renders exactly
-//     the raster span the reference's cursor would cover -- any chunk pattern (Pulse.cpp:102-209) gives the
-//     reference's image; renderAll keeps the reference's behaviour (imageHeight *pixels*, Render.cpp:217-221);
+//   * renderBegin snapshots camera.view / camera.eye (Render.cpp:116-134); renderAll keeps the reference's
+//     behaviour (imageHeight *pixels*, Render.cpp:217-221);
+//   * renderNext(pixels) -- policy "frame" (default): the first call after renderBegin renders the
+//     whole rest of the frame on the device into a second framebuffer, and every call only advances the cursor;
+//     the frame becomes the image when the cursor reaches its end.  A caller that leaves a frame early --
+//     renderBegin or setImageSize mid-frame (Pulse.cpp:110-124), a scene or fov change, or an imagePixel /
+//     copyImage read before the end -- gets exactly the reference's state: the random streams are rewound
+//     (rfx_frame_rng_rewind) and exactly the span the cursor covered is rendered into the image, as the reference
+//     would have.  Policy "span" (RFX_DROPIN_POLICY=span, or setRenderPolicy) renders each call's span as it
+//     comes.  Any chunk pattern gives the reference's images and random streams under either policy;
 //   * the float framebuffer (std::vector<Color> image, Render.h:10) lives in HBM and is read back on demand;
 //     imagePixel / copyImage then apply the caller's own Color::operator/ and Color::argb, as the reference.
 // Random streams: the reference seeds its two per-TU LCG streams from rand() at static init (trace_math.h:34),
@@ -40,9 +47,66 @@ class Render {
 
   rfx_renderer *r = nullptr;
   void *d_image = nullptr;
+  void *d_spec = nullptr;  // policy "frame": the frame being rendered ahead of the cursor
   size_t d_capacity = 0;
   unsigned long long uploaded = ~0ull;
   mutable bool host_valid = false;
+  bool whole_frame = true;                // policy "frame"
+  bool spec_active = false;               // d_spec holds this frame's pixels [spec_begin, W*H) ahead of the cursor
+  uint64_t spec_begin = 0;
+  float spec_fov = 0.0f;
+  unsigned long long spec_revision = 0;
+
+  static bool policy_env()
+  {
+    const char *v = getenv("RFX_DROPIN_POLICY");
+    return !(v && !strcmp(v, "span"));
+  }
+  rfx_frame frame_of(uint64_t p0, uint64_t p1) const
+  {
+    rfx_frame f;
+    memset(&f, 0, sizeof(f));
+    f.eye[0] = renderCameraEye.x; f.eye[1] = renderCameraEye.y; f.eye[2] = renderCameraEye.z;
+    memcpy(f.view, &renderCameraView.m[0][0], sizeof(f.view));
+    f.fov = camera.fov;  // rz = W/2/tanf(camera.fov/2): the live camera's fov, as Render.cpp:148
+    f.width = imageWidth;
+    f.height = imageHeight;
+    f.reflect_num = renderReflectNum;
+    f.sample_num = renderSampleNum;
+    f.additive = renderAdditive;
+    f.additive_counter = additiveCounter;
+    f.nranks = 1;
+    f.pixel_begin = p0;
+    f.pixel_end = p1;
+    return f;
+  }
+  void upload_scene()
+  {
+    if (uploaded != scene.revision())
+    {
+      rfx_dropin::check(rfx_renderer_set_scene(r, scene.handle()), "rfx_renderer_set_scene");
+      uploaded = scene.revision();
+    }
+  }
+  // Leave the frame rendered ahead at the cursor: rewind the random streams to its start and render exactly the span
+  // [spec_begin, cursor) into the image, as the reference's renderNext calls had (the rest keeps its old pixels).
+  void settle(bool keep_pixels = true)
+  {
+    if (!spec_active) return;
+    spec_active = false;
+    rfx_dropin::check(rfx_frame_rng_rewind(r), "Render: rewind");
+    const uint64_t c = (uint64_t)cury * imageWidth + curx;
+    if (c > spec_begin)
+    {
+      const float fov = camera.fov;
+      camera.fov = spec_fov;  // the span as it was rendered ahead
+      const rfx_frame f = frame_of(spec_begin, c);
+      camera.fov = fov;
+      rfx_dropin::check(rfx_render_frame(r, &f, (float *)(keep_pixels ? d_image : d_spec), nullptr, nullptr, nullptr),
+                        "Render: settle");
+    }
+    host_valid = false;
+  }
 
   static uint32_t seed_env(const char *name, uint32_t dflt)
   {
@@ -53,6 +117,7 @@ class Render {
   {
     if (host_valid) return;
     Render *self = const_cast<Render *>(this);
+    self->settle();  // a read mid-frame sees the reference's image: the span rendered so far, old pixels after it
     const size_t n = (size_t)imageWidth * imageHeight;
     if (self->image.size() < n) self->image.resize(n);
     if (n) rfx_dropin::check(rfx_memcpy_d2h(r, &self->image.front(), d_image, n * sizeof(float) * 3), "Render: read back");
@@ -75,11 +140,13 @@ class Render {
     rfx_dropin::check(rfx_renderer_create(&r, 0), "rfx_renderer_create");
     rfx_dropin::check(rfx_renderer_set_rng(r, seed_env("RFX_SPHERE_SEED", 1350490027u), seed_env("RFX_JITTER_SEED", 424238335u)),
                       "rfx_renderer_set_rng");
+    whole_frame = policy_env();
     loadScene(exePath);
   }
   ~Render()
   {
     if (d_image) rfx_device_free(r, d_image);
+    if (d_spec) rfx_device_free(r, d_spec);
     rfx_renderer_destroy(r);
   }
   Render(const Render &) = delete;
@@ -114,12 +181,16 @@ class Render {
   {
     if (width > 0 && height > 0)
     {
+      settle(false);  // a frame left mid-way: the random streams as far as the cursor got (Render.cpp:57-80)
       const size_t bytes = (size_t)width * height * sizeof(float) * 3;
       if (bytes > d_capacity)
       {
         if (d_image) rfx_device_free(r, d_image);
         d_image = nullptr;
         rfx_dropin::check(rfx_device_alloc(r, bytes, &d_image), "Render::setImageSize");
+        if (d_spec) rfx_device_free(r, d_spec);
+        d_spec = nullptr;
+        if (whole_frame) rfx_dropin::check(rfx_device_alloc(r, bytes, &d_spec), "Render::setImageSize");
         d_capacity = bytes;
       }
       std::vector<float> zero((size_t)width * height * 3, 0.0f);
@@ -160,6 +231,7 @@ class Render {
 
   void renderBegin(int reflectNum, int sampleNum, bool additive)  // Render.cpp:116-134
   {
+    settle();  // the last frame left mid-way keeps what the reference's cursor rendered
     renderReflectNum = reflectNum;
     renderSampleNum = sampleNum;
     renderAdditive = additive;
@@ -181,30 +253,41 @@ class Render {
     const uint64_t total = (uint64_t)imageWidth * imageHeight;
     const uint64_t p0 = (uint64_t)cury * imageWidth + curx;
     const uint64_t p1 = p0 + pixels < total ? p0 + pixels : total;
-    if (uploaded != scene.revision())
+    if (spec_active && (scene.revision() != spec_revision || camera.fov != spec_fov))
+      settle();  // what was rendered ahead no longer holds for the rest of the frame
+    upload_scene();
+    if (whole_frame && d_spec && !spec_active && p1 < total)
     {
-      rfx_dropin::check(rfx_renderer_set_scene(r, scene.handle()), "rfx_renderer_set_scene");
-      uploaded = scene.revision();
+      // render the rest of the frame [p0, total) ahead into d_spec; it starts as the image (old pixels that an
+      // additive frame accumulates onto, block-preview fills of corners before p0)
+      if (p0 > 0 || (renderSampleNum > 0 && additiveCounter > 1))
+        rfx_dropin::check(rfx_memcpy_d2d(r, d_spec, d_image, (size_t)total * sizeof(float) * 3), "Render::renderNext");
+      const rfx_frame f = frame_of(p0, total);
+      rfx_dropin::check(rfx_render_frame(r, &f, (float *)d_spec, nullptr, nullptr, nullptr), "Render::renderNext");
+      spec_active = true;
+      spec_begin = p0;
+      spec_fov = camera.fov;
+      spec_revision = scene.revision();
     }
-    rfx_frame f;
-    memset(&f, 0, sizeof(f));
-    f.eye[0] = renderCameraEye.x; f.eye[1] = renderCameraEye.y; f.eye[2] = renderCameraEye.z;
-    memcpy(f.view, &renderCameraView.m[0][0], sizeof(f.view));
-    f.fov = camera.fov;  // rz = W/2/tanf(camera.fov/2): the live camera's fov, as Render.cpp:148
-    f.width = imageWidth;
-    f.height = imageHeight;
-    f.reflect_num = renderReflectNum;
-    f.sample_num = renderSampleNum;
-    f.additive = renderAdditive;
-    f.additive_counter = additiveCounter;
-    f.nranks = 1;
-    f.pixel_begin = p0;
-    f.pixel_end = p1;
-    rfx_dropin::check(rfx_render_frame(r, &f, (float *)d_image, nullptr, nullptr, nullptr), "Render::renderNext");
-    host_valid = false;
+    else if (!spec_active)
+    {
+      const rfx_frame f = frame_of(p0, p1);
+      rfx_dropin::check(rfx_render_frame(r, &f, (float *)d_image, nullptr, nullptr, nullptr), "Render::renderNext");
+    }
+    host_valid = false;  // the reference's image has changed (a read mid-frame settles the frame rendered ahead)
     curx = (unsigned int)(p1 % imageWidth);
     cury = (unsigned int)(p1 / imageWidth);
-    if (p1 == total) inProgress = false;
+    if (p1 == total)
+    {
+      inProgress = false;
+      if (spec_active)  // the frame rendered ahead is complete: it is the image
+      {
+        void *t = d_image;
+        d_image = d_spec;
+        d_spec = t;
+        spec_active = false;
+      }
+    }
     return inProgress;
   }
 
@@ -220,4 +303,12 @@ class Render {
   }
 
   rfx_renderer *renderer() const { return r; }
+  // "frame" (true, default): render the rest of the frame at the first renderNext after renderBegin; "span" (false):
+  // render each renderNext's span as it comes (Render.cpp:136-215 chunk by chunk)
+  void setRenderPolicy(bool wholeFrame)
+  {
+    settle();
+    whole_frame = wholeFrame;
+    if (whole_frame && !d_spec && d_capacity) rfx_dropin::check(rfx_device_alloc(r, d_capacity, &d_spec), "Render");
+  }
 };

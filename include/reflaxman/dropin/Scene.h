@@ -15,6 +15,7 @@
 // copy double-deletes, so its callers only ever assign a fresh temporary: Render.cpp:32); Sphere and
 // Triangle are handles (the caller never calls trace() on them: Scene::trace is the renderer's).
 #pragma once
+#include <atomic>
 #include <map>
 #include <memory>
 #include <stdexcept>
@@ -47,6 +48,7 @@ class Sphere {
   int objectIndex() const { return object; }
 
  private:
+  friend class Scene;
   Scene *scene;
   int object;
 };
@@ -60,15 +62,16 @@ class Triangle {
   int objectIndex() const { return object; }
 
  private:
+  friend class Scene;
   Scene *scene;
   int object;
 };
 
 class Scene {
  public:
-  Scene() : h(rfx_scene_create(0.0f, 0.0f, 0.0f, 0.0f)) {}
+  Scene() : h(rfx_scene_create(0.0f, 0.0f, 0.0f, 0.0f)) { bump(); }
   Scene(const Color &diffLightColor, float diffLightPower)
-      : h(rfx_scene_create(diffLightColor.r, diffLightColor.g, diffLightColor.b, diffLightPower)) {}
+      : h(rfx_scene_create(diffLightColor.r, diffLightColor.g, diffLightColor.b, diffLightPower)) { bump(); }
   ~Scene() { release(); }
   Scene(const Scene &) = delete;
   Scene &operator=(const Scene &) = delete;
@@ -79,7 +82,6 @@ class Scene {
     {
       release();
       take(o);
-      ++version;
     }
     return *this;
   }
@@ -92,7 +94,7 @@ class Scene {
     const int obj = rfx_scene_add_sphere(h, c, radius, material.type == Material::mtDielectric ? RFX_DIELECTRIC : RFX_METAL,
                                          col, material.reflectivity, material.transparency);
     rfx_dropin::check(obj, "Scene::addSphere");
-    ++version;
+    bump();
     spheres.emplace_back(new Sphere(this, obj));
     return spheres.back().get();
   }
@@ -107,7 +109,7 @@ class Scene {
     const int obj = rfx_scene_add_triangle(h, a, b, c, material.type == Material::mtDielectric ? RFX_DIELECTRIC : RFX_METAL,
                                            col, material.reflectivity, material.transparency);
     rfx_dropin::check(obj, "Scene::addTriangle");
-    ++version;
+    bump();
     triangles.emplace_back(new Triangle(this, obj));
     return triangles.back().get();
   }
@@ -118,7 +120,7 @@ class Scene {
     rfx_dropin::xyz(origin, o);
     rfx_dropin::rgb(color, col);
     rfx_dropin::check(rfx_scene_add_light(h, o, radius, col, power), "Scene::addLight");
-    ++version;
+    bump();
     if (radius <= 1.0842021724855044e-19f) radius = 1.0842021724855044e-19f;  // VERY_SMALL_NUMBER clamp, Scene.cpp:50-53
     lights.emplace_back(new OmniLight(origin, radius, color, power));  // the caller's record, as the reference returns
     return lights.back().get();
@@ -131,7 +133,7 @@ class Scene {
   {
     const int idx = rfx_scene_add_texture_file(h, fileName, nullptr);
     rfx_dropin::check(idx, "Scene::addTexture");
-    ++version;
+    bump();
     textures.emplace_back(new Texture(fileName));
     texture_index[textures.back().get()] = idx;
     return textures.back().get();
@@ -141,14 +143,14 @@ class Scene {
   {
     const int ok = rfx_scene_set_skybox_file(h, fileName);
     rfx_dropin::check(ok, "Scene::setSkyboxTexture");
-    ++version;
+    bump();
     return ok == 1;
   }
 
   // renderer side
   rfx_scene *handle() const { return h; }
   unsigned long long revision() const { return version; }
-  void touch() { ++version; }
+  void touch() { bump(); }
   int textureIndex(const Texture *t) const
   {
     const std::map<const Texture *, int>::const_iterator it = texture_index.find(t);
@@ -175,7 +177,16 @@ class Scene {
     lights = std::move(o.lights);
     textures = std::move(o.textures);
     texture_index = std::move(o.texture_index);
-    version = o.version + 1;
+    for (auto &sp : spheres) sp->scene = this;  // the handles belong to this scene now
+    for (auto &tr : triangles) tr->scene = this;
+    bump();
+  }
+  // Revisions come from one process-wide counter, so no two states of any Scene object share one: Render::renderNext
+  // re-uploads whenever the revision differs from the uploaded one (a freshly assigned Scene included).
+  void bump()
+  {
+    static std::atomic<unsigned long long> counter(0);
+    version = ++counter;
   }
 
   rfx_scene *h = nullptr;

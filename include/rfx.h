@@ -198,6 +198,18 @@ int rfx_frame_rng_emit(rfx_renderer *r, const rfx_frame *frame, uint32_t nslices
 int rfx_render_frame_emitted(rfx_renderer *r, const rfx_frame *frame, float *d_rgb, uint32_t *d_argb,
                              uint64_t *d_counters, void *stream);
 int rfx_frame_rng_discard(rfx_renderer *r);
+/* The sphere-stream state the next traced frame starts from: the emitted frame's when one is pending (returns 1),
+ * else the current state (returns 0).  Synchronises with the renderer's stream; the emit must have completed (order
+ * the renderer's stream after the emit's, or synchronise the device).  A single-GPU renderer seeded with it renders
+ * that frame (bench.py's steady-state parity check). */
+int rfx_frame_rng_pending(rfx_renderer *r, uint32_t *frame_start);
+
+/* Undo the random-stream advance of the last call, which must be an rfx_render_frame (else RFX_ERR_STATE): both
+ * streams return to that frame's start, its pixels stay as written.  The drop-in Render (dropin/Render.h) renders a
+ * whole frame at the first renderNext after renderBegin; when the caller leaves that frame early (renderBegin or
+ * setImageSize mid-frame, Pulse.cpp:110-124) it rewinds and renders exactly the span the reference's cursor covered,
+ * so the streams end where the reference's do (Render.cpp:136-215, trace_math.h:34-39). */
+int rfx_frame_rng_rewind(rfx_renderer *r);
 
 /* Optional per-phase timing of rfx_render_frame with HIP events recorded on the launch stream:
  * enable, render, then read the summed device time (ms) of the RNG pre-pass and of the trace kernel
@@ -215,6 +227,8 @@ int rfx_device_alloc(rfx_renderer *r, size_t bytes, void **dptr);
 int rfx_device_free(rfx_renderer *r, void *dptr);
 int rfx_memcpy_d2h(rfx_renderer *r, void *dst, const void *src, size_t bytes);
 int rfx_memcpy_h2d(rfx_renderer *r, void *dst, const void *src, size_t bytes);
+/* device-to-device copy on the renderer's stream (asynchronous) */
+int rfx_memcpy_d2d(rfx_renderer *r, void *dst, const void *src, size_t bytes);
 int rfx_synchronize(rfx_renderer *r);
 
 /* Sample the RNG stream: the first n randomInsideSphere draws from `seed` (Vector3.cpp:176-188),

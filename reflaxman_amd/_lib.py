@@ -81,6 +81,8 @@ SIGNATURES = [
     ("rfx_render_frame_emitted", C.c_int, [C.c_void_p, C.POINTER(Frame), C.c_void_p, C.c_void_p, C.c_void_p,
                                            C.c_void_p]),
     ("rfx_frame_rng_discard", C.c_int, [C.c_void_p]),
+    ("rfx_frame_rng_pending", C.c_int, [C.c_void_p, _u32p]),
+    ("rfx_frame_rng_rewind", C.c_int, [C.c_void_p]),
     ("rfx_renderer_set_timing", C.c_int, [C.c_void_p, C.c_int]),
     ("rfx_renderer_set_tile_order", C.c_int, [C.c_void_p, C.c_int]),
     ("rfx_renderer_set_prim_masks", C.c_int, [C.c_void_p, C.c_int]),
@@ -91,6 +93,7 @@ SIGNATURES = [
     ("rfx_device_free", C.c_int, [C.c_void_p, C.c_void_p]),
     ("rfx_memcpy_d2h", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]),
     ("rfx_memcpy_h2d", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]),
+    ("rfx_memcpy_d2d", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]),
     ("rfx_synchronize", C.c_int, [C.c_void_p]),
     ("rfx_rand_dirs", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint64, _fp, _u32p]),
     ("rfx_kat_objects", C.c_int, [C.c_void_p, _fp, C.POINTER(C.c_int32), C.c_uint64, _fp]),

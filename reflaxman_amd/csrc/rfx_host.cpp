@@ -480,6 +480,11 @@ struct rfx_renderer {
   uint32_t *d_rd_alt = nullptr; uint64_t rd_alt_cap = 0;  // emit-ahead: the second randDir buffer
   int emit_pending = -1;  // emit-ahead: buffer (0 d_rd, 1 d_rd_alt) of an emitted, untraced frame, or -1
   int trace_buf = 0;      // buffer the last enqueued trace read
+  uint64_t emit_key[8] = {};  // the emitted frame's plan (traces, band, geometry): rfx_render_frame_emitted must match it
+  // rfx_frame_rng_rewind: the last call was an rfx_render_frame; its start states (the sphere stream's is the other
+  // seed word while rewind_flip) can be restored
+  bool rewind_ok = false, rewind_flip = false;
+  uint32_t rewind_jitter = 0;
   uint32_t *d_blk_cnt = nullptr; uint64_t blk_cap = 0;
   uint64_t *d_blk_off = nullptr;     // band emits: the scanned block offsets ...
   uint32_t *d_rng_range = nullptr;   // ... and the band's first / last / final block
@@ -1088,6 +1093,7 @@ extern "C" int rfx_renderer_set_rng(rfx_renderer *r, uint32_t sphere_seed, uint3
   HIP_CHECK(hipMemcpyAsync(seed_cur(r), &sphere_seed, sizeof(uint32_t), hipMemcpyHostToDevice, r->stream));
   HIP_CHECK(hipStreamSynchronize(r->stream));
   r->jitter_seed = jitter_seed;
+  r->rewind_ok = false;
   return RFX_OK;
 }
 
@@ -1154,6 +1160,7 @@ static int enqueue_rng(rfx_renderer *r, uint64_t traces, hipStream_t st)
   HIP_CHECK(launch_rng_finish(seed_cur(r), r->d_jump, seed_next(r), r->d_blk_cnt, r->d_rng_masks, nblk, traces,
                               r->d_rd, r->d_err, 1, 1, 1, 0, 1, st));
   r->seed_idx ^= 1u;
+  r->rewind_ok = false;
   return RFX_OK;
 }
 
@@ -1414,6 +1421,21 @@ extern "C" int rfx_render_frame_counted_ev(rfx_renderer *r, const rfx_frame *f, 
   return finish_frame(r, pl, d_blk_counts, nullptr, nblk, d_rgb, d_argb, d_counters, (hipEvent_t)emitted_event);
 }
 
+// What an emitted frame's randDirs depend on: the traces and their band, and the frame geometry that maps pixels to
+// trace indices.  rfx_render_frame_emitted refuses a frame whose plan differs (its rows' randDirs were never written).
+static void plan_key(const FramePlan &pl, uint64_t key[8])
+{
+  const FrameParams &P = pl.P;
+  key[0] = pl.traces;
+  key[1] = pl.band_lo;
+  key[2] = pl.band_hi;
+  key[3] = ((uint64_t)P.W << 32) | P.H;
+  key[4] = ((uint64_t)(uint32_t)P.ss << 32) | P.row_block;
+  key[5] = ((uint64_t)P.rank << 32) | P.nranks;
+  key[6] = ((uint64_t)P.row0 << 32) | P.grid_rows;
+  key[7] = P.p_begin ^ (P.p_end << 1) ^ (P.trace_base << 2);
+}
+
 // Emit-ahead (multi-GPU): the emit of frame i + 1 on a side stream while frame i traces.  Two randDir buffers: an emit
 // writes the one the last enqueued trace does not read, and the next rfx_render_frame_emitted traces from it.
 extern "C" int rfx_frame_rng_emit(rfx_renderer *r, const rfx_frame *f, uint32_t nslices, const uint32_t *d_blk_counts,
@@ -1440,6 +1462,7 @@ extern "C" int rfx_frame_rng_emit(rfx_renderer *r, const rfx_frame *f, uint32_t 
                        (hipEvent_t)emitted_event)) != RFX_OK)
     return rc;
   r->emit_pending = buf;
+  plan_key(pl, r->emit_key);
   return RFX_OK;
 }
 
@@ -1452,6 +1475,11 @@ extern "C" int rfx_render_frame_emitted(rfx_renderer *r, const rfx_frame *f, flo
   if (!d_rgb) return fail(RFX_ERR_ARG, "render_frame_emitted: null framebuffer");
   if (pl.traces == 0) return RFX_OK;
   if (r->emit_pending < 0) return fail(RFX_ERR_STATE, "render_frame_emitted: no emitted frame (rfx_frame_rng_emit)");
+  uint64_t key[8];
+  plan_key(pl, key);
+  if (memcmp(key, r->emit_key, sizeof(key)) != 0)
+    return fail(RFX_ERR_STATE, "render_frame_emitted: the frame differs from the emitted one (band, geometry or traces); "
+                               "rfx_frame_rng_discard it first");
   const int buf = r->emit_pending;
   r->emit_pending = -1;
   r->trace_buf = buf;
@@ -1465,12 +1493,25 @@ extern "C" int rfx_render_frame_emitted(rfx_renderer *r, const rfx_frame *f, flo
 extern "C" int rfx_frame_rng_discard(rfx_renderer *r)
 {
   if (!r) return fail(RFX_ERR_ARG, "frame_rng_discard: null renderer");
+  r->rewind_ok = false;
   if (r->emit_pending >= 0)
   {
     r->seed_idx ^= 1u;
     r->emit_pending = -1;
   }
   return RFX_OK;
+}
+
+extern "C" int rfx_frame_rng_pending(rfx_renderer *r, uint32_t *frame_start)
+{
+  if (!r || !frame_start) return fail(RFX_ERR_ARG, "frame_rng_pending: bad args");
+  int rc;
+  if ((rc = set_dev(r)) != RFX_OK) return rc;
+  // an emitted frame read the state word it left behind (emit_frame flipped seed_idx past it)
+  const uint32_t *w = r->emit_pending >= 0 ? r->d_seed + (r->seed_idx ^ 1u) : seed_cur(r);
+  HIP_CHECK(hipMemcpyAsync(frame_start, w, sizeof(uint32_t), hipMemcpyDeviceToHost, r->stream));
+  HIP_CHECK(hipStreamSynchronize(r->stream));
+  return r->emit_pending >= 0 ? 1 : 0;
 }
 
 extern "C" int rfx_render_frame(rfx_renderer *r, const rfx_frame *f, float *d_rgb, uint32_t *d_argb,
@@ -1480,7 +1521,14 @@ extern "C" int rfx_render_frame(rfx_renderer *r, const rfx_frame *f, float *d_rg
   int rc;
   if (!d_rgb) return fail(RFX_ERR_ARG, "render_frame: null framebuffer");
   if ((rc = plan_frame(r, f, stream, pl)) != RFX_OK) return rc;
-  if (pl.traces == 0) return RFX_OK;  // a span with no block corner traces nothing (and draws no randDir)
+  const uint32_t jitter0 = r->jitter_seed;
+  if (pl.traces == 0)  // a span with no block corner traces nothing (and draws no randDir)
+  {
+    r->rewind_ok = true;
+    r->rewind_flip = false;
+    r->rewind_jitter = jitter0;
+    return RFX_OK;
+  }
   const uint64_t nblk = rng_layout(pl.traces, 1, nullptr);
   if ((rc = ensure_rng_workspace(r, pl.traces, nblk)) != RFX_OK) return rc;
   if ((rc = timing_event(r, pl.st)) != RFX_OK) return rc;
@@ -1488,13 +1536,30 @@ extern "C" int rfx_render_frame(rfx_renderer *r, const rfx_frame *f, float *d_rg
     return fail(RFX_ERR_STATE, "render_frame: an emitted frame awaits rfx_render_frame_emitted (or rfx_frame_rng_discard)");
   // one device counts every block, so the emit can take its accept flags instead of regenerating them
   HIP_CHECK(launch_rng_count(seed_cur(r), r->d_jump, r->d_blk_cnt, 0, nblk, r->d_rng_masks, pl.st));
-  return finish_frame(r, pl, r->d_blk_cnt, r->d_rng_masks, nblk, d_rgb, d_argb, d_counters);
+  if ((rc = finish_frame(r, pl, r->d_blk_cnt, r->d_rng_masks, nblk, d_rgb, d_argb, d_counters)) != RFX_OK) return rc;
+  r->rewind_ok = true;
+  r->rewind_flip = true;
+  r->rewind_jitter = jitter0;
+  return RFX_OK;
+}
+
+// Undo the random-stream advance of the last rfx_render_frame (its pixels stay as written): the pre-pass read the
+// frame's start state from one seed word and wrote the end state to the other, so flipping back restores the start.
+extern "C" int rfx_frame_rng_rewind(rfx_renderer *r)
+{
+  if (!r) return fail(RFX_ERR_ARG, "frame_rng_rewind: null renderer");
+  if (!r->rewind_ok) return fail(RFX_ERR_STATE, "frame_rng_rewind: the last call was not rfx_render_frame");
+  if (r->rewind_flip) r->seed_idx ^= 1u;
+  r->jitter_seed = r->rewind_jitter;
+  r->rewind_ok = false;
+  return RFX_OK;
 }
 
 static int plan_frame(rfx_renderer *r, const rfx_frame *f, void *stream, FramePlan &plan)
 {
   if (!r || !f) return fail(RFX_ERR_ARG, "render_frame: bad args");
   if (!r->has_scene) return fail(RFX_ERR_STATE, "render_frame: no scene uploaded");
+  r->rewind_ok = false;  // every render path moves on from the last rfx_render_frame
   if (!f->width || !f->height || f->reflect_num <= 0 || f->sample_num == 0)
     return fail(RFX_ERR_ARG, "render_frame: W=%u H=%u reflect_num=%d sample_num=%d", f->width, f->height,
                 f->reflect_num, f->sample_num);
@@ -1605,6 +1670,15 @@ extern "C" int rfx_memcpy_d2h(rfx_renderer *r, void *dst, const void *src, size_
   if (!r) return fail(RFX_ERR_ARG, "memcpy: null renderer");
   HIP_CHECK(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, r->stream));
   HIP_CHECK(hipStreamSynchronize(r->stream));
+  return RFX_OK;
+}
+
+extern "C" int rfx_memcpy_d2d(rfx_renderer *r, void *dst, const void *src, size_t n)
+{
+  if (!r || (n && (!dst || !src))) return fail(RFX_ERR_ARG, "memcpy_d2d: bad args");
+  int rc;
+  if ((rc = set_dev(r)) != RFX_OK) return rc;
+  if (n) HIP_CHECK(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, r->stream));
   return RFX_OK;
 }
 

@@ -57,6 +57,12 @@ class RfxStripOps:
     def rng_discard(self):
         _lib.check(self.L.rfx_frame_rng_discard(self.r._h), "frame_rng_discard")
 
+    def rng_pending(self) -> int:
+        """The sphere-stream state the next traced frame starts from (rfx_frame_rng_pending; synchronises)."""
+        s = C.c_uint32()
+        _lib.check(self.L.rfx_frame_rng_pending(self.r._h, C.byref(s)), "frame_rng_pending")
+        return s.value
+
     def set_rows(self, y0: int, y1: int):
         """Band partition: this rank traces rows [y0, y1) (rfx.h: row_block 0, pixel span of whole rows)."""
         self.frame.row_block = 0
@@ -143,9 +149,11 @@ class _CountedFrame:
         self.counts = torch.zeros(world * self.bps, dtype=torch.int32, device=device)
         cuda = device.type == "cuda"
         if count_ahead is None:
-            count_ahead = world > 1 and dist.get_backend() == "nccl"
+            # on for RCCL, and for gloo ranks sharing one GPU (the one-box rehearsal runs the same stream and
+            # buffer choreography, its all-gathers staged through host memory on the side stream)
+            count_ahead = world > 1 and (dist.get_backend() == "nccl" or self._host_staged())
         # (asked for explicitly it also runs at world 1: the device-side ordering test, tests/test_gpu_multirank.py)
-        self.count_ahead = bool(count_ahead) and not self._host_staged()
+        self.count_ahead = bool(count_ahead)
         self.count_group = dist.new_group(list(range(world))) if self.count_ahead else None
         self.count_stream = torch.cuda.Stream(device=device) if self.count_ahead and cuda else None
         self.emitted = torch.cuda.Event() if self.count_ahead and cuda else None
@@ -160,6 +168,7 @@ class _CountedFrame:
         for e in self.trace_done:
             e.record(torch.cuda.current_stream(device))
         self._n = 0  # frames rendered (emit-ahead bookkeeping)
+        self._emit_events: Optional[list] = None  # time_emits(): (start, end) events around each side-stream emit
 
     def _frame_counts(self):
         """This frame's all-gathered slice counts in self.counts, ordered before the emit on this stream."""
@@ -209,9 +218,28 @@ class _CountedFrame:
             if w is not None:
                 w.wait()  # the side stream waits for the all-gather
             self.count_stream.wait_event(self.trace_done[(self._n - 1) % 2])  # the last reader of the emit's buffer
+            ev = None
+            if self._emit_events is not None:
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record(self.count_stream)
+                self._emit_events.append(ev)
             self.ops.rng_emit(self.world, self.counts.data_ptr(), stream=self.count_stream.cuda_stream,
                               emitted_event=self.emitted.cuda_event)
+            if ev is not None:
+                ev[1].record(self.count_stream)
         self.emit_ready = True
+
+    def time_emits(self, enable: bool) -> Optional[float]:
+        """Time the look-ahead emits on the side stream (HIP events there): enable, render, then disable to read the
+        average ms per emit (synchronises; None without emit-ahead or emits)."""
+        if enable:
+            self._emit_events = [] if self.emit_ahead else None
+            return None
+        ev, self._emit_events = self._emit_events, None
+        if not ev:
+            return None
+        torch.cuda.synchronize(self.device)
+        return sum(s.elapsed_time(e) for s, e in ev) / len(ev)
 
     def _count_next(self):
         """Count the next frame's slice and start its all-gather, ordered after this frame's emit only."""
@@ -248,13 +276,17 @@ class _CountedFrame:
         mine = self.counts[self.rank * self.bps:(self.rank + 1) * self.bps]
         if dist.get_backend() == "nccl":
             return dist.all_gather_into_tensor(self.counts, mine.clone(), group=group, async_op=async_op)
+        if self._host_staged():
+            # gloo ranks on one GPU: through host memory on the current stream (the side stream of a look-ahead:
+            # .cpu() waits for the count there, the copy back is ordered before the emit); completes here
+            h = self.counts.cpu()
+            dist.all_gather(list(h.split(self.bps)), h[self.rank * self.bps:(self.rank + 1) * self.bps].clone(),
+                            group=group)
+            self.counts.copy_(h, non_blocking=False)
+            return None
         if async_op:  # gloo on CPU (the orchestration tests): the exchange completes here
             dist.all_gather(list(self.counts.split(self.bps)), mine.clone(), group=group)
             return None
-        elif self._host_staged():
-            h = self.counts.cpu()
-            dist.all_gather(list(h.split(self.bps)), h[self.rank * self.bps:(self.rank + 1) * self.bps].clone())
-            self.counts.copy_(h)
         else:
             dist.all_gather(list(self.counts.split(self.bps)), mine.clone())
 

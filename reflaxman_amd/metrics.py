@@ -129,6 +129,37 @@ def pmc_record(directory: str, config, lib_sha: str, device_sha: str = None):
     return None
 
 
+def roofline(executed, traffic, flops_launch: float, trace_ms: float, px_launch: int) -> dict:
+    """bench.py's `roofline` object for the trace kernel.  The bound is the FP32 VALU (no dense contraction, HBM
+    traffic ~16 B/px): `achieved` is the executed VALU lane-op rate of one launch (PMC record of this workload and
+    build, rated at this run's HIP-event launch time) against the 78.6 T lane-op/s peak, so `frac` is a hardware
+    fraction <= 1 -- null when no PMC record matches.  The reference-equivalent algorithmic rate (SURVEY 8(d)
+    counting rule over the reference's brute-force tests, which exact culling and the BVH skip) is reported beside
+    it as `effective_ref_flops`: it is effective work, and exceeds the peak on C5."""
+    t = trace_ms * 1e-3
+    ach = flops_launch / t / 1e12
+    out = {
+        "bound": "valu",
+        "achieved": executed["achieved_T_lane_ops"] if executed and "achieved_T_lane_ops" in executed else None,
+        "peak": round(PEAK_VALU_LANE_OPS / 1e12, 1), "unit": "T VALU lane-op/s",
+        "frac": executed["frac_lane_ops"] if executed and "frac_lane_ops" in executed else None,
+        "traffic": traffic,
+        "frac_kind": "executed VALU lane-ops per launch (SQ_INSTS_VALU x 64 x lane utilisation, rocprofv3 --pmc of this "
+                     "workload and library build) / HIP-event launch time / 78.6 T lane-op/s (256 CU x 128 FP32 lanes "
+                     "x 2.4 GHz, non-FMA: parity forbids contraction); null without a matching PMC record",
+        "avg_launch_ms": round(trace_ms, 4),
+        "executed": executed,
+        "effective_ref_flops": {
+            "achieved": round(ach, 3), "unit": "TFLOP/s", "flops_per_launch": int(flops_launch),
+            "peak": PEAK_FP32_VALU_TFLOPS, "frac": round(ach / PEAK_FP32_VALU_TFLOPS, 4),
+            "frac_vs_nofma_peak": round(ach / PEAK_FP32_NOFMA_TFLOPS, 4),
+            "kind": "reference-equivalent algorithmic FLOPs / launch time: effective work, not utilisation"},
+        "algo_hbm_bytes_per_launch": px_launch * ALGO_BYTES_PER_PIXEL,
+        "algo_hbm_GBps": round(px_launch * ALGO_BYTES_PER_PIXEL / t / 1e9, 1),
+    }
+    return out
+
+
 def executed_work(rec, trace_ms: float):
     """Executed VALU work of one trace launch from a PMC record, rated at this run's kernel time."""
     if not rec:

@@ -1,24 +1,37 @@
 // Headless platform for the reference's own application controller (src/common/Pulse.cpp, unmodified):
-// a BasePlatformInterface with a fake clock drives Pulse through its screenshot flow -- F2, a resolution
-// key, an SSAA key, then exec() until the BMP is written (Pulse.cpp:156-209, 346-438) -- and prints the
-// file name.  Built twice by tests/test_dropin_pulse.py:
-//   * against the reference's Render.cpp / Scene.cpp ... (the CPU renderer): the golden screenshot;
+// a BasePlatformInterface with a fake clock drives Pulse.  Built twice by tools/pulse_build.py:
+//   * against the reference's Render.cpp / Scene.cpp ... (the CPU renderer): the goldens;
 //   * against include/reflaxman/dropin/{Render,Scene}.h + librfx.so: the same Pulse on the MI355X.
-// Usage: pulse_headless OUTDIR/ RES_KEY(1-9) SS_KEY(1-9) [WIN_W WIN_H]
+//
+// Usage:
+//   pulse_headless OUTDIR/ RES_KEY(1-9) SS_KEY(1-9) [WIN_W WIN_H]
+//       the screenshot flow -- F2, a resolution key, an SSAA key, then exec() until the BMP is written
+//       (Pulse.cpp:156-209, 346-438) -- prints the file name;
+//   pulse_headless OUTDIR/ session WIN_W WIN_H TICK_US [nohash]
+//       an interactive session (Pulse::renderImage, Pulse.cpp:102-154): still frames (depth 15, additive), keys
+//       pressed in the middle of a frame (the frame is abandoned: Pulse.cpp:110), motion frames with the keys held
+//       (block preview, depth 4, sampleNum adapted from the frame time: Pulse.cpp:112-118), keys released (the
+//       camera decelerates, Camera.cpp:110-239, then still frames accumulate again).  Every completed frame is read
+//       back the way the window does it (getRenderImagePixel over the client area, linux/main.cpp:53-88) and
+//       hashed; one line per frame: "frame I execs N ms T hash H".  T is the wall time of the frame's exec() calls
+//       (the read-back excluded).  The fake clock advances TICK_US per reading, so Pulse's chunk doubling and
+//       sample adaptation are the same in both builds.
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <sys/stat.h>
 
+#include <chrono>
 #include <string>
 
 #include "Pulse.h"
 
 class HeadlessPlatform : public BasePlatformInterface {
  public:
-  HeadlessPlatform(const std::string &dir, unsigned w, unsigned h) : dir_(dir), w_(w), h_(h), t_(1) {}
+  HeadlessPlatform(const std::string &dir, unsigned w, unsigned h, uint64_t tick)
+      : dir_(dir), w_(w), h_(h), t_(1), tick_(tick) {}
   std::string getExePath() { return dir_; }
-  uint64_t getPerformanceCounter() { return t_ += 1000; }  // 1 ms per reading: chunks double every call
+  uint64_t getPerformanceCounter() { return t_ += tick_; }
   uint64_t getPerformanceFrequency() { return 1000000; }
   uint64_t getSystemTime() { return 0x0123456789ABCDEFull; }
   void getMainWindowClientSize(unsigned int *const width, unsigned int *const height) { *width = w_; *height = h_; }
@@ -28,19 +41,14 @@ class HeadlessPlatform : public BasePlatformInterface {
  private:
   std::string dir_;
   unsigned w_, h_;
-  uint64_t t_;
+  uint64_t t_, tick_;
 };
 
 static const KEY_CODE kDigit[9] = {KEY_1, KEY_2, KEY_3, KEY_4, KEY_5, KEY_6, KEY_7, KEY_8, KEY_9};
 
-int main(int argc, char **argv)
+static int screenshot(const std::string &dir, int res, int ss, unsigned ww, unsigned wh)
 {
-  if (argc < 4) { fprintf(stderr, "usage: pulse_headless OUTDIR/ RES_KEY SS_KEY [WIN_W WIN_H]\n"); return 2; }
-  const std::string dir = argv[1];
-  const int res = atoi(argv[2]), ss = atoi(argv[3]);
-  const unsigned ww = argc > 5 ? (unsigned)atoi(argv[4]) : 320, wh = argc > 5 ? (unsigned)atoi(argv[5]) : 240;
-  if (res < 1 || res > 9 || ss < 1 || ss > 9) return 2;
-  HeadlessPlatform plat(dir, ww, wh);
+  HeadlessPlatform plat(dir, ww, wh, 1000);  // 1 ms per reading: chunks double every call
   Pulse pulse(&plat);
   pulse.onResize(ww, wh);                 // stInit -> stCameraControl, Render::setImageSize
   pulse.onKeyEvent(KEY_F2, true);         // -> resolution menu
@@ -61,4 +69,80 @@ int main(int argc, char **argv)
   }
   fprintf(stderr, "no screenshot written\n");
   return 1;
+}
+
+// FNV-1a 64 over the window's pixels as linux/main.cpp:82-84 reads them (x fastest, y from 0)
+static uint64_t frame_hash(Pulse &pulse, unsigned w, unsigned h)
+{
+  uint64_t x = 1469598103934665603ull;
+  for (unsigned y = 0; y < h; ++y)
+    for (unsigned i = 0; i < w; ++i)
+    {
+      const uint32_t p = pulse.getRenderImagePixel(i, y);
+      for (int b = 0; b < 4; ++b)
+      {
+        x ^= (p >> (8 * b)) & 0xFFu;
+        x *= 1099511628211ull;
+      }
+    }
+  return x;
+}
+
+static int session(const std::string &dir, unsigned w, unsigned h, uint64_t tick, bool hash)
+{
+  HeadlessPlatform plat(dir, w, h, tick);
+  Pulse pulse(&plat);
+  pulse.onResize(w, h);
+  typedef std::chrono::steady_clock clk;
+  int frame = 0;
+  long execs = 0;
+  double ms = 0.0;
+  // run exec() until the next frame completes (or `limit` calls), timing the calls
+  auto run = [&](long limit) -> bool {
+    for (long i = 0; i < limit; ++i)
+    {
+      const clk::time_point t0 = clk::now();
+      pulse.exec();
+      ms += std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+      ++execs;
+      if (pulse.imageReady)
+      {
+        const uint64_t hv = hash ? frame_hash(pulse, w, h) : 0;
+        printf("frame %d execs %ld ms %.4f hash %016llx\n", frame++, execs, ms, (unsigned long long)hv);
+        fflush(stdout);
+        execs = 0;
+        ms = 0.0;
+        pulse.imageReady = false;  // the window drew it (linux/main.cpp:87)
+        return true;
+      }
+    }
+    return false;
+  };
+  const long kMax = 100000000L;
+  for (int i = 0; i < 2; ++i) run(kMax);      // still frames: depth 15, additive
+  run(7);                                     // seven chunks into the third still frame ...
+  pulse.onKeyEvent(KEY_RIGHT, true);          // ... keys go down: the frame is abandoned for a motion frame
+  pulse.onKeyEvent(KEY_W, true);
+  for (int i = 0; i < 6; ++i) run(kMax);      // motion frames: block preview, depth 4
+  pulse.onKeyEvent(KEY_RIGHT, false);
+  pulse.onKeyEvent(KEY_W, false);
+  for (int i = 0; i < 8; ++i) run(kMax);      // the camera decelerates, then still frames accumulate again
+  return 0;
+}
+
+int main(int argc, char **argv)
+{
+  if (argc >= 6 && !strcmp(argv[2], "session"))
+    return session(argv[1], (unsigned)atoi(argv[3]), (unsigned)atoi(argv[4]), (uint64_t)strtoull(argv[5], nullptr, 0),
+                   !(argc > 6 && !strcmp(argv[6], "nohash")));
+  if (argc < 4)
+  {
+    fprintf(stderr, "usage: pulse_headless OUTDIR/ RES_KEY SS_KEY [WIN_W WIN_H] | OUTDIR/ session W H TICK_US [nohash]\n");
+    return 2;
+  }
+  const std::string dir = argv[1];
+  const int res = atoi(argv[2]), ss = atoi(argv[3]);
+  const unsigned ww = argc > 5 ? (unsigned)atoi(argv[4]) : 320, wh = argc > 5 ? (unsigned)atoi(argv[5]) : 240;
+  if (res < 1 || res > 9 || ss < 1 || ss > 9) return 2;
+  return screenshot(dir, res, ss, ww, wh);
 }

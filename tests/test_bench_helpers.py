@@ -24,3 +24,22 @@ def test_weak_and_strong_frame_sizes():
     assert bench.frame_size(8, 7680, 4320, "strong") == (7680, 4320)
     w, h = bench.frame_size(4, 3840, 2160, "weak")
     assert (w, h) == (7680, 4320)
+
+
+def test_roofline_frac_is_a_hardware_fraction():
+    """roofline.frac is the executed VALU lane-op fraction (<= 1) from a PMC record, or null without one; the
+    reference-equivalent rate (above the peak on C5) lives in effective_ref_flops."""
+    import glob
+    import json
+    from reflaxman_amd import metrics
+    recs = [json.load(open(p)) for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc", "*.json")))]
+    assert recs
+    for rec in recs:
+        # the record's own kernel time: GRBM_GUI_ACTIVE is summed over the 8 XCDs, at 2.4 GHz
+        ms = rec["counters"]["GRBM_GUI_ACTIVE"] / 8 / 2.4e6
+        ex = metrics.executed_work(rec, ms)
+        r = metrics.roofline(ex, rec.get("hbm_bytes_per_launch"), 5e12, ms, 8294400)
+        assert 0 < r["frac"] <= 1 and r["achieved"] <= r["peak"], (rec.get("config"), ms, r["frac"])
+        assert r["unit"] == "T VALU lane-op/s" and r["peak"] == 78.6
+    r = metrics.roofline(None, None, 9e12, 3.35, 8294400)  # C5-like effective work: above the peak ...
+    assert r["frac"] is None and r["effective_ref_flops"]["frac"] > 1  # ... but never as `frac`

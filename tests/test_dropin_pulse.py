@@ -47,3 +47,32 @@ def test_pulse_screenshot_matches_reference(tmp_path):
     data = open(path, "rb").read()
     assert len(data) == c["bytes"]
     assert hashlib.sha256(data).hexdigest() == c["sha_bmp"]
+
+
+def run_session(tmp_path, c, policy, hash_frames=True):
+    """The interactive session of tests/native/pulse_headless.cpp through the drop-in; returns the parsed frame lines."""
+    if not os.path.exists(DROPIN):
+        pytest.fail("tests/native/_build/pulse_dropin missing: run __graft_entry__.build() where /root/reference exists")
+    env = {**os.environ, "RFX_SPHERE_SEED": str(c["RFX_SPHERE_SEED"]), "RFX_JITTER_SEED": str(c["RFX_JITTER_SEED"]),
+           "RFX_DROPIN_POLICY": policy}
+    cmd = [DROPIN, str(tmp_path) + "/", "session", str(c["W"]), str(c["H"]), str(c["tick_us"])]
+    r = subprocess.run(cmd + ([] if hash_frames else ["nohash"]), capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return [l.split() for l in r.stdout.splitlines() if l.startswith("frame ")]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tick", [1000, 2000])
+@pytest.mark.parametrize("policy", ["frame", "span"])
+def test_pulse_interactive_session_matches_reference(tmp_path, tick, policy):
+    """Pulse's interactive loop (Pulse.cpp:102-154) through the drop-in, against the same session through the
+    reference's CPU renderer: still additive frames at depth 15, a key press that abandons a frame after 7 chunks,
+    motion frames in block preview at depth 4 (sampleNum held at -1, or walked down to -8 by the slower fake clock),
+    release, deceleration, still frames again.  Every completed frame, read back as the window reads it
+    (getRenderImagePixel over the client area), hashes to the reference's; the per-frame chunk counts are the same.
+    Policy "frame" renders each frame whole at its first renderNext (and settles the abandoned one exactly); "span"
+    renders each chunk as it comes."""
+    c = manifest()["cases"][f"pulse_session_640x480_tick{tick}"]
+    frames = run_session(tmp_path, c, policy)
+    assert [f[7] for f in frames] == c["hashes"]
+    assert [int(f[3]) for f in frames] == c["execs"]

@@ -33,6 +33,13 @@ def test_bench_multirank_frame_matches_single_gpu(world, partition):
     out = json.loads(line)
     assert out["n_gpus"] == world
     assert out["parity"]["multi_rank_frame_equals_single_gpu"] is True
+    # the step after the timed ones, down the steady-state path (look-aheads on: gloo ranks on one GPU stage their
+    # all-gathers through host memory on the side stream), equals a single-GPU render of the same stream frame
+    assert out["steady_state_parity"]["equals_single_gpu"] is True
+    assert "count-ahead" in out["config"]["parallelism"] and "emit-ahead" in out["config"]["parallelism"]
+    b = out["strong_scaling_baseline"]
+    assert b["value"] > 0 and b["efficiency"] > 0
+    assert out["roofline"]["frac"] is None or out["roofline"]["frac"] <= 1
     assert out["value"] > 0
     if partition == "bands":
         b = out["band_bounds"]

@@ -343,6 +343,24 @@ def main():
                                                          file=os.path.basename(r.stdout.strip()), **seeds)
             print("pulse screenshot", flush=True)
 
+        # an interactive session of the same Pulse (still frames, a key press that abandons a frame, motion frames in
+        # block preview, release, deceleration, still frames again): the hash of every completed frame as the window
+        # reads it.  TICK 1000 us keeps sampleNum at -1 (a fast renderer's path); 2000 us walks it down to -8.
+        if want("pulse_session"):
+            sys.path.insert(0, os.path.join(ROOT, "tools"))
+            import pulse_build
+            exe = pulse_build.build("reference", os.path.join(tmp, "pulse_ref_s"))
+            seeds = {"RFX_SPHERE_SEED": DEFAULT_SEED, "RFX_JITTER_SEED": 424238335}
+            for tick in (1000, 2000):
+                W, H = 640, 480
+                r = subprocess.run([exe, tmp + "/", "session", str(W), str(H), str(tick)], check=True,
+                                   capture_output=True, text=True, env={**os.environ, **{k: str(v) for k, v in seeds.items()}})
+                frames = [l.split() for l in r.stdout.splitlines() if l.startswith("frame ")]
+                cases[f"pulse_session_{W}x{H}_tick{tick}"] = dict(
+                    kind="pulse_session", W=W, H=H, tick_us=tick, execs=[int(f[3]) for f in frames],
+                    hashes=[f[7] for f in frames], **seeds)
+                print(f"pulse session tick {tick}: {len(frames)} frames", flush=True)
+
         # stress bands (4K width) with stream advance
         for y0 in (0, 1080):
             key = f"band_stress4096_3840x2160_d12_y{y0}_r4"
