@@ -441,12 +441,6 @@ extern "C" uint32_t rfx_strip_row_to_y(uint32_t r, uint32_t rb, uint32_t rank, u
 // trace 0.41 ms unsorted vs 0.34 at N = 4 per eighth of the frame, tools/root_overhead.py)
 #define RFX_TILE_ORDER_MIN_TILES 49152
 #endif
-#ifndef RFX_WAVE_TILES  // schedule unit: the wave's 8x8 tile (1) or the workgroup's 16x8 (0); tools/ab.py, C3: -2.7% trace
-#define RFX_WAVE_TILES 1
-#endif
-#ifndef RFX_PRIM_MASK  // small scenes: precomputed primary-bundle cull masks (1) or per-launch bundles (0)
-#define RFX_PRIM_MASK 1
-#endif
 constexpr size_t kPrimWords = 5;  // per wave tile (rfx_trace.h kPrimStride)
 
 #ifndef RFX_QUEUE_SORT
@@ -711,12 +705,10 @@ static void spatial_order(std::vector<uint32_t> &idx, size_t a, size_t b, const 
 // Pair BVH of a large scene: leaves are the device sphere pairs (2j, 2j + 1, neighbours); internal nodes
 // split their pairs where the surface-area heuristic is lowest (every position of the pair centres sorted
 // along each axis), as long as the split keeps the tree within the kernel's stack depth, else at the
-// median of the pair centres along the longest axis.  Each node stores its two
+// median of the pair centres along the longest axis (SAH against median splits alone: C5 -0.8%, round 2).  Each
+// node stores its two
 // children's boxes (spheres grown by their radii); the kernel widens them by its exact-cull margin per ray.
 // Returns the node index (or ~pair for a leaf) of range [a, b) of `pairs`; depth: internal levels below.
-#ifndef RFX_BVH_SAH  // pair BVH splits: surface-area heuristic (1) or median (0); tools/ab.py, C5: -0.8%
-#define RFX_BVH_SAH 1
-#endif
 #ifndef RFX_BVH_STACK
 #define RFX_BVH_STACK 16  // the kernel's per-lane traversal stack (rfx_trace.h kBvhStack)
 #endif
@@ -737,7 +729,6 @@ int build_pair_bvh(std::vector<BvhNode> &nodes, std::vector<uint32_t> &pairs, si
   for (int k = 1; k < 3; ++k)
     if (hi[k] - lo[k] > hi[axis] - lo[axis]) axis = k;
   size_t mid = a + (b - a) / 2;
-#if RFX_BVH_SAH
   // surface-area heuristic over sorted pair centres (all three axes, every split position), while the depth
   // budget allows an unbalanced split: the subtree of n leaves must still fit RFX_BVH_STACK levels
   const size_t cnt = b - a;
@@ -779,7 +770,6 @@ int build_pair_bvh(std::vector<BvhNode> &nodes, std::vector<uint32_t> &pairs, si
     axis = best_axis;
     mid = best_mid;
   }
-#endif
   std::nth_element(pairs.begin() + a, pairs.begin() + mid, pairs.begin() + b, [&](uint32_t x, uint32_t y) {
     return box[x].c[axis] < box[y].c[axis] || (box[x].c[axis] == box[y].c[axis] && x < y);
   });
@@ -809,9 +799,6 @@ int build_pair_bvh(std::vector<BvhNode> &nodes, std::vector<uint32_t> &pairs, si
 
 #ifndef RFX_BVH_STACK
 #define RFX_BVH_STACK 16  // the kernel's per-lane traversal stack (rfx_trace.h kBvhStack)
-#endif
-#ifndef RFX_BVH_STACK16
-#define RFX_BVH_STACK16 1  // the kernel's stack slots are int16 (rfx_trace.h BvhSlot)
 #endif
 
 extern "C" int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *s)
@@ -983,7 +970,6 @@ extern "C" int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *s)
   std::vector<BvhNode> bvh;
   int bvh_depth = 0;
   double bvh_ref[3] = {0.0, 0.0, 0.0};
-#ifndef RFX_NO_BVH
   if (nsph > 32)
   {
     const size_t npairs = (nsph + 1) / 2;
@@ -1009,11 +995,8 @@ extern "C" int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *s)
     }
     build_pair_bvh(bvh, pairs, 0, npairs, box, bvh_ref, 0, bvh_depth);
     if (bvh_depth > RFX_BVH_STACK) { bvh.clear(); bvh_depth = 0; }  // deeper than the kernel's stack: chunk loops
-#if RFX_BVH_STACK16
-    if (bvh.size() > 32767 || npairs > 32768) { bvh.clear(); bvh_depth = 0; }  // int16 stack slots
-#endif
+    if (bvh.size() > 32767 || npairs > 32768) { bvh.clear(); bvh_depth = 0; }  // int16 stack slots (rfx_trace.h)
   }
-#endif
   std::vector<PlaneGeo> pg;
   std::vector<MatRec> pm;
   for (const HostPlane &p : s->planes)
@@ -1295,7 +1278,7 @@ static int trace_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *rd, float
   const bool plain = P.ss == 1 && !P.additive && !P.accumulate;
   const int park_after = r->park_after < 0 ? (small ? 0 : RFX_PARK_AFTER) : r->park_after;
   const bool park = park_after > 0 && plain && !d_counters && P.depth > park_after && P.grid_rows;
-  const bool sort_queue = park && r->queue_sort && RFX_WAVE_TILES;  // keys are written by the wave-tile kernel
+  const bool sort_queue = park && r->queue_sort;
   if (park)
   {
     if (pl.traces > r->queue_cap)
@@ -1326,14 +1309,14 @@ static int trace_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *rd, float
   P.counters = (unsigned long long *)d_counters;
   // mode 1 schedules only launches of at least RFX_TILE_ORDER_MIN_TILES tiles: on shorter ones the sort's
   // latency (three small launches and a cross-stream wait, ~15 us) is not hidden by the RNG pre-pass
-  const bool sched = P.grid_rows && r->tile_mode && !d_counters && !(RFX_WAVE_TILES && P.ss < 0) &&
+  const bool sched = P.grid_rows && r->tile_mode && !d_counters && P.ss >= 0 &&
                      (r->tile_mode != 1 || trace_tiles(P) >= RFX_TILE_ORDER_MIN_TILES);
   uint64_t key = 0;
   bool record = false;
   if (sched && (rc = tile_schedule(r, P, st, key, record)) != RFX_OK) return rc;
   // primary-bundle cull masks: small scenes, plain frames, culling launches; recomputed only when the camera,
   // the frame geometry or the scene changed (the bench's frames all reuse one set)
-  if (small && plain && !d_counters && !park && P.grid_rows && RFX_WAVE_TILES && RFX_PRIM_MASK && r->prim_mode)
+  if (small && plain && !d_counters && !park && P.grid_rows && r->prim_mode)
   {
     struct Key { float cam[15]; uint32_t W, H, grid_rows, row0, row_block, rank, nranks; int32_t depth;
                  uint64_t p_begin, p_end, gen; } k;

@@ -679,7 +679,7 @@ static dim3 trace_grid(const FrameParams &P)
 uint32_t trace_tiles(const FrameParams &P)
 {
   const dim3 g = trace_grid(P);
-  return (RFX_WAVE_TILES ? kWgWaves : 1u) * g.x * g.y;
+  return kWgWaves * g.x * g.y;
 }
 
 // the per-view masks of a small scene's plain frame (prim_cull_kernel), kPrimStride words per wave tile
@@ -697,7 +697,7 @@ hipError_t launch_trace(const DevScene &S, const FrameParams &P, bool stats, hip
 {
   const dim3 grid = trace_grid(P);
   FrameParams Pt = P;
-  Pt.tiles_x = kTileWavesX * grid.x;  // wave tiles per row (RFX_WAVE_TILES)
+  Pt.tiles_x = kTileWavesX * grid.x;  // wave tiles per row (the schedule's unit)
   const int mode = P.ss < 0 ? kModeBlock : (P.ss == 1 && !P.additive && !P.accumulate) ? kModePlain : kModeSsaa;
   // the stats build counts the reference's every test, so it never culls
   const int cfg = (S.n_light > 32 ? kCfgManyLights : 0) | (stats ? 0 : kCfgCull) |

@@ -678,23 +678,14 @@ constexpr int kBvhStack = 16;
 #define RFX_NARROW_BUNDLE_COS 0.9995f
 #endif
 constexpr float kNarrowBundleCos = RFX_NARROW_BUNDLE_COS;  // rfx_host.cpp RFX_BVH_STACK: deeper hierarchies fall back to the chunk loops
-// Stack slots: int16 node / ~pair indices (1; the host builds no BVH for 32768 or more nodes or pairs) or int32
-// (0).  Halving the stack's LDS (8 -> 4 KB per workgroup) makes C5 6.3% faster (tools/ab.py): workgroups
+// Stack slots: int16 node / ~pair indices (the host builds no BVH for 32768 or more nodes or pairs).  Halving the
+// stack's LDS against int32 slots (8 -> 4 KB per workgroup) made C5 6.3% faster (tools/ab.py, round 2): workgroups
 // holding less LDS fit the CU's LDS with more slack as they finish out of order.
-#ifndef RFX_BVH_STACK16
-#define RFX_BVH_STACK16 1
-#endif
-#if RFX_BVH_STACK16
 typedef int16_t BvhSlot;
-#else
-typedef int32_t BvhSlot;
-#endif
 __shared__ BvhSlot s_bvh_stack[kBvhStack * kWgThreads];
 
-#ifndef RFX_BVH_NODE_MARGIN  // box margins from the node's stored term and one per-ray distance (1) or per box (0)
-#define RFX_BVH_NODE_MARGIN 1
-#endif
-struct RayInv { float ix, iy, iz, dm; };  // dm: kCullRel |o - bvh_ref|_1 + 1e-6 (RFX_BVH_NODE_MARGIN)
+// box margins from the node's stored term and one per-ray distance (round 2: C5 -8.5% against a margin per box)
+struct RayInv { float ix, iy, iz, dm; };  // dm: kCullRel |o - bvh_ref|_1 + 1e-6
 __device__ __forceinline__ RayInv ray_inv(const DevScene &S, v3 o, v3 ray)
 {
   const float dm = kCullRel * (fabsf(o.x - S.bvh_rx) + fabsf(o.y - S.bvh_ry) + fabsf(o.z - S.bvh_rz)) + 1e-6f;
@@ -706,14 +697,9 @@ __device__ __forceinline__ RayInv ray_inv(const DevScene &S, v3 o, v3 ray)
 __device__ __forceinline__ bool bvh_box(const BvhNode &n, int c, v3 o, const RayInv &ri, float &tn)
 {
   const float lx = n.lx[c], ly = n.ly[c], lz = n.lz[c], hx = n.hx[c], hy = n.hy[c], hz = n.hz[c];
-#if RFX_BVH_NODE_MARGIN
-  // |o - c|_1 + half-size_1 <= |o - ref|_1 + mt[c]: a margin at least the per-box one below
+  // |o - c|_1 + half-size_1 <= |o - ref|_1 + mt[c] (c the box centre): the margin is at least
+  // kCullRel (|o - c|_1 + half-size_1) + 1e-6, the per-box bound of the culling argument
   const float m = ri.dm + kCullRel * n.mt[c];
-#else
-  const float cx = 0.5f * (lx + hx), cy = 0.5f * (ly + hy), cz = 0.5f * (lz + hz);
-  const float m = kCullRel * (fabsf(o.x - cx) + fabsf(o.y - cy) + fabsf(o.z - cz) +
-                              0.5f * ((hx - lx) + (hy - ly) + (hz - lz))) + 1e-6f;
-#endif
   const float ax = (lx - m - o.x) * ri.ix, bx = (hx + m - o.x) * ri.ix;
   const float ay = (ly - m - o.y) * ri.iy, by = (hy + m - o.y) * ri.iy;
   const float az = (lz - m - o.z) * ri.iz, bz = (hz + m - o.z) * ri.iz;
@@ -1524,10 +1510,6 @@ __device__ __forceinline__ v3 rd_from_state(uint32_t s)
 
 __device__ __forceinline__ v3 load_rd(const FrameParams &P, uint64_t i) { return rd_from_state(P.rd_state[i]); }
 
-#ifndef RFX_WAVE_TILES  // schedule unit: the wave's 8x8 tile (1) or the workgroup's 16x8 (0); tools/ab.py, C3: -2.7% trace
-#define RFX_WAVE_TILES 1
-#endif
-
 // Shader clock, low 32 bits.  A plain asm statement (no side effects declared, so the compiler may still
 // serve the scene loads that follow through the scalar cache -- __builtin_readcyclecounter would count as a
 // memory clobber for them); it waits for its own result.
@@ -1585,17 +1567,9 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
   stage_powf_tables();
   if constexpr (SMALL) stage_small_scene(S);
   RFX_PROF_INIT();
-  // the tile this workgroup renders: with a tile order (longest-processing-time first, from the previous
-  // frame's measured tile costs) the most expensive tiles start first and the cheap ones fill the tail
-  const uint32_t tile = P.tile_order ? P.tile_order[blockIdx.y * gridDim.x + blockIdx.x] : blockIdx.y * gridDim.x + blockIdx.x;
-  // tile cost: the start clock (low 32 bits) and the tile index wait in LDS, so the bounce loop keeps no
-  // register for them
-  __shared__ uint32_t s_clk0, s_tile;
-  if (P.tile_cost && threadIdx.x == 0)
-  {
-    s_clk0 = clock32();
-    s_tile = tile;
-  }
+  // tile cost: the workgroup's start clock (low 32 bits) waits in LDS, so the bounce loop keeps no register for it
+  __shared__ uint32_t s_clk0;
+  if (P.tile_cost && threadIdx.x == 0) s_clk0 = clock32();
   __syncthreads();
   Cnt cnt;
   if constexpr (STATS)
@@ -1604,9 +1578,10 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
     for (int k = 0; k < C_COUNT; ++k) cnt.c[k] = 0;
   }
   const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
-#if RFX_WAVE_TILES
-  // the schedule's unit is the wave's 8x8 tile: wave v of workgroup w renders tile tile_order[kWgWaves w + v]
-  // of the (kTileWavesX gridDim.x) x (kTileWavesY gridDim.y) tile grid (identity: the workgroup's own tiles)
+  // the schedule's unit is the wave's 8x8 tile (round 2: -2.7% trace against the workgroup's 16x8): wave v of
+  // workgroup w renders tile tile_order[kWgWaves w + v] of the (kTileWavesX gridDim.x) x (kTileWavesY gridDim.y)
+  // tile grid -- with a tile order (longest-processing-time first, from an earlier launch's measured tile costs)
+  // the most expensive tiles start first and the cheap ones fill the tail; without, the workgroup's own tiles
   const uint32_t wv = __builtin_amdgcn_readfirstlane(wave), wid = blockIdx.y * gridDim.x + blockIdx.x;
   const uint32_t w8 = kTileWavesX * gridDim.x;
   const uint32_t t8 = P.tile_order ? P.tile_order[kWgWaves * wid + wv]
@@ -1615,12 +1590,6 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
   // the tile index waits in LDS across the bounce loop: the epilogue re-derives the output coordinates from it
   // instead of keeping (spilling) them
   if (lane == 0) s_tile8[wv] = t8;
-  (void)tile;
-#else
-  const uint32_t lx = (wave % kTileWavesX) * 8u + (lane & 7u), ly = (wave / kTileWavesX) * 8u + (lane >> 3);
-  const uint32_t bx = tile % gridDim.x, by = tile / gridDim.x;
-  const uint32_t gx = bx * kTileW + lx, gy = by * kTileH + ly;
-#endif
   m33 view;
   view.m11 = P.v11; view.m12 = P.v12; view.m13 = P.v13;
   view.m21 = P.v21; view.m22 = P.v22; view.m23 = P.v23;
@@ -1653,13 +1622,11 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
           if (P.argb) P.argb[(size_t)qy * P.W + qx] = a;
         }
     }
-    if (P.tile_cost && __lane_id() == 0) P.tile_cost[s_tile] = clock32() - s_clk0;  // one lane per wave, the last stays
   }
   else
   {
     const uint32_t x = gx;
     const uint32_t y = P.nranks > 1 ? strip_row_to_y(gy, P) : gy + P.row0;
-    const uint32_t orow = P.nranks > 1 ? gy : y;
     const uint64_t p = (uint64_t)y * P.W + x;
     const bool valid = gx < P.W && gy < P.grid_rows && p >= P.p_begin && p < P.p_end;
     const uint64_t pr = p - P.p_begin;
@@ -1672,16 +1639,8 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
       const v3 ray = mmul(view, mk(rx + 0.0f + 0.0f, ry + 0.0f + 0.0f, P.rz));
       v3 rd = mk(0.0f, 0.0f, 0.0f);
       if (valid) rd = load_rd(P, pr);
-#if RFX_WAVE_TILES
       const ParkTile park{P.park_after, P.queue, P.queue_count, P, wv, w8};
-#else
-      const Park park{P.park_after, P.queue, P.queue_count, (uint32_t)pr, (uint32_t)((size_t)orow * P.W + x)};
-#endif
-#if RFX_WAVE_TILES
       const uint64_t *pm_tile = SMALL && CULL && !STATS && P.prim_mask ? P.prim_mask + (size_t)kPrimStride * t8 : nullptr;
-#else
-      const uint64_t *pm_tile = nullptr;
-#endif
       const col c = trace_from<STATS, CULL, MANYL, SMALL, PLANES, PARK>(S, eye, ray, mkc(1.0f, 1.0f, 1.0f),
                                                                   mkc(0.0f, 0.0f, 0.0f), 0, P.depth, rd, lut, cnt,
                                                                   valid, park, parked, pm_tile);
@@ -1717,22 +1676,18 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
       }
       out = fin;
     }
-#if RFX_WAVE_TILES
     // output coordinates again, from the tile index in LDS (volatile: re-read, not kept live)
     const uint32_t t8e = ((volatile uint32_t *)s_tile8)[wv];
     uint32_t le = lane;
     asm volatile("" : "+v"(le));  // a fresh lane value: its row/column are recomputed, not kept live
     const uint32_t x0e = (t8e % w8) * 8u, row0e = (t8e / w8) * 8u + (P.nranks > 1 ? 0u : P.row0);
     const uint32_t xe = x0e + (le & 7u), rowe = row0e + (le >> 3), wslot = wv;
-#else
-    const uint32_t xe = x, rowe = orow, le = lane, x0e = 0, row0e = 0, wslot = wave;
-#endif
     if (MODE == kModeSsaa && P.accumulate && valid)                                  // Render.cpp:191-194
     {
       const float *d = P.img + ((size_t)rowe * P.W + xe) * 3;
       out = mkc(d[0] + out.r, d[1] + out.g, d[2] + out.b);
     }
-    const bool staged = RFX_WAVE_TILES && (P.W & 3u) == 0 &&
+    const bool staged = (P.W & 3u) == 0 &&
                         ((reinterpret_cast<uintptr_t>(P.img) | reinterpret_cast<uintptr_t>(P.argb)) & 15u) == 0 &&
                         __builtin_amdgcn_ballot_w64(valid && !parked) == ~0ull;
     if (staged)
@@ -1744,12 +1699,8 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
       d[0] = out.r; d[1] = out.g; d[2] = out.b;
       if (P.argb) P.argb[o] = argb(out);                                           // Render::copyImage
     }
-#if RFX_WAVE_TILES
-    if (P.tile_cost && __lane_id() == 0)  // per wave tile, located from the live pixel (x, orow)
+    if (P.tile_cost && __lane_id() == 0)  // per wave tile, from its output coordinates
       P.tile_cost[(P.nranks > 1 ? rowe : rowe - P.row0) / 8u * P.tiles_x + xe / 8u] = clock32() - s_clk0;
-#else
-    if (P.tile_cost && __lane_id() == 0) P.tile_cost[s_tile] = clock32() - s_clk0;  // one lane per wave, the last stays
-#endif
   }
   flush_counters<STATS>(P, cnt);
   RFX_PROF_FLUSH();

@@ -13,9 +13,10 @@
 //       (block preview, depth 4, sampleNum adapted from the frame time: Pulse.cpp:112-118), keys released (the
 //       camera decelerates, Camera.cpp:110-239, then still frames accumulate again).  Every completed frame is read
 //       back the way the window does it (getRenderImagePixel over the client area, linux/main.cpp:53-88) and
-//       hashed; one line per frame: "frame I execs N ms T hash H".  T is the wall time of the frame's exec() calls
-//       (the read-back excluded).  The fake clock advances TICK_US per reading, so Pulse's chunk doubling and
-//       sample adaptation are the same in both builds.
+//       hashed; one line per frame: "frame I execs N ms T hash H read R".  T is the wall time of the frame's exec()
+//       calls, R that of the window's first pixel read (which waits for the frame and copies it to the host).
+//       The fake clock advances TICK_US per reading, so Pulse's chunk doubling and sample adaptation are the same
+//       in both builds.
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -107,8 +108,13 @@ static int session(const std::string &dir, unsigned w, unsigned h, uint64_t tick
       ++execs;
       if (pulse.imageReady)
       {
+        // the window's first pixel read waits for the frame on the device and copies it back (Render::imagePixel)
+        const clk::time_point t1 = clk::now();
+        (void)pulse.getRenderImagePixel(0, 0);
+        const double read_ms = std::chrono::duration<double, std::milli>(clk::now() - t1).count();
         const uint64_t hv = hash ? frame_hash(pulse, w, h) : 0;
-        printf("frame %d execs %ld ms %.4f hash %016llx\n", frame++, execs, ms, (unsigned long long)hv);
+        printf("frame %d execs %ld ms %.4f hash %016llx read %.4f\n", frame++, execs, ms, (unsigned long long)hv,
+               read_ms);
         fflush(stdout);
         execs = 0;
         ms = 0.0;

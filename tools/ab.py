@@ -32,7 +32,6 @@ _HIP = C.CDLL("libamdhip64.so")
 
 VARIANTS = {
     "base": [],
-    "nobvh": ["RFX_NO_BVH"],
     "nopark": ["RFX_PARK_AFTER=0"],
     "park1": ["RFX_PARK_AFTER=1"],
     "park3": ["RFX_PARK_AFTER=3"],
@@ -51,11 +50,7 @@ VARIANTS = {
     "every1": ["RFX_TILE_SORT_EVERY=1"],
     "every2": ["RFX_TILE_SORT_EVERY=2"],
     "every8": ["RFX_TILE_SORT_EVERY=8"],
-    "wgtiles": ["RFX_WAVE_TILES=0"],
     "every16": ["RFX_TILE_SORT_EVERY=16"],
-    "stack32": ["RFX_BVH_STACK16=0"],
-    "boxmargin": ["RFX_BVH_NODE_MARGIN=0"],
-    "median": ["RFX_BVH_SAH=0"],
     "qsort": ["RFX_QUEUE_SORT=1"],
     "lpt16k": ["RFX_TILE_ORDER_MIN_TILES=16384"],
     "lpt4k": ["RFX_TILE_ORDER_MIN_TILES=4096"],

@@ -25,7 +25,7 @@ def main():
     W, H = 3840, 2160
     depth = int(sys.argv[2]) if len(sys.argv) > 2 else 8
     r = ab.Runner("segs", path, scenes.get_scene(sys.argv[1] if len(sys.argv) > 1 else "synth16"), W, H, depth,
-                  1350490027)
+                  1350490027, regroup=0)  # whole traces in one kernel: every pixel's own segment count
     r.render(1)
     assert r.L.rfx_synchronize(r.r) == 0
     rgb = np.empty(W * H * 3, np.float32)
@@ -35,6 +35,7 @@ def main():
     mean, mx = t.mean(), t.max(axis=1).mean()
     hist = np.bincount(seg.astype(np.int64).ravel(), minlength=10)
     print({"segments_per_ray": float(mean), "wave_max_mean": float(mx), "loop_lane_util": float(mean / mx),
+           "alive_after": {k: int((seg > k).sum()) for k in (1, 2, 3, 4)},
            "hist": hist.tolist(), "wave_max_hist": np.bincount(t.max(axis=1).astype(np.int64), minlength=10).tolist()})
 
 
