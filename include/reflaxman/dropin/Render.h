@@ -14,6 +14,9 @@
 //     (rfx_frame_rng_rewind) and exactly the span the cursor covered is rendered into the image, as the reference
 //     would have.  Policy "span" (RFX_DROPIN_POLICY=span, or setRenderPolicy) renders each call's span as it
 //     comes.  Any chunk pattern gives the reference's images and random streams under either policy;
+//   * several GPUs of this process (RFX_DEVICES=0,1,... in the environment): frames rendered ahead with
+//     sampleNum > 0 (still frames, screenshots) are cut into row bands over the devices (rfx_group_render_frame);
+//     block previews and spans stay on the first device, which carries the random streams;
 //   * the float framebuffer (std::vector<Color> image, Render.h:10) lives in HBM and is read back on demand;
 //     imagePixel / copyImage then apply the caller's own Color::operator/ and Color::argb, as the reference.
 // Random streams: the reference seeds its two per-TU LCG streams from rand() at static init (trace_math.h:34),
@@ -46,6 +49,7 @@ class Render {
   Vector3 renderCameraEye;
 
   rfx_renderer *r = nullptr;
+  rfx_group *group = nullptr;  // RFX_DEVICES with two or more devices: r is its member 0
   void *d_image = nullptr;
   void *d_spec = nullptr;  // policy "frame": the frame being rendered ahead of the cursor
   size_t d_capacity = 0;
@@ -84,7 +88,8 @@ class Render {
   {
     if (uploaded != scene.revision())
     {
-      rfx_dropin::check(rfx_renderer_set_scene(r, scene.handle()), "rfx_renderer_set_scene");
+      rfx_dropin::check(group ? rfx_group_set_scene(group, scene.handle()) : rfx_renderer_set_scene(r, scene.handle()),
+                        "rfx_renderer_set_scene");
       uploaded = scene.revision();
     }
   }
@@ -137,7 +142,23 @@ class Render {
         additiveCounter(0), inProgress(false)
   {
     static_assert(sizeof(Color) == 3 * sizeof(float), "Color must be three floats (Color.h)");
-    rfx_dropin::check(rfx_renderer_create(&r, 0), "rfx_renderer_create");
+    std::vector<int> devs;
+    if (const char *v = getenv("RFX_DEVICES"))
+      for (const char *p = v; *p;)
+      {
+        char *e = nullptr;
+        const long d = strtol(p, &e, 10);
+        if (e == p) break;
+        devs.push_back((int)d);
+        p = *e ? e + 1 : e;
+      }
+    if (devs.size() >= 2)
+    {
+      rfx_dropin::check(rfx_group_create(&group, &devs.front(), (int)devs.size()), "rfx_group_create");
+      r = rfx_group_renderer(group, 0);
+    }
+    else
+      rfx_dropin::check(rfx_renderer_create(&r, devs.empty() ? 0 : devs[0]), "rfx_renderer_create");
     rfx_dropin::check(rfx_renderer_set_rng(r, seed_env("RFX_SPHERE_SEED", 1350490027u), seed_env("RFX_JITTER_SEED", 424238335u)),
                       "rfx_renderer_set_rng");
     whole_frame = policy_env();
@@ -147,7 +168,10 @@ class Render {
   {
     if (d_image) rfx_device_free(r, d_image);
     if (d_spec) rfx_device_free(r, d_spec);
-    rfx_renderer_destroy(r);
+    if (group)
+      rfx_group_destroy(group);
+    else
+      rfx_renderer_destroy(r);
   }
   Render(const Render &) = delete;
   Render &operator=(const Render &) = delete;
@@ -263,7 +287,10 @@ class Render {
       if (p0 > 0 || (renderSampleNum > 0 && additiveCounter > 1))
         rfx_dropin::check(rfx_memcpy_d2d(r, d_spec, d_image, (size_t)total * sizeof(float) * 3), "Render::renderNext");
       const rfx_frame f = frame_of(p0, total);
-      rfx_dropin::check(rfx_render_frame(r, &f, (float *)d_spec, nullptr, nullptr, nullptr), "Render::renderNext");
+      if (group && p0 == 0 && renderSampleNum > 0)  // the whole frame in row bands over the group's devices
+        rfx_dropin::check(rfx_group_render_frame(group, &f, (float *)d_spec, nullptr, nullptr), "Render::renderNext");
+      else
+        rfx_dropin::check(rfx_render_frame(r, &f, (float *)d_spec, nullptr, nullptr, nullptr), "Render::renderNext");
       spec_active = true;
       spec_begin = p0;
       spec_fov = camera.fov;

@@ -211,6 +211,31 @@ int rfx_frame_rng_pending(rfx_renderer *r, uint32_t *frame_start);
  * so the streams end where the reference's do (Render.cpp:136-215, trace_math.h:34-39). */
 int rfx_frame_rng_rewind(rfx_renderer *r);
 
+/* ---------------------------------------------------------------- Device groups (multi-GPU, one process)
+ * A group renders the frame of Render::renderNext (Render.cpp:136-215) on several devices of this process: row bands,
+ * one per member, each member counting its slice of the frame's random stream and pushing it to the others (the one
+ * exchange step), then emitting and tracing its band; members 1..n-1 copy their band rows into the
+ * caller's frame on member 0's device over xGMI (hipMemcpyPeerAsync).  The assembled frame is the single-GPU frame
+ * bit for bit.  Bands start equal (8-row multiples) and are re-cut from measured per-member trace times every 8
+ * frames (completed measurements only: no frame waits), unless fixed with rfx_group_set_bands.  Member 0's renderer
+ * carries the group's random streams: a frame starts every member from member 0's state, so the caller may render
+ * other frames (block preview, spans) on member 0 alone in between, and rfx_frame_rng_rewind on member 0 undoes a
+ * group frame.  For C/C++ callers without torch.distributed (dropin/Render.h: RFX_DEVICES=0,1,...); the
+ * multi-process form is reflaxman_amd/dist.py over RCCL. */
+typedef struct rfx_group rfx_group;
+int rfx_group_create(rfx_group **out, const int *devices, int n);  /* a device may repeat (one-GPU rehearsal) */
+void rfx_group_destroy(rfx_group *g);
+int rfx_group_size(const rfx_group *g);
+rfx_renderer *rfx_group_renderer(rfx_group *g, int member);       /* per-member settings (tile order, ...) */
+int rfx_group_set_scene(rfx_group *g, const rfx_scene *scene);
+/* fixed bands: bounds[0] = 0 < bounds[1] < ... < bounds[n] = height rows; bounds NULL = automatic (default) */
+int rfx_group_set_bands(rfx_group *g, uint32_t height, const uint32_t *bounds);
+int rfx_group_get_bands(const rfx_group *g, uint32_t *bounds);     /* the bands of the last frame (n + 1 rows) */
+/* One whole frame (sample_num > 0; SSAA, additive and accumulation included; the partition fields of `frame` must be
+ * rank 0 of 1 and the span the whole frame) into d_rgb / d_argb (W*H*3 floats / W*H words, or NULL) on member 0's
+ * device, ordered after and before the caller's work on `stream` (member 0's stream; NULL = its renderer's). */
+int rfx_group_render_frame(rfx_group *g, const rfx_frame *frame, float *d_rgb, uint32_t *d_argb, void *stream);
+
 /* Optional per-phase timing of rfx_render_frame with HIP events recorded on the launch stream:
  * enable, render, then read the summed device time (ms) of the RNG pre-pass and of the trace kernel
  * over the frames since the last read (synchronises; resets the sums). */

@@ -83,6 +83,14 @@ SIGNATURES = [
     ("rfx_frame_rng_discard", C.c_int, [C.c_void_p]),
     ("rfx_frame_rng_pending", C.c_int, [C.c_void_p, _u32p]),
     ("rfx_frame_rng_rewind", C.c_int, [C.c_void_p]),
+    ("rfx_group_create", C.c_int, [C.POINTER(C.c_void_p), C.POINTER(C.c_int), C.c_int]),
+    ("rfx_group_destroy", None, [C.c_void_p]),
+    ("rfx_group_size", C.c_int, [C.c_void_p]),
+    ("rfx_group_renderer", C.c_void_p, [C.c_void_p, C.c_int]),
+    ("rfx_group_set_scene", C.c_int, [C.c_void_p, C.c_void_p]),
+    ("rfx_group_set_bands", C.c_int, [C.c_void_p, C.c_uint32, _u32p]),
+    ("rfx_group_get_bands", C.c_int, [C.c_void_p, _u32p]),
+    ("rfx_group_render_frame", C.c_int, [C.c_void_p, C.POINTER(Frame), C.c_void_p, C.c_void_p, C.c_void_p]),
     ("rfx_renderer_set_timing", C.c_int, [C.c_void_p, C.c_int]),
     ("rfx_renderer_set_tile_order", C.c_int, [C.c_void_p, C.c_int]),
     ("rfx_renderer_set_prim_masks", C.c_int, [C.c_void_p, C.c_int]),

@@ -1,0 +1,418 @@
+// Multi-GPU frames from one process (include/rfx.h rfx_group_*): the frame of Render::renderNext
+// (Render.cpp:136-215) cut into row bands, one per device of the group, for C/C++ callers that have no
+// torch.distributed -- the drop-in Render (include/reflaxman/dropin/Render.h) among them.
+//
+// Per frame, on each member's stream:
+//   1. the member's random stream is set to member 0's (the caller may have rendered on member 0 alone);
+//   2. the member counts the accepted LCG triples of its 1/n slice of the frame's random stream and pushes its
+//      slice of counts to every other member (hipMemcpyPeerAsync over xGMI): the one exchange step of the
+//      partitioned pre-pass, n x ~1K words;
+//   3. once every slice has arrived, it emits the randDirs of its band and traces the band
+//      (rfx_render_frame_counted_ev with the band partition of rfx_frame);
+//   4. members 1..n-1 copy their band rows into the caller's frame on member 0's device (peer copies), and the
+//      caller's stream waits for them.
+// The bands start equal (multiples of 8 rows) and are re-cut from the measured per-member trace times every
+// kBalanceEvery frames (the frame's cumulative cost cut into n equal parts, as reflaxman_amd/dist.py
+// balanced_bounds), reading only events that have already completed: no frame waits for a measurement.
+// The assembled frame equals the single-GPU frame bit for bit (tests/test_gpu_group.py).
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "rfx_internal.h"
+
+namespace {
+constexpr int kBalanceEvery = 8;
+constexpr uint32_t kGrain = 8;
+
+int hip_fail(hipError_t e, const char *what)
+{
+  return rfx_detail_fail(RFX_ERR_HIP, (std::string(what) + ": " + hipGetErrorString(e)).c_str());
+}
+#define GCHECK(expr)                                  \
+  do {                                                \
+    hipError_t e_ = (expr);                           \
+    if (e_ != hipSuccess) return hip_fail(e_, #expr); \
+  } while (0)
+#define RCHECK(expr)             \
+  do {                           \
+    int rc_ = (expr);            \
+    if (rc_ != RFX_OK) return rc_; \
+  } while (0)
+
+// strictly increasing bounds, each band at least `grain` rows where the frame allows it (dist.py _fix_bounds)
+std::vector<uint32_t> fix_bounds(std::vector<double> b, uint32_t H, uint32_t grain)
+{
+  const size_t n = b.size() - 1;
+  const uint32_t g = H >= grain * n ? grain : 1;
+  std::vector<uint32_t> out(n + 1);
+  out[0] = 0;
+  for (size_t r = 1; r < n; ++r)
+  {
+    double y = std::max(b[r], (double)out[r - 1] + g);
+    y = std::min(y, (double)H - (double)g * (n - r));
+    out[r] = (uint32_t)y;
+  }
+  out[n] = H;
+  return out;
+}
+
+std::vector<uint32_t> equal_bounds(uint32_t H, size_t n)
+{
+  std::vector<double> b(n + 1);
+  for (size_t r = 0; r <= n; ++r) b[r] = r == n ? H : std::round((double)H * r / n / kGrain) * kGrain;
+  return fix_bounds(b, H, kGrain);
+}
+
+// cut the frame's cumulative cost (band r's density time / rows, uniform over its rows) into n equal parts
+std::vector<uint32_t> balanced_bounds(const std::vector<uint32_t> &bounds, const std::vector<double> &t, uint32_t H)
+{
+  const size_t n = bounds.size() - 1;
+  std::vector<double> rows(n), dens(n);
+  double known = 0.0;
+  int nk = 0;
+  for (size_t r = 0; r < n; ++r)
+  {
+    rows[r] = bounds[r + 1] - bounds[r];
+    if (rows[r] > 0 && t[r] > 0) { known += t[r] / rows[r]; ++nk; }
+  }
+  const double mean = nk ? known / nk : 1.0;
+  double total = 0.0;
+  for (size_t r = 0; r < n; ++r)
+  {
+    dens[r] = rows[r] > 0 && t[r] > 0 ? t[r] / rows[r] : mean;
+    total += dens[r] * rows[r];
+  }
+  std::vector<double> out(n + 1);
+  out[0] = 0;
+  size_t r = 0;
+  double acc = 0.0;
+  for (size_t k = 1; k < n; ++k)
+  {
+    const double target = total * k / n;
+    while (r < n - 1 && acc + dens[r] * rows[r] < target) { acc += dens[r] * rows[r]; ++r; }
+    out[k] = std::round((bounds[r] + (target - acc) / dens[r]) / kGrain) * kGrain;
+  }
+  out[n] = H;
+  return fix_bounds(out, H, kGrain);
+}
+}  // namespace
+
+struct rfx_group {
+  std::vector<int> dev;
+  std::vector<rfx_renderer *> r;
+  std::vector<hipStream_t> own;                  // members 1..n-1: their streams (member 0: the caller's)
+  std::vector<uint32_t *> cnt[2];                // per member: n x bps count words, double-buffered by frame parity
+  uint64_t cnt_words = 0, bps = 0;
+  std::vector<float *> rgb;                      // members 1..n-1: whole-frame scratch (their band rows written)
+  std::vector<uint32_t *> argb;
+  size_t px_cap = 0;
+  std::vector<hipEvent_t> ev_start, ev_cnt, ev_emit[2], ev_t1, ev_done;
+  std::vector<uint32_t> bounds;
+  bool fixed = false;
+  uint32_t W = 0, H = 0;
+  uint64_t frames = 0;
+  std::vector<double> acc;                       // balancing: summed trace ms per member
+  int acc_frames = 0;
+  bool timing_pending = false;
+  int timing_parity = 0;
+  size_t n() const { return r.size(); }
+};
+
+static void destroy(rfx_group *g)
+{
+  for (size_t i = 0; i < g->dev.size(); ++i)
+  {
+    (void)hipSetDevice(g->dev[i]);
+    if (i < g->own.size() && g->own[i]) (void)hipStreamSynchronize(g->own[i]);
+  }
+  for (size_t i = 0; i < g->dev.size(); ++i)
+  {
+    (void)hipSetDevice(g->dev[i]);
+    for (int b = 0; b < 2; ++b)
+      if (i < g->cnt[b].size()) (void)hipFree(g->cnt[b][i]);
+    if (i < g->rgb.size()) (void)hipFree(g->rgb[i]);
+    if (i < g->argb.size()) (void)hipFree(g->argb[i]);
+    for (std::vector<hipEvent_t> *v : {&g->ev_start, &g->ev_cnt, &g->ev_emit[0], &g->ev_emit[1], &g->ev_t1, &g->ev_done})
+      if (i < v->size() && (*v)[i]) (void)hipEventDestroy((*v)[i]);
+    if (i < g->own.size() && g->own[i]) (void)hipStreamDestroy(g->own[i]);
+  }
+  for (rfx_renderer *r : g->r) rfx_renderer_destroy(r);
+  delete g;
+}
+
+extern "C" void rfx_group_destroy(rfx_group *g)
+{
+  if (g) destroy(g);
+}
+
+static int create(rfx_group *g, const int *devices, int n)
+{
+  for (int i = 0; i < n; ++i)
+  {
+    rfx_renderer *r = nullptr;
+    RCHECK(rfx_renderer_create(&r, devices[i]));
+    g->r.push_back(r);
+    g->dev.push_back(devices[i]);
+  }
+  // peer access between distinct devices (band and count copies over xGMI)
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j)
+    {
+      if (g->dev[i] == g->dev[j]) continue;
+      int can = 0;
+      GCHECK(hipDeviceCanAccessPeer(&can, g->dev[i], g->dev[j]));
+      if (!can) continue;  // hipMemcpyPeerAsync still works, staged by the runtime
+      GCHECK(hipSetDevice(g->dev[i]));
+      const hipError_t e = hipDeviceEnablePeerAccess(g->dev[j], 0);
+      if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) return hip_fail(e, "hipDeviceEnablePeerAccess");
+      (void)hipGetLastError();
+    }
+  for (int i = 0; i < n; ++i)
+  {
+    GCHECK(hipSetDevice(g->dev[i]));
+    hipStream_t s = nullptr;
+    if (i > 0) GCHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    g->own.push_back(s);
+    hipEvent_t e[6];
+    for (hipEvent_t &x : e) GCHECK(hipEventCreate(&x));
+    g->ev_start.push_back(e[0]);
+    g->ev_cnt.push_back(e[1]);
+    g->ev_emit[0].push_back(e[2]);
+    g->ev_emit[1].push_back(e[3]);
+    g->ev_t1.push_back(e[4]);
+    g->ev_done.push_back(e[5]);
+    // the double-buffer waits of the first two frames find recorded events
+    hipStream_t st = i > 0 ? s : rfx_detail_stream(g->r[0]);
+    GCHECK(hipEventRecord(e[2], st));
+    GCHECK(hipEventRecord(e[3], st));
+    g->cnt[0].push_back(nullptr);
+    g->cnt[1].push_back(nullptr);
+    g->rgb.push_back(nullptr);
+    g->argb.push_back(nullptr);
+  }
+  g->acc.assign(n, 0.0);
+  return RFX_OK;
+}
+
+extern "C" int rfx_group_create(rfx_group **out, const int *devices, int n)
+{
+  if (!out || !devices || n <= 0 || n > 64) return rfx_detail_fail(RFX_ERR_ARG, "group_create: 1..64 devices");
+  *out = nullptr;
+  rfx_group *g = new rfx_group();
+  const int rc = create(g, devices, n);
+  if (rc != RFX_OK)
+  {
+    destroy(g);
+    return rc;
+  }
+  *out = g;
+  return RFX_OK;
+}
+
+extern "C" int rfx_group_size(const rfx_group *g) { return g ? (int)g->n() : 0; }
+
+extern "C" rfx_renderer *rfx_group_renderer(rfx_group *g, int i)
+{
+  return g && i >= 0 && (size_t)i < g->n() ? g->r[i] : nullptr;
+}
+
+extern "C" int rfx_group_set_scene(rfx_group *g, const rfx_scene *s)
+{
+  if (!g || !s) return rfx_detail_fail(RFX_ERR_ARG, "group_set_scene: bad args");
+  for (rfx_renderer *r : g->r) RCHECK(rfx_renderer_set_scene(r, s));
+  return RFX_OK;
+}
+
+extern "C" int rfx_group_set_bands(rfx_group *g, uint32_t height, const uint32_t *bounds)
+{
+  if (!g) return rfx_detail_fail(RFX_ERR_ARG, "group_set_bands: null group");
+  if (!bounds)
+  {
+    g->fixed = false;
+    g->bounds.clear();
+    return RFX_OK;
+  }
+  const size_t n = g->n();
+  if (bounds[0] != 0 || bounds[n] != height) return rfx_detail_fail(RFX_ERR_ARG, "group_set_bands: 0 .. height");
+  for (size_t i = 0; i < n; ++i)
+    if (bounds[i] >= bounds[i + 1]) return rfx_detail_fail(RFX_ERR_ARG, "group_set_bands: bands must be non-empty");
+  g->bounds.assign(bounds, bounds + n + 1);
+  g->fixed = true;
+  g->H = height;
+  return RFX_OK;
+}
+
+extern "C" int rfx_group_get_bands(const rfx_group *g, uint32_t *bounds)
+{
+  if (!g || !bounds) return rfx_detail_fail(RFX_ERR_ARG, "group_get_bands: bad args");
+  if (g->bounds.empty()) return rfx_detail_fail(RFX_ERR_STATE, "group_get_bands: no frame rendered yet");
+  std::copy(g->bounds.begin(), g->bounds.end(), bounds);
+  return RFX_OK;
+}
+
+// the last frame's per-member trace times, once all are complete (never waits): every kBalanceEvery frames re-cut
+static int collect_times(rfx_group *g)
+{
+  if (!g->timing_pending || g->fixed) return RFX_OK;
+  const size_t n = g->n();
+  for (size_t i = 0; i < n; ++i)
+  {
+    GCHECK(hipSetDevice(g->dev[i]));
+    if (hipEventQuery(g->ev_t1[i]) != hipSuccess) return RFX_OK;  // not yet: try after the next frame
+  }
+  g->timing_pending = false;
+  for (size_t i = 0; i < n; ++i)
+  {
+    float ms = 0.0f;
+    GCHECK(hipSetDevice(g->dev[i]));
+    GCHECK(hipEventElapsedTime(&ms, g->ev_emit[g->timing_parity][i], g->ev_t1[i]));
+    g->acc[i] += ms;
+  }
+  if (++g->acc_frames >= kBalanceEvery)
+  {
+    g->bounds = balanced_bounds(g->bounds, g->acc, g->H);
+    g->acc.assign(n, 0.0);
+    g->acc_frames = 0;
+  }
+  return RFX_OK;
+}
+
+static int ensure_buffers(rfx_group *g, const rfx_frame &f0)
+{
+  const size_t n = g->n();
+  uint64_t bps = 0;
+  RCHECK(rfx_frame_rng_blocks(g->r[0], &f0, (uint32_t)n, &bps));
+  g->bps = bps;
+  if (bps * n > g->cnt_words)
+  {
+    for (size_t i = 0; i < n; ++i)
+    {
+      GCHECK(hipSetDevice(g->dev[i]));
+      GCHECK(hipDeviceSynchronize());  // frames still in flight read the old arrays
+      for (int b = 0; b < 2; ++b)
+      {
+        (void)hipFree(g->cnt[b][i]);
+        g->cnt[b][i] = nullptr;
+        GCHECK(hipMalloc(&g->cnt[b][i], bps * n * sizeof(uint32_t)));
+      }
+    }
+    g->cnt_words = bps * n;
+  }
+  const size_t px = (size_t)f0.width * f0.height;
+  if (px > g->px_cap)
+  {
+    for (size_t i = 1; i < n; ++i)
+    {
+      GCHECK(hipSetDevice(g->dev[i]));
+      GCHECK(hipStreamSynchronize(g->own[i]));
+      (void)hipFree(g->rgb[i]); (void)hipFree(g->argb[i]);
+      g->rgb[i] = nullptr; g->argb[i] = nullptr;
+      GCHECK(hipMalloc(&g->rgb[i], px * 3 * sizeof(float)));
+      GCHECK(hipMalloc(&g->argb[i], px * sizeof(uint32_t)));
+    }
+    g->px_cap = px;
+  }
+  return RFX_OK;
+}
+
+extern "C" int rfx_group_render_frame(rfx_group *g, const rfx_frame *f, float *d_rgb, uint32_t *d_argb, void *stream)
+{
+  if (!g || !f || !d_rgb) return rfx_detail_fail(RFX_ERR_ARG, "group_render_frame: bad args");
+  const size_t n = g->n();
+  const uint32_t W = f->width, H = f->height;
+  const uint64_t npx = (uint64_t)W * H;
+  if (f->sample_num <= 0 || (f->nranks > 1) || !((f->pixel_begin == 0 && f->pixel_end == 0) ||
+                                                  (f->pixel_begin == 0 && f->pixel_end == npx)))
+    return rfx_detail_fail(RFX_ERR_ARG, "group_render_frame: a whole frame with sample_num > 0 (no partition fields)");
+  hipStream_t s0 = stream ? (hipStream_t)stream : rfx_detail_stream(g->r[0]);
+  if (n == 1 || H < n)
+    return rfx_render_frame(g->r[0], f, d_rgb, d_argb, nullptr, s0);
+  if (W != g->W || H != g->H || g->bounds.size() != n + 1)
+  {
+    if (g->fixed && H != g->H) return rfx_detail_fail(RFX_ERR_ARG, "group_render_frame: fixed bands of another height");
+    if (!g->fixed) g->bounds = equal_bounds(H, n);
+    g->W = W;
+    g->H = H;
+    g->acc.assign(n, 0.0);
+    g->acc_frames = 0;
+    g->timing_pending = false;
+  }
+  RCHECK(collect_times(g));
+  std::vector<rfx_frame> fr(n, *f);
+  for (size_t i = 0; i < n; ++i)
+  {
+    fr[i].row_block = 0;
+    fr[i].rank = (uint32_t)i;
+    fr[i].nranks = (uint32_t)n;
+    fr[i].pixel_begin = (uint64_t)g->bounds[i] * W;
+    fr[i].pixel_end = (uint64_t)g->bounds[i + 1] * W;
+  }
+  RCHECK(ensure_buffers(g, fr[0]));
+  const int b = (int)(g->frames & 1);
+  const bool accumulate = f->additive_counter > 1;
+  std::vector<hipStream_t> st(n);
+  for (size_t i = 0; i < n; ++i) st[i] = i ? g->own[i] : s0;
+  // 0. after the caller's work on its stream; member 0's stream state is the group's
+  GCHECK(hipSetDevice(g->dev[0]));
+  GCHECK(hipEventRecord(g->ev_start[0], s0));
+  const uint32_t jitter = rfx_detail_jitter(g->r[0]);
+  for (size_t i = 1; i < n; ++i)
+  {
+    GCHECK(hipSetDevice(g->dev[i]));
+    GCHECK(hipStreamWaitEvent(st[i], g->ev_start[0], 0));
+    GCHECK(hipMemcpyPeerAsync(rfx_detail_seed_word(g->r[i]), g->dev[i], rfx_detail_seed_word(g->r[0]), g->dev[0],
+                              sizeof(uint32_t), st[i]));
+    rfx_detail_set_jitter(g->r[i], jitter);
+  }
+  // 1. each member counts its slice of the frame's random stream and pushes it to every other member
+  const size_t sl = g->bps * sizeof(uint32_t);
+  for (size_t i = 0; i < n; ++i)
+  {
+    RCHECK(rfx_frame_rng_count(g->r[i], &fr[i], (uint32_t)i, (uint32_t)n, g->cnt[b][i], st[i]));
+    GCHECK(hipSetDevice(g->dev[i]));
+    for (size_t j = 0; j < n; ++j)
+    {
+      if (j == i) continue;
+      GCHECK(hipStreamWaitEvent(st[i], g->ev_emit[b][j], 0));  // j's emit of two frames ago read this array
+      GCHECK(hipMemcpyPeerAsync(g->cnt[b][j] + i * g->bps, g->dev[j], g->cnt[b][i] + i * g->bps, g->dev[i], sl, st[i]));
+    }
+    GCHECK(hipEventRecord(g->ev_cnt[i], st[i]));
+  }
+  // 2. every slice arrived: emit the band's randDirs and trace the band; 3. bands to the caller's frame
+  for (size_t i = 0; i < n; ++i)
+  {
+    GCHECK(hipSetDevice(g->dev[i]));
+    for (size_t j = 0; j < n; ++j)
+      if (j != i) GCHECK(hipStreamWaitEvent(st[i], g->ev_cnt[j], 0));
+    const uint64_t y0 = g->bounds[i], rows = g->bounds[i + 1] - y0;
+    float *img = i ? g->rgb[i] : d_rgb;
+    uint32_t *a = i ? (d_argb ? g->argb[i] : nullptr) : d_argb;
+    if (accumulate && i)  // the accumulated rows this member adds to (Render.cpp:191-194)
+      GCHECK(hipMemcpyPeerAsync(img + y0 * W * 3, g->dev[i], d_rgb + y0 * W * 3, g->dev[0], rows * W * 12, st[i]));
+    const uint32_t j0 = rfx_detail_jitter(g->r[i]);
+    RCHECK(rfx_render_frame_counted_ev(g->r[i], &fr[i], (uint32_t)n, g->cnt[b][i], img, a, nullptr, st[i],
+                                       g->ev_emit[b][i]));
+    rfx_detail_set_rewindable(g->r[i], j0);
+    GCHECK(hipSetDevice(g->dev[i]));
+    GCHECK(hipEventRecord(g->ev_t1[i], st[i]));
+    if (i)
+    {
+      GCHECK(hipMemcpyPeerAsync(d_rgb + y0 * W * 3, g->dev[0], img + y0 * W * 3, g->dev[i], rows * W * 12, st[i]));
+      if (d_argb)
+        GCHECK(hipMemcpyPeerAsync(d_argb + y0 * W, g->dev[0], a + y0 * W, g->dev[i], rows * W * 4, st[i]));
+      GCHECK(hipEventRecord(g->ev_done[i], st[i]));
+    }
+  }
+  GCHECK(hipSetDevice(g->dev[0]));
+  for (size_t i = 1; i < n; ++i) GCHECK(hipStreamWaitEvent(s0, g->ev_done[i], 0));
+  g->timing_parity = b;
+  g->timing_pending = true;
+  ++g->frames;
+  return RFX_OK;
+}

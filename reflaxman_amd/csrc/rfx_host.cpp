@@ -1804,3 +1804,18 @@ extern "C" int rfx_kat_argb(rfx_renderer *r, const float *rgb, uint64_t n, uint3
   if (!r || (n && (!rgb || !out))) return fail(RFX_ERR_ARG, "kat_argb: bad args");
   return kat_run(r, 3, 0, rgb, (size_t)n * 3, nullptr, n, out, (size_t)n);
 }
+
+// ============================================================== internals shared with rfx_group.cpp (rfx_internal.h)
+int rfx_detail_fail(int code, const char *msg) { return fail(code, "%s", msg); }
+uint32_t *rfx_detail_seed_word(rfx_renderer *r) { return seed_cur(r); }
+uint32_t rfx_detail_jitter(const rfx_renderer *r) { return r->jitter_seed; }
+void rfx_detail_set_jitter(rfx_renderer *r, uint32_t jitter) { r->jitter_seed = jitter; }
+hipStream_t rfx_detail_stream(const rfx_renderer *r) { return r->stream; }
+// the last call on r was a counted frame (one pre-pass flip, jitter advanced from jitter0): rfx_frame_rng_rewind
+// may undo it, as after rfx_render_frame
+void rfx_detail_set_rewindable(rfx_renderer *r, uint32_t jitter0)
+{
+  r->rewind_ok = true;
+  r->rewind_flip = true;
+  r->rewind_jitter = jitter0;
+}

@@ -49,12 +49,28 @@ def test_pulse_screenshot_matches_reference(tmp_path):
     assert hashlib.sha256(data).hexdigest() == c["sha_bmp"]
 
 
-def run_session(tmp_path, c, policy, hash_frames=True):
+@pytest.mark.gpu
+def test_pulse_screenshot_on_a_device_group(tmp_path):
+    """The same screenshot with the drop-in's frames cut into row bands over a group of 3 members (RFX_DEVICES; all
+    device 0 on the one-GPU box): byte-identical BMP."""
+    c = manifest()["cases"]["pulse_screenshot_800x600_ss2"]
+    if not os.path.exists(DROPIN):
+        pytest.fail("tests/native/_build/pulse_dropin missing: run __graft_entry__.build() where /root/reference exists")
+    env = {**os.environ, "RFX_SPHERE_SEED": str(c["RFX_SPHERE_SEED"]), "RFX_JITTER_SEED": str(c["RFX_JITTER_SEED"]),
+           "RFX_DEVICES": "0,0,0"}
+    r = subprocess.run([DROPIN, str(tmp_path) + "/", str(c["res_key"]), str(c["ss_key"])], capture_output=True,
+                       text=True, env=env, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    data = open(r.stdout.strip(), "rb").read()
+    assert hashlib.sha256(data).hexdigest() == c["sha_bmp"]
+
+
+def run_session(tmp_path, c, policy, hash_frames=True, devices=None):
     """The interactive session of tests/native/pulse_headless.cpp through the drop-in; returns the parsed frame lines."""
     if not os.path.exists(DROPIN):
         pytest.fail("tests/native/_build/pulse_dropin missing: run __graft_entry__.build() where /root/reference exists")
     env = {**os.environ, "RFX_SPHERE_SEED": str(c["RFX_SPHERE_SEED"]), "RFX_JITTER_SEED": str(c["RFX_JITTER_SEED"]),
-           "RFX_DROPIN_POLICY": policy}
+           "RFX_DROPIN_POLICY": policy, **({"RFX_DEVICES": devices} if devices else {})}
     cmd = [DROPIN, str(tmp_path) + "/", "session", str(c["W"]), str(c["H"]), str(c["tick_us"])]
     r = subprocess.run(cmd + ([] if hash_frames else ["nohash"]), capture_output=True, text=True, env=env, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
@@ -76,3 +92,13 @@ def test_pulse_interactive_session_matches_reference(tmp_path, tick, policy):
     frames = run_session(tmp_path, c, policy)
     assert [f[7] for f in frames] == c["hashes"]
     assert [int(f[3]) for f in frames] == c["execs"]
+
+
+@pytest.mark.gpu
+def test_pulse_interactive_session_on_a_device_group(tmp_path):
+    """The interactive session with RFX_DEVICES=0,0 (a 2-member group on the one-GPU box): the still frames
+    (sampleNum 1, additive: accumulation over the group's bands) go through rfx_group_render_frame, the motion frames
+    (block preview) and the settled abandoned frame through member 0; every frame hashes to the reference's."""
+    c = manifest()["cases"]["pulse_session_640x480_tick2000"]
+    frames = run_session(tmp_path, c, "frame", devices="0,0")
+    assert [f[7] for f in frames] == c["hashes"]

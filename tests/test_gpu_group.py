@@ -1,0 +1,151 @@
+"""Device groups (include/rfx.h rfx_group_*): the multi-GPU frame for C/C++ callers, one process driving several
+devices.  On the one-GPU box every member is device 0 (n renderers, n streams, the same peer copies); the frames must
+equal a single renderer's bit for bit over a run of frames -- the random stream carried across them
+(trace_math.h:34-39), bands re-cut by the balancer, SSAA and additive accumulation (Render.cpp:174-194), frames on
+member 0 alone in between and a rewound frame -- and C4's first frame equals the reference's SHA-256.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from helpers import manifest, sha
+from reflaxman_amd import _lib, scenes
+
+pytestmark = pytest.mark.gpu
+SEED = 1350490027
+
+
+class Group:
+    def __init__(self, n, scene):
+        self.L = _lib.load()
+        self.g = C.c_void_p()
+        devs = (C.c_int * n)(*([0] * n))
+        _lib.check(self.L.rfx_group_create(C.byref(self.g), devs, n), "group_create")
+        _lib.check(self.L.rfx_group_set_scene(self.g, scene._h), "group_set_scene")
+        self.r0 = C.c_void_p(self.L.rfx_group_renderer(self.g, 0))
+        _lib.check(self.L.rfx_renderer_set_rng(self.r0, SEED, 7))
+        self.n = n
+
+    def render(self, f, rgb, argb):
+        _lib.check(self.L.rfx_group_render_frame(self.g, C.byref(f), C.c_void_p(rgb.data_ptr()),
+                                                 C.c_void_p(argb.data_ptr()), None), "group_render_frame")
+
+    def bands(self):
+        b = (C.c_uint32 * (self.n + 1))()
+        _lib.check(self.L.rfx_group_get_bands(self.g, b))
+        return list(b)
+
+    def close(self):
+        self.L.rfx_group_destroy(self.g)
+
+
+def _single(scene):
+    from reflaxman_amd.render import Renderer
+    r = Renderer(sphere_seed=SEED, jitter_seed=7)
+    r.set_scene(scene)
+    return r
+
+
+def _bufs(torch, W, H):
+    return (torch.zeros(H * W * 3, dtype=torch.float32, device="cuda"),
+            torch.zeros(H * W, dtype=torch.int32, device="cuda"))
+
+
+def test_group_frames_equal_single_gpu_over_a_run():
+    """4 members, 12 plain frames of the C3 scene at 1920x1080 d8: every frame equals the single renderer's; the
+    balancer has re-cut the bands by the end."""
+    import torch
+    from reflaxman_amd.render import build_scene, make_frame
+    scene, cam = build_scene(scenes.get_scene("synth16"))
+    W, H = 1920, 1080
+    g, one = Group(4, scene), _single(scene)
+    f = make_frame(cam, W, H, 8, 1)
+    rgb, argb = _bufs(torch, W, H)
+    rgb1, argb1 = _bufs(torch, W, H)
+    seen = set()
+    for i in range(12):
+        g.render(f, rgb, argb)
+        one.render_frame(f, rgb1.data_ptr(), argb1.data_ptr())
+        torch.cuda.synchronize()
+        seen.add(tuple(g.bands()))
+        assert torch.equal(rgb, rgb1) and torch.equal(argb, argb1), i
+    assert len(seen) >= 2, seen  # the equal cut, then a balanced one
+    b = g.bands()
+    assert b[0] == 0 and b[-1] == H and all(b[k] < b[k + 1] for k in range(4))
+    g.close()
+    one.close()
+
+
+def test_group_ssaa_additive_and_member0_frames():
+    """SSAA 2x2 additive frames (jitter stream, accumulation over 3 frames), a block preview and a cursor span on
+    member 0 alone in between, and a rewound group frame: the same images and streams as one renderer."""
+    import torch
+    from reflaxman_amd.render import build_scene, make_frame
+    scene, cam = build_scene(scenes.get_scene("default"))
+    W, H = 320, 240
+    g, one = Group(3, scene), _single(scene)
+    rgb, argb = _bufs(torch, W, H)
+    rgb1, argb1 = _bufs(torch, W, H)
+    L = _lib.load()
+
+    def both(f, group=True):
+        if group:
+            g.render(f, rgb, argb)
+        else:
+            _lib.check(L.rfx_render_frame(g.r0, C.byref(f), C.c_void_p(rgb.data_ptr()), C.c_void_p(argb.data_ptr()),
+                                          None, None))
+        one.render_frame(f, rgb1.data_ptr(), argb1.data_ptr())
+        torch.cuda.synchronize()
+        return torch.equal(rgb, rgb1) and torch.equal(argb, argb1)
+
+    for k in range(1, 4):  # Render::renderBegin(additive): additiveCounter 1, 2, 3
+        assert both(make_frame(cam, W, H, 4, 2, additive=True, additive_counter=k)), k
+    assert both(make_frame(cam, W, H, 4, -4), group=False)                       # block preview on member 0
+    assert both(make_frame(cam, W, H, 4, 1, pixel_begin=0, pixel_end=777), group=False)  # a cursor span
+    f = make_frame(cam, W, H, 6, 1)
+    assert both(f)
+    # rewind the group frame (member 0 carries the stream) and render it again: the same frame
+    _lib.check(L.rfx_frame_rng_rewind(g.r0))
+    first = (rgb.clone(), argb.clone())
+    g.render(f, rgb, argb)
+    torch.cuda.synchronize()
+    assert torch.equal(rgb, first[0]) and torch.equal(argb, first[1])
+    assert both(f)  # and the stream continues as the single renderer's after it
+    s0, s1 = C.c_uint32(), C.c_uint32()
+    _lib.check(L.rfx_renderer_get_rng(g.r0, C.byref(s0), None))
+    s1 = one.get_rng()[0]
+    assert s0.value == s1
+    g.close()
+    one.close()
+
+
+def test_group_c4_fixed_bands_reference_hash():
+    """C4 (7680x4320 d8) on 8 members with fixed uneven bands: SHA-256 of the frame equals the reference's."""
+    import torch
+    from reflaxman_amd.render import build_scene, make_frame
+    c = manifest()["cases"]["hash_synth16_7680x4320_d8"]
+    scene, cam = build_scene(scenes.get_scene("synth16"))
+    W, H = c["W"], c["H"]
+    g = Group(8, scene)
+    bounds = (C.c_uint32 * 9)(0, 600, 1096, 1600, 2160, 2704, 3240, 3800, H)
+    _lib.check(g.L.rfx_group_set_bands(g.g, H, bounds))
+    rgb, argb = _bufs(torch, W, H)
+    g.render(make_frame(cam, W, H, c["depth"], 1), rgb, argb)
+    torch.cuda.synchronize()
+    assert g.bands() == list(bounds)
+    assert sha(argb.cpu().numpy().view(np.uint32)) == c["sha_argb"]
+    assert sha(rgb.cpu().numpy()) == c["sha_f32"]
+    g.close()
+
+
+def test_group_rejects_block_preview_and_partitions():
+    import torch
+    from reflaxman_amd.render import build_scene, make_frame
+    scene, cam = build_scene(scenes.get_scene("default"))
+    g = Group(2, scene)
+    rgb, argb = _bufs(torch, 64, 48)
+    for f in (make_frame(cam, 64, 48, 4, -2), make_frame(cam, 64, 48, 4, 1, pixel_begin=0, pixel_end=100),
+              make_frame(cam, 64, 48, 4, 1, row_block=8, rank=0, nranks=2)):
+        assert g.L.rfx_group_render_frame(g.g, C.byref(f), C.c_void_p(rgb.data_ptr()), None, None) == -1
+    g.close()
