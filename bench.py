@@ -478,21 +478,47 @@ def main():
 
     e2e = None
     if world == 1:
-        # end to end with the frame handed back to the host (pinned buffers, PCIe D2H of the f32 RGB and
-        # ARGB8 frames): reported beside `value`, never as it
-        h_rgb = torch.empty(img.numel(), dtype=img.dtype, pin_memory=True)
-        h_argb = torch.empty(argb.numel(), dtype=argb.dtype, pin_memory=True)
-        n_e2e = min(args.steps, 5)
+        # end to end with the frame handed back to the host: reported beside `value`, never as it.
+        # (1) the display path: the ARGB8 plane (what a window shows, Pulse.cpp:455-458) of frame i copied to pinned
+        #     host memory on a copy stream while frame i + 1 renders into the other of two device frame sets;
+        # (2) both planes (f32 RGB + ARGB8) copied after each frame, serially.
+        n_e2e = min(args.steps, 10)
+        sets = [(img, argb), (torch.empty_like(img), torch.empty_like(argb))]
+        h_argb = [torch.empty(argb.numel(), dtype=argb.dtype, pin_memory=True) for _ in range(2)]
+        copy = torch.cuda.Stream(device=dev)
+        done = [torch.cuda.Event(), torch.cuda.Event()]
+        copied = [torch.cuda.Event(), torch.cuda.Event()]
+        for e in done + copied:
+            e.record(stream)
         torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for i in range(n_e2e):
+            k = i % 2
+            stream.wait_event(copied[k])  # set k's last frame has reached the host
+            rr.render_frame(frame, sets[k][0].data_ptr(), sets[k][1].data_ptr(), 0, stream.cuda_stream)
+            done[k].record(stream)
+            copy.wait_event(done[k])
+            with torch.cuda.stream(copy):
+                h_argb[k].copy_(sets[k][1], non_blocking=True)
+            copied[k].record(copy)
+        torch.cuda.synchronize()
+        ovl_s = (time.perf_counter() - t1) / n_e2e
+        h_rgb = torch.empty(img.numel(), dtype=img.dtype, pin_memory=True)
+        h_argb1 = torch.empty(argb.numel(), dtype=argb.dtype, pin_memory=True)
         t1 = time.perf_counter()
         for _ in range(n_e2e):
             step()
             h_rgb.copy_(img, non_blocking=True)
-            h_argb.copy_(argb, non_blocking=True)
+            h_argb1.copy_(argb, non_blocking=True)
             torch.cuda.current_stream().synchronize()
         e2e_s = (time.perf_counter() - t1) / n_e2e
-        e2e = {"ms_per_frame": round(e2e_s * 1e3, 4), "Mrays_per_s": round(traces / e2e_s / 1e6, 2),
-               "d2h_bytes_per_frame": int(img.numel() * 4 + argb.numel() * 4), "frames": n_e2e}
+        e2e = {"ms_per_frame": round(ovl_s * 1e3, 4), "Mrays_per_s": round(traces / ovl_s / 1e6, 2),
+               "d2h_bytes_per_frame": int(argb.numel() * 4), "frames": n_e2e,
+               "kind": "ARGB8 plane to pinned host memory, frame i's copy overlapped with frame i+1's render",
+               "serial_both_planes": {"ms_per_frame": round(e2e_s * 1e3, 4),
+                                      "Mrays_per_s": round(traces / e2e_s / 1e6, 2),
+                                      "d2h_bytes_per_frame": int(img.numel() * 4 + argb.numel() * 4)}}
+        del sets
 
     if rank != 0:
         dist.destroy_process_group()

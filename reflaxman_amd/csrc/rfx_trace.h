@@ -1168,13 +1168,101 @@ __device__ __forceinline__ uint32_t queue_key(const DevScene &S, v3 o, v3 d)
   return oct << 9 | m;
 }
 
+// Per wave: the epilogue's staging of the wave's 64 pixels (store_wave_tile: 192 RGB floats + 64 ARGB words); before
+// the epilogue, the shadow pack's query slots (RFX_SHADOW_PACK)
+__shared__ __attribute__((aligned(16))) uint32_t s_out[kWgWaves][256];
+
+#ifndef RFX_SHADOW_PACK
+#define RFX_SHADOW_PACK 0
+#endif
+#if RFX_SHADOW_PACK
+// Lock-step of the workgroup's two waves (RFX_SHADOW_PACK experiment): the bounce loop runs while any lane of either
+// wave is alive (double-buffered flags by iteration parity: one barrier per iteration)
+__shared__ uint32_t s_any[2][kWgWaves];
+__shared__ uint32_t s_pack_cnt[2][kWgWaves];
+__device__ __forceinline__ bool wg_any(bool x, uint32_t &parity)
+{
+  const uint32_t wv = threadIdx.x >> 6;
+  const bool w = __ballot(x) != 0;
+  if (__lane_id() == 0) s_any[parity][wv] = w;
+  __syncthreads();
+  bool r = false;
+  for (uint32_t i = 0; i < kWgWaves; ++i) r |= s_any[parity][i] != 0;
+  parity ^= 1u;
+  return r;
+}
+
+// Shadow any-hit of a small scene with the workgroup's waves in lock-step: when the facing lanes of both waves fit one
+// wave, wave 0 runs them all on full lanes (its idle lanes take wave 1's queries through LDS) while wave 1 waits.
+template <bool PLANES>
+__device__ __forceinline__ bool shadow_pack(const DevScene &S, const CullRec *cull, v3 drop, v3 sray, bool facing,
+                                            int skip_sph, int skip_tri, int skip_pln, Cnt &cnt, uint32_t &parity)
+{
+  static_assert(kWgWaves == 2, "shadow pack: two waves per workgroup");
+  uint32_t *L = &s_out[0][0];  // 512 words: 64 queries x 7 words, then 64 result words
+  const uint32_t wv = threadIdx.x >> 6, lane = __lane_id();
+  const uint64_t fb = __ballot(facing), lt = (1ull << lane) - 1ull;
+  if (lane == 0) s_pack_cnt[parity][wv] = (uint32_t)__popcll(fb);
+  __syncthreads();
+  const uint32_t c0 = s_pack_cnt[parity][0], c1 = s_pack_cnt[parity][1];
+  parity ^= 1u;
+  bool occ = false;
+  if (!(c0 && c1 && c0 + c1 <= 64))
+  {
+    if (fb)
+    {
+      uint64_t om = S.cull_valid;
+      const Bundle SB = make_bundle(drop, sray, facing);
+      if (SB.ok) om = cull_small(cull, S.cull_valid, SB);
+      if (facing) occ = occluded_small<false, PLANES>(S, drop, sray, skip_sph, skip_tri, skip_pln, om, cnt);
+    }
+    return occ;
+  }
+  const uint32_t e = (uint32_t)__popcll(fb & lt);  // wave 1: this lane's query slot
+  if (wv == 1 && facing)
+  {
+    float *q = reinterpret_cast<float *>(L + 7 * e);
+    q[0] = drop.x; q[1] = drop.y; q[2] = drop.z; q[3] = sray.x; q[4] = sray.y; q[5] = sray.z;
+    L[7 * e + 6] = (uint32_t)(skip_sph + 1) | (uint32_t)(skip_tri + 1) << 10 | (uint32_t)(skip_pln + 1) << 20;
+  }
+  __syncthreads();
+  if (wv == 0)
+  {
+    const uint32_t k = (uint32_t)__popcll(~fb & lt);  // the k-th idle lane takes wave 1's k-th query
+    const bool borrowed = !facing && k < c1;
+    if (borrowed)
+    {
+      const float *q = reinterpret_cast<const float *>(L + 7 * k);
+      drop = mk(q[0], q[1], q[2]);
+      sray = mk(q[3], q[4], q[5]);
+      const uint32_t sk = L[7 * k + 6];
+      skip_sph = (int)(sk & 1023u) - 1;
+      skip_tri = (int)((sk >> 10) & 1023u) - 1;
+      skip_pln = (int)(sk >> 20) - 1;
+    }
+    const bool act = facing || borrowed;
+    uint64_t om = S.cull_valid;
+    const Bundle SB = make_bundle(drop, sray, act);
+    if (SB.ok) om = cull_small(cull, S.cull_valid, SB);
+    if (act) occ = occluded_small<false, PLANES>(S, drop, sray, skip_sph, skip_tri, skip_pln, om, cnt);
+    if (borrowed) L[448 + k] = occ ? 1u : 0u;
+  }
+  __syncthreads();
+  if (wv == 1 && facing) occ = L[448 + e] != 0;
+  return occ;
+}
+#endif
+
 // Scene::trace from a mid-trace state (mulc, pix after `refl` segments); park: see Park.  *parked: this lane's
 // trace was queued and its returned colour is not final.
-template <bool STATS, bool CULL, bool MANYL, bool SMALL, bool PLANES, bool PARK, class PK>
+template <bool STATS, bool CULL, bool MANYL, bool SMALL, bool PLANES, bool PARK, class PK, bool LOCK = false>
 __device__ __forceinline__ col trace_from(const DevScene &S, v3 origin, v3 ray, col mulc, col pix, int refl, int depth,
                                           v3 rd, const float *lut, Cnt &cnt, bool valid, const PK &park, bool &parked,
                                           const uint64_t *pm_tile = nullptr)
 {
+#if RFX_SHADOW_PACK
+  uint32_t lock_parity = 0, pack_parity = 0;
+#endif
   // the first segment of a plain small-scene trace: this tile's per-view masks (prim_cull_kernel) -- the closest
   // hit's, then one per light for its shadow rays
   bool seg0 = pm_tile != nullptr;
@@ -1186,7 +1274,11 @@ __device__ __forceinline__ col trace_from(const DevScene &S, v3 origin, v3 ray, 
   int nseg = 0;  // diagnostic build only (tools/segstats.py): the trace's segment count replaces its colour
 #endif
   RFX_PROF_BEGIN(P_SEG);
+#if RFX_SHADOW_PACK
+  while (LOCK ? wg_any(alive, lock_parity) : __ballot(alive) != 0)
+#else
   while (__ballot(alive))
+#endif
   {
 #ifdef RFX_DEBUG_SEGS
     if (alive) ++nseg;
@@ -1270,6 +1362,18 @@ __device__ __forceinline__ col trace_from(const DevScene &S, v3 origin, v3 ray, 
             sray = add(dtl, mul(rd, L.radius));                                  // Scene.cpp:129
           }
         }
+#if RFX_SHADOW_PACK
+        if constexpr (LOCK)
+        {
+          if (!(!MANYL && seg0 && q < kPrimLights))  // (the first segment's precomputed masks are per tile: no pack)
+          {
+            if (shadow_pack<PLANES>(S, T.cull(), drop, sray, facing, skip_sph, skip_tri, skip_pln, cnt, pack_parity))
+              facing = false;
+            if (facing) lit |= 1u << q;
+            continue;
+          }
+        }
+#endif
         if (__ballot(facing))
         {
           if constexpr (SMALL)
@@ -1528,7 +1632,6 @@ __device__ __forceinline__ uint32_t clock32()
 __device__ __forceinline__ void store_wave_tile(const FrameParams &P, uint32_t x0, uint32_t row0, col out,
                                                 uint32_t lane, uint32_t wave)
 {
-  __shared__ __attribute__((aligned(16))) uint32_t s_out[kWgWaves][256];  // 192 RGB floats + 64 ARGB words
   uint32_t *s = s_out[wave];
   s[3 * lane] = __float_as_uint(out.r);
   s[3 * lane + 1] = __float_as_uint(out.g);
@@ -1641,7 +1744,8 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
       if (valid) rd = load_rd(P, pr);
       const ParkTile park{P.park_after, P.queue, P.queue_count, P, wv, w8};
       const uint64_t *pm_tile = SMALL && CULL && !STATS && P.prim_mask ? P.prim_mask + (size_t)kPrimStride * t8 : nullptr;
-      const col c = trace_from<STATS, CULL, MANYL, SMALL, PLANES, PARK>(S, eye, ray, mkc(1.0f, 1.0f, 1.0f),
+      constexpr bool LOCK = RFX_SHADOW_PACK && SMALL && CULL && !STATS && !MANYL && !PARK;
+      const col c = trace_from<STATS, CULL, MANYL, SMALL, PLANES, PARK, ParkTile, LOCK>(S, eye, ray, mkc(1.0f, 1.0f, 1.0f),
                                                                   mkc(0.0f, 0.0f, 0.0f), 0, P.depth, rd, lut, cnt,
                                                                   valid, park, parked, pm_tile);
       out = cadd(mkc(0.0f, 0.0f, 0.0f), c);                                      // Render.cpp:185 (/ 1.0f exact)

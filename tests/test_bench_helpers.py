@@ -43,3 +43,22 @@ def test_roofline_frac_is_a_hardware_fraction():
         assert r["unit"] == "T VALU lane-op/s" and r["peak"] == 78.6
     r = metrics.roofline(None, None, 9e12, 3.35, 8294400)  # C5-like effective work: above the peak ...
     assert r["frac"] is None and r["effective_ref_flops"]["frac"] > 1  # ... but never as `frac`
+
+
+def test_no_committed_line_has_frac_above_one():
+    """Every bench line committed under profiles/ carries a hardware fraction (or null) in roofline.frac."""
+    import glob
+    import json
+    seen = 0
+    for p in glob.glob(os.path.join(ROOT, "profiles", "**", "*.json"), recursive=True):
+        text = open(p).read()
+        for chunk in [text] + text.splitlines():
+            try:
+                d = json.loads(chunk)
+            except ValueError:
+                continue
+            if isinstance(d, dict) and isinstance(d.get("roofline"), dict):
+                seen += 1
+                f = d["roofline"].get("frac")
+                assert f is None or 0 <= f <= 1, (p, f)
+    assert seen > 0
