@@ -1143,11 +1143,12 @@ __device__ __forceinline__ bool occluded(const DevScene &S, v3 o, v3 ray, bool l
 // appended to the queue instead (one atomic per wave, packed lane order) and the trace ends here; the bounce
 // kernel resumes it from exactly that state, so every float op is the same.
 struct Park {
-  int after;           // segments before parking (<= 0: never)
+  int after;            // segments before parking (<= 0: never)
   QRay *queue;
   uint32_t *count;
-  uint32_t trace, out;  // this lane's randDir trace index and output pixel
-  __device__ __forceinline__ void ids(uint32_t &t, uint32_t &o) const { t = trace; o = out; }
+  uint32_t *queue_out;  // per entry: the output pixel
+  uint32_t out;         // this lane's output pixel
+  __device__ __forceinline__ void put_out(uint32_t slot) const { queue_out[slot] = out; }
   __device__ __forceinline__ uint32_t *keys() const { return nullptr; }
 };
 
@@ -1526,11 +1527,9 @@ __device__ __forceinline__ col trace_from(const DevScene &S, v3 origin, v3 ray, 
           q.ox = origin.x; q.oy = origin.y; q.oz = origin.z; q.dx = ray.x;
           q.dy = ray.y; q.dz = ray.z; q.mr = mulc.r; q.mg = mulc.g;
           q.mb = mulc.b; q.pr = pix.r; q.pg = pix.g; q.pb = pix.b;
-          uint32_t qt, qo;
-          park.ids(qt, qo);
-          q.trace = qt; q.out = qo; q.refl = (uint32_t)refl; q.pad = 0;
           const uint32_t slot = base + (uint32_t)__popcll(pm & ((1ull << __lane_id()) - 1ull));
           park.queue[slot] = q;
+          park.put_out(slot);
           if (uint32_t *keys = park.keys()) keys[slot] = queue_key(S, origin, ray);
           parked = true;
           alive = false;
@@ -1552,7 +1551,7 @@ __device__ __forceinline__ col trace(const DevScene &S, v3 origin, v3 ray, int d
 {
   bool parked;
   return trace_from<STATS, CULL, MANYL, SMALL, PLANES, false>(S, origin, ray, mkc(1.0f, 1.0f, 1.0f), mkc(0.0f, 0.0f, 0.0f), 0,
-                                                       depth, rd, lut, cnt, valid, Park{0, nullptr, nullptr, 0, 0},
+                                                       depth, rd, lut, cnt, valid, Park{0, nullptr, nullptr, nullptr, 0},
                                                        parked);
 }
 
@@ -1582,28 +1581,35 @@ __device__ __forceinline__ uint32_t strip_row_to_y(uint32_t r, const FrameParams
 // the wave's schedule tile (index into the wave-tile grid), kept in LDS across the bounce loop
 __shared__ uint32_t s_tile8[kWgWaves];
 
-// Park info of a plain-pixel trace-kernel lane: its randDir trace index and output pixel are re-derived from the
-// wave's tile index in LDS when the trace parks (a fresh lane id through an empty asm), instead of being kept
-// live across the bounce loop (C3 park instantiation: 13 -> 2 VGPR spills)
+// Park info of a plain-pixel trace-kernel lane: its output pixel is re-derived from the wave's tile index in LDS when
+// the trace parks (a fresh lane id through an empty asm), instead of being kept live across the bounce loop (C3 park
+// instantiation: 13 -> 2 VGPR spills); the bounce kernel derives the randDir trace index from it (queue_trace)
 struct ParkTile {
   int after;
   QRay *queue;
   uint32_t *count;
   const FrameParams &P;
   uint32_t wv, w8;
-  __device__ __forceinline__ void ids(uint32_t &t, uint32_t &o) const
+  __device__ __forceinline__ void put_out(uint32_t slot) const
   {
     const uint32_t t8 = ((volatile uint32_t *)s_tile8)[wv];
     uint32_t le = __lane_id();
     asm volatile("" : "+v"(le));
     const uint32_t gx = (t8 % w8) * 8u + (le & 7u), gy = (t8 / w8) * 8u + (le >> 3);
-    const uint32_t y = P.nranks > 1 ? strip_row_to_y(gy, P) : gy + P.row0;
-    const uint32_t orow = P.nranks > 1 ? gy : y;
-    t = (uint32_t)((uint64_t)y * P.W + gx - P.p_begin);
-    o = (uint32_t)((size_t)orow * P.W + gx);
+    const uint32_t orow = P.nranks > 1 ? gy : gy + P.row0;  // strips: the strip-local row
+    P.queue_out[slot] = (uint32_t)((size_t)orow * P.W + gx);
   }
   __device__ __forceinline__ uint32_t *keys() const { return P.queue_key; }
 };
+
+// the randDir trace index of a parked trace from its output pixel (ParkTile::put_out): the pixel's frame row y,
+// raster index y W + x, minus the launch's first pixel (Render.cpp:152-156, one sample per pixel)
+__device__ __forceinline__ uint32_t queue_trace(const FrameParams &P, uint32_t out)
+{
+  if (P.nranks <= 1) return (uint32_t)(out - P.p_begin);
+  const uint32_t gy = out / P.W, x = out - gy * P.W;
+  return (uint32_t)((uint64_t)strip_row_to_y(gy, P) * P.W + x - P.p_begin);
+}
 
 // trace i's randomInsideSphere draw (Vector3.cpp:176-188) from the LCG state before its accepted triple
 __device__ __forceinline__ v3 rd_from_state(uint32_t s)
@@ -1916,18 +1922,24 @@ __global__ RFX_TRACE_BOUNDS void bounce_kernel(DevScene S, FrameParams P)
     const uint32_t i = base + lane;
     const bool valid = i < n;
     QRay q{};
-    if (valid) q = P.queue[P.queue_order ? P.queue_order[i] : i];
-    const v3 rd = valid ? load_rd(P, q.trace) : mk(0.0f, 0.0f, 0.0f);
+    uint32_t qo = 0;
+    if (valid)
+    {
+      const uint32_t e = P.queue_order ? P.queue_order[i] : i;
+      q = P.queue[e];
+      qo = P.queue_out[e];
+    }
+    const v3 rd = valid ? load_rd(P, queue_trace(P, qo)) : mk(0.0f, 0.0f, 0.0f);
     bool parked;
     const col c = trace_from<false, CULL, MANYL, SMALL, PLANES, false>(
-        S, mk(q.ox, q.oy, q.oz), mk(q.dx, q.dy, q.dz), mkc(q.mr, q.mg, q.mb), mkc(q.pr, q.pg, q.pb), (int)q.refl, P.depth,
-        rd, lut, cnt, valid, Park{0, nullptr, nullptr, 0, 0}, parked);
+        S, mk(q.ox, q.oy, q.oz), mk(q.dx, q.dy, q.dz), mkc(q.mr, q.mg, q.mb), mkc(q.pr, q.pg, q.pb), P.park_after,
+        P.depth, rd, lut, cnt, valid, Park{0, nullptr, nullptr, nullptr, 0}, parked);
     if (valid)
     {
       const col out = cadd(mkc(0.0f, 0.0f, 0.0f), c);                            // Render.cpp:185
-      float *d = P.img + (size_t)q.out * 3;
+      float *d = P.img + (size_t)qo * 3;
       d[0] = out.r; d[1] = out.g; d[2] = out.b;
-      if (P.argb) P.argb[q.out] = argb(out);
+      if (P.argb) P.argb[qo] = argb(out);
     }
   }
 }
