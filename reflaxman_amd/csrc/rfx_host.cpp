@@ -509,7 +509,6 @@ struct rfx_renderer {
   uint64_t scene_gen = 0;  // bumped by every set_scene
   int prim_mode = 1;       // rfx_renderer_set_prim_masks
   QRay *d_queue = nullptr;
-  uint32_t *d_qout = nullptr;  // per parked trace: its output pixel
   uint64_t queue_cap = 0;
   uint32_t *d_qctr = nullptr;   // count, claim counter, then the sort's kQueueBuckets histogram words
   uint32_t *d_qkey = nullptr, *d_qorder = nullptr;  // regroup sort: per entry its bucket; entries in bucket order
@@ -618,7 +617,7 @@ extern "C" void rfx_renderer_destroy(rfx_renderer *r)
   (void)hipFree(r->d_rng_range);
   (void)hipFree(r->d_img); (void)hipFree(r->d_argb); (void)hipFree(r->d_cnt);
   (void)hipFree(r->d_queue); (void)hipFree(r->d_qctr); (void)hipFree(r->d_prim_mask);
-  (void)hipFree(r->d_qkey); (void)hipFree(r->d_qorder); (void)hipFree(r->d_qout);
+  (void)hipFree(r->d_qkey); (void)hipFree(r->d_qorder);
   for (hipEvent_t e : r->events) (void)hipEventDestroy(e);
   if (r->tile_stream) (void)hipStreamSynchronize(r->tile_stream);
   (void)hipFree(r->d_tile_cost); (void)hipFree(r->d_tile_order); (void)hipFree(r->d_tile_scratch);
@@ -1284,12 +1283,11 @@ static int trace_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *rd, float
   {
     if (pl.traces > r->queue_cap)
     {
-      (void)hipFree(r->d_queue); (void)hipFree(r->d_qkey); (void)hipFree(r->d_qorder); (void)hipFree(r->d_qout);
+      (void)hipFree(r->d_queue); (void)hipFree(r->d_qkey); (void)hipFree(r->d_qorder);
       r->d_queue = nullptr;
-      r->d_qkey = r->d_qorder = r->d_qout = nullptr;
+      r->d_qkey = r->d_qorder = nullptr;
       r->queue_cap = 0;
       HIP_CHECK(hipMalloc(&r->d_queue, pl.traces * sizeof(QRay)));
-      HIP_CHECK(hipMalloc(&r->d_qout, pl.traces * sizeof(uint32_t)));
       HIP_CHECK(hipMalloc(&r->d_qkey, pl.traces * sizeof(uint32_t)));
       HIP_CHECK(hipMalloc(&r->d_qorder, pl.traces * sizeof(uint32_t)));
       r->queue_cap = pl.traces;
@@ -1298,7 +1296,6 @@ static int trace_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *rd, float
     if (!r->d_qctr) HIP_CHECK(hipMalloc(&r->d_qctr, qwords * sizeof(uint32_t)));
     HIP_CHECK(hipMemsetAsync(r->d_qctr, 0, (sort_queue ? qwords : 2) * sizeof(uint32_t), st));
     P.queue = r->d_queue;
-    P.queue_out = r->d_qout;
     P.queue_count = r->d_qctr;
     P.queue_next = r->d_qctr + 1;
     P.park_after = park_after;

@@ -1143,12 +1143,11 @@ __device__ __forceinline__ bool occluded(const DevScene &S, v3 o, v3 ray, bool l
 // appended to the queue instead (one atomic per wave, packed lane order) and the trace ends here; the bounce
 // kernel resumes it from exactly that state, so every float op is the same.
 struct Park {
-  int after;            // segments before parking (<= 0: never)
+  int after;           // segments before parking (<= 0: never)
   QRay *queue;
   uint32_t *count;
-  uint32_t *queue_out;  // per entry: the output pixel
-  uint32_t out;         // this lane's output pixel
-  __device__ __forceinline__ void put_out(uint32_t slot) const { queue_out[slot] = out; }
+  uint32_t trace, out;  // this lane's randDir trace index and output pixel
+  __device__ __forceinline__ void ids(uint32_t &t, uint32_t &o) const { t = trace; o = out; }
   __device__ __forceinline__ uint32_t *keys() const { return nullptr; }
 };
 
@@ -1169,101 +1168,16 @@ __device__ __forceinline__ uint32_t queue_key(const DevScene &S, v3 o, v3 d)
   return oct << 9 | m;
 }
 
-// Per wave: the epilogue's staging of the wave's 64 pixels (store_wave_tile: 192 RGB floats + 64 ARGB words); before
-// the epilogue, the shadow pack's query slots (RFX_SHADOW_PACK)
+// Per wave: the epilogue's staging of the wave's 64 pixels (store_wave_tile: 192 RGB floats + 64 ARGB words)
 __shared__ __attribute__((aligned(16))) uint32_t s_out[kWgWaves][256];
-
-#ifndef RFX_SHADOW_PACK
-#define RFX_SHADOW_PACK 0
-#endif
-#if RFX_SHADOW_PACK
-// Lock-step of the workgroup's two waves (RFX_SHADOW_PACK experiment): the bounce loop runs while any lane of either
-// wave is alive (double-buffered flags by iteration parity: one barrier per iteration)
-__shared__ uint32_t s_any[2][kWgWaves];
-__shared__ uint32_t s_pack_cnt[2][kWgWaves];
-__device__ __forceinline__ bool wg_any(bool x, uint32_t &parity)
-{
-  const uint32_t wv = threadIdx.x >> 6;
-  const bool w = __ballot(x) != 0;
-  if (__lane_id() == 0) s_any[parity][wv] = w;
-  __syncthreads();
-  bool r = false;
-  for (uint32_t i = 0; i < kWgWaves; ++i) r |= s_any[parity][i] != 0;
-  parity ^= 1u;
-  return r;
-}
-
-// Shadow any-hit of a small scene with the workgroup's waves in lock-step: when the facing lanes of both waves fit one
-// wave, wave 0 runs them all on full lanes (its idle lanes take wave 1's queries through LDS) while wave 1 waits.
-template <bool PLANES>
-__device__ __forceinline__ bool shadow_pack(const DevScene &S, const CullRec *cull, v3 drop, v3 sray, bool facing,
-                                            int skip_sph, int skip_tri, int skip_pln, Cnt &cnt, uint32_t &parity)
-{
-  static_assert(kWgWaves == 2, "shadow pack: two waves per workgroup");
-  uint32_t *L = &s_out[0][0];  // 512 words: 64 queries x 7 words, then 64 result words
-  const uint32_t wv = threadIdx.x >> 6, lane = __lane_id();
-  const uint64_t fb = __ballot(facing), lt = (1ull << lane) - 1ull;
-  if (lane == 0) s_pack_cnt[parity][wv] = (uint32_t)__popcll(fb);
-  __syncthreads();
-  const uint32_t c0 = s_pack_cnt[parity][0], c1 = s_pack_cnt[parity][1];
-  parity ^= 1u;
-  bool occ = false;
-  if (!(c0 && c1 && c0 + c1 <= 64))
-  {
-    if (fb)
-    {
-      uint64_t om = S.cull_valid;
-      const Bundle SB = make_bundle(drop, sray, facing);
-      if (SB.ok) om = cull_small(cull, S.cull_valid, SB);
-      if (facing) occ = occluded_small<false, PLANES>(S, drop, sray, skip_sph, skip_tri, skip_pln, om, cnt);
-    }
-    return occ;
-  }
-  const uint32_t e = (uint32_t)__popcll(fb & lt);  // wave 1: this lane's query slot
-  if (wv == 1 && facing)
-  {
-    float *q = reinterpret_cast<float *>(L + 7 * e);
-    q[0] = drop.x; q[1] = drop.y; q[2] = drop.z; q[3] = sray.x; q[4] = sray.y; q[5] = sray.z;
-    L[7 * e + 6] = (uint32_t)(skip_sph + 1) | (uint32_t)(skip_tri + 1) << 10 | (uint32_t)(skip_pln + 1) << 20;
-  }
-  __syncthreads();
-  if (wv == 0)
-  {
-    const uint32_t k = (uint32_t)__popcll(~fb & lt);  // the k-th idle lane takes wave 1's k-th query
-    const bool borrowed = !facing && k < c1;
-    if (borrowed)
-    {
-      const float *q = reinterpret_cast<const float *>(L + 7 * k);
-      drop = mk(q[0], q[1], q[2]);
-      sray = mk(q[3], q[4], q[5]);
-      const uint32_t sk = L[7 * k + 6];
-      skip_sph = (int)(sk & 1023u) - 1;
-      skip_tri = (int)((sk >> 10) & 1023u) - 1;
-      skip_pln = (int)(sk >> 20) - 1;
-    }
-    const bool act = facing || borrowed;
-    uint64_t om = S.cull_valid;
-    const Bundle SB = make_bundle(drop, sray, act);
-    if (SB.ok) om = cull_small(cull, S.cull_valid, SB);
-    if (act) occ = occluded_small<false, PLANES>(S, drop, sray, skip_sph, skip_tri, skip_pln, om, cnt);
-    if (borrowed) L[448 + k] = occ ? 1u : 0u;
-  }
-  __syncthreads();
-  if (wv == 1 && facing) occ = L[448 + e] != 0;
-  return occ;
-}
-#endif
 
 // Scene::trace from a mid-trace state (mulc, pix after `refl` segments); park: see Park.  *parked: this lane's
 // trace was queued and its returned colour is not final.
-template <bool STATS, bool CULL, bool MANYL, bool SMALL, bool PLANES, bool PARK, class PK, bool LOCK = false>
+template <bool STATS, bool CULL, bool MANYL, bool SMALL, bool PLANES, bool PARK, class PK>
 __device__ __forceinline__ col trace_from(const DevScene &S, v3 origin, v3 ray, col mulc, col pix, int refl, int depth,
                                           v3 rd, const float *lut, Cnt &cnt, bool valid, const PK &park, bool &parked,
                                           const uint64_t *pm_tile = nullptr)
 {
-#if RFX_SHADOW_PACK
-  uint32_t lock_parity = 0, pack_parity = 0;
-#endif
   // the first segment of a plain small-scene trace: this tile's per-view masks (prim_cull_kernel) -- the closest
   // hit's, then one per light for its shadow rays
   bool seg0 = pm_tile != nullptr;
@@ -1275,11 +1189,7 @@ __device__ __forceinline__ col trace_from(const DevScene &S, v3 origin, v3 ray, 
   int nseg = 0;  // diagnostic build only (tools/segstats.py): the trace's segment count replaces its colour
 #endif
   RFX_PROF_BEGIN(P_SEG);
-#if RFX_SHADOW_PACK
-  while (LOCK ? wg_any(alive, lock_parity) : __ballot(alive) != 0)
-#else
   while (__ballot(alive))
-#endif
   {
 #ifdef RFX_DEBUG_SEGS
     if (alive) ++nseg;
@@ -1363,18 +1273,6 @@ __device__ __forceinline__ col trace_from(const DevScene &S, v3 origin, v3 ray, 
             sray = add(dtl, mul(rd, L.radius));                                  // Scene.cpp:129
           }
         }
-#if RFX_SHADOW_PACK
-        if constexpr (LOCK)
-        {
-          if (!(!MANYL && seg0 && q < kPrimLights))  // (the first segment's precomputed masks are per tile: no pack)
-          {
-            if (shadow_pack<PLANES>(S, T.cull(), drop, sray, facing, skip_sph, skip_tri, skip_pln, cnt, pack_parity))
-              facing = false;
-            if (facing) lit |= 1u << q;
-            continue;
-          }
-        }
-#endif
         if (__ballot(facing))
         {
           if constexpr (SMALL)
@@ -1527,9 +1425,11 @@ __device__ __forceinline__ col trace_from(const DevScene &S, v3 origin, v3 ray, 
           q.ox = origin.x; q.oy = origin.y; q.oz = origin.z; q.dx = ray.x;
           q.dy = ray.y; q.dz = ray.z; q.mr = mulc.r; q.mg = mulc.g;
           q.mb = mulc.b; q.pr = pix.r; q.pg = pix.g; q.pb = pix.b;
+          uint32_t qt, qo;
+          park.ids(qt, qo);
+          q.trace = qt; q.out = qo; q.refl = (uint32_t)refl; q.pad = 0;
           const uint32_t slot = base + (uint32_t)__popcll(pm & ((1ull << __lane_id()) - 1ull));
           park.queue[slot] = q;
-          park.put_out(slot);
           if (uint32_t *keys = park.keys()) keys[slot] = queue_key(S, origin, ray);
           parked = true;
           alive = false;
@@ -1551,7 +1451,7 @@ __device__ __forceinline__ col trace(const DevScene &S, v3 origin, v3 ray, int d
 {
   bool parked;
   return trace_from<STATS, CULL, MANYL, SMALL, PLANES, false>(S, origin, ray, mkc(1.0f, 1.0f, 1.0f), mkc(0.0f, 0.0f, 0.0f), 0,
-                                                       depth, rd, lut, cnt, valid, Park{0, nullptr, nullptr, nullptr, 0},
+                                                       depth, rd, lut, cnt, valid, Park{0, nullptr, nullptr, 0, 0},
                                                        parked);
 }
 
@@ -1581,35 +1481,28 @@ __device__ __forceinline__ uint32_t strip_row_to_y(uint32_t r, const FrameParams
 // the wave's schedule tile (index into the wave-tile grid), kept in LDS across the bounce loop
 __shared__ uint32_t s_tile8[kWgWaves];
 
-// Park info of a plain-pixel trace-kernel lane: its output pixel is re-derived from the wave's tile index in LDS when
-// the trace parks (a fresh lane id through an empty asm), instead of being kept live across the bounce loop (C3 park
-// instantiation: 13 -> 2 VGPR spills); the bounce kernel derives the randDir trace index from it (queue_trace)
+// Park info of a plain-pixel trace-kernel lane: its randDir trace index and output pixel are re-derived from the
+// wave's tile index in LDS when the trace parks (a fresh lane id through an empty asm), instead of being kept
+// live across the bounce loop (C3 park instantiation: 13 -> 2 VGPR spills)
 struct ParkTile {
   int after;
   QRay *queue;
   uint32_t *count;
   const FrameParams &P;
   uint32_t wv, w8;
-  __device__ __forceinline__ void put_out(uint32_t slot) const
+  __device__ __forceinline__ void ids(uint32_t &t, uint32_t &o) const
   {
     const uint32_t t8 = ((volatile uint32_t *)s_tile8)[wv];
     uint32_t le = __lane_id();
     asm volatile("" : "+v"(le));
     const uint32_t gx = (t8 % w8) * 8u + (le & 7u), gy = (t8 / w8) * 8u + (le >> 3);
-    const uint32_t orow = P.nranks > 1 ? gy : gy + P.row0;  // strips: the strip-local row
-    P.queue_out[slot] = (uint32_t)((size_t)orow * P.W + gx);
+    const uint32_t y = P.nranks > 1 ? strip_row_to_y(gy, P) : gy + P.row0;
+    const uint32_t orow = P.nranks > 1 ? gy : y;
+    t = (uint32_t)((uint64_t)y * P.W + gx - P.p_begin);
+    o = (uint32_t)((size_t)orow * P.W + gx);
   }
   __device__ __forceinline__ uint32_t *keys() const { return P.queue_key; }
 };
-
-// the randDir trace index of a parked trace from its output pixel (ParkTile::put_out): the pixel's frame row y,
-// raster index y W + x, minus the launch's first pixel (Render.cpp:152-156, one sample per pixel)
-__device__ __forceinline__ uint32_t queue_trace(const FrameParams &P, uint32_t out)
-{
-  if (P.nranks <= 1) return (uint32_t)(out - P.p_begin);
-  const uint32_t gy = out / P.W, x = out - gy * P.W;
-  return (uint32_t)((uint64_t)strip_row_to_y(gy, P) * P.W + x - P.p_begin);
-}
 
 // trace i's randomInsideSphere draw (Vector3.cpp:176-188) from the LCG state before its accepted triple
 __device__ __forceinline__ v3 rd_from_state(uint32_t s)
@@ -1750,8 +1643,7 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
       if (valid) rd = load_rd(P, pr);
       const ParkTile park{P.park_after, P.queue, P.queue_count, P, wv, w8};
       const uint64_t *pm_tile = SMALL && CULL && !STATS && P.prim_mask ? P.prim_mask + (size_t)kPrimStride * t8 : nullptr;
-      constexpr bool LOCK = RFX_SHADOW_PACK && SMALL && CULL && !STATS && !MANYL && !PARK;
-      const col c = trace_from<STATS, CULL, MANYL, SMALL, PLANES, PARK, ParkTile, LOCK>(S, eye, ray, mkc(1.0f, 1.0f, 1.0f),
+      const col c = trace_from<STATS, CULL, MANYL, SMALL, PLANES, PARK>(S, eye, ray, mkc(1.0f, 1.0f, 1.0f),
                                                                   mkc(0.0f, 0.0f, 0.0f), 0, P.depth, rd, lut, cnt,
                                                                   valid, park, parked, pm_tile);
       out = cadd(mkc(0.0f, 0.0f, 0.0f), c);                                      // Render.cpp:185 (/ 1.0f exact)
@@ -1922,24 +1814,18 @@ __global__ RFX_TRACE_BOUNDS void bounce_kernel(DevScene S, FrameParams P)
     const uint32_t i = base + lane;
     const bool valid = i < n;
     QRay q{};
-    uint32_t qo = 0;
-    if (valid)
-    {
-      const uint32_t e = P.queue_order ? P.queue_order[i] : i;
-      q = P.queue[e];
-      qo = P.queue_out[e];
-    }
-    const v3 rd = valid ? load_rd(P, queue_trace(P, qo)) : mk(0.0f, 0.0f, 0.0f);
+    if (valid) q = P.queue[P.queue_order ? P.queue_order[i] : i];
+    const v3 rd = valid ? load_rd(P, q.trace) : mk(0.0f, 0.0f, 0.0f);
     bool parked;
     const col c = trace_from<false, CULL, MANYL, SMALL, PLANES, false>(
-        S, mk(q.ox, q.oy, q.oz), mk(q.dx, q.dy, q.dz), mkc(q.mr, q.mg, q.mb), mkc(q.pr, q.pg, q.pb), P.park_after,
-        P.depth, rd, lut, cnt, valid, Park{0, nullptr, nullptr, nullptr, 0}, parked);
+        S, mk(q.ox, q.oy, q.oz), mk(q.dx, q.dy, q.dz), mkc(q.mr, q.mg, q.mb), mkc(q.pr, q.pg, q.pb), (int)q.refl, P.depth,
+        rd, lut, cnt, valid, Park{0, nullptr, nullptr, 0, 0}, parked);
     if (valid)
     {
       const col out = cadd(mkc(0.0f, 0.0f, 0.0f), c);                            // Render.cpp:185
-      float *d = P.img + (size_t)qo * 3;
+      float *d = P.img + (size_t)q.out * 3;
       d[0] = out.r; d[1] = out.g; d[2] = out.b;
-      if (P.argb) P.argb[qo] = argb(out);
+      if (P.argb) P.argb[q.out] = argb(out);
     }
   }
 }

@@ -96,14 +96,14 @@ struct DevScene {
 };
 
 // A trace parked between bounce segments (large scenes, plain pixels): the state Scene::trace carries from
-// one segment to the next (Scene.cpp:80-234: origin, ray, mulColor, pixelColor).  48 B: one lane stores / loads
-// it with three 16-B accesses.  Its output pixel goes to a parallel u32 array (FrameParams::queue_out); the randDir
-// trace index follows from the pixel, and every parked trace has done FrameParams::park_after segments.
+// one segment to the next (Scene.cpp:80-234: origin, ray, mulColor, pixelColor, refl), the trace index of its
+// randDir and the output pixel.  64 B: one lane stores / loads it with four 16-B accesses.
 constexpr uint32_t kQueueBuckets = 4096;  // regroup sort buckets (rfx_trace.h queue_key)
 struct alignas(16) QRay {
   float ox, oy, oz, dx;
   float dy, dz, mr, mg;
   float mb, pr, pg, pb;
+  uint32_t trace, out, refl, pad;
 };
 
 struct FrameParams {
@@ -131,7 +131,6 @@ struct FrameParams {
   // queue (queue_count: entries) instead of continuing; the bounce kernel then runs the queue in packed waves,
   // claiming 64 entries at a time from queue_next.  park_after <= 0: no parking.
   QRay *queue;
-  uint32_t *queue_out;          // per parked trace: its output pixel (strip-local row at nranks > 1)
   uint32_t *queue_count, *queue_next;
   int32_t park_after;
   // regroup sort (RFX_QUEUE_SORT): queue_key[i] is entry i's bucket (direction octant, origin cell), written at park
