@@ -32,6 +32,29 @@ def test_pulse_compiles_against_dropin_headers(tmp_path):
     assert os.path.getsize(exe) > 0
 
 
+@pytest.mark.skipif(not os.path.isdir("/root/reference/src/common"), reason="needs the reference sources")
+def test_dropin_scene_revisions_and_moved_handles(tmp_path):
+    """dropin/Scene.h: every Scene state has its own revision (a re-assigned Scene never repeats an earlier one, so
+    Render::renderNext re-uploads it), and a moved Scene's Triangle handles act on the Scene they now belong to.  Host
+    calls only: runs on the CPU (tests/native/dropin_scene_revision.cpp)."""
+    ref = "/root/reference/src/common"
+    src = tmp_path / "src"
+    src.mkdir()
+    keep = ["Color", "Material", "OmniLight", "Texture", "Vector3", "trace_math", "Matrix33"]
+    for n in [f + e for f in keep for e in (".h", ".cpp")] + ["image_headers.h", "defaults.h"]:
+        if os.path.exists(os.path.join(ref, n)):
+            os.symlink(os.path.join(ref, n), src / n)
+    lib = os.path.join(ROOT, "reflaxman_amd", "lib")
+    exe = str(tmp_path / "rev")
+    cmd = ["g++", "-std=c++11", "-O2", "-ffp-contract=off", "-DNDEBUG", "-w", "-I", str(src),
+           "-I", os.path.join(ROOT, "include", "reflaxman", "dropin"), "-I", os.path.join(ROOT, "include"),
+           os.path.join(ROOT, "tests", "native", "dropin_scene_revision.cpp"),
+           *[str(src / (f + ".cpp")) for f in keep], "-L", lib, "-lrfx", f"-Wl,-rpath,{lib}", "-o", exe]
+    subprocess.run(cmd, check=True, capture_output=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and r.stdout.strip() == "ok", r.stdout + r.stderr
+
+
 @pytest.mark.gpu
 def test_pulse_screenshot_matches_reference(tmp_path):
     c = manifest()["cases"]["pulse_screenshot_800x600_ss2"]
