@@ -1,0 +1,12 @@
+# One GPU call (after the PMC records of this library are in profiles/pmc): the default bench line, every config's
+# line, the drop-in's interactive cost through Pulse, and gloo rehearsals of the N > 1 bench on one GPU.
+# Usage (repo root, via gpurun): bash tools/r03_lines.sh <outdir under gpurun_out>
+O=$PWD/gpurun_out/${1:-lines}
+mkdir -p $O
+timeout -k 10 300 python -u bench.py > $O/bench_c3.json 2> $O/bench_c3.err || exit 1
+bash tools/configs_round.sh ${1:-lines}/configs || exit 2
+timeout -k 10 300 python -u tools/pulse_session_time.py --reps 5 --out $O/pulse_session_640x480.json > $O/pulse.log 2>&1 || exit 3
+for n in 2 4; do
+  timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 --master-port $((29500 + n)) bench.py --gpus $n --backend gloo --one-device --steps 20 --warmup 3 --no-cpu-baseline > $O/rehearsal_c4_n${n}_bands_gloo_one_device.json 2> $O/rehearsal_n$n.err || exit 4
+done
+exit 0
