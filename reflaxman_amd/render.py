@@ -311,6 +311,11 @@ class Renderer:
         a view repeats (default), 2 before every launch, 0 off.  No pixel changes."""
         check(_lib.load().rfx_renderer_set_prim_masks(self._h, int(mode)), "set_prim_masks")
 
+    def set_lookahead(self, mode: int):
+        """Next frame's RNG pre-pass beside this frame's trace (rfx.h rfx_renderer_set_lookahead): 1 small frames
+        (default), 2 every frame, 0 off.  No pixel changes."""
+        check(_lib.load().rfx_renderer_set_lookahead(self._h, int(mode)), "set_lookahead")
+
     def set_regroup(self, park_after: int):
         """Ray regrouping (rfx.h rfx_renderer_set_regroup): -1 default (large scenes, after 3 segments), 0 off,
         n >= 1 park traces alive after n segments for the packed bounce kernel.  No pixel changes."""
