@@ -430,7 +430,10 @@ def main():
         step()
     torch.cuda.synchronize()
     rr.get_timing()
-    rr.set_timing(True)
+    # HIP events on every n-th timed frame (at least 5 samples): three event records per frame cost ~10 us of C1's
+    # ~50 us frame, so timing every frame would slow the frames it measures
+    timing_every = max(1, min(8, args.steps // 5))
+    rr.set_timing(timing_every)
     if world > 1:
         sf.time_emits(True)
         dist.barrier()
@@ -558,7 +561,7 @@ def main():
                                    + ("+count-ahead" if sf.count_ahead else "")
                                    + ("+emit-ahead" if sf.emit_ahead else "")) if world > 1 else "single-gpu"},
         "roofline": roofline,
-        "phases_ms": {"rng_prepass": round(pre_avg, 4), "trace": round(trace_avg, 4),
+        "phases_ms": {"rng_prepass": round(pre_avg, 4), "trace": round(trace_avg, 4), "timed_every_nth_frame": timing_every,
                       **({"rng_prepass_kind": "look-ahead emit on the side stream, beside the previous trace (HIP "
                                               "events on that stream): off the critical path"}
                          if emit_side is not None else {})},

@@ -125,12 +125,6 @@ int rfx_renderer_set_regroup_sort(rfx_renderer *r, int on);
  * view stays.  1 (default) = built when a view repeats (the second frame of a still camera on), so a camera that
  * moves every frame never pays for them; 2 = built before every launch; 0 = off (per-launch bundles). */
 int rfx_renderer_set_prim_masks(rfx_renderer *r, int mode);
-/* Look-ahead of rfx_render_frame (no pixel changes): once a frame's randDirs are emitted, the next frame's RNG pre-pass
- * (the same frame plan) runs on a side stream into a second randDir buffer while this frame traces; a following
- * rfx_render_frame with the same plan traces from it, any other call forgets it first (the stream state is restored).
- * 1 (default) = on frames of fewer than 16384 8x8 wave tiles (whose trace leaves the chip idle: C1's 640x480), 2 = on
- * every frame, 0 = off. */
-int rfx_renderer_set_lookahead(rfx_renderer *r, int mode);
 /* The reference's two LCG streams (trace_math.h:34-39): Vector3.cpp's (randomInsideSphere) and
  * Render.cpp's (additive jitter).  Both persist across frames exactly as the reference's would. */
 int rfx_renderer_set_rng(rfx_renderer *r, uint32_t sphere_seed, uint32_t jitter_seed);
@@ -244,7 +238,8 @@ int rfx_group_render_frame(rfx_group *g, const rfx_frame *frame, float *d_rgb, u
 
 /* Optional per-phase timing of rfx_render_frame with HIP events recorded on the launch stream:
  * enable, render, then read the summed device time (ms) of the RNG pre-pass and of the trace kernel
- * over the frames since the last read (synchronises; resets the sums). */
+ * over the timed frames since the last read, and their number (synchronises; resets the sums).  enable = 1 times
+ * every frame, n > 1 every n-th frame (three event records per timed frame cost ~10 us of a 640x480 frame's ~50). */
 int rfx_renderer_set_timing(rfx_renderer *r, int enable);
 int rfx_renderer_get_timing(rfx_renderer *r, double *prepass_ms, double *trace_ms, uint64_t *frames);
 

@@ -358,9 +358,7 @@ extern "C" int rfx_group_render_frame(rfx_group *g, const rfx_frame *f, float *d
   const bool accumulate = f->additive_counter > 1;
   std::vector<hipStream_t> st(n);
   for (size_t i = 0; i < n; ++i) st[i] = i ? g->own[i] : s0;
-  // 0. after the caller's work on its stream; member 0's stream state is the group's (a frame member 0 rendered alone
-  // may have emitted the next one ahead: forget it)
-  RCHECK(rfx_detail_discard_lookahead(g->r[0]));
+  // 0. after the caller's work on its stream; member 0's stream state is the group's
   GCHECK(hipSetDevice(g->dev[0]));
   GCHECK(hipEventRecord(g->ev_start[0], s0));
   const uint32_t jitter = rfx_detail_jitter(g->r[0]);

@@ -449,15 +449,6 @@ constexpr size_t kPrimWords = 5;  // per wave tile (rfx_trace.h kPrimStride)
 // above park-3 unsorted).  Park order keeps a tile's survivors together, which a coarse cell key cannot beat.
 #define RFX_QUEUE_SORT 0
 #endif
-#ifndef RFX_LOOKAHEAD_DEFAULT
-// 1: look ahead on frames whose trace grid leaves the chip idle (fewer than RFX_LOOKAHEAD_MAX_TILES wave tiles: C1's
-// 640x480 has 4,800; the next frame's pre-pass then runs on the free slots beside this frame's trace), 2: on every
-// frame, 0: never
-#define RFX_LOOKAHEAD_DEFAULT 1
-#endif
-#ifndef RFX_LOOKAHEAD_MAX_TILES
-#define RFX_LOOKAHEAD_MAX_TILES 16384
-#endif
 #ifndef RFX_PARK_AFTER
 #define RFX_PARK_AFTER 3  // large-scene plain frames: segments before a live trace is parked for the bounce kernel
 #endif
@@ -488,17 +479,6 @@ struct rfx_renderer {
   // seed word while rewind_flip) can be restored
   bool rewind_ok = false, rewind_flip = false;
   uint32_t rewind_jitter = 0;
-  // Look-ahead of single-renderer frames (rfx_renderer_set_lookahead): once a frame's randDirs are emitted, the next
-  // frame's pre-pass (same plan) runs on la_stream into the other randDir buffer while this frame traces; the next
-  // rfx_render_frame with the same plan traces from it, any other call discards it first (la_discard).  d_seed[2]
-  // keeps the served frame's start state for rfx_frame_rng_rewind (the look-ahead's emit overwrites its word).
-  int la_mode = RFX_LOOKAHEAD_DEFAULT;
-  hipStream_t la_stream = nullptr;
-  hipEvent_t la_emitted = nullptr, la_done = nullptr, la_traced[2] = {nullptr, nullptr};
-  bool la_pending = false;
-  int la_buf = 0;
-  uint64_t la_key[8] = {};
-  hipStream_t la_last_st = nullptr;  // the stream of the frame the look-ahead follows
   uint32_t *d_blk_cnt = nullptr; uint64_t blk_cap = 0;
   uint64_t *d_blk_off = nullptr;     // band emits: the scanned block offsets ...
   uint32_t *d_rng_range = nullptr;   // ... and the band's first / last / final block
@@ -533,8 +513,11 @@ struct rfx_renderer {
   uint32_t *d_qctr = nullptr;   // count, claim counter, then the sort's kQueueBuckets histogram words
   uint32_t *d_qkey = nullptr, *d_qorder = nullptr;  // regroup sort: per entry its bucket; entries in bucket order
   int queue_sort = RFX_QUEUE_SORT;  // rfx_renderer_set_regroup_sort
-  // per-phase event timing: triples {start, after pre-pass, after trace}
-  bool timing = false;
+  // per-phase event timing: triples {start, after pre-pass, after trace} on every timing_every-th frame (the events'
+  // own cost stays off the other frames: ~10 us per frame for three records at C1's 640x480)
+  bool timing = false, timing_this = false;
+  uint32_t timing_every = 1;
+  uint64_t timing_seq = 0;
   std::vector<hipEvent_t> events;
   size_t events_used = 0;
 };
@@ -542,29 +525,9 @@ struct rfx_renderer {
 static uint32_t *seed_cur(rfx_renderer *r) { return r->d_seed + r->seed_idx; }
 static uint32_t *seed_next(rfx_renderer *r) { return r->d_seed + (r->seed_idx ^ 1u); }
 
-// Forget a pending look-ahead (every entry point that uses or moves the random stream calls this first, unless it
-// takes the look-ahead): `st` waits for its kernels, and the stream state returns to before it.
-static int la_discard(rfx_renderer *r, hipStream_t st)
-{
-  if (!r->la_pending) return RFX_OK;
-  HIP_CHECK(hipStreamWaitEvent(st ? st : r->stream, r->la_done, 0));
-  r->seed_idx ^= 1u;
-  r->la_pending = false;
-  return RFX_OK;
-}
-
-extern "C" int rfx_renderer_set_lookahead(rfx_renderer *r, int mode)
-{
-  if (!r || mode < 0 || mode > 2) return fail(RFX_ERR_ARG, "renderer_set_lookahead: 0, 1 or 2");
-  int rc;
-  if ((rc = la_discard(r, r->la_last_st)) != RFX_OK) return rc;
-  r->la_mode = mode;
-  return RFX_OK;
-}
-
 static int timing_event(rfx_renderer *r, hipStream_t st)
 {
-  if (!r->timing) return RFX_OK;
+  if (!r->timing_this) return RFX_OK;
   if (r->events_used == r->events.size())
   {
     hipEvent_t e;
@@ -575,10 +538,20 @@ static int timing_event(rfx_renderer *r, hipStream_t st)
   return RFX_OK;
 }
 
+// the first event of a frame: decides whether this frame is one of the timed ones
+static int timing_start(rfx_renderer *r, hipStream_t st)
+{
+  r->timing_this = r->timing && r->timing_seq++ % r->timing_every == 0;
+  return timing_event(r, st);
+}
+
 extern "C" int rfx_renderer_set_timing(rfx_renderer *r, int enable)
 {
-  if (!r) return fail(RFX_ERR_ARG, "set_timing: null renderer");
+  if (!r || enable < 0) return fail(RFX_ERR_ARG, "set_timing: null renderer or negative period");
   r->timing = enable != 0;
+  r->timing_every = enable > 1 ? (uint32_t)enable : 1u;
+  r->timing_seq = 0;
+  r->timing_this = false;
   r->events_used = 0;
   return RFX_OK;
 }
@@ -622,13 +595,13 @@ extern "C" int rfx_renderer_create(rfx_renderer **out, int device)
   int rc;
   if ((rc = set_dev(r)) != RFX_OK) { delete r; return rc; }
   if (hipStreamCreateWithFlags(&r->own_stream, hipStreamNonBlocking) != hipSuccess ||
-      hipMalloc(&r->d_seed, 3 * sizeof(uint32_t)) != hipSuccess || hipMalloc(&r->d_err, sizeof(int)) != hipSuccess)
+      hipMalloc(&r->d_seed, 2 * sizeof(uint32_t)) != hipSuccess || hipMalloc(&r->d_err, sizeof(int)) != hipSuccess)
   {
     delete r;
     return fail(RFX_ERR_HIP, "renderer_create: HIP allocation failed");
   }
   r->stream = r->own_stream;
-  const uint32_t seeds[3] = {1350490027u, 1350490027u, 1350490027u};
+  const uint32_t seeds[2] = {1350490027u, 1350490027u};
   if (hipMemcpy(r->d_seed, seeds, sizeof(seeds), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemset(r->d_err, 0, sizeof(int)) != hipSuccess)
   {
@@ -651,7 +624,6 @@ extern "C" void rfx_renderer_destroy(rfx_renderer *r)
   if (!r) return;
   (void)hipSetDevice(r->device);
   (void)hipStreamSynchronize(r->stream);
-  if (r->la_stream) (void)hipStreamSynchronize(r->la_stream);
   free_scene(r);
   (void)hipFree(r->d_seed); (void)hipFree(r->d_err); (void)hipFree(r->d_rd); (void)hipFree(r->d_rd_alt);
   (void)hipFree(r->d_blk_cnt); (void)hipFree(r->d_jump); (void)hipFree(r->d_rng_masks); (void)hipFree(r->d_blk_off);
@@ -666,9 +638,6 @@ extern "C" void rfx_renderer_destroy(rfx_renderer *r)
   if (r->tile_join) (void)hipEventDestroy(r->tile_join);
   if (r->tile_stream) (void)hipStreamDestroy(r->tile_stream);
   if (r->own_stream) (void)hipStreamDestroy(r->own_stream);
-  for (hipEvent_t e : {r->la_emitted, r->la_done, r->la_traced[0], r->la_traced[1]})
-    if (e) (void)hipEventDestroy(e);
-  if (r->la_stream) (void)hipStreamDestroy(r->la_stream);
   delete r;
 }
 
@@ -1117,7 +1086,6 @@ extern "C" int rfx_renderer_set_rng(rfx_renderer *r, uint32_t sphere_seed, uint3
   if (!r) return fail(RFX_ERR_ARG, "set_rng: null renderer");
   int rc;
   if ((rc = set_dev(r)) != RFX_OK) return rc;
-  if ((rc = la_discard(r, r->stream)) != RFX_OK) return rc;
   HIP_CHECK(hipMemcpyAsync(seed_cur(r), &sphere_seed, sizeof(uint32_t), hipMemcpyHostToDevice, r->stream));
   HIP_CHECK(hipStreamSynchronize(r->stream));
   r->jitter_seed = jitter_seed;
@@ -1130,7 +1098,6 @@ extern "C" int rfx_renderer_get_rng(rfx_renderer *r, uint32_t *sphere_seed, uint
   if (!r) return fail(RFX_ERR_ARG, "get_rng: null renderer");
   int rc;
   if ((rc = set_dev(r)) != RFX_OK) return rc;
-  if ((rc = la_discard(r, r->stream)) != RFX_OK) return rc;
   uint32_t s = 0;
   int err = 0;
   HIP_CHECK(hipMemcpyAsync(&s, seed_cur(r), sizeof(uint32_t), hipMemcpyDeviceToHost, r->stream));
@@ -1153,8 +1120,6 @@ static uint64_t rng_layout(uint64_t traces, uint32_t nslices, uint64_t *per_slic
 
 static int ensure_rng_workspace(rfx_renderer *r, uint64_t traces, uint64_t nblk)
 {
-  if ((traces > r->rd_cap || nblk > r->blk_cap) && r->la_stream)
-    HIP_CHECK(hipStreamSynchronize(r->la_stream));  // a look-ahead may still write the buffers replaced below
   if (traces > r->rd_cap)
   {
     (void)hipFree(r->d_rd);
@@ -1224,7 +1189,6 @@ extern "C" int rfx_frame_rng_count(rfx_renderer *r, const rfx_frame *f, uint32_t
   int rc;
   if ((rc = plan_frame(r, f, stream, pl)) != RFX_OK) return rc;
   if (!d_blk_counts || !nslices || slice >= nslices) return fail(RFX_ERR_ARG, "frame_rng_count: bad slice");
-  if ((rc = la_discard(r, pl.st)) != RFX_OK) return rc;
   uint64_t bps = 0;
   const uint64_t nblk = rng_layout(pl.traces, nslices, &bps);
   if ((rc = ensure_rng_workspace(r, pl.traces, nblk)) != RFX_OK) return rc;
@@ -1446,11 +1410,10 @@ extern "C" int rfx_render_frame_counted_ev(rfx_renderer *r, const rfx_frame *f, 
   int rc;
   if ((rc = plan_frame(r, f, stream, pl)) != RFX_OK) return rc;
   if (!d_rgb || !d_blk_counts || !nslices) return fail(RFX_ERR_ARG, "render_frame_counted: bad args");
-  if ((rc = la_discard(r, pl.st)) != RFX_OK) return rc;
   if (pl.traces == 0) return RFX_OK;
   const uint64_t nblk = rng_layout(pl.traces, nslices, nullptr);
   if ((rc = ensure_rng_workspace(r, pl.traces, nblk)) != RFX_OK) return rc;
-  if ((rc = timing_event(r, pl.st)) != RFX_OK) return rc;
+  if ((rc = timing_start(r, pl.st)) != RFX_OK) return rc;
   return finish_frame(r, pl, d_blk_counts, nullptr, nblk, d_rgb, d_argb, d_counters, (hipEvent_t)emitted_event);
 }
 
@@ -1478,7 +1441,6 @@ extern "C" int rfx_frame_rng_emit(rfx_renderer *r, const rfx_frame *f, uint32_t 
   int rc;
   if ((rc = plan_frame(r, f, stream, pl)) != RFX_OK) return rc;
   if (!d_blk_counts || !nslices) return fail(RFX_ERR_ARG, "frame_rng_emit: bad args");
-  if ((rc = la_discard(r, pl.st)) != RFX_OK) return rc;
   if (r->emit_pending >= 0) return fail(RFX_ERR_STATE, "frame_rng_emit: the last emitted frame has not been traced");
   if (pl.traces == 0) return RFX_OK;
   const uint64_t nblk = rng_layout(pl.traces, nslices, nullptr);
@@ -1517,7 +1479,7 @@ extern "C" int rfx_render_frame_emitted(rfx_renderer *r, const rfx_frame *f, flo
   const int buf = r->emit_pending;
   r->emit_pending = -1;
   r->trace_buf = buf;
-  if ((rc = timing_event(r, pl.st)) != RFX_OK) return rc;  // (the emit ran on its own stream: no pre-pass time)
+  if ((rc = timing_start(r, pl.st)) != RFX_OK) return rc;  // (the emit ran on its own stream: no pre-pass time)
   if ((rc = timing_event(r, pl.st)) != RFX_OK) return rc;
   return trace_frame(r, pl, buf ? r->d_rd_alt : r->d_rd, d_rgb, d_argb, d_counters);
 }
@@ -1527,8 +1489,6 @@ extern "C" int rfx_render_frame_emitted(rfx_renderer *r, const rfx_frame *f, flo
 extern "C" int rfx_frame_rng_discard(rfx_renderer *r)
 {
   if (!r) return fail(RFX_ERR_ARG, "frame_rng_discard: null renderer");
-  int rc;
-  if ((rc = la_discard(r, r->la_last_st)) != RFX_OK) return rc;
   r->rewind_ok = false;
   if (r->emit_pending >= 0)
   {
@@ -1543,64 +1503,11 @@ extern "C" int rfx_frame_rng_pending(rfx_renderer *r, uint32_t *frame_start)
   if (!r || !frame_start) return fail(RFX_ERR_ARG, "frame_rng_pending: bad args");
   int rc;
   if ((rc = set_dev(r)) != RFX_OK) return rc;
-  if ((rc = la_discard(r, r->stream)) != RFX_OK) return rc;
   // an emitted frame read the state word it left behind (emit_frame flipped seed_idx past it)
   const uint32_t *w = r->emit_pending >= 0 ? r->d_seed + (r->seed_idx ^ 1u) : seed_cur(r);
   HIP_CHECK(hipMemcpyAsync(frame_start, w, sizeof(uint32_t), hipMemcpyDeviceToHost, r->stream));
   HIP_CHECK(hipStreamSynchronize(r->stream));
   return r->emit_pending >= 0 ? 1 : 0;
-}
-
-// A single-renderer frame whose trace grid leaves the chip idle gets the next frame's pre-pass ahead (see la_*)
-static bool lookahead_eligible(rfx_renderer *r, const FramePlan &pl)
-{
-  if (!r->la_mode || pl.band || pl.P.nranks > 1 || !pl.P.grid_rows) return false;
-  return r->la_mode == 2 || trace_tiles(pl.P) < RFX_LOOKAHEAD_MAX_TILES;
-}
-
-// After a frame's trace is enqueued: record the trace as its buffer's last reader, and (ahead) emit the next frame of
-// the same plan on la_stream into the other randDir buffer -- after this frame's emit (the stream state past it), after
-// the trace before this one (the last reader of that buffer), with this frame's start state backed up first.
-static int lookahead(rfx_renderer *r, const FramePlan &pl, uint64_t nblk, bool ahead, bool served)
-{
-  if (!r->la_stream)
-  {
-    HIP_CHECK(hipStreamCreateWithFlags(&r->la_stream, hipStreamNonBlocking));
-    HIP_CHECK(hipEventCreateWithFlags(&r->la_emitted, hipEventDisableTiming));
-    HIP_CHECK(hipEventCreateWithFlags(&r->la_done, hipEventDisableTiming));
-    for (hipEvent_t &e : r->la_traced)
-    {
-      HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      HIP_CHECK(hipEventRecord(e, pl.st));
-    }
-  }
-  HIP_CHECK(hipEventRecord(r->la_traced[r->trace_buf], pl.st));
-  r->la_last_st = pl.st;
-  if (!ahead) return RFX_OK;
-  if (r->rd_alt_cap < pl.traces)
-  {
-    HIP_CHECK(hipStreamSynchronize(r->la_stream));
-    HIP_CHECK(hipStreamSynchronize(pl.st));
-    (void)hipFree(r->d_rd_alt);
-    r->d_rd_alt = nullptr;
-    r->rd_alt_cap = 0;
-    HIP_CHECK(hipMalloc(&r->d_rd_alt, pl.traces * sizeof(uint32_t)));
-    r->rd_alt_cap = pl.traces;
-  }
-  const int buf = r->trace_buf ^ 1;
-  if (!served) HIP_CHECK(hipStreamWaitEvent(r->la_stream, r->la_emitted, 0));  // (served: in la_stream's own order)
-  HIP_CHECK(hipStreamWaitEvent(r->la_stream, r->la_traced[buf], 0));
-  HIP_CHECK(hipMemcpyAsync(r->d_seed + 2, seed_next(r), sizeof(uint32_t), hipMemcpyDeviceToDevice, r->la_stream));
-  HIP_CHECK(launch_rng_count(seed_cur(r), r->d_jump, r->d_blk_cnt, 0, nblk, r->d_rng_masks, r->la_stream));
-  FramePlan lp = pl;
-  lp.st = r->la_stream;
-  int rc;
-  if ((rc = emit_frame(r, lp, r->d_blk_cnt, r->d_rng_masks, nblk, buf ? r->d_rd_alt : r->d_rd, r->la_done)) != RFX_OK)
-    return rc;
-  r->la_pending = true;
-  r->la_buf = buf;
-  plan_key(pl, r->la_key);
-  return RFX_OK;
 }
 
 extern "C" int rfx_render_frame(rfx_renderer *r, const rfx_frame *f, float *d_rgb, uint32_t *d_argb,
@@ -1611,7 +1518,7 @@ extern "C" int rfx_render_frame(rfx_renderer *r, const rfx_frame *f, float *d_rg
   if (!d_rgb) return fail(RFX_ERR_ARG, "render_frame: null framebuffer");
   if ((rc = plan_frame(r, f, stream, pl)) != RFX_OK) return rc;
   const uint32_t jitter0 = r->jitter_seed;
-  if (pl.traces == 0)  // a span with no block corner traces nothing (and draws no randDir; a look-ahead stays next)
+  if (pl.traces == 0)  // a span with no block corner traces nothing (and draws no randDir)
   {
     r->rewind_ok = true;
     r->rewind_flip = false;
@@ -1620,37 +1527,12 @@ extern "C" int rfx_render_frame(rfx_renderer *r, const rfx_frame *f, float *d_rg
   }
   const uint64_t nblk = rng_layout(pl.traces, 1, nullptr);
   if ((rc = ensure_rng_workspace(r, pl.traces, nblk)) != RFX_OK) return rc;
-  if ((rc = timing_event(r, pl.st)) != RFX_OK) return rc;
+  if ((rc = timing_start(r, pl.st)) != RFX_OK) return rc;
   if (r->emit_pending >= 0)
     return fail(RFX_ERR_STATE, "render_frame: an emitted frame awaits rfx_render_frame_emitted (or rfx_frame_rng_discard)");
-  bool served = false;
-  if (r->la_pending)
-  {
-    uint64_t key[8];
-    plan_key(pl, key);
-    if (memcmp(key, r->la_key, sizeof(key)) == 0)
-    {
-      // this frame's randDirs were emitted ahead, beside the last frame's trace
-      HIP_CHECK(hipStreamWaitEvent(pl.st, r->la_done, 0));
-      r->la_pending = false;
-      r->trace_buf = r->la_buf;
-      served = true;
-      if ((rc = timing_event(r, pl.st)) != RFX_OK) return rc;  // (no pre-pass on this stream)
-      if ((rc = trace_frame(r, pl, r->la_buf ? r->d_rd_alt : r->d_rd, d_rgb, d_argb, d_counters)) != RFX_OK) return rc;
-    }
-    else if ((rc = la_discard(r, pl.st)) != RFX_OK)
-      return rc;
-  }
-  const bool ahead = lookahead_eligible(r, pl);
-  if (!served)
-  {
-    // one device counts every block, so the emit can take its accept flags instead of regenerating them
-    HIP_CHECK(launch_rng_count(seed_cur(r), r->d_jump, r->d_blk_cnt, 0, nblk, r->d_rng_masks, pl.st));
-    if ((rc = finish_frame(r, pl, r->d_blk_cnt, r->d_rng_masks, nblk, d_rgb, d_argb, d_counters,
-                           ahead ? r->la_emitted : nullptr)) != RFX_OK)
-      return rc;
-  }
-  if ((rc = lookahead(r, pl, nblk, ahead, served)) != RFX_OK) return rc;
+  // one device counts every block, so the emit can take its accept flags instead of regenerating them
+  HIP_CHECK(launch_rng_count(seed_cur(r), r->d_jump, r->d_blk_cnt, 0, nblk, r->d_rng_masks, pl.st));
+  if ((rc = finish_frame(r, pl, r->d_blk_cnt, r->d_rng_masks, nblk, d_rgb, d_argb, d_counters)) != RFX_OK) return rc;
   r->rewind_ok = true;
   r->rewind_flip = true;
   r->rewind_jitter = jitter0;
@@ -1663,17 +1545,7 @@ extern "C" int rfx_frame_rng_rewind(rfx_renderer *r)
 {
   if (!r) return fail(RFX_ERR_ARG, "frame_rng_rewind: null renderer");
   if (!r->rewind_ok) return fail(RFX_ERR_STATE, "frame_rng_rewind: the last call was not rfx_render_frame");
-  if (r->la_pending && r->rewind_flip)
-  {
-    // the look-ahead's emit overwrote the frame's start word: restore it from its copy, after the look-ahead
-    int rc;
-    if ((rc = set_dev(r)) != RFX_OK) return rc;
-    if ((rc = la_discard(r, r->la_last_st)) != RFX_OK) return rc;
-    HIP_CHECK(hipMemcpyAsync(seed_cur(r), r->d_seed + 2, sizeof(uint32_t), hipMemcpyDeviceToDevice,
-                             r->la_last_st ? r->la_last_st : r->stream));
-  }
-  else if (r->rewind_flip)
-    r->seed_idx ^= 1u;
+  if (r->rewind_flip) r->seed_idx ^= 1u;
   r->jitter_seed = r->rewind_jitter;
   r->rewind_ok = false;
   return RFX_OK;
@@ -1862,7 +1734,6 @@ extern "C" int rfx_rand_dirs(rfx_renderer *r, uint32_t seed, uint64_t n, float *
   if (!r || !out3 || !n) return fail(RFX_ERR_ARG, "rand_dirs: bad args");
   int rc;
   if ((rc = set_dev(r)) != RFX_OK) return rc;
-  if ((rc = la_discard(r, r->stream)) != RFX_OK) return rc;
   uint32_t saved = 0;
   HIP_CHECK(hipMemcpyAsync(&saved, seed_cur(r), sizeof(uint32_t), hipMemcpyDeviceToHost, r->stream));
   HIP_CHECK(hipStreamSynchronize(r->stream));
@@ -1955,7 +1826,6 @@ void rfx_detail_set_jitter(rfx_renderer *r, uint32_t jitter) { r->jitter_seed = 
 hipStream_t rfx_detail_stream(const rfx_renderer *r) { return r->stream; }
 // the last call on r was a counted frame (one pre-pass flip, jitter advanced from jitter0): rfx_frame_rng_rewind
 // may undo it, as after rfx_render_frame
-int rfx_detail_discard_lookahead(rfx_renderer *r) { return la_discard(r, r->la_last_st); }
 void rfx_detail_set_rewindable(rfx_renderer *r, uint32_t jitter0)
 {
   r->rewind_ok = true;

@@ -11,4 +11,3 @@ uint32_t rfx_detail_jitter(const rfx_renderer *r);
 void rfx_detail_set_jitter(rfx_renderer *r, uint32_t jitter);
 hipStream_t rfx_detail_stream(const rfx_renderer *r);
 void rfx_detail_set_rewindable(rfx_renderer *r, uint32_t jitter0);
-int rfx_detail_discard_lookahead(rfx_renderer *r);  // a pending single-renderer look-ahead (rfx_host.cpp la_*)

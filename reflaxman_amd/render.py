@@ -311,11 +311,6 @@ class Renderer:
         a view repeats (default), 2 before every launch, 0 off.  No pixel changes."""
         check(_lib.load().rfx_renderer_set_prim_masks(self._h, int(mode)), "set_prim_masks")
 
-    def set_lookahead(self, mode: int):
-        """Next frame's RNG pre-pass beside this frame's trace (rfx.h rfx_renderer_set_lookahead): 1 small frames
-        (default), 2 every frame, 0 off.  No pixel changes."""
-        check(_lib.load().rfx_renderer_set_lookahead(self._h, int(mode)), "set_lookahead")
-
     def set_regroup(self, park_after: int):
         """Ray regrouping (rfx.h rfx_renderer_set_regroup): -1 default (large scenes, after 3 segments), 0 off,
         n >= 1 park traces alive after n segments for the packed bounce kernel.  No pixel changes."""
@@ -326,8 +321,10 @@ class Renderer:
         by direction octant and origin cell, or in park order (default).  No pixel changes."""
         check(_lib.load().rfx_renderer_set_regroup_sort(self._h, int(bool(on))), "set_regroup_sort")
 
-    def set_timing(self, enable: bool):
-        check(_lib.load().rfx_renderer_set_timing(self._h, int(bool(enable))), "set_timing")
+    def set_timing(self, enable):
+        """HIP-event timing of the frames (rfx.h rfx_renderer_set_timing): True / 1 every frame, n > 1 every n-th
+        frame, False / 0 off."""
+        check(_lib.load().rfx_renderer_set_timing(self._h, int(enable)), "set_timing")
 
     def get_timing(self):
         """(prepass_ms, trace_ms, frames) summed over the frames since the last call (HIP events)."""

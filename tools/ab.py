@@ -52,8 +52,6 @@ VARIANTS = {
     "every8": ["RFX_TILE_SORT_EVERY=8"],
     "every16": ["RFX_TILE_SORT_EVERY=16"],
     "qsort": ["RFX_QUEUE_SORT=1"],
-    "nola": ["RFX_LOOKAHEAD_DEFAULT=0"],
-    "la2": ["RFX_LOOKAHEAD_DEFAULT=2"],
     "lpt16k": ["RFX_TILE_ORDER_MIN_TILES=16384"],
     "lpt4k": ["RFX_TILE_ORDER_MIN_TILES=4096"],
 }
