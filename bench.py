@@ -179,11 +179,18 @@ def cpu_allcore(desc, W, H, depth, gpu_rgb, gpu_argb, rate_1core, seconds=8.0):
 
 
 def one_gpu_line(cfg_name, W, H, depth):
-    """The committed 1-GPU bench line of the same frame (profiles/r02/configs/), the denominator of a strong-scaling
-    efficiency at N > 1 (this run does not re-measure it), or None."""
-    d = os.path.join(ROOT, "profiles", "r02", "configs")
-    if not os.path.isdir(d):
-        return None
+    """The committed 1-GPU bench line of the same frame (the newest profiles/rNN/configs/), a cross-check of the
+    strong-scaling baseline this run measures itself, or None."""
+    import glob
+    dirs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]", "configs")), reverse=True)  # newest round
+    for d in dirs:
+        line = _one_gpu_line_in(d, cfg_name, W, H, depth)
+        if line:
+            return line
+    return None
+
+
+def _one_gpu_line_in(d, cfg_name, W, H, depth):
     for name in sorted(os.listdir(d)):
         if not name.startswith(cfg_name + "_") or not name.endswith(".json"):
             continue
@@ -194,7 +201,7 @@ def one_gpu_line(cfg_name, W, H, depth):
         c = rec.get("config", {})
         if rec.get("n_gpus") == 1 and (c.get("width"), c.get("height"), c.get("depth")) == (W, H, depth):
             return {"value": rec["value"], "unit": rec["unit"], "ms_per_step": rec["ms_per_step"],
-                    "source": os.path.join("profiles", "r02", "configs", name)}
+                    "source": os.path.relpath(os.path.join(d, name), ROOT)}
     return None
 
 
