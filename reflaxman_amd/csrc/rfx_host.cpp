@@ -28,19 +28,15 @@ namespace rfx {
 uint64_t rng_blocks_for(uint64_t traces);
 void rng_jump_table(uint64_t nblk, uint32_t *out);
 hipError_t launch_rng_count(const uint32_t *d_seed, const uint32_t *d_jump, uint32_t *d_blk_cnt, uint64_t blk0,
-                            uint64_t nblk_slice, hipStream_t st);
+                            uint64_t nblk_slice, uint16_t *d_masks, hipStream_t st);
 hipError_t launch_rng_finish(const uint32_t *d_seed, const uint32_t *d_jump, uint32_t *d_next_seed,
-                             const uint32_t *d_blk_cnt, uint64_t nblk, uint64_t traces,
+                             const uint32_t *d_blk_cnt, const uint16_t *d_masks, uint64_t nblk, uint64_t traces,
                              uint32_t *d_rd_state, int *d_err, uint64_t ss2, uint64_t W, uint32_t row_block,
                              uint32_t rank, uint32_t nranks, hipStream_t st);
 hipError_t launch_rng_finish_band(const uint32_t *d_seed, const uint32_t *d_jump, uint32_t *d_next_seed,
                                   const uint32_t *d_blk_cnt, uint64_t nblk, uint64_t traces, uint32_t *d_rd_state,
                                   int *d_err, uint64_t lo, uint64_t hi, uint64_t *d_off, uint32_t *d_range,
                                   hipStream_t st);
-hipError_t launch_rng_scan_emit(const uint32_t *d_seed, const uint32_t *d_jump, uint32_t *d_next_seed, uint64_t nblk,
-                                uint64_t traces, uint32_t *d_rd_state, int *d_err, uint64_t *d_look, uint32_t *d_ticket,
-                                uint32_t epoch, uint64_t ss2, uint64_t W, uint32_t row_block, uint32_t rank,
-                                uint32_t nranks, bool band, uint64_t lo, uint64_t hi, hipStream_t st);
 hipError_t launch_trace(const DevScene &S, const FrameParams &P, bool stats, hipStream_t st);
 hipError_t launch_prim_cull(const DevScene &S, const FrameParams &P, uint64_t *masks, hipStream_t st);
 hipError_t launch_queue_sort(const uint32_t *count, const uint32_t *key, uint32_t *hist, uint32_t *order, hipStream_t st);
@@ -486,8 +482,7 @@ struct rfx_renderer {
   uint32_t *d_blk_cnt = nullptr; uint64_t blk_cap = 0;
   uint64_t *d_blk_off = nullptr;     // band emits: the scanned block offsets ...
   uint32_t *d_rng_range = nullptr;   // ... and the band's first / last / final block
-  // single-pass pre-pass (rng_scan_emit): one look-back granule per block, the block ticket counter, the launch epoch
-  uint64_t *d_look = nullptr; uint32_t *d_ticket = nullptr; uint32_t look_epoch = 0;
+  uint16_t *d_rng_masks = nullptr;  // one device's accept flags per pre-pass thread (rng_count -> rng_emit)
   uint32_t *d_jump = nullptr;  // LCG jump table for blk_cap blocks (rng_jump_table)
   // host staging for rfx_render_frame_host
   float *d_img = nullptr; uint32_t *d_argb = nullptr; uint64_t *d_cnt = nullptr; size_t img_cap = 0;
@@ -631,8 +626,7 @@ extern "C" void rfx_renderer_destroy(rfx_renderer *r)
   (void)hipStreamSynchronize(r->stream);
   free_scene(r);
   (void)hipFree(r->d_seed); (void)hipFree(r->d_err); (void)hipFree(r->d_rd); (void)hipFree(r->d_rd_alt);
-  (void)hipFree(r->d_blk_cnt); (void)hipFree(r->d_jump); (void)hipFree(r->d_look); (void)hipFree(r->d_blk_off);
-  (void)hipFree(r->d_ticket);
+  (void)hipFree(r->d_blk_cnt); (void)hipFree(r->d_jump); (void)hipFree(r->d_rng_masks); (void)hipFree(r->d_blk_off);
   (void)hipFree(r->d_rng_range);
   (void)hipFree(r->d_img); (void)hipFree(r->d_argb); (void)hipFree(r->d_cnt);
   (void)hipFree(r->d_queue); (void)hipFree(r->d_qctr); (void)hipFree(r->d_prim_mask);
@@ -1136,19 +1130,12 @@ static int ensure_rng_workspace(rfx_renderer *r, uint64_t traces, uint64_t nblk)
   }
   if (nblk > r->blk_cap)
   {
-    (void)hipFree(r->d_blk_cnt); (void)hipFree(r->d_jump); (void)hipFree(r->d_look); (void)hipFree(r->d_blk_off);
-    r->d_blk_cnt = nullptr; r->d_jump = nullptr; r->d_look = nullptr; r->d_blk_off = nullptr; r->blk_cap = 0;
+    (void)hipFree(r->d_blk_cnt); (void)hipFree(r->d_jump); (void)hipFree(r->d_rng_masks); (void)hipFree(r->d_blk_off);
+    r->d_blk_cnt = nullptr; r->d_jump = nullptr; r->d_rng_masks = nullptr; r->d_blk_off = nullptr; r->blk_cap = 0;
     HIP_CHECK(hipMalloc(&r->d_blk_cnt, nblk * sizeof(uint32_t)));
     HIP_CHECK(hipMalloc(&r->d_blk_off, nblk * sizeof(uint64_t)));
     if (!r->d_rng_range) HIP_CHECK(hipMalloc(&r->d_rng_range, 4 * sizeof(uint32_t)));
-    // look-back granules: epoch 0 is never launched, so zeroed words are unready
-    HIP_CHECK(hipMalloc(&r->d_look, nblk * sizeof(uint64_t)));
-    HIP_CHECK(hipMemset(r->d_look, 0, nblk * sizeof(uint64_t)));
-    if (!r->d_ticket)
-    {
-      HIP_CHECK(hipMalloc(&r->d_ticket, sizeof(uint32_t)));
-      HIP_CHECK(hipMemset(r->d_ticket, 0, sizeof(uint32_t)));
-    }
+    HIP_CHECK(hipMalloc(&r->d_rng_masks, nblk * 256 * sizeof(uint16_t)));
     std::vector<uint32_t> jump(2 * (256 + nblk));
     rng_jump_table(nblk, jump.data());
     HIP_CHECK(hipMalloc(&r->d_jump, jump.size() * sizeof(uint32_t)));
@@ -1158,44 +1145,17 @@ static int ensure_rng_workspace(rfx_renderer *r, uint64_t traces, uint64_t nblk)
   return RFX_OK;
 }
 
-// The whole pre-pass on one device in one launch (rng_scan_emit: count, look-back scan and emit) into rd; the sphere
-// stream moves past the frame: d_seed[seed_idx] -> pre-pass -> the other word, which becomes current.  Frames of 2^31
-// traces or more (the look-back granules carry 31-bit counts) take the two-launch form.
-static int scan_emit(rfx_renderer *r, uint64_t nblk, uint64_t traces, uint32_t *rd, uint64_t ss2, uint64_t W,
-                     uint32_t row_block, uint32_t rank, uint32_t nranks, bool band, uint64_t lo, uint64_t hi,
-                     hipStream_t st)
-{
-  if (traces >= (1ull << 31) - (1ull << 24))
-  {
-    HIP_CHECK(launch_rng_count(seed_cur(r), r->d_jump, r->d_blk_cnt, 0, nblk, st));
-    if (band)
-      HIP_CHECK(launch_rng_finish_band(seed_cur(r), r->d_jump, seed_next(r), r->d_blk_cnt, nblk, traces, rd, r->d_err,
-                                       lo, hi, r->d_blk_off, r->d_rng_range, st));
-    else
-      HIP_CHECK(launch_rng_finish(seed_cur(r), r->d_jump, seed_next(r), r->d_blk_cnt, nblk, traces, rd, r->d_err, ss2, W,
-                                  row_block, rank, nranks, st));
-  }
-  else
-  {
-    if (++r->look_epoch == 0)  // after 2^32 launches: clear every granule before an epoch repeats
-    {
-      HIP_CHECK(hipMemsetAsync(r->d_look, 0, r->blk_cap * sizeof(uint64_t), st));
-      r->look_epoch = 1;
-    }
-    HIP_CHECK(launch_rng_scan_emit(seed_cur(r), r->d_jump, seed_next(r), nblk, traces, rd, r->d_err, r->d_look,
-                                   r->d_ticket, r->look_epoch, ss2, W, row_block, rank, nranks, band, lo, hi, st));
-  }
-  r->seed_idx ^= 1u;
-  return RFX_OK;
-}
-
-// Whole pre-pass on one device: every block counted here (rfx_rand_dirs).
+// Whole pre-pass on one device: every block counted here (the 1-GPU path, and the redundant form of the
+// multi-GPU one).  Sphere stream: d_seed[seed_idx] -> pre-pass -> the other word, which becomes current.
 static int enqueue_rng(rfx_renderer *r, uint64_t traces, hipStream_t st)
 {
   int rc;
   const uint64_t nblk = rng_layout(traces, 1, nullptr);
   if ((rc = ensure_rng_workspace(r, traces, nblk)) != RFX_OK) return rc;
-  if ((rc = scan_emit(r, nblk, traces, r->d_rd, 1, 1, 1, 0, 1, false, 0, UINT64_MAX, st)) != RFX_OK) return rc;
+  HIP_CHECK(launch_rng_count(seed_cur(r), r->d_jump, r->d_blk_cnt, 0, nblk, r->d_rng_masks, st));
+  HIP_CHECK(launch_rng_finish(seed_cur(r), r->d_jump, seed_next(r), r->d_blk_cnt, r->d_rng_masks, nblk, traces,
+                              r->d_rd, r->d_err, 1, 1, 1, 0, 1, st));
+  r->seed_idx ^= 1u;
   r->rewind_ok = false;
   return RFX_OK;
 }
@@ -1232,7 +1192,7 @@ extern "C" int rfx_frame_rng_count(rfx_renderer *r, const rfx_frame *f, uint32_t
   uint64_t bps = 0;
   const uint64_t nblk = rng_layout(pl.traces, nslices, &bps);
   if ((rc = ensure_rng_workspace(r, pl.traces, nblk)) != RFX_OK) return rc;
-  HIP_CHECK(launch_rng_count(seed_cur(r), r->d_jump, d_blk_counts, (uint64_t)slice * bps, bps, pl.st));
+  HIP_CHECK(launch_rng_count(seed_cur(r), r->d_jump, d_blk_counts, (uint64_t)slice * bps, bps, nullptr, pl.st));
   return RFX_OK;
 }
 
@@ -1281,26 +1241,17 @@ static int tile_schedule(rfx_renderer *r, FrameParams &P, hipStream_t st, uint64
 
 // The randDirs of a planned frame into rd (the scan of the counts and the scatter; the stream state moves past the
 // frame), then the caller's event, if any.
-static int emit_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *d_counts, uint64_t nblk, uint32_t *rd,
-                      hipEvent_t emitted)
+static int emit_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *d_counts, const uint16_t *d_masks, uint64_t nblk,
+                      uint32_t *rd, hipEvent_t emitted)
 {
   const FrameParams &P = pl.P;
   const hipStream_t st = pl.st;
   const uint64_t ss2 = P.ss > 0 ? (uint64_t)(P.ss * P.ss) : 1;
-  int rc;
-  if (!d_counts)  // one device counts every block: the single-pass pre-pass
-  {
-    if ((rc = scan_emit(r, nblk, pl.traces, rd, ss2, P.W, P.row_block, P.rank, P.nranks, pl.band, pl.band_lo,
-                        pl.band_hi, st)) != RFX_OK)
-      return rc;
-    if (emitted) HIP_CHECK(hipEventRecord(emitted, st));
-    return RFX_OK;
-  }
   if (pl.band)
     HIP_CHECK(launch_rng_finish_band(seed_cur(r), r->d_jump, seed_next(r), d_counts, nblk, pl.traces, rd, r->d_err,
                                      pl.band_lo, pl.band_hi, r->d_blk_off, r->d_rng_range, st));
   else
-    HIP_CHECK(launch_rng_finish(seed_cur(r), r->d_jump, seed_next(r), d_counts, nblk, pl.traces, rd,
+    HIP_CHECK(launch_rng_finish(seed_cur(r), r->d_jump, seed_next(r), d_counts, d_masks, nblk, pl.traces, rd,
                                 r->d_err, ss2, P.W, P.row_block, P.rank, P.nranks, st));
   r->seed_idx ^= 1u;
   // the caller's event: the randDirs are written and the next frame's stream state is known (the next frame's
@@ -1312,13 +1263,14 @@ static int emit_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *d_counts, 
 static int trace_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *rd, float *d_rgb, uint32_t *d_argb,
                        uint64_t *d_counters);
 
-static int finish_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *d_counts, uint64_t nblk, float *d_rgb,
-                        uint32_t *d_argb, uint64_t *d_counters, hipEvent_t emitted = nullptr)
+static int finish_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *d_counts, const uint16_t *d_masks,
+                        uint64_t nblk, float *d_rgb, uint32_t *d_argb, uint64_t *d_counters,
+                        hipEvent_t emitted = nullptr)
 {
   int rc;
   if (r->emit_pending >= 0)
     return fail(RFX_ERR_STATE, "render_frame: an emitted frame awaits rfx_render_frame_emitted (or rfx_frame_rng_discard)");
-  if ((rc = emit_frame(r, pl, d_counts, nblk, r->d_rd, emitted)) != RFX_OK) return rc;
+  if ((rc = emit_frame(r, pl, d_counts, d_masks, nblk, r->d_rd, emitted)) != RFX_OK) return rc;
   r->trace_buf = 0;
   if ((rc = timing_event(r, pl.st)) != RFX_OK) return rc;
   return trace_frame(r, pl, r->d_rd, d_rgb, d_argb, d_counters);
@@ -1462,7 +1414,7 @@ extern "C" int rfx_render_frame_counted_ev(rfx_renderer *r, const rfx_frame *f, 
   const uint64_t nblk = rng_layout(pl.traces, nslices, nullptr);
   if ((rc = ensure_rng_workspace(r, pl.traces, nblk)) != RFX_OK) return rc;
   if ((rc = timing_start(r, pl.st)) != RFX_OK) return rc;
-  return finish_frame(r, pl, d_blk_counts, nblk, d_rgb, d_argb, d_counters, (hipEvent_t)emitted_event);
+  return finish_frame(r, pl, d_blk_counts, nullptr, nblk, d_rgb, d_argb, d_counters, (hipEvent_t)emitted_event);
 }
 
 // What an emitted frame's randDirs depend on: the traces and their band, and the frame geometry that maps pixels to
@@ -1502,7 +1454,7 @@ extern "C" int rfx_frame_rng_emit(rfx_renderer *r, const rfx_frame *f, uint32_t 
     r->rd_alt_cap = pl.traces;
   }
   const int buf = r->trace_buf == 0 ? 1 : 0;  // not the buffer of the last enqueued trace
-  if ((rc = emit_frame(r, pl, d_blk_counts, nblk, buf ? r->d_rd_alt : r->d_rd,
+  if ((rc = emit_frame(r, pl, d_blk_counts, nullptr, nblk, buf ? r->d_rd_alt : r->d_rd,
                        (hipEvent_t)emitted_event)) != RFX_OK)
     return rc;
   r->emit_pending = buf;
@@ -1578,8 +1530,9 @@ extern "C" int rfx_render_frame(rfx_renderer *r, const rfx_frame *f, float *d_rg
   if ((rc = timing_start(r, pl.st)) != RFX_OK) return rc;
   if (r->emit_pending >= 0)
     return fail(RFX_ERR_STATE, "render_frame: an emitted frame awaits rfx_render_frame_emitted (or rfx_frame_rng_discard)");
-  // one device counts every block: count, scan and emit in one launch (rng_scan_emit)
-  if ((rc = finish_frame(r, pl, nullptr, nblk, d_rgb, d_argb, d_counters)) != RFX_OK) return rc;
+  // one device counts every block, so the emit can take its accept flags instead of regenerating them
+  HIP_CHECK(launch_rng_count(seed_cur(r), r->d_jump, r->d_blk_cnt, 0, nblk, r->d_rng_masks, pl.st));
+  if ((rc = finish_frame(r, pl, r->d_blk_cnt, r->d_rng_masks, nblk, d_rgb, d_argb, d_counters)) != RFX_OK) return rc;
   r->rewind_ok = true;
   r->rewind_flip = true;
   r->rewind_jitter = jitter0;
@@ -1739,7 +1692,6 @@ extern "C" int rfx_synchronize(rfx_renderer *r)
   HIP_CHECK(hipStreamSynchronize(r->stream));
   int err = 0;
   HIP_CHECK(hipMemcpy(&err, r->d_err, sizeof(int), hipMemcpyDeviceToHost));
-  if (err == 2) return fail(RFX_ERR_RNG, "RNG pre-pass: a look-back wait exceeded its bound");
   if (err) return fail(RFX_ERR_RNG, "RNG pre-pass ran short of accepted triples");
   return RFX_OK;
 }

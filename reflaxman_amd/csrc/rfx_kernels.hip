@@ -191,40 +191,24 @@ constexpr LcgJump lcg_jump_const(int draws)
 }
 constexpr LcgJump kHalfJump = lcg_jump_const(3 * kHalfRun);
 
-// A thread's 16-triple run from its start state s: the LCG state before each triple (st) and the accept flags
-// (acc, bit j for triple j); returns the accepted count.
-__device__ __forceinline__ uint32_t thread_run(uint32_t s, uint32_t (&st)[kTriplesPerThread], uint32_t &acc)
-{
-  uint32_t s2 = kHalfJump.a * s + kHalfJump.c, c = 0;
-  float x, y, z;
-  acc = 0;
-#pragma unroll
-  for (int j = 0; j < kHalfRun; ++j)
-  {
-    st[j] = s;
-    st[j + kHalfRun] = s2;
-    const bool a = triple(s, x, y, z), a2 = triple(s2, x, y, z);
-    acc |= (a ? 1u : 0u) << j | (a2 ? 1u : 0u) << (j + kHalfRun);
-    c += (a ? 1u : 0u) + (a2 ? 1u : 0u);
-  }
-  return c;
-}
-
 // accepted-triple count of blocks [blk0, blk0 + gridDim.x): one slice of the stream (multi-GPU: one per rank)
+// masks (optional, one device): each thread's 16 accept flags, so that rng_emit regenerates only the LCG states
 __global__ __launch_bounds__(kRngBlock) void rng_count(const uint32_t *seed, const uint32_t *jump, uint32_t *blk_cnt,
-                                                       uint64_t blk0)
+                                                       uint64_t blk0, uint16_t *masks)
 {
   const uint64_t b = blk0 + blockIdx.x;
   uint32_t s = thread_state(*seed, jump, b, threadIdx.x);
   uint32_t s2 = kHalfJump.a * s + kHalfJump.c;
-  uint32_t c = 0;
+  uint32_t c = 0, acc = 0;
   float x, y, z;
 #pragma unroll
   for (int j = 0; j < kHalfRun; ++j)
   {
     const bool a = triple(s, x, y, z), a2 = triple(s2, x, y, z);
+    acc |= (a ? 1u : 0u) << j | (a2 ? 1u : 0u) << (j + kHalfRun);
     c += (a ? 1u : 0u) + (a2 ? 1u : 0u);
   }
+  if (masks) masks[b * kRngBlock + threadIdx.x] = (uint16_t)acc;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
   __shared__ uint32_t wsum[kRngBlock / 64];
@@ -261,58 +245,10 @@ __device__ __forceinline__ bool owned(uint64_t idx, const EmitFilter &f)
 // LCG steps and three exact conversions.
 constexpr int kScanThreads = 1024;
 
-// Exclusive scan of the threads' accept counts c across the workgroup: this thread's block-local rank of its first
-// accepted triple; tot, the workgroup's count.  Every thread calls it (one barrier).
-__device__ __forceinline__ uint32_t block_rank(uint32_t c, uint32_t *wsum, uint32_t &tot)
-{
-  const uint32_t lane = threadIdx.x & 63;
-  uint32_t inc = c;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1)
-  {
-    const uint32_t v = __shfl_up(inc, o, 64);
-    if (lane >= (uint32_t)o) inc += v;
-  }
-  if (lane == 63) wsum[threadIdx.x >> 6] = inc;
-  __syncthreads();
-  uint32_t wbase = 0;
-  tot = 0;
-#pragma unroll
-  for (uint32_t w = 0; w < kRngBlock / 64; ++w)
-  {
-    wbase += w < (threadIdx.x >> 6) ? wsum[w] : 0u;
-    tot += wsum[w];
-  }
-  return wbase + (inc - c);
-}
-
-// The block's accepted triples, at block-local ranks li.. of each thread, become traces [off, off + cnt): their LCG
-// states go to LDS at their rank and leave with coalesced 4-byte stores (the traces this rank owns).  The thread
-// holding trace need-1's triple writes the state after it: the next frame's stream state.
-__device__ __forceinline__ void emit_states(uint64_t off, uint32_t cnt, uint32_t li, const uint32_t (&st)[kTriplesPerThread],
-                                            uint32_t acc, uint64_t need, uint32_t *rd_state, uint32_t *next_seed,
-                                            const EmitFilter &flt, uint32_t *sst)
-{
-#pragma unroll
-  for (int j = 0; j < kTriplesPerThread; ++j)
-    if ((acc >> j) & 1u)
-    {
-      if (off + li == need - 1) *next_seed = lcg_step(lcg_step(lcg_step(st[j])));
-      if (li < cnt) sst[li] = st[j];
-      ++li;
-    }
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < cnt; i += kRngBlock)
-  {
-    const uint64_t idx = off + i;
-    if (owned(idx, flt)) rd_state[idx] = sst[i];
-  }
-}
-
 // One block of the emit: block b's accepted triples are the traces [off, off + blk_cnt[b]).  Every thread of the
 // workgroup calls it with the same b and off.
 __device__ __forceinline__ void emit_block(uint32_t b, uint64_t off, const uint32_t *seed, const uint32_t *jump,
-                                           const uint32_t *blk_cnt, uint64_t need,
+                                           const uint32_t *blk_cnt, const uint16_t *masks, uint64_t need,
                                            uint32_t *rd_state, uint32_t *next_seed, const EmitFilter &flt,
                                            uint32_t *sst, uint32_t *wsum)
 {
@@ -329,15 +265,70 @@ __device__ __forceinline__ void emit_block(uint32_t b, uint64_t off, const uint3
     for (uint64_t st = s_lo; st <= s_hi && !any; ++st) any = (st % flt.nranks) == flt.rank;
     if (!any) return;
   }
-  uint32_t st[kTriplesPerThread], acc;
-  const uint32_t c = thread_run(thread_state(*seed, jump, b, threadIdx.x), st, acc);
-  uint32_t tot;
-  const uint32_t li = block_rank(c, wsum, tot);
-  emit_states(off, cnt, li, st, acc, need, rd_state, next_seed, flt, sst);
+  uint32_t s = thread_state(*seed, jump, b, threadIdx.x);
+  uint32_t s2 = kHalfJump.a * s + kHalfJump.c;
+  uint32_t st[kTriplesPerThread];
+  uint32_t acc = 0, c = 0;
+  if (masks)
+  {
+    // the accept flags rng_count recorded: only the LCG states are regenerated (3 steps per triple)
+    acc = masks[(uint64_t)b * kRngBlock + threadIdx.x];
+    c = (uint32_t)__popc(acc);
+#pragma unroll
+    for (int j = 0; j < kHalfRun; ++j)
+    {
+      st[j] = s;
+      st[j + kHalfRun] = s2;
+      s = lcg_step(lcg_step(lcg_step(s)));
+      s2 = lcg_step(lcg_step(lcg_step(s2)));
+    }
+  }
+  else
+  {
+    float x, y, z;
+#pragma unroll
+    for (int j = 0; j < kHalfRun; ++j)
+    {
+      st[j] = s;
+      st[j + kHalfRun] = s2;
+      const bool a = triple(s, x, y, z), a2 = triple(s2, x, y, z);
+      acc |= (a ? 1u : 0u) << j | (a2 ? 1u : 0u) << (j + kHalfRun);
+      c += (a ? 1u : 0u) + (a2 ? 1u : 0u);
+    }
+  }
+  // exclusive scan of c across the workgroup
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t inc = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1)
+  {
+    const uint32_t v = __shfl_up(inc, o, 64);
+    if (lane >= (uint32_t)o) inc += v;
+  }
+  if (lane == 63) wsum[threadIdx.x >> 6] = inc;
+  __syncthreads();
+  uint32_t wbase = 0;
+  for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) wbase += wsum[w];
+  uint32_t li = wbase + (inc - c);                                               // block-local rank
+#pragma unroll
+  for (int j = 0; j < kTriplesPerThread; ++j)
+    if ((acc >> j) & 1u)
+    {
+      // trace need-1's triple: the stream state after it is the next frame's state
+      if (off + li == need - 1) *next_seed = lcg_step(lcg_step(lcg_step(st[j])));
+      if (li < cnt) sst[li] = st[j];
+      ++li;
+    }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < cnt; i += kRngBlock)
+  {
+    const uint64_t idx = off + i;
+    if (owned(idx, flt)) rd_state[idx] = sst[i];
+  }
 }
 
 __global__ __launch_bounds__(kRngBlock) void rng_emit(const uint32_t *seed, const uint32_t *jump, const uint32_t *blk_cnt,
-                                                      uint64_t need, uint32_t *rd_state,
+                                                      const uint16_t *masks, uint64_t need, uint32_t *rd_state,
                                                       uint32_t *next_seed, int *err, EmitFilter flt)
 {
   __shared__ uint32_t sst[kTriplesPerBlock];
@@ -356,112 +347,7 @@ __global__ __launch_bounds__(kRngBlock) void rng_emit(const uint32_t *seed, cons
   const uint64_t off = s_off;
   // the last block flags a stream too short for the frame (host: RFX_ERR_RNG)
   if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0 && off + blk_cnt[blockIdx.x] < need) *err = 1;
-  emit_block(blockIdx.x, off, seed, jump, blk_cnt, need, rd_state, next_seed, flt, sst, wsum);
-}
-
-// Single-pass pre-pass (one device counts the whole stream: rfx_render_frame): count, scan and emit in one launch.
-// Each block generates its 4096 triples once and keeps their LCG states in registers, publishes its accept count, learns
-// the counts before it by a decoupled look-back, publishes its inclusive prefix and writes its traces' states -- one
-// launch and one LCG pass instead of rng_count + rng_emit.
-//
-// Look-back granules (MI355X_MICROARCH.md, inter-workgroup visibility: the data is the flag): one 8-byte word per
-// block, {tag = this launch's epoch, value}; value bit 31 marks an inclusive prefix, else the block's own count.  Every
-// access to a granule, and to the ticket counter, is an agent-scope read-modify-write atomic (exchange to publish,
-// add 0 to poll), so all of them meet at the one point where the chip's atomics are ordered, whichever XCD's L2 the
-// block runs under.  A new epoch per launch makes every older word unready, so the words need no reset.  Blocks take
-// their stream position from a ticket counter, not blockIdx: a block waits only on tickets taken before its own, by
-// blocks already running, so the look-back makes progress whatever the dispatch order.  The block taking the last
-// ticket resets the counter for the next launch.  Every spin is bounded (err = 2, rfx_synchronize reports it).
-constexpr uint32_t kLookPrefix = 0x80000000u;
-constexpr uint32_t kLookSpinLimit = 1u << 16;
-
-__device__ __forceinline__ void look_put(uint64_t *g, uint32_t epoch, uint32_t v)
-{
-  (void)__hip_atomic_exchange(g, ((uint64_t)epoch << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ uint64_t look_get(uint64_t *g)
-{
-  uint64_t zero = 0;
-  asm volatile("" : "+v"(zero));  // opaque: the compiler turns a literal add-0 into a plain atomic load
-  return __hip_atomic_fetch_add(g, zero, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ uint32_t wave_sum(uint32_t v)
-{
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-
-// Wave 0 of block b > 0: the accepted triples of blocks [0, b), from the nearest predecessor holding its inclusive
-// prefix plus the counts after it.  Windows of 64 predecessors, newest first; a window is used up to its first
-// prefix once every granule before that is ready.
-__device__ __forceinline__ uint32_t look_back(uint64_t *look, uint32_t b, uint32_t epoch, int *err)
-{
-  const int64_t lane = threadIdx.x & 63;
-  uint32_t excl = 0, spins = 0;
-  for (int64_t top = (int64_t)b - 1; top >= 0;)
-  {
-    const int64_t idx = top - lane;
-    const uint64_t x = idx >= 0 ? look_get(look + idx) : 0ull;
-    const bool ready = idx < 0 || (uint32_t)(x >> 32) == epoch;
-    const bool prefix = idx >= 0 && ready && ((uint32_t)x & kLookPrefix);
-    const uint64_t unready = __ballot(!ready), pm = __ballot(prefix);
-    const int first_nr = unready ? __builtin_ctzll(unready) : 64, first_p = pm ? __builtin_ctzll(pm) : 64;
-    if (first_p < first_nr)
-      return excl + wave_sum(lane <= first_p ? ((uint32_t)x & ~kLookPrefix) : 0u);
-    if (first_nr == 64)
-    {
-      excl += wave_sum(idx >= 0 ? (uint32_t)x : 0u);  // 64 counts, no prefix among them
-      top -= 64;
-      continue;
-    }
-    if (++spins > kLookSpinLimit)
-    {
-      if (lane == 0) (void)__hip_atomic_exchange(err, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return 0;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-  return excl;
-}
-
-__global__ __launch_bounds__(kRngBlock) void rng_scan_emit(const uint32_t *seed, const uint32_t *jump, uint64_t need,
-                                                           uint32_t *rd_state, uint32_t *next_seed, int *err,
-                                                           uint64_t *look, uint32_t *ticket, uint32_t nblk,
-                                                           uint32_t epoch, EmitFilter flt)
-{
-  __shared__ uint32_t sst[kTriplesPerBlock];
-  __shared__ uint32_t wsum[kRngBlock / 64];
-  __shared__ uint32_t s_b, s_excl;
-  if (threadIdx.x == 0)
-  {
-    const uint32_t t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (t == nblk - 1) (void)__hip_atomic_exchange(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_b = t;
-  }
-  __syncthreads();
-  const uint32_t b = s_b;
-  uint32_t st[kTriplesPerThread], acc;
-  const uint32_t c = thread_run(thread_state(*seed, jump, b, threadIdx.x), st, acc);
-  uint32_t tot;
-  const uint32_t li = block_rank(c, wsum, tot);
-  if (threadIdx.x < 64)
-  {
-    if (threadIdx.x == 0) look_put(look + b, epoch, b == 0 ? (kLookPrefix | tot) : tot);
-    const uint32_t excl = b == 0 ? 0u : look_back(look, b, epoch, err);
-    if (threadIdx.x == 0)
-    {
-      if (b != 0) look_put(look + b, epoch, kLookPrefix | (excl + tot));
-      s_excl = excl;
-      if (b == nblk - 1 && (uint64_t)excl + tot < need) *err = 1;  // stream too short for the frame (RFX_ERR_RNG)
-    }
-  }
-  __syncthreads();
-  const uint64_t off = s_excl;
-  if (off >= need) return;
-  emit_states(off, (uint32_t)min((uint64_t)tot, need - off), li, st, acc, need, rd_state, next_seed, flt, sst);
+  emit_block(blockIdx.x, off, seed, jump, blk_cnt, masks, need, rd_state, next_seed, flt, sst, wsum);
 }
 
 // Band emit (multi-GPU band partition): only the blocks holding the band's traces [flt.lo, flt.hi), and the block of
@@ -549,7 +435,7 @@ __global__ __launch_bounds__(kRngBlock) void rng_emit_band(const uint32_t *seed,
   {
     const uint32_t b = j <= last - first ? first + j : fin;
     if (b >= nblk) break;  // (a stream too short for the frame leaves the range unset: the error flag is raised)
-    emit_block(b, off[b], seed, jump, blk_cnt, need, rd_state, next_seed, flt, sst, wsum);
+    emit_block(b, off[b], seed, jump, blk_cnt, nullptr, need, rd_state, next_seed, flt, sst, wsum);
     __syncthreads();  // sst / wsum are reused by the next block
   }
 }
@@ -716,38 +602,23 @@ void rng_jump_table(uint64_t nblk, uint32_t *out)
 
 // first half of the pre-pass: accept counts of blocks [blk0, blk0 + nblk_slice)
 hipError_t launch_rng_count(const uint32_t *d_seed, const uint32_t *d_jump, uint32_t *d_blk_cnt, uint64_t blk0,
-                            uint64_t nblk_slice, hipStream_t st)
+                            uint64_t nblk_slice, uint16_t *d_masks, hipStream_t st)
 {
   if (nblk_slice)
-    hipLaunchKernelGGL(rng_count, dim3((uint32_t)nblk_slice), dim3(kRngBlock), 0, st, d_seed, d_jump, d_blk_cnt, blk0);
+    hipLaunchKernelGGL(rng_count, dim3((uint32_t)nblk_slice), dim3(kRngBlock), 0, st, d_seed, d_jump, d_blk_cnt, blk0,
+                       d_masks);
   return hipGetLastError();
 }
 
 // second half: scan all nblk counts, scatter the randDirs this rank needs, carry the stream state
 hipError_t launch_rng_finish(const uint32_t *d_seed, const uint32_t *d_jump, uint32_t *d_next_seed,
-                             const uint32_t *d_blk_cnt, uint64_t nblk, uint64_t traces,
+                             const uint32_t *d_blk_cnt, const uint16_t *d_masks, uint64_t nblk, uint64_t traces,
                              uint32_t *d_rd_state, int *d_err, uint64_t ss2, uint64_t W, uint32_t row_block,
                              uint32_t rank, uint32_t nranks, hipStream_t st)
 {
   const EmitFilter flt{ss2 ? ss2 : 1, W ? W : 1, row_block ? row_block : 1, rank, nranks ? nranks : 1, 0, UINT64_MAX};
-  hipLaunchKernelGGL(rng_emit, dim3((uint32_t)nblk), dim3(kRngBlock), 0, st, d_seed, d_jump, d_blk_cnt, traces, d_rd_state,
-                     d_next_seed, d_err, flt);
-  return hipGetLastError();
-}
-
-// the whole pre-pass in one launch (rng_scan_emit): every block of the stream, the randDirs this device owns -- strips
-// (nranks > 1, row_block > 0) or, with band, the traces [lo, hi) -- and the next frame's stream state.  d_look: nblk
-// granules; d_ticket: one word, 0 before the first launch (each launch leaves it 0); epoch: never 0, new per launch.
-hipError_t launch_rng_scan_emit(const uint32_t *d_seed, const uint32_t *d_jump, uint32_t *d_next_seed, uint64_t nblk,
-                                uint64_t traces, uint32_t *d_rd_state, int *d_err, uint64_t *d_look, uint32_t *d_ticket,
-                                uint32_t epoch, uint64_t ss2, uint64_t W, uint32_t row_block, uint32_t rank,
-                                uint32_t nranks, bool band, uint64_t lo, uint64_t hi, hipStream_t st)
-{
-  const EmitFilter flt = band ? EmitFilter{1, 1, 1, 0, 1, lo, hi}
-                              : EmitFilter{ss2 ? ss2 : 1, W ? W : 1, row_block ? row_block : 1, rank, nranks ? nranks : 1,
-                                           0, UINT64_MAX};
-  hipLaunchKernelGGL(rng_scan_emit, dim3((uint32_t)nblk), dim3(kRngBlock), 0, st, d_seed, d_jump, traces, d_rd_state,
-                     d_next_seed, d_err, d_look, d_ticket, (uint32_t)nblk, epoch, flt);
+  hipLaunchKernelGGL(rng_emit, dim3((uint32_t)nblk), dim3(kRngBlock), 0, st, d_seed, d_jump, d_blk_cnt, d_masks,
+                     traces, d_rd_state, d_next_seed, d_err, flt);
   return hipGetLastError();
 }
 

@@ -3,9 +3,11 @@
 one process -- the wall time to enqueue the K frames (no synchronisation) and the wall time until they are complete.
 When enqueueing takes as long as rendering, the frame rate is bound by the host's launch path, not by the GPU.
 
-Forms: "single" -- rfx_render_frame, whose pre-pass is one launch (rng_scan_emit: count, look-back scan, emit);
-"two" -- rfx_frame_rng_count + rfx_render_frame_counted, the two-launch pre-pass the multi-GPU slices use
-(rng_count, then rng_emit).  Both render the same pixels (tests/test_gpu_prepass.py).
+Forms: "single" -- rfx_render_frame (rng_count recording each thread's accept flags, then rng_emit regenerating only
+the accepted states); "two" -- rfx_frame_rng_count + rfx_render_frame_counted, the sliced pre-pass the multi-GPU ranks
+use (rng_count, then rng_emit re-running the accept tests).  Both render the same pixels (tests/test_gpu_steady.py).
+Round 3 also timed a one-launch form here (rng_scan_emit, commit d409089: count, decoupled look-back, emit) against
+"two": DESIGN.md, measured and dropped.
 
     python tools/frame_host_cost.py [--scene default --width 640 --height 480 --depth 4 --frames 400]
 """
