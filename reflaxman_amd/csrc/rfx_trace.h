@@ -1513,6 +1513,39 @@ __device__ __forceinline__ v3 rd_from_state(uint32_t s)
 
 __device__ __forceinline__ v3 load_rd(const FrameParams &P, uint64_t i) { return rd_from_state(P.rd_state[i]); }
 
+// Diagnostic build only (RFX_DEBUG_WAVES, tools/wave_timeline.py): each plain-mode wave's start and end on the
+// chip's constant 100 MHz clock (s_memrealtime), by wave tile, for the last launch -- the shape of a launch's
+// critical path (dispatch ramp, tile durations, tail).
+#ifdef RFX_DEBUG_WAVES
+constexpr uint32_t kWaveTimeMax = 1u << 18;
+constexpr uint32_t kBounceTimeBase = 1u << 17;  // the bounce kernel's 64-trace batches, after the trace kernel's tiles
+static __device__ unsigned long long g_wave_time[2 * kWaveTimeMax];
+__device__ __forceinline__ uint64_t realtime64()
+{
+  uint64_t c;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(c));
+  return c;
+}
+#define RFX_WAVE_T0() const uint64_t wave_t0_ = realtime64()
+#define RFX_WAVE_T1(tile)                                                                  \
+  do {                                                                                      \
+    const uint64_t t1_ = realtime64();                                                     \
+    if (__lane_id() == 0 && (tile) < kWaveTimeMax)                                         \
+    {                                                                                       \
+      g_wave_time[2 * (tile)] = wave_t0_;                                                   \
+      g_wave_time[2 * (tile) + 1] = t1_;                                                    \
+    }                                                                                       \
+  } while (0)
+#else
+constexpr uint32_t kBounceTimeBase = 0;
+#define RFX_WAVE_T0() \
+  do {                \
+  } while (0)
+#define RFX_WAVE_T1(tile) \
+  do {                    \
+  } while (0)
+#endif
+
 // Shader clock, low 32 bits.  A plain asm statement (no side effects declared, so the compiler may still
 // serve the scene loads that follow through the scalar cache -- __builtin_readcyclecounter would count as a
 // memory clobber for them); it waits for its own result.
@@ -1564,6 +1597,7 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
 {
   constexpr bool CULL = (CFG & kCfgCull) != 0, MANYL = (CFG & kCfgManyLights) != 0, SMALL = (CFG & kCfgSmall) != 0;
   constexpr bool PLANES = (CFG & kCfgPlanes) != 0, PARK = MODE == kModePlain && !STATS && (CFG & kCfgPark) != 0;
+  RFX_WAVE_T0();
   __shared__ float lut[256];
   for (uint32_t i = threadIdx.x; i < 256; i += kWgThreads) lut[i] = (float)i / 255.0f;  // Color.cpp:11-13
   stage_powf_tables();
@@ -1703,6 +1737,7 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
     }
     if (P.tile_cost && __lane_id() == 0)  // per wave tile, from its output coordinates
       P.tile_cost[(P.nranks > 1 ? rowe : rowe - P.row0) / 8u * P.tiles_x + xe / 8u] = clock32() - s_clk0;
+    RFX_WAVE_T1(t8e);
   }
   flush_counters<STATS>(P, cnt);
   RFX_PROF_FLUSH();
@@ -1811,6 +1846,7 @@ __global__ RFX_TRACE_BOUNDS void bounce_kernel(DevScene S, FrameParams P)
     if (lane == 0) base = atomicAdd(P.queue_next, 64u);
     base = __builtin_amdgcn_readfirstlane(base);
     if (base >= n) break;
+    RFX_WAVE_T0();
     const uint32_t i = base + lane;
     const bool valid = i < n;
     QRay q{};
@@ -1827,6 +1863,7 @@ __global__ RFX_TRACE_BOUNDS void bounce_kernel(DevScene S, FrameParams P)
       d[0] = out.r; d[1] = out.g; d[2] = out.b;
       if (P.argb) P.argb[q.out] = argb(out);
     }
+    RFX_WAVE_T1(kBounceTimeBase + base / 64u);
   }
 }
 

@@ -34,3 +34,14 @@ extern "C" int rfx_debug_prof_read(unsigned long long *out, int reset)
   return 2 * rfx::P_COUNT;
 }
 #endif
+
+#ifdef RFX_DEBUG_WAVES
+// each wave tile's (start, end) s_memrealtime of the last plain launch, tiles [0, n); returns the tiles read
+extern "C" int rfx_debug_wave_time_read(unsigned long long *out, int n)
+{
+  if (n < 0 || (uint32_t)n > rfx::kWaveTimeMax) n = (int)rfx::kWaveTimeMax;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rfx::g_wave_time), 2 * (size_t)n * sizeof(unsigned long long)) != hipSuccess)
+    return -1;
+  return n;
+}
+#endif

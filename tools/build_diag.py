@@ -1,9 +1,10 @@
 """Build the diagnostic librfx variants tools/regionprof.py and tools/segstats.py load (CPU; hipcc only).
 
-    python tools/build_diag.py      # -> reflaxman_amd/lib/diag/librfx_{prof,segs}.so
+    python tools/build_diag.py      # -> reflaxman_amd/lib/diag/librfx_{prof,segs,waves}.so
 
 librfx_prof.so: RFX_DEBUG_PROF (s_memtime region sums and bundle cull statistics);
-librfx_segs.so: RFX_DEBUG_SEGS (each trace's segment count replaces its colour).
+librfx_segs.so: RFX_DEBUG_SEGS (each trace's segment count replaces its colour);
+librfx_waves.so: RFX_DEBUG_WAVES (each plain-mode wave's start and end time, tools/wave_timeline.py).
 """
 import os
 import shutil
@@ -14,7 +15,7 @@ sys.path.insert(0, ROOT)
 
 from reflaxman_amd import _build  # noqa: E402
 
-DIAG = {"prof": ["RFX_DEBUG_PROF"], "segs": ["RFX_DEBUG_SEGS"]}
+DIAG = {"prof": ["RFX_DEBUG_PROF"], "segs": ["RFX_DEBUG_SEGS"], "waves": ["RFX_DEBUG_WAVES"]}
 
 
 def main():
