@@ -94,6 +94,7 @@ SIGNATURES = [
     ("rfx_renderer_set_timing", C.c_int, [C.c_void_p, C.c_int]),
     ("rfx_renderer_set_tile_order", C.c_int, [C.c_void_p, C.c_int]),
     ("rfx_renderer_set_prim_masks", C.c_int, [C.c_void_p, C.c_int]),
+    ("rfx_renderer_set_tile_split", C.c_int, [C.c_void_p, C.c_int]),
     ("rfx_renderer_set_regroup", C.c_int, [C.c_void_p, C.c_int]),
     ("rfx_renderer_set_regroup_sort", C.c_int, [C.c_void_p, C.c_int]),
     ("rfx_renderer_get_timing", C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double), _u64p]),
@@ -117,10 +118,13 @@ def lib_path() -> str:
     return _build.LIB
 
 
-def bind(path: str):
-    """Load and bind any build of librfx.so (e.g. a variant build for A/B timing)."""
+def bind(path: str, partial: bool = False):
+    """Load and bind any build of librfx.so (e.g. a variant build for A/B timing).  partial: an older build (tools/
+    build_rev.py) may lack entry points added since; those are left unbound instead of failing."""
     L = C.CDLL(os.path.abspath(path))
     for name, res, args in SIGNATURES:
+        if partial and not hasattr(L, name):
+            continue
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args

@@ -54,6 +54,9 @@ VARIANTS = {
     "qsort": ["RFX_QUEUE_SORT=1"],
     "lpt16k": ["RFX_TILE_ORDER_MIN_TILES=16384"],
     "lpt4k": ["RFX_TILE_ORDER_MIN_TILES=4096"],
+    "nosplit": ["RFX_SPLIT_MAX_TILES=0"],
+    "split16k": ["RFX_SPLIT_MAX_TILES=16384"],
+    "split40k": ["RFX_SPLIT_MAX_TILES=40000"],
 }
 
 
@@ -94,7 +97,7 @@ def build_scene_with(L, desc):
 class Runner:
     def __init__(self, name, path, desc, W, H, depth, seed, tile_order=None, regroup=None, prim=None):
         self.name = name
-        L = self.L = _lib.bind(path)
+        L = self.L = _lib.bind(path, partial=True)
         self.scene, eye, view, fov = build_scene_with(L, desc)
         self.r = C.c_void_p()
         rc = L.rfx_renderer_create(C.byref(self.r), 0)
