@@ -125,11 +125,6 @@ int rfx_renderer_set_regroup_sort(rfx_renderer *r, int on);
  * view stays.  1 (default) = built when a view repeats (the second frame of a still camera on), so a camera that
  * moves every frame never pays for them; 2 = built before every launch; 0 = off (per-launch bundles). */
 int rfx_renderer_set_prim_masks(rfx_renderer *r, int mode);
-/* Split tiles (no pixel changes): plain frames traced in raster order give each 8x8 tile a workgroup of two waves,
- * four rows each, instead of one wave -- for small frames, whose waves all fit the chip at once and whose frame time is
- * the latency of their longest tiles.  1 (default) = frames of at most 8192 tiles (640x480: 4,800), 2 = every plain
- * frame without a tile schedule, 0 = off. */
-int rfx_renderer_set_tile_split(rfx_renderer *r, int mode);
 /* The reference's two LCG streams (trace_math.h:34-39): Vector3.cpp's (randomInsideSphere) and
  * Render.cpp's (additive jitter).  Both persist across frames exactly as the reference's would. */
 int rfx_renderer_set_rng(rfx_renderer *r, uint32_t sphere_seed, uint32_t jitter_seed);

@@ -94,7 +94,6 @@ SIGNATURES = [
     ("rfx_renderer_set_timing", C.c_int, [C.c_void_p, C.c_int]),
     ("rfx_renderer_set_tile_order", C.c_int, [C.c_void_p, C.c_int]),
     ("rfx_renderer_set_prim_masks", C.c_int, [C.c_void_p, C.c_int]),
-    ("rfx_renderer_set_tile_split", C.c_int, [C.c_void_p, C.c_int]),
     ("rfx_renderer_set_regroup", C.c_int, [C.c_void_p, C.c_int]),
     ("rfx_renderer_set_regroup_sort", C.c_int, [C.c_void_p, C.c_int]),
     ("rfx_renderer_get_timing", C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double), _u64p]),

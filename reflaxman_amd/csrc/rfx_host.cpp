@@ -442,12 +442,6 @@ extern "C" uint32_t rfx_strip_row_to_y(uint32_t r, uint32_t rb, uint32_t rank, u
 #define RFX_TILE_ORDER_MIN_TILES 49152
 #endif
 constexpr size_t kPrimWords = 5;  // per wave tile (rfx_trace.h kPrimStride)
-#ifndef RFX_SPLIT_MAX_TILES
-// split tiles (rfx_renderer_set_tile_split mode 1): plain frames of at most this many 8x8 tiles, i.e. frames whose waves
-// all fit the chip's wave slots at once (C1 640x480: 4,800 tiles; 256 CUs x 4 SIMDs x 7 waves = 7,168 slots), so that
-// the frame is the latency of its longest tiles (tools/wave_timeline.py)
-#define RFX_SPLIT_MAX_TILES 8192
-#endif
 
 #ifndef RFX_QUEUE_SORT
 // regrouped frames: the bounce kernel takes the parked traces bucket by bucket (1) or in park order (0).  tools/ab.py,
@@ -514,7 +508,6 @@ struct rfx_renderer {
   std::vector<uint8_t> prim_seen;  // the view of the last plain small-scene launch
   uint64_t scene_gen = 0;  // bumped by every set_scene
   int prim_mode = 1;       // rfx_renderer_set_prim_masks
-  int split_mode = 1;      // rfx_renderer_set_tile_split
   QRay *d_queue = nullptr;
   uint64_t queue_cap = 0;
   uint32_t *d_qctr = nullptr;   // count, claim counter, then the sort's kQueueBuckets histogram words
@@ -663,13 +656,6 @@ extern "C" int rfx_renderer_set_prim_masks(rfx_renderer *r, int mode)
   r->prim_mode = mode;
   r->prim_key.clear();
   r->prim_seen.clear();
-  return RFX_OK;
-}
-
-extern "C" int rfx_renderer_set_tile_split(rfx_renderer *r, int mode)
-{
-  if (!r || mode < 0 || mode > 2) return fail(RFX_ERR_ARG, "renderer_set_tile_split: mode 0, 1 or 2");
-  r->split_mode = mode;
   return RFX_OK;
 }
 
@@ -1341,10 +1327,6 @@ static int trace_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *rd, float
   uint64_t key = 0;
   bool record = false;
   if (sched && (rc = tile_schedule(r, P, st, key, record)) != RFX_OK) return rc;
-  // split tiles: plain frames traced in raster order whose tiles all fit the wave slots at once (mode 1), or every
-  // such frame (mode 2): two waves per 8x8 tile, so the longest tiles -- the frame's critical path -- finish sooner
-  P.split = plain && !park && !sched && !d_counters && P.grid_rows && r->split_mode &&
-            (r->split_mode == 2 || trace_tiles(P) <= RFX_SPLIT_MAX_TILES);
   // primary-bundle cull masks: small scenes, plain frames, culling launches; recomputed only when the camera,
   // the frame geometry or the scene changed (the bench's frames all reuse one set)
   if (small && plain && !d_counters && !park && P.grid_rows && r->prim_mode)

@@ -695,11 +695,9 @@ hipError_t launch_prim_cull(const DevScene &S, const FrameParams &P, uint64_t *m
 
 hipError_t launch_trace(const DevScene &S, const FrameParams &P, bool stats, hipStream_t st)
 {
-  const dim3 g = trace_grid(P);
-  // split tiles: one workgroup per 8x8 tile of the same tile grid (trace_kernel)
-  const dim3 grid = P.split ? dim3(kTileWavesX * g.x, kTileWavesY * g.y) : g;
+  const dim3 grid = trace_grid(P);
   FrameParams Pt = P;
-  Pt.tiles_x = kTileWavesX * g.x;  // wave tiles per row (the schedule's unit)
+  Pt.tiles_x = kTileWavesX * grid.x;  // wave tiles per row (the schedule's unit)
   const int mode = P.ss < 0 ? kModeBlock : (P.ss == 1 && !P.additive && !P.accumulate) ? kModePlain : kModeSsaa;
   // the stats build counts the reference's every test, so it never culls
   const int cfg = (S.n_light > 32 ? kCfgManyLights : 0) | (stats ? 0 : kCfgCull) |

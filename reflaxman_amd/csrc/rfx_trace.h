@@ -1619,14 +1619,10 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
   // tile grid -- with a tile order (longest-processing-time first, from an earlier launch's measured tile costs)
   // the most expensive tiles start first and the cheap ones fill the tail; without, the workgroup's own tiles
   const uint32_t wv = __builtin_amdgcn_readfirstlane(wave), wid = blockIdx.y * gridDim.x + blockIdx.x;
-  // split tiles (plain pixels of small frames, FrameParams::split): workgroup w takes tile w (same numbering: the grid is
-  // the tile grid), wave v its rows 4v..4v+3 on lanes 0-31
-  const bool split = MODE == kModePlain && P.split;
-  const uint32_t w8 = split ? gridDim.x : kTileWavesX * gridDim.x;
-  const uint32_t t8 = split ? wid
-                    : P.tile_order ? P.tile_order[kWgWaves * wid + wv]
+  const uint32_t w8 = kTileWavesX * gridDim.x;
+  const uint32_t t8 = P.tile_order ? P.tile_order[kWgWaves * wid + wv]
                                    : (blockIdx.y * kTileWavesY + wv / kTileWavesX) * w8 + blockIdx.x * kTileWavesX + wv % kTileWavesX;
-  const uint32_t gx = (t8 % w8) * 8u + (lane & 7u), gy = (t8 / w8) * 8u + (split ? 4u * wv : 0u) + (lane >> 3);
+  const uint32_t gx = (t8 % w8) * 8u + (lane & 7u), gy = (t8 / w8) * 8u + (lane >> 3);
   // the tile index waits in LDS across the bounce loop: the epilogue re-derives the output coordinates from it
   // instead of keeping (spilling) them
   if (lane == 0) s_tile8[wv] = t8;
@@ -1668,7 +1664,7 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
     const uint32_t x = gx;
     const uint32_t y = P.nranks > 1 ? strip_row_to_y(gy, P) : gy + P.row0;
     const uint64_t p = (uint64_t)y * P.W + x;
-    const bool valid = gx < P.W && gy < P.grid_rows && p >= P.p_begin && p < P.p_end && (!split || lane < 32u);
+    const bool valid = gx < P.W && gy < P.grid_rows && p >= P.p_begin && p < P.p_end;
     const uint64_t pr = p - P.p_begin;
     const float rx = (float)x - P.wh, ry = (float)y - P.hh;                       // Render.cpp:152-153
     col out;
@@ -1720,7 +1716,7 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
     const uint32_t t8e = ((volatile uint32_t *)s_tile8)[wv];
     uint32_t le = lane;
     asm volatile("" : "+v"(le));  // a fresh lane value: its row/column are recomputed, not kept live
-    const uint32_t x0e = (t8e % w8) * 8u, row0e = (t8e / w8) * 8u + (split ? 4u * wv : 0u) + (P.nranks > 1 ? 0u : P.row0);
+    const uint32_t x0e = (t8e % w8) * 8u, row0e = (t8e / w8) * 8u + (P.nranks > 1 ? 0u : P.row0);
     const uint32_t xe = x0e + (le & 7u), rowe = row0e + (le >> 3), wslot = wv;
     if (MODE == kModeSsaa && P.accumulate && valid)                                  // Render.cpp:191-194
     {

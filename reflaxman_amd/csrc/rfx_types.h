@@ -127,9 +127,6 @@ struct FrameParams {
   const uint32_t *tile_order;   // workgroup i renders tile tile_order[i] (previous frame's LPT order), or null: tile i
   uint32_t *tile_cost;          // per tile: its clock cycles this frame (the next frame's order), or null
   uint32_t tiles_x;             // schedule tiles per grid row (set by launch_trace)
-  // split tiles (plain pixels, small frames): each workgroup takes ONE 8x8 tile and its two waves 4 rows each, lanes
-  // 32-63 idle -- a latency-bound frame's longest tiles then run on two SIMDs at once (rfx_renderer_set_tile_split)
-  uint32_t split;
   // ray regrouping (plain pixels, large scenes): a trace still alive after park_after segments is appended to
   // queue (queue_count: entries) instead of continuing; the bounce kernel then runs the queue in packed waves,
   // claiming 64 entries at a time from queue_next.  park_after <= 0: no parking.

@@ -311,11 +311,6 @@ class Renderer:
         a view repeats (default), 2 before every launch, 0 off.  No pixel changes."""
         check(_lib.load().rfx_renderer_set_prim_masks(self._h, int(mode)), "set_prim_masks")
 
-    def set_tile_split(self, mode: int):
-        """Split tiles of small plain frames (rfx.h rfx_renderer_set_tile_split): 1 frames of at most 8192 tiles
-        (default), 2 every plain frame without a tile schedule, 0 off -- two waves per 8x8 tile.  No pixel changes."""
-        check(_lib.load().rfx_renderer_set_tile_split(self._h, int(mode)), "set_tile_split")
-
     def set_regroup(self, park_after: int):
         """Ray regrouping (rfx.h rfx_renderer_set_regroup): -1 default (large scenes, after 3 segments), 0 off,
         n >= 1 park traces alive after n segments for the packed bounce kernel.  No pixel changes."""

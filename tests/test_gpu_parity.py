@@ -115,26 +115,6 @@ def test_tile_order_changes_no_pixel(name, W, H, depth, ss, additive, chunks):
     assert len(frames[0]) == 9 and frames[0] == frames[1]
 
 
-@pytest.mark.parametrize("name,W,H,depth,chunks", [
-    ("default", 640, 480, 4, None),          # C1, which splits by default
-    ("synth16", 203, 117, 8, None),          # ragged: partial tiles, an odd number of tile columns
-    ("synth16", 320, 180, 8, [5000, 777]),   # chunked renderNext: the cursor span and first row change every call
-    ("planes", 160, 90, 8, None),
-])
-def test_tile_split_changes_no_pixel(name, W, H, depth, chunks):
-    """Split tiles (two waves of 4 rows per 8x8 tile) render every frame exactly as one wave per tile does."""
-    frames = []
-    for mode in (0, 2):
-        got = []
-        _, _, r = gpu_render(scene(name), W, H, depth, frames=4, tile_split=mode, chunks=chunks,
-                             each_frame=lambda rgb, argb: got.append((sha(rgb), sha(argb))))
-        r.close()
-        frames.append(got)
-    assert len(frames[0]) == 4 and frames[0] == frames[1]
-    if (name, W, H, depth) == ("default", 640, 480, 4):
-        assert frames[1][0] == (CASES["hash_default_640x480_d4"]["sha_f32"], CASES["hash_default_640x480_d4"]["sha_argb"])
-
-
 def test_tile_order_default_full_size():
     """C3 at full size, where the default schedule is on: 6 frames, bit-identical to raster order."""
     frames = []

@@ -54,9 +54,6 @@ VARIANTS = {
     "qsort": ["RFX_QUEUE_SORT=1"],
     "lpt16k": ["RFX_TILE_ORDER_MIN_TILES=16384"],
     "lpt4k": ["RFX_TILE_ORDER_MIN_TILES=4096"],
-    "nosplit": ["RFX_SPLIT_MAX_TILES=0"],
-    "split16k": ["RFX_SPLIT_MAX_TILES=16384"],
-    "split40k": ["RFX_SPLIT_MAX_TILES=40000"],
 }
 
 
