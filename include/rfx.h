@@ -112,9 +112,10 @@ int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *scene);
  * Block-preview frames (sample_num < 0) always run in raster order. */
 int rfx_renderer_set_tile_order(rfx_renderer *r, int mode);
 /* Ray regrouping of plain one-sample frames (no pixel changes): a trace still alive after park_after bounce
- * segments is parked in an HBM queue and resumed by a second kernel in packed waves (lanes whose traces ended
- * no longer idle in their tile's wave).  -1 (default) = after 3 segments on scenes with more than 32 spheres
- * or triangles, off on small ones; 0 = off; n >= 1 = after n segments on any scene. */
+ * segments is parked in an HBM queue and resumed by a second kernel whose lanes each take the next queued trace as
+ * soon as theirs ends (lanes whose traces ended no longer idle in their tile's wave).  -1 (default) = after 2
+ * segments on scenes with more than 32 spheres or triangles, off on small ones; 0 = off; n >= 1 = after n segments
+ * on any scene. */
 int rfx_renderer_set_regroup(rfx_renderer *r, int park_after);
 /* regrouped frames: 1 = the parked traces are counting-sorted by direction octant and origin cell before the bounce
  * kernel takes them, 0 (default) = taken in park order (a tile's survivors together: faster on C5).

@@ -442,6 +442,9 @@ extern "C" uint32_t rfx_strip_row_to_y(uint32_t r, uint32_t rb, uint32_t rank, u
 #define RFX_TILE_ORDER_MIN_TILES 49152
 #endif
 constexpr size_t kPrimWords = 5;  // per wave tile (rfx_trace.h kPrimStride)
+#ifndef RFX_BOUNCE_GROUPS_PER_CU
+#define RFX_BOUNCE_GROUPS_PER_CU 14
+#endif
 
 #ifndef RFX_QUEUE_SORT
 // regrouped frames: the bounce kernel takes the parked traces bucket by bucket (1) or in park order (0).  tools/ab.py,
@@ -450,13 +453,14 @@ constexpr size_t kPrimWords = 5;  // per wave tile (rfx_trace.h kPrimStride)
 #define RFX_QUEUE_SORT 0
 #endif
 #ifndef RFX_PARK_AFTER
-#define RFX_PARK_AFTER 3  // large-scene plain frames: segments before a live trace is parked for the bounce kernel
+#define RFX_PARK_AFTER 2  // large-scene plain frames: segments before a live trace is parked for the bounce kernel
 #endif
 #ifndef RFX_TILE_SORT_EVERY
 #define RFX_TILE_SORT_EVERY 4  // tools/ab.py, C3: every launch -7.5% trace time vs raster order, every 4th -9.4%, every 16th -9.8%
 #endif
 struct rfx_renderer {
   int device = 0;
+  int cus = 256;  // compute units of the device (the bounce kernel's grid: one resident wave per slot)
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
   // scene on device
@@ -601,6 +605,8 @@ extern "C" int rfx_renderer_create(rfx_renderer **out, int device)
     return fail(RFX_ERR_HIP, "renderer_create: HIP allocation failed");
   }
   r->stream = r->own_stream;
+  if (hipDeviceGetAttribute(&r->cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || r->cus <= 0)
+    r->cus = 256;
   const uint32_t seeds[2] = {1350490027u, 1350490027u};
   if (hipMemcpy(r->d_seed, seeds, sizeof(seeds), hipMemcpyHostToDevice) != hipSuccess ||
       hipMemset(r->d_err, 0, sizeof(int)) != hipSuccess)
@@ -1369,9 +1375,10 @@ static int trace_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *rd, float
   if (P.grid_rows) HIP_CHECK(launch_trace(r->dev, P, d_counters != nullptr, st));
   if (park)
   {
-    // one pass of packed waves over the queue: enough workgroups to fill the chip, each claiming 64 traces at a time
+    // packed waves over the queue, as many as the chip holds at once (RFX_BOUNCE_GROUPS_PER_CU workgroups of two waves
+    // per CU: 7 waves per SIMD); a lane whose trace ends takes the next entry, so no wave waits for a slot
     const uint64_t waves = (pl.traces + 63) / 64;
-    const uint32_t groups = (uint32_t)std::min<uint64_t>((waves + 1) / 2, 4096);
+    const uint32_t groups = (uint32_t)std::min<uint64_t>((waves + 1) / 2, (uint64_t)r->cus * RFX_BOUNCE_GROUPS_PER_CU);
     const int cfg = 1 | (r->dev.n_light > 32 ? 2 : 0) | (small ? 4 : 0) | (r->dev.n_pln ? 8 : 0);  // rfx_trace.h kCfg*
     if (sort_queue) HIP_CHECK(launch_queue_sort(r->d_qctr, r->d_qkey, r->d_qctr + 2, r->d_qorder, st));
     launch_bounce(cfg, dim3(groups), r->dev, P, st);

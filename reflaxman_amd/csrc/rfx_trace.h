@@ -1147,6 +1147,7 @@ struct Park {
   QRay *queue;
   uint32_t *count;
   uint32_t trace, out;  // this lane's randDir trace index and output pixel
+  static constexpr bool kRefill = false;
   __device__ __forceinline__ void ids(uint32_t &t, uint32_t &o) const { t = trace; o = out; }
   __device__ __forceinline__ uint32_t *keys() const { return nullptr; }
 };
@@ -1436,6 +1437,8 @@ __device__ __forceinline__ col trace_from(const DevScene &S, v3 origin, v3 ray, 
         }
       }
     }
+    // the bounce kernel: traces that ended this segment write their pixels, idle lanes take new ones (Refill)
+    if constexpr (PK::kRefill) park.refill(alive, origin, ray, mulc, pix, refl, rd);
   }
   RFX_PROF_END(P_SEG);
 #ifdef RFX_DEBUG_SEGS
@@ -1501,6 +1504,7 @@ struct ParkTile {
     t = (uint32_t)((uint64_t)y * P.W + gx - P.p_begin);
     o = (uint32_t)((size_t)orow * P.W + gx);
   }
+  static constexpr bool kRefill = false;
   __device__ __forceinline__ uint32_t *keys() const { return P.queue_key; }
 };
 
@@ -1828,6 +1832,60 @@ __global__ RFX_TRACE_BOUNDS void prim_cull_kernel(DevScene S, FrameParams P, uin
 // as the trace kernel would have (Render.cpp:185 and the ARGB epilogue).  Waves exit once the queue is
 // drained; the queue holds traces from all over the frame, so waves no longer idle on lanes whose traces
 // ended (the trace kernel's tail of 1-2 live lanes per wave at depth 3+).
+// The bounce kernel's lanes (ray regrouping, large scenes) take a new parked trace as soon as theirs ends: at the end of
+// every segment a lane whose trace ended writes its pixel (Render.cpp:185), and the wave's idle lanes claim the next
+// queue entries with one atomic -- so a wave stays full while its traces end at different segments, until the queue
+// is drained.  Each trace resumes from its own parked state, so every float op is the one the trace kernel would have
+// run.
+__shared__ uint32_t s_refill_out[kWgWaves][64];  // per lane: the output pixel of its trace in flight (~0u: none)
+
+struct Refill {
+  const FrameParams &P;
+  uint32_t n;             // queue entries
+  uint32_t wv;            // the wave's slot in its workgroup
+  mutable bool drained;   // wave-uniform: every entry has been claimed
+  static constexpr bool kRefill = true;
+  __device__ __forceinline__ void ids(uint32_t &t, uint32_t &o) const { t = o = 0u; }  // (never parks)
+  __device__ __forceinline__ uint32_t *keys() const { return nullptr; }
+  __device__ __forceinline__ void refill(bool &alive, v3 &origin, v3 &ray, col &mulc, col &pix, int &refl, v3 &rd) const
+  {
+    const uint32_t lane = __lane_id();
+    uint32_t out = s_refill_out[wv][lane];
+    if (!alive && out != ~0u)
+    {
+      const col o = cadd(mkc(0.0f, 0.0f, 0.0f), pix);                               // Render.cpp:185
+      float *d = P.img + (size_t)out * 3;
+      d[0] = o.r; d[1] = o.g; d[2] = o.b;
+      if (P.argb) P.argb[out] = argb(o);
+      out = ~0u;
+    }
+    const uint64_t idle = __ballot(out == ~0u);
+    if (idle && !drained)
+    {
+      const int first = __ffsll((long long)idle) - 1;
+      const uint32_t k = (uint32_t)__popcll(idle);
+      uint32_t base = 0;
+      if (lane == (uint32_t)first) base = atomicAdd(P.queue_next, k);
+      base = __builtin_amdgcn_readlane(base, first);
+      if (base + k >= n) drained = true;
+      const uint32_t slot = base + (uint32_t)__popcll(idle & ((1ull << lane) - 1ull));
+      if (out == ~0u && slot < n)
+      {
+        const QRay q = P.queue[P.queue_order ? P.queue_order[slot] : slot];
+        origin = mk(q.ox, q.oy, q.oz);
+        ray = mk(q.dx, q.dy, q.dz);
+        mulc = mkc(q.mr, q.mg, q.mb);
+        pix = mkc(q.pr, q.pg, q.pb);
+        refl = (int)q.refl;
+        rd = load_rd(P, q.trace);
+        out = q.out;
+        alive = refl < P.depth;
+      }
+    }
+    s_refill_out[wv][lane] = out;
+  }
+};
+
 template <int CFG>
 __global__ RFX_TRACE_BOUNDS void bounce_kernel(DevScene S, FrameParams P)
 {
@@ -1839,32 +1897,19 @@ __global__ RFX_TRACE_BOUNDS void bounce_kernel(DevScene S, FrameParams P)
   if constexpr (SMALL) stage_small_scene(S);
   __syncthreads();
   Cnt cnt;
-  const uint32_t n = *P.queue_count, lane = __lane_id();
-  for (;;)
-  {
-    uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(P.queue_next, 64u);
-    base = __builtin_amdgcn_readfirstlane(base);
-    if (base >= n) break;
-    RFX_WAVE_T0();
-    const uint32_t i = base + lane;
-    const bool valid = i < n;
-    QRay q{};
-    if (valid) q = P.queue[P.queue_order ? P.queue_order[i] : i];
-    const v3 rd = valid ? load_rd(P, q.trace) : mk(0.0f, 0.0f, 0.0f);
-    bool parked;
-    const col c = trace_from<false, CULL, MANYL, SMALL, PLANES, false>(
-        S, mk(q.ox, q.oy, q.oz), mk(q.dx, q.dy, q.dz), mkc(q.mr, q.mg, q.mb), mkc(q.pr, q.pg, q.pb), (int)q.refl, P.depth,
-        rd, lut, cnt, valid, Park{0, nullptr, nullptr, 0, 0}, parked);
-    if (valid)
-    {
-      const col out = cadd(mkc(0.0f, 0.0f, 0.0f), c);                            // Render.cpp:185
-      float *d = P.img + (size_t)q.out * 3;
-      d[0] = out.r; d[1] = out.g; d[2] = out.b;
-      if (P.argb) P.argb[q.out] = argb(out);
-    }
-    RFX_WAVE_T1(kBounceTimeBase + base / 64u);
-  }
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  s_refill_out[wv][__lane_id()] = ~0u;
+  const Refill rf{P, *P.queue_count, wv, false};
+  bool alive = false;
+  v3 origin = mk(0.0f, 0.0f, 0.0f), ray = origin, rd = origin;
+  col mulc = mkc(0.0f, 0.0f, 0.0f), pix = mulc;
+  int refl = 0;
+  rf.refill(alive, origin, ray, mulc, pix, refl, rd);  // the wave's first 64 traces
+  RFX_WAVE_T0();
+  bool parked;
+  (void)trace_from<false, CULL, MANYL, SMALL, PLANES, false>(S, origin, ray, mulc, pix, refl, P.depth, rd, lut, cnt, alive,
+                                                             rf, parked);
+  RFX_WAVE_T1(kBounceTimeBase + kWgWaves * blockIdx.x + wv);
 }
 
 // ------------------------------------------------------------- launch of one family (the rfx_trace_*.hip TUs)

@@ -51,3 +51,15 @@ void launch_bounce(int cfg, dim3 grid, const DevScene &S, const FrameParams &P, 
 }
 
 }  // namespace rfx
+
+#ifdef RFX_DEBUG_WAVES
+// this translation unit's copy of the wave timeline (the parking trace kernels and the bounce kernel; the others are
+// read by rfx_debug_wave_time_read in rfx_trace_plain_fast.hip)
+extern "C" int rfx_debug_wave_time_read_park(unsigned long long *out, int n)
+{
+  if (n < 0 || (uint32_t)n > rfx::kWaveTimeMax) n = (int)rfx::kWaveTimeMax;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(rfx::g_wave_time), 2 * (size_t)n * sizeof(unsigned long long)) != hipSuccess)
+    return -1;
+  return n;
+}
+#endif

@@ -128,8 +128,8 @@ struct FrameParams {
   uint32_t *tile_cost;          // per tile: its clock cycles this frame (the next frame's order), or null
   uint32_t tiles_x;             // schedule tiles per grid row (set by launch_trace)
   // ray regrouping (plain pixels, large scenes): a trace still alive after park_after segments is appended to
-  // queue (queue_count: entries) instead of continuing; the bounce kernel then runs the queue in packed waves,
-  // claiming 64 entries at a time from queue_next.  park_after <= 0: no parking.
+  // queue (queue_count: entries) instead of continuing; the bounce kernel then runs the queue in packed waves whose
+  // idle lanes claim the next entries from queue_next.  park_after <= 0: no parking.
   QRay *queue;
   uint32_t *queue_count, *queue_next;
   int32_t park_after;

@@ -312,7 +312,7 @@ class Renderer:
         check(_lib.load().rfx_renderer_set_prim_masks(self._h, int(mode)), "set_prim_masks")
 
     def set_regroup(self, park_after: int):
-        """Ray regrouping (rfx.h rfx_renderer_set_regroup): -1 default (large scenes, after 3 segments), 0 off,
+        """Ray regrouping (rfx.h rfx_renderer_set_regroup): -1 default (large scenes, after 2 segments), 0 off,
         n >= 1 park traces alive after n segments for the packed bounce kernel.  No pixel changes."""
         check(_lib.load().rfx_renderer_set_regroup(self._h, int(park_after)), "set_regroup")
 

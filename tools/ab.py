@@ -54,6 +54,8 @@ VARIANTS = {
     "qsort": ["RFX_QUEUE_SORT=1"],
     "lpt16k": ["RFX_TILE_ORDER_MIN_TILES=16384"],
     "lpt4k": ["RFX_TILE_ORDER_MIN_TILES=4096"],
+    "bg16": ["RFX_BOUNCE_GROUPS_PER_CU=16"],
+    "bg8": ["RFX_BOUNCE_GROUPS_PER_CU=8"],
 }
 
 

@@ -66,10 +66,14 @@ def main():
     n = ((a.width + 7) // 8) * ((a.height + 7) // 8)
     cap = 1 << 18
     assert n <= BOUNCE_BASE, "frame too large for the timeline buffer"
-    buf = (C.c_ulonglong * (2 * cap))()
-    r.L.rfx_debug_wave_time_read.argtypes = [C.c_void_p, C.c_int]
-    assert r.L.rfx_debug_wave_time_read(buf, cap) == cap
-    t = np.frombuffer(buf, np.uint64).reshape(cap, 2).astype(np.int64)
+    # each translation unit holds its own timeline: the plain kernels', and the parking trace and bounce kernels'
+    t = np.zeros((cap, 2), np.int64)
+    for fn in ("rfx_debug_wave_time_read", "rfx_debug_wave_time_read_park"):
+        buf = (C.c_ulonglong * (2 * cap))()
+        getattr(r.L, fn).argtypes = [C.c_void_p, C.c_int]
+        assert getattr(r.L, fn)(buf, cap) == cap
+        u = np.frombuffer(buf, np.uint64).reshape(cap, 2).astype(np.int64)
+        t = np.where((u[:, 1] > t[:, 1])[:, None], u, t)  # the newer record of each slot
     tr = t[:n]
     t0 = tr[:, 0].min()
     out = {"frame": f"{a.scene} {a.width}x{a.height} d{a.depth}", "trace_kernel": summary(tr, t0)}
