@@ -1,7 +1,9 @@
-# One GPU call: the PMC passes (one counter group per run) of the trace kernel at the configs that have no
-# record yet -- C1, C2 depth 1 and 4, the C4 frame on one GPU -- summarised into profiles/pmc records, then every
-# config's bench line again so each carries roofline.frac.  Records and lines land under gpurun_out/<outdir>.
-# Usage (repo root, via gpurun): bash tools/pmc_configs.sh <outdir under gpurun_out>
+# One GPU call: the PMC passes (one counter group per run) of the trace kernel (+ its bounce kernel) at every
+# config bench.py reports -- C1, C2 depth 1 and 4, C3, the C4 frame on one GPU, C5 -- summarised into
+# profiles/pmc records keyed by the library's device-code hash.  Records land under gpurun_out/<outdir>/records
+# (copy them into profiles/pmc/ afterwards); with --lines, every config's bench line again so each carries
+# roofline.frac.  Any device-code change invalidates every record: re-run this after the last kernel change.
+# Usage (repo root, via gpurun): bash tools/pmc_configs.sh <outdir under gpurun_out> [--lines]
 R=$PWD
 O=$R/gpurun_out/${1:-pmc_configs}
 mkdir -p $O/records
@@ -14,14 +16,18 @@ run_cfg() {  # name  scene W H depth  bench args...
   timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc2_$name -o run -- python3 $args > $O/pmc2_$name.log 2>&1 || return 8
   timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc3_$name -o run -- python3 $args > $O/pmc3_$name.log 2>&1 || return 9
   timeout -s KILL 120 rocprofv3 --pmc SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS GRBM_GUI_ACTIVE --output-format csv -d $O/pmc4_$name -o run -- python3 $args > $O/pmc4_$name.log 2>&1 || return 10
-  python3 $R/tools/pmc_summary.py --kernel "trace_kernel<false" --out $O/records/$name.json --config $scene $W $H $depth 1 \
+  python3 $R/tools/pmc_summary.py --kernel "trace_kernel<false,bounce_kernel" --out $O/records/$name.json --config $scene $W $H $depth 1 \
     $(find $O/pmc1_$name $O/pmc2_$name $O/pmc3_$name $O/pmc4_$name -name '*counter_collection.csv') > $O/summary_$name.json || return 11
 }
+run_cfg c3_synth16_3840x2160_d8 synth16 3840 2160 8 --config c3 --steps 3 --warmup 1 || exit $?
+run_cfg c5_stress4096_3840x2160_d12 stress4096 3840 2160 12 --config c5 --steps 2 --warmup 1 || exit $?
 run_cfg c1_default_640x480_d4 default 640 480 4 --config c1 --steps 20 --warmup 3 || exit $?
 run_cfg c2_default_1920x1080_d1 default 1920 1080 1 --config c2 --depth 1 --steps 10 --warmup 2 || exit $?
 run_cfg c2_default_1920x1080_d4 default 1920 1080 4 --config c2 --steps 10 --warmup 2 || exit $?
 run_cfg c4_synth16_7680x4320_d8 synth16 7680 4320 8 --config c4 --steps 3 --warmup 1 || exit $?
-cp $O/records/*.json $R/profiles/pmc/ || exit 12
-cd $R
-bash tools/configs_round.sh ${1:-pmc_configs}/configs || exit 13
+if [ "$2" = "--lines" ]; then
+  cp $O/records/*.json $R/profiles/pmc/ || exit 12
+  cd $R
+  bash tools/configs_round.sh ${1:-pmc_configs}/configs || exit 13
+fi
 exit 0
