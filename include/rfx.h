@@ -272,12 +272,17 @@ int rfx_rand_dirs(rfx_renderer *r, uint32_t seed, uint64_t n, float *out3, uint3
  *   rfx_kat_texels: texture >= 0: Texture::getTexelColor(u, v) (in n x 2, Texture.cpp:231-269) of that scene
  *       texture; texture < 0: Skybox::getTexelColor(ray) (in n x 3, Skybox.cpp:39-106) -> out n x 3;
  *   rfx_kat_powf: powf(x, y) as Scene.cpp:175,196 evaluate it (in n x 2 -> out n);
- *   rfx_kat_argb: Color::argb (Color.cpp:114-117) (in n x 3 -> out n).
+ *   rfx_kat_argb: Color::argb (Color.cpp:114-117) (in n x 3 -> out n);
+ *   rfx_kat_powf_cube: the Fresnel site's powf(x, 3) (Scene.cpp:196) as the bounce loop evaluates it (the double
+ *       cube where it provably rounds like glibc, rfx_powf.h powf_cube_fast) against glibc's algorithm on the device,
+ *       for every float x in [0, 1]: counts[0] = mismatches (0 expected), counts[1] = inputs that took glibc's
+ *       algorithm.
  */
 int rfx_kat_objects(rfx_renderer *r, const float *rays, const int32_t *objects, uint64_t n, float *out);
 int rfx_kat_texels(rfx_renderer *r, int texture, const float *in, uint64_t n, float *out);
 int rfx_kat_powf(rfx_renderer *r, const float *xy, uint64_t n, float *out);
 int rfx_kat_argb(rfx_renderer *r, const float *rgb, uint64_t n, uint32_t *out);
+int rfx_kat_powf_cube(rfx_renderer *r, uint64_t counts[2]);
 
 #ifdef __cplusplus
 }

@@ -108,6 +108,7 @@ SIGNATURES = [
     ("rfx_kat_texels", C.c_int, [C.c_void_p, C.c_int, _fp, C.c_uint64, _fp]),
     ("rfx_kat_powf", C.c_int, [C.c_void_p, _fp, C.c_uint64, _fp]),
     ("rfx_kat_argb", C.c_int, [C.c_void_p, _fp, C.c_uint64, _u32p]),
+    ("rfx_kat_powf_cube", C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
 ]
 
 _lib = None

@@ -46,6 +46,7 @@ hipError_t launch_tile_order(const uint32_t *cost, uint32_t n, uint32_t *order, 
 void launch_bounce(int cfg, dim3 grid, const DevScene &S, const FrameParams &P, hipStream_t st);
 hipError_t launch_kat(int what, const DevScene &S, int tex, const void *in, const int32_t *objs, uint32_t n, void *out,
                       hipStream_t st);
+hipError_t launch_kat_powf_cube(uint32_t first, uint32_t n, unsigned long long *counts, hipStream_t st);
 }  // namespace rfx
 
 using namespace rfx;
@@ -1817,6 +1818,25 @@ extern "C" int rfx_kat_powf(rfx_renderer *r, const float *xy, uint64_t n, float 
 {
   if (!r || (n && (!xy || !out))) return fail(RFX_ERR_ARG, "kat_powf: bad args");
   return kat_run(r, 2, 0, xy, (size_t)n * 2, nullptr, n, out, (size_t)n);
+}
+
+extern "C" int rfx_kat_powf_cube(rfx_renderer *r, uint64_t counts[2])
+{
+  if (!r || !counts) return fail(RFX_ERR_ARG, "kat_powf_cube: bad args");
+  unsigned long long *d = nullptr;
+  hipError_t e = hipMalloc(&d, 2 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemsetAsync(d, 0, 2 * sizeof(unsigned long long), r->stream);
+  // every float in [0, 1]: bit patterns 0 .. 0x3f800000, in launches of 2^28
+  for (uint64_t first = 0; e == hipSuccess && first <= 0x3f800000ull; first += 1ull << 28)
+    e = launch_kat_powf_cube((uint32_t)first, (uint32_t)std::min<uint64_t>(1ull << 28, 0x3f800001ull - first), d, r->stream);
+  unsigned long long h[2] = {0, 0};
+  if (e == hipSuccess) e = hipStreamSynchronize(r->stream);
+  if (e == hipSuccess) e = hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  if (e != hipSuccess) return fail(RFX_ERR_HIP, "kat_powf_cube: %s", hipGetErrorString(e));
+  counts[0] = h[0];
+  counts[1] = h[1];
+  return RFX_OK;
 }
 
 extern "C" int rfx_kat_argb(rfx_renderer *r, const float *rgb, uint64_t n, uint32_t *out)

@@ -555,7 +555,34 @@ __global__ __launch_bounds__(kKatThreads) void kat_powf(const float *xy, uint32_
   stage_powf_tables();
   __syncthreads();
   const uint32_t i = blockIdx.x * kKatThreads + threadIdx.x;
-  if (i < n) out[i] = powf_dev(xy[2 * (size_t)i], xy[2 * (size_t)i + 1]);
+  if (i < n)
+  {
+    const float x = xy[2 * (size_t)i], y = xy[2 * (size_t)i + 1];
+    out[i] = y == 3.0f ? powf3_dev(x) : powf_dev(x, y);  // Scene.cpp:196 runs the cube form, :175 the general one
+  }
+}
+
+// powf3_dev(x) against powf_dev(x, 3) for the float bit patterns first .. first + n - 1 (every float in [0, 1] is
+// 0 .. 0x3f800000): counts[0] += mismatches, counts[1] += lanes that took glibc's algorithm
+__global__ __launch_bounds__(kKatThreads) void kat_powf_cube(uint32_t first, uint32_t n, unsigned long long *counts)
+{
+  stage_powf_tables();
+  __syncthreads();
+  const uint32_t i = blockIdx.x * kKatThreads + threadIdx.x;
+  bool bad = false, slow = false;
+  if (i < n)
+  {
+    const float x = __uint_as_float(first + i);
+    float p;
+    slow = !powf_cube_fast(x, p);
+    bad = __float_as_uint(powf3_dev(x)) != __float_as_uint(powf_dev(x, 3.0f));
+  }
+  const uint64_t mb = __ballot(bad), ms = __ballot(slow);
+  if ((threadIdx.x & 63u) == 0 && (mb | ms))
+  {
+    atomicAdd(&counts[0], (unsigned long long)__popcll(mb));
+    atomicAdd(&counts[1], (unsigned long long)__popcll(ms));
+  }
 }
 
 // Color::argb (Color.cpp:114-117) as the epilogue evaluates it: rgb n x 3 -> out n
@@ -666,6 +693,13 @@ hipError_t launch_kat(int what, const DevScene &S, int tex, const void *in, cons
     case 2: hipLaunchKernelGGL(kat_powf, kat_grid(n), dim3(kKatThreads), 0, st, (const float *)in, n, (float *)out); break;
     default: hipLaunchKernelGGL(kat_argb, kat_grid(n), dim3(kKatThreads), 0, st, (const float *)in, n, (uint32_t *)out); break;
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_kat_powf_cube(uint32_t first, uint32_t n, unsigned long long *counts, hipStream_t st)
+{
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(kat_powf_cube, kat_grid(n), dim3(kKatThreads), 0, st, first, n, counts);
   return hipGetLastError();
 }
 

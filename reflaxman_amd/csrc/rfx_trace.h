@@ -142,6 +142,15 @@ __device__ __forceinline__ float powf_dev(float x, float y)
   return powf_glibc_t(x, y, s_powf_log, s_powf_exp, s_powf_add);
 }
 
+// powf(x, 3) for x in [0, 1] (the Fresnel term): the double cube where it provably rounds like glibc, glibc's
+// algorithm for the few lanes where it may not (rfx_powf.h powf_cube_fast)
+__device__ __forceinline__ float powf3_dev(float x)
+{
+  float p;
+  if (!powf_cube_fast(x, p)) p = powf_dev(x, 3.0f);
+  return p;
+}
+
 // Small scenes (<= 32 spheres, <= 32 triangles): the per-object records the hit lanes gather by their
 // own object index (winner geometry and material, the cull lane table) staged in LDS per workgroup.
 __shared__ SphereGeo s_sph_geo[32];
@@ -652,13 +661,26 @@ __device__ __forceinline__ bool strictly_closer(float sq, float best_sq)
   return sq < best_sq && (best_sq == INFINITY || sq < sq_lower_bound(sqrt_rn(best_sq)));
 }
 
+// Outside a 2^-20 band around best_sq the rounded distances are ordered like the squares: sq < RN(best_sq (1 - 2^-20))
+// gives sqrt_rn(sq) < sqrt_rn(best_sq), sq > RN(best_sq (1 + 2^-20)) gives sqrt_rn(sq) > sqrt_rn(best_sq) (sqrt_rn and the
+// products each round by at most 2^-24 relative; all squares here are normal).  Only candidates inside the band take the
+// exact test above (tests/test_sqrt_bounds.py checks both claims).  best_sq = +inf: every finite sq is below.
+constexpr float kTakeBelow = 0x1.ffffep-1f;  // 1 - 2^-20
+constexpr float kTakeAbove = 0x1.00001p+0f;  // 1 + 2^-20
+
 // the comparison key of a candidate and the two decisions on it (Hit::sq holds the winner's key)
 constexpr float kNoHitKey = INFINITY;
 __device__ __forceinline__ float hit_key(float sq) { return sq; }
-__device__ __forceinline__ bool sph_takes(float sq, float best_sq) { return strictly_closer(sq, best_sq); }
+__device__ __forceinline__ bool sph_takes(float sq, float best_sq)
+{
+  if (sq < best_sq * kTakeBelow) return true;
+  return strictly_closer(sq, best_sq);
+}
 // dist < best || (dist == best && obj < best_obj)
 __device__ __forceinline__ bool tri_takes(float sq, float best_sq, int obj, int best_obj)
 {
+  if (sq < best_sq * kTakeBelow) return true;
+  if (!(sq <= best_sq * kTakeAbove)) return false;
   return sq < best_sq ? (obj < best_obj || strictly_closer(sq, best_sq))
                       : (obj < best_obj && sqrt_rn(sq) == sqrt_rn(best_sq));
 }
@@ -1377,7 +1399,7 @@ __device__ __forceinline__ col trace_from(const DevScene &S, v3 origin, v3 ray, 
         RFX_CNT(C_DIELECTRIC);
         const float aa = rayLen * normLen;
         const float cosA = (aa > kVerySmall) ? clampf(dot(ray, neg(norm)) / aa, 0.0f, 1.0f) : 0.0f;
-        const float r = 0.2f + 0.8f * powf_dev(1.0f - cosA, 3.0f);
+        const float r = 0.2f + 0.8f * powf3_dev(1.0f - cosA);
         fin = cadd(cmul(cscale(color, 1.0f - r), sumL), sumS);
         fin = cmul(fin, mulc);
         mulc = cscale(mulc, r);

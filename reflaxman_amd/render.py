@@ -354,6 +354,12 @@ class Renderer:
         check(_lib.load().rfx_kat_powf(self._h, _lib.fptr(xy), xy.shape[0], _lib.fptr(out)), "rfx_kat_powf")
         return out
 
+    def kat_powf_cube(self):
+        """(mismatches, glibc-path inputs) of the Fresnel cube form vs glibc's algorithm over every float in [0, 1]."""
+        counts = (C.c_uint64 * 2)()
+        check(_lib.load().rfx_kat_powf_cube(self._h, counts), "rfx_kat_powf_cube")
+        return int(counts[0]), int(counts[1])
+
     def kat_argb(self, rgb: np.ndarray) -> np.ndarray:
         rgb = np.ascontiguousarray(rgb, np.float32)
         out = np.zeros(rgb.shape[0], np.uint32)

@@ -5,6 +5,10 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <algorithm>
+#include <atomic>
+#include <thread>
+#include <vector>
 #include "rfx_powf.h"
 
 static unsigned long long bad = 0, total = 0;
@@ -21,8 +25,39 @@ static void check(float x, float y)
   }
 }
 
+// -cube: the Fresnel cube form (rfx_powf.h powf_cube_fast, glibc's algorithm where it declines) against the live libm
+// powf(x, 3) on every float x in [0, 1], on every host thread
+static int check_cube()
+{
+  std::atomic<unsigned long long> bad{0}, slow{0};
+  const unsigned T = std::max(1u, std::thread::hardware_concurrency());
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < T; ++t)
+    th.emplace_back([&, t] {
+      unsigned long long b = 0, s = 0;
+      for (unsigned u = t; u <= 0x3f800000u; u += T)
+      {
+        float x, p;
+        memcpy(&x, &u, 4);
+        if (!rfx::powf_cube_fast(x, p)) { p = rfx::powf_glibc(x, 3.0f); ++s; }
+        const float a = powf(x, 3.0f);
+        if (memcmp(&a, &p, 4))
+        {
+          if (b < 5) fprintf(stderr, "MISMATCH x=%a libm=%a cube=%a\n", x, a, p);
+          ++b;
+        }
+      }
+      bad += b;
+      slow += s;
+    });
+  for (auto &x : th) x.join();
+  printf("%u floats in [0, 1], %llu took glibc's algorithm, %llu mismatches\n", 0x3f800001u, slow.load(), bad.load());
+  return bad.load() ? 1 : 0;
+}
+
 int main(int argc, char **argv)
 {
+  if (argc == 2 && !strcmp(argv[1], "-cube")) return check_cube();
   if (argc == 4 && !strcmp(argv[1], "-f"))
   {
     // -f IN OUT: (x, y) f32 pairs from IN -> the restatement's powf(x, y) to OUT (KAT replay)

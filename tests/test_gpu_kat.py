@@ -135,6 +135,17 @@ def test_kat_powf():
     assert_same(out, g["out"], "kat_pow")
 
 
+def test_kat_powf_cube_every_float():
+    """The Fresnel site's powf(x, 3) (Scene.cpp:196) takes the double cube where it provably rounds like glibc: on
+    the device it equals glibc's algorithm for every float in [0, 1] (tests/test_powf.py checks the host copy against
+    the live libm on the same floats)."""
+    r = Renderer()
+    bad, slow = r.kat_powf_cube()
+    r.close()
+    assert bad == 0
+    assert 0 < slow < 0x3f800001
+
+
 def test_kat_argb():
     g = load("kat_argb")
     r = Renderer()

@@ -12,7 +12,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def checker(tmp_path_factory):
     exe = str(tmp_path_factory.mktemp("powf") / "powf_check")
     subprocess.run(["g++", "-std=c++17", "-O2", "-ffp-contract=off", "-Wno-unknown-pragmas",
-                    "-I" + os.path.join(ROOT, "reflaxman_amd", "csrc"),
+                    "-pthread", "-I" + os.path.join(ROOT, "reflaxman_amd", "csrc"),
                     os.path.join(ROOT, "tests", "native", "powf_check.cpp"), "-o", exe, "-lm"], check=True)
     return exe
 
@@ -41,3 +41,12 @@ def test_powf_restatement_matches_reference_kat(checker, tmp_path):
     subprocess.run([checker, "-f", str(fi), str(fo)], check=True)
     ours = np.fromfile(fo, np.float32)
     assert ours.tobytes() == g["out"].tobytes(), np.argwhere(ours != g["out"])[:5]
+
+
+def test_fresnel_cube_form_every_float(checker):
+    """Scene.cpp:196's powf(x, 3) as the bounce loop evaluates it -- the double cube where every value within 2^-32 of
+    it rounds alike, glibc's algorithm elsewhere (rfx_powf.h powf_cube_fast) -- equals the live libm on every float
+    in [0, 1] (the term's whole domain: x = 1 - cosA with cosA clamped to [0, 1])."""
+    r = subprocess.run([checker, "-cube"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert " 0 mismatches" in r.stdout

@@ -69,3 +69,39 @@ def test_strictly_closer_equals_rounded_distance_compare():
         ref = bool(np.sqrt(sq) < np.sqrt(best_sq))
         mine = bool(sq < best_sq and sq < sq_lower_bound(np.sqrt(best_sq)))
         assert ref == mine, (sq, best_sq)
+
+
+K_TAKE_BELOW = F32(float.fromhex("0x1.ffffep-1"))  # rfx_trace.h kTakeBelow = 1 - 2^-20
+K_TAKE_ABOVE = F32(float.fromhex("0x1.00001p+0"))  # rfx_trace.h kTakeAbove = 1 + 2^-20
+
+
+def test_take_band_orders_rounded_distances():
+    """rfx_trace.h sph_takes / tri_takes decide outside a 2^-20 band around best_sq without square roots:
+    sq < RN(best_sq (1 - 2^-20)) must give sqrt_rn(sq) < sqrt_rn(best_sq), sq > RN(best_sq (1 + 2^-20)) must give
+    sqrt_rn(sq) > sqrt_rn(best_sq).  Checked at the band's edges (the floats just outside it) for best_sq over the
+    normal range of squared distances, every significand pattern near binade edges included."""
+    rng = np.random.default_rng(7)
+    best = np.concatenate([
+        (rng.uniform(-27.0, 40.0, 400000)).astype(np.float64),
+    ])
+    best = np.exp2(best).astype(F32)
+    # binade edges: 1, succ(1), pred(2) ... scaled over the range
+    edge = np.array([1.0, 1.0000001, 1.9999999, 1.5, 1.4142135], np.float64)
+    best = np.concatenate([best, (edge[None, :] * np.exp2(np.arange(-27, 40))[:, None]).astype(F32).ravel()])
+    best = best[np.isfinite(best) & (best > 0)]
+    lo = (best * K_TAKE_BELOW).astype(F32)
+    hi = (best * K_TAKE_ABOVE).astype(F32)
+    below = np.nextafter(lo, F32(0), dtype=F32)           # largest sq with sq < lo
+    above = np.nextafter(hi, F32(np.inf), dtype=F32)      # smallest sq with sq > hi
+    rb = np.sqrt(best)
+    assert np.all(np.sqrt(below) < rb)
+    assert np.all(np.sqrt(above) > rb)
+    # also a spread of candidates inside the fast regions
+    for f in (0.5, 0.9, 0.99999, 0.999999):
+        sq = (best * F32(f)).astype(F32)
+        m = sq < lo
+        assert np.all(np.sqrt(sq[m]) < rb[m])
+    for f in (1.000002, 1.00001, 1.5):
+        sq = (best * F32(f)).astype(F32)
+        m = np.isfinite(sq) & (sq > hi)
+        assert np.all(np.sqrt(sq[m]) > rb[m])
