@@ -335,13 +335,25 @@ __device__ __forceinline__ bool pair_may_hit(f2 b, f2 d)
 // The rest of Sphere::trace for one sphere given its b and d: on a hit returns t and |ray t|^2.
 // `(ray * t).length() > DELTA` (Sphere.cpp:61-64) is tested as |ray t|^2 >= kSqDeltaSphere: the same
 // decision without the square root (rfx_math.h).
-template <bool STATS, bool SHADOW>
+// SEL (large-scene loops): one branch, the rest computed and decided without branching.  tools/ab.py, trace ms: C5
+// 3.143 -> 3.067 (-2.4%); the small-scene kernel +9% with it (its SGPR spills 23 -> 51), so the small loops keep the
+// early outs.
+template <bool STATS, bool SHADOW, bool SEL = false>
 __device__ __forceinline__ bool sphere_tail(float b, float d, v3 ray, const RayConst &k, float &t_out,
                                             float &sq_out, Cnt &cnt)
 {
   RFX_CNT(SHADOW ? C_SH_SPH_TESTS : C_SPH_TESTS);
   if constexpr (STATS)
     if (!(b > 0.0f)) RFX_CNT(SHADOW ? C_SH_SPH_B : C_SPH_B);
+  if constexpr (!STATS && SEL)
+  {
+    if (!(d >= 0.0f && k.a_ok && b < 0.0f)) return false;
+    const float t = (-b - sqrt_rn(d)) / k.a2;
+    const float sq = sqlen(mul(ray, t));
+    t_out = t;
+    sq_out = sq;
+    return t > kVerySmall && sq >= kSqDeltaSphere;
+  }
   if (!(d >= 0.0f && k.a_ok)) return false;
   // b >= 0 (or NaN): -b - sqrt(d) <= 0, so t <= 0 and `t > VERY_SMALL_NUMBER` rejects -- exact early out
   if constexpr (!STATS)
@@ -771,12 +783,12 @@ __device__ __forceinline__ void closest_spheres_bvh(const DevScene &S, v3 origin
       if (pair_may_hit(b, d))
       {
         float t, sq;
-        if (sphere_tail<STATS, false>(b.x, d.x, ray, k, t, sq, cnt))
+        if (sphere_tail<STATS, false, true>(b.x, d.x, ray, k, t, sq, cnt))
         {
           const int obj = S.sph_info[4 * j];
           if (tri_takes(sq, h.sq, obj, h.obj)) { h.sq = sq; h.obj = obj; h.i = 2 * j; h.t = t; }
         }
-        if (sphere_tail<STATS, false>(b.y, d.y, ray, k, t, sq, cnt))
+        if (sphere_tail<STATS, false, true>(b.y, d.y, ray, k, t, sq, cnt))
         {
           const int obj = S.sph_info[4 * j + 2];
           if (tri_takes(sq, h.sq, obj, h.obj)) { h.sq = sq; h.obj = obj; h.i = 2 * j + 1; h.t = t; }
@@ -823,8 +835,8 @@ __device__ __forceinline__ bool occluded_spheres_bvh(const DevScene &S, v3 o, v3
       pair_bd(S.sph_pair[j], o, k, b, d);
       // the hit object is filtered out after its test, which does not change the boolean
       if (pair_may_hit(b, d) &&
-          ((sphere_tail<STATS, true>(b.x, d.x, ray, k, t, sq, cnt) && 2 * j != skip_sph) ||
-           (sphere_tail<STATS, true>(b.y, d.y, ray, k, t, sq, cnt) && 2 * j + 1 != skip_sph)))
+          ((sphere_tail<STATS, true, true>(b.x, d.x, ray, k, t, sq, cnt) && 2 * j != skip_sph) ||
+           (sphere_tail<STATS, true, true>(b.y, d.y, ray, k, t, sq, cnt) && 2 * j + 1 != skip_sph)))
         return true;
     }
     if (sp == 0) return false;
@@ -913,13 +925,13 @@ __device__ __forceinline__ void closest_hit(const DevScene &S, v3 origin, v3 ray
         if constexpr (!STATS)
           if (!pair_may_hit(b, d)) continue;  // both miss: one branch
         float t, sq;
-        if (sphere_tail<STATS, false>(b.x, d.x, ray, k, t, sq, cnt))
+        if (sphere_tail<STATS, false, true>(b.x, d.x, ray, k, t, sq, cnt))
         {
           const float key = hit_key(sq);
           const int obj = S.sph_info[4 * j];
           if (tri_takes(key, h.sq, obj, h.obj)) { h.sq = key; h.obj = obj; h.i = 2 * j; h.t = t; }
         }
-        if ((!STATS || 2 * j + 1 < S.n_sph) && sphere_tail<STATS, false>(b.y, d.y, ray, k, t, sq, cnt))
+        if ((!STATS || 2 * j + 1 < S.n_sph) && sphere_tail<STATS, false, true>(b.y, d.y, ray, k, t, sq, cnt))
         {
           const float key = hit_key(sq);
           const int obj = S.sph_info[4 * j + 2];
@@ -1118,8 +1130,8 @@ __device__ __forceinline__ bool occluded(const DevScene &S, v3 o, v3 ray, bool l
           else if (pair_may_hit(b, d))
           {
             // the hit object is filtered out after its test, which does not change the boolean
-            if (sphere_tail<STATS, true>(b.x, d.x, ray, k, t, sq, cnt) && 2 * j != skip_sph) occ = true;
-            else if (sphere_tail<STATS, true>(b.y, d.y, ray, k, t, sq, cnt) && 2 * j + 1 != skip_sph) occ = true;
+            if (sphere_tail<STATS, true, true>(b.x, d.x, ray, k, t, sq, cnt) && 2 * j != skip_sph) occ = true;
+            else if (sphere_tail<STATS, true, true>(b.y, d.y, ray, k, t, sq, cnt) && 2 * j + 1 != skip_sph) occ = true;
           }
         }
         if (__ballot(live && !occ) == 0) return occ;
