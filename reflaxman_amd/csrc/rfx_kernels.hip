@@ -336,7 +336,27 @@ __global__ __launch_bounds__(kRngBlock) void rng_emit(const uint32_t *seed, cons
   // this block's first trace: the accept counts of the blocks before it, summed by the block (the count
   // array is a few KB and L2-resident, so no separate scan pass)
   uint32_t part = 0;
-  for (uint32_t k = threadIdx.x; k < blockIdx.x; k += kRngBlock) part += blk_cnt[k];
+  if (((uintptr_t)blk_cnt & 15u) == 0)
+  {
+    // 16-byte loads, up to four per thread in flight before any is summed: one round trip to L2 per 4096 counts
+    const uint4 *v4 = reinterpret_cast<const uint4 *>(blk_cnt);
+    const uint32_t nvec = blockIdx.x >> 2;
+    for (uint32_t k0 = 0; k0 < nvec; k0 += 4 * kRngBlock)
+    {
+      uint4 a[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+      {
+        const uint32_t k = k0 + (uint32_t)u * kRngBlock + threadIdx.x;
+        a[u] = k < nvec ? v4[k] : make_uint4(0u, 0u, 0u, 0u);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) part += a[u].x + a[u].y + a[u].z + a[u].w;
+    }
+    if (threadIdx.x < (blockIdx.x & 3u)) part += blk_cnt[(nvec << 2) + threadIdx.x];
+  }
+  else
+    for (uint32_t k = threadIdx.x; k < blockIdx.x; k += kRngBlock) part += blk_cnt[k];
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
   __shared__ uint64_t s_off;
