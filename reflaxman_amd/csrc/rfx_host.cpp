@@ -911,7 +911,7 @@ extern "C" int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *s)
     for (const v3 &q : {t.v0, t.v1, t.v2})
       r2 = fmax(r2, (q.x - cx) * (q.x - cx) + (q.y - cy) * (q.y - cy) + (q.z - cz) * (q.z - cz));
     float r = (float)(sqrt(r2) * 1.0001 + 1e-6);
-    if (!(t.cond < 1000.0)) r = INFINITY;
+    if (!(t.cond < 300.0)) r = INFINITY;
     bd.push_back({(float)cx, (float)cy, (float)cz, r});
   }
   // small-scene lane table (rfx_types.h CullRec)
@@ -938,7 +938,7 @@ extern "C" int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *s)
       const Bound &b = bd[s->spheres.size() + i];
       CullRec c{};
       c.x = b.x; c.y = b.y; c.z = b.z; c.r = b.r;
-      if (t.cond < 1000.0)
+      if (t.cond < 300.0)
       {
         // plane of the triangle in double: unit normal of (v1 - v0) x (v2 - v0), offset n . v0
         const double ax = (double)t.v1.x - t.v0.x, ay = (double)t.v1.y - t.v0.y, az = (double)t.v1.z - t.v0.z;

@@ -467,13 +467,14 @@ __device__ __forceinline__ bool plane_hit(const PlaneGeo &g, v3 o, v3 ray, float
 // ------------------------------------------------------------- wave ray bundles (exact culling)
 // The live rays of a wave form a bundle: origins within rw of (cx, cy, cz) -- the first live lane's
 // origin -- and directions within the half-angle acos(cosa) of that lane's direction (ax, ay, az).
-// A ray the reference's float test reports as hitting a sphere passes within r + 8.1e-4 |o - c| of the
-// centre (rounding of d = b^2 - 4ac, DESIGN.md "Exact culling"); kCullRel = 4e-3 covers that five times,
-// so an object whose bounding sphere, grown by rw and kCullRel (L + rw), lies outside the bundle's cone
+// A ray the reference's float test reports as hitting a sphere passes within r + 1.25e-3 |o - c| of the
+// centre (rounding of d = b^2 - 4ac is at most 104 u a |vco|^2, DESIGN.md "Exact work skipping"; observed worst
+// 7.6e-5, tests/test_cull_bound.py); kCullRel = 2e-3 covers the bound 1.6 times (round 2 used 4e-3: C5 trace -7%
+// with 2e-3, tools/ab.py), so an object whose bounding sphere, grown by rw and kCullRel (L + rw), lies outside the bundle's cone
 // is missed by every lane of the wave and its exact test is skipped for the whole wave.  Skipping a test
 // that misses changes no result: the closest hit and the any-hit only ever take hits.  Every cull
 // decision is a conjunction of comparisons, so a NaN anywhere keeps the object.
-constexpr float kCullRel = 4e-3f;
+constexpr float kCullRel = 2e-3f;
 
 // per-view primary masks (prim_cull_kernel): per wave tile, the closest hit's mask and the shadow masks of the
 // first kPrimLights lights
@@ -701,7 +702,7 @@ __device__ __forceinline__ bool tri_takes(float sq, float best_sq, int obj, int 
 // Each lane walks the pair BVH (rfx_types.h BvhNode) with its own ray: both children's boxes are tested per
 // step, the nearer one is entered first and the farther one pushed on a per-lane stack in LDS.  The boxes are
 // widened per ray by the exact-cull margin of the wave bundles (a sphere the reference's float test reports as
-// hit lies within r + 8.1e-4 |o - c| of the ray; kCullRel = 4e-3 covers it five times, with |o - c| bounded
+// hit lies within r + 1.25e-3 |o - c| of the ray; kCullRel = 2e-3 covers it 1.6 times, with |o - c| bounded
 // by the L1 distance to the box centre plus its L1 half-size), so a box the ray misses holds no sphere the
 // reference could report: skipping it changes no result.  Closest hit: a child whose entry distance exceeds
 // the best hit so far (with 0.1% slack over rounding; sphere distances computed by the reference are at least
