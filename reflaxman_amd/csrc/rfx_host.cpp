@@ -810,7 +810,17 @@ int build_pair_bvh(std::vector<BvhNode> &nodes, std::vector<uint32_t> &pairs, si
     n.child[c] = kids[c];
     // margin term of the child against the reference point ref (the root box centre), rounded up
     double mt = 0.0;
-    for (int k = 0; k < 3; ++k) mt += fabs(ref[k] - 0.5 * (l[k] + h[k])) + 0.5 * (h[k] - l[k]);
+    {
+      // Euclidean: |ref - centre|_2 + the half-diagonal (round 3; the L1 form made C5 2.2% slower)
+      double cd = 0.0, hd = 0.0;
+      for (int k = 0; k < 3; ++k)
+      {
+        const double dc = ref[k] - 0.5 * (l[k] + h[k]), dh = 0.5 * (h[k] - l[k]);
+        cd += dc * dc;
+        hd += dh * dh;
+      }
+      mt = sqrt(cd) + sqrt(hd);
+    }
     n.mt[c] = nextafterf((float)(mt * 1.0001), INFINITY);
   }
   return id;

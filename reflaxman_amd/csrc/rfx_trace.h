@@ -703,7 +703,7 @@ __device__ __forceinline__ bool tri_takes(float sq, float best_sq, int obj, int 
 // step, the nearer one is entered first and the farther one pushed on a per-lane stack in LDS.  The boxes are
 // widened per ray by the exact-cull margin of the wave bundles (a sphere the reference's float test reports as
 // hit lies within r + 1.25e-3 |o - c| of the ray; kCullRel = 2e-3 covers it 1.6 times, with |o - c| bounded
-// by the L1 distance to the box centre plus its L1 half-size), so a box the ray misses holds no sphere the
+// by the distance to the box centre plus its half-diagonal), so a box the ray misses holds no sphere the
 // reference could report: skipping it changes no result.  Closest hit: a child whose entry distance exceeds
 // the best hit so far (with 0.1% slack over rounding; sphere distances computed by the reference are at least
 // the entry distance into their widened box) cannot win or tie and is skipped too.  Leaves run the exact
@@ -720,10 +720,11 @@ typedef int16_t BvhSlot;
 __shared__ BvhSlot s_bvh_stack[kBvhStack * kWgThreads];
 
 // box margins from the node's stored term and one per-ray distance (round 2: C5 -8.5% against a margin per box)
-struct RayInv { float ix, iy, iz, dm; };  // dm: kCullRel |o - bvh_ref|_1 + 1e-6
+struct RayInv { float ix, iy, iz, dm; };  // dm: kCullRel |o - bvh_ref|_2 + 1e-6 (approximate root, widened 1e-4)
 __device__ __forceinline__ RayInv ray_inv(const DevScene &S, v3 o, v3 ray)
 {
-  const float dm = kCullRel * (fabsf(o.x - S.bvh_rx) + fabsf(o.y - S.bvh_ry) + fabsf(o.z - S.bvh_rz)) + 1e-6f;
+  const float ex = o.x - S.bvh_rx, ey = o.y - S.bvh_ry, ez = o.z - S.bvh_rz;
+  const float dm = kCullRel * (__builtin_amdgcn_sqrtf(ex * ex + ey * ey + ez * ez) * 1.0001f) + 1e-6f;
   return RayInv{__builtin_amdgcn_rcpf(ray.x), __builtin_amdgcn_rcpf(ray.y), __builtin_amdgcn_rcpf(ray.z), dm};
 }
 
@@ -732,8 +733,8 @@ __device__ __forceinline__ RayInv ray_inv(const DevScene &S, v3 o, v3 ray)
 __device__ __forceinline__ bool bvh_box(const BvhNode &n, int c, v3 o, const RayInv &ri, float &tn)
 {
   const float lx = n.lx[c], ly = n.ly[c], lz = n.lz[c], hx = n.hx[c], hy = n.hy[c], hz = n.hz[c];
-  // |o - c|_1 + half-size_1 <= |o - ref|_1 + mt[c] (c the box centre): the margin is at least
-  // kCullRel (|o - c|_1 + half-size_1) + 1e-6, the per-box bound of the culling argument
+  // |o - c|_2 + half-diagonal <= |o - ref|_2 + mt[c] (c the box centre): the margin is at least
+  // kCullRel (|o - c|_2 + half-diagonal) + 1e-6, the per-box bound of the culling argument
   const float m = ri.dm + kCullRel * n.mt[c];
   const float ax = (lx - m - o.x) * ri.ix, bx = (hx + m - o.x) * ri.ix;
   const float ay = (ly - m - o.y) * ri.iy, by = (hy + m - o.y) * ri.iy;

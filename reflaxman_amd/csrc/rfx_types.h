@@ -55,7 +55,7 @@ struct alignas(16) CullTri { float v0x, v0y, v0z, nu, gux, guy, guz, nv, gvx, gv
 // Bounding-volume hierarchy over the sphere pairs of a large scene (rfx_host.cpp build_pair_bvh): an internal
 // node holds its two children's boxes (the spheres grown by their radii) and their indices: c >= 0 an internal
 // node, c < 0 the leaf pair ~c (spheres 2(~c), 2(~c) + 1 of the device arrays, which are in spatial order).
-// mt[c]: |ref - centre of child c|_1 + its L1 half-size (ref: DevScene::bvh_ref), so that kCullRel (|o - ref|_1 + mt[c])
+// mt[c]: |ref - centre of child c|_2 + its half-diagonal (ref: DevScene::bvh_ref), so that kCullRel (|o - ref|_2 + mt[c])
 // bounds the kernel's per-ray box margin from above with one add per child (triangle inequality)
 struct alignas(16) BvhNode { float lx[2], ly[2], lz[2], hx[2], hy[2], hz[2]; int32_t child[2]; float mt[2]; };
 // Plane(pos, norm, material) (Plane.h:6-14): the normal as given (the reference never normalises it)
