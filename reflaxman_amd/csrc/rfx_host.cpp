@@ -44,6 +44,10 @@ uint32_t trace_tiles(const FrameParams &P);
 size_t tile_order_scratch();
 hipError_t launch_tile_order(const uint32_t *cost, uint32_t n, uint32_t *order, uint32_t *scratch, hipStream_t st);
 void launch_bounce(int cfg, dim3 grid, const DevScene &S, const FrameParams &P, hipStream_t st);
+hipError_t launch_bounce_lds(int cfg, uint32_t groups, const DevScene &S, const FrameParams &P, hipStream_t st);
+constexpr int kLdsBvhWaves = 16;  // rfx_trace.h kLdsBvhThreads / 64
+// rfx_trace.h lds_bvh_bytes: 56 B per node, 16 int16 stack slots per lane, 64 output slots per wave
+constexpr size_t lds_bvh_bytes_host(int n_bvh) { return (size_t)n_bvh * 56 + 2 * 16 * 64 * kLdsBvhWaves + 4 * 64 * kLdsBvhWaves; }
 hipError_t launch_kat(int what, const DevScene &S, int tex, const void *in, const int32_t *objs, uint32_t n, void *out,
                       hipStream_t st);
 hipError_t launch_kat_powf_cube(uint32_t first, uint32_t n, unsigned long long *counts, hipStream_t st);
@@ -1064,6 +1068,25 @@ extern "C" int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *s)
       (rc = upload(r, pg, &d.pln_geo)) || (rc = upload(r, pm, &d.pln_mat)) || (rc = upload(r, loc, &d.obj_loc)) ||
       (rc = upload(r, bvh, &d.bvh)))
     return rc;
+  {
+    // the bounce kernel's LDS copy of the node links and margin terms (rfx_types.h DevScene::bvh_aux): mt rounded up
+    // to a multiple of mstep (one step more than the ceiling, so the float decode stays above)
+    float mt_max = 0.0f;
+    for (const BvhNode &n : bvh) mt_max = fmaxf(mt_max, fmaxf(n.mt[0], n.mt[1]));
+    const float mstep = mt_max > 0.0f ? mt_max / 65000.0f : 1.0f;
+    std::vector<uint32_t> aux(2 * bvh.size());
+    for (size_t i = 0; i < bvh.size(); ++i)
+    {
+      const BvhNode &n = bvh[i];
+      uint32_t q[2];
+      for (int c = 0; c < 2; ++c) q[c] = (uint32_t)std::min(65535.0, ceil((double)n.mt[c] / mstep) + 1.0);
+      aux[2 * i] = ((uint32_t)(uint16_t)(int16_t)n.child[0]) | ((uint32_t)(uint16_t)(int16_t)n.child[1] << 16);
+      aux[2 * i + 1] = q[0] | q[1] << 16;
+    }
+    if ((rc = upload(r, aux, &d.bvh_aux))) return rc;
+    d.bvh_mstep = mstep;
+    d.n_bvh = (int32_t)bvh.size();
+  }
   d.n_sph = (int32_t)sg.size();
   d.n_tri = (int32_t)tg.size();
   d.n_light = (int32_t)lr.size();
@@ -1392,7 +1415,16 @@ static int trace_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *rd, float
     const uint32_t groups = (uint32_t)std::min<uint64_t>((waves + 1) / 2, (uint64_t)r->cus * RFX_BOUNCE_GROUPS_PER_CU);
     const int cfg = 1 | (r->dev.n_light > 32 ? 2 : 0) | (small ? 4 : 0) | (r->dev.n_pln ? 8 : 0);  // rfx_trace.h kCfg*
     if (sort_queue) HIP_CHECK(launch_queue_sort(r->d_qctr, r->d_qkey, r->d_qctr + 2, r->d_qorder, st));
-    launch_bounce(cfg, dim3(groups), r->dev, P, st);
+    // a BVH whose nodes fit the workgroup's LDS (56 B each beside the stacks: up to ~2,100 nodes, i.e. 4,200 spheres):
+    // the LDS-staged bounce kernel, one 16-wave workgroup per CU (C5 trace + bounce -4..6%, tools/ab.py); else the
+    // two-wave workgroups walking the nodes in global memory
+    if (!small && r->dev.n_bvh > 0 && lds_bvh_bytes_host(r->dev.n_bvh) + 4096 <= 160 * 1024)
+    {
+      const uint32_t lgroups = (uint32_t)std::min<uint64_t>((waves + kLdsBvhWaves - 1) / kLdsBvhWaves, (uint64_t)r->cus);
+      HIP_CHECK(launch_bounce_lds(cfg, lgroups, r->dev, P, st));
+    }
+    else
+      launch_bounce(cfg, dim3(groups), r->dev, P, st);
     HIP_CHECK(hipGetLastError());
   }
   if (record)

@@ -719,6 +719,38 @@ constexpr float kNarrowBundleCos = RFX_NARROW_BUNDLE_COS;  // rfx_host.cpp RFX_B
 typedef int16_t BvhSlot;
 __shared__ BvhSlot s_bvh_stack[kBvhStack * kWgThreads];
 
+// Where the BVH walkers read nodes and keep their per-lane stacks: the scene's node array in global memory and the
+// workgroup's LDS stack (kernels of kWgThreads threads), or -- the LDS-staged bounce kernel (RFX_LDS_BVH) -- node
+// boxes and links staged in the workgroup's LDS by its kLdsBvhThreads threads.
+constexpr int kLdsBvhThreads = 1024;
+struct BvhGlobal {
+  static constexpr int kStride = kWgThreads;
+  __device__ __forceinline__ BvhNode node(const DevScene &S, int i) const { return S.bvh[i]; }
+  __device__ __forceinline__ BvhSlot *stack() const { return s_bvh_stack + threadIdx.x; }
+};
+struct BvhLds {
+  const float4 *box;  // 3 per node: the first 48 B of BvhNode (both children's boxes)
+  const uint2 *aux;   // DevScene::bvh_aux
+  BvhSlot *stk;
+  float mstep;
+  static constexpr int kStride = kLdsBvhThreads;
+  __device__ __forceinline__ BvhNode node(const DevScene &, int i) const
+  {
+    BvhNode n;
+    const float4 a = box[3 * i], b = box[3 * i + 1], c = box[3 * i + 2];
+    n.lx[0] = a.x; n.lx[1] = a.y; n.ly[0] = a.z; n.ly[1] = a.w;
+    n.lz[0] = b.x; n.lz[1] = b.y; n.hx[0] = b.z; n.hx[1] = b.w;
+    n.hy[0] = c.x; n.hy[1] = c.y; n.hz[0] = c.z; n.hz[1] = c.w;
+    const uint2 x = aux[i];
+    n.child[0] = (int32_t)(int16_t)(x.x & 0xFFFFu);
+    n.child[1] = (int32_t)(int16_t)(x.x >> 16);
+    n.mt[0] = (float)(x.y & 0xFFFFu) * mstep;
+    n.mt[1] = (float)(x.y >> 16) * mstep;
+    return n;
+  }
+  __device__ __forceinline__ BvhSlot *stack() const { return stk + threadIdx.x; }
+};
+
 // box margins from the node's stored term and one per-ray distance (round 2: C5 -8.5% against a margin per box)
 struct RayInv { float ix, iy, iz, dm; };  // dm: kCullRel |o - bvh_ref|_2 + 1e-6 (approximate root, widened 1e-4)
 __device__ __forceinline__ RayInv ray_inv(const DevScene &S, v3 o, v3 ray)
@@ -747,19 +779,19 @@ __device__ __forceinline__ bool bvh_box(const BvhNode &n, int c, v3 o, const Ray
 }
 
 // closest sphere hit of one lane's ray over the BVH (Scene.cpp:86-106 restricted to the spheres)
-template <bool STATS>
+template <bool STATS, class NS>
 __device__ __forceinline__ void closest_spheres_bvh(const DevScene &S, v3 origin, v3 ray, const RayConst &k, Hit &h,
-                                                    Cnt &cnt)
+                                                    Cnt &cnt, const NS &ns)
 {
   const RayInv ri = ray_inv(S, origin, ray);
   const float a = 0.5f * k.a2;                // |ray|^2 (exact: a2 = 2a)
-  BvhSlot *stack = s_bvh_stack + threadIdx.x;
+  BvhSlot *stack = ns.stack();
   int sp = 0, node = 0;
   for (;;)
   {
     if (node >= 0)
     {
-      const BvhNode n = S.bvh[node];
+      const BvhNode n = ns.node(S, node);
       float t0, t1;
       // a child entered beyond the best hit cannot hold a closer (or tying) sphere
       const bool h0 = bvh_box(n, 0, origin, ri, t0) && !(t0 * t0 * a > h.sq * 1.001f);
@@ -767,7 +799,7 @@ __device__ __forceinline__ void closest_spheres_bvh(const DevScene &S, v3 origin
       if (h0 && h1)
       {
         const bool first0 = !(t1 < t0);
-        stack[kWgThreads * sp++] = first0 ? n.child[1] : n.child[0];
+        stack[NS::kStride * sp++] = first0 ? n.child[1] : n.child[0];
         node = first0 ? n.child[0] : n.child[1];
         continue;
       }
@@ -798,29 +830,29 @@ __device__ __forceinline__ void closest_spheres_bvh(const DevScene &S, v3 origin
       }
     }
     if (sp == 0) break;
-    node = stack[kWgThreads * --sp];
+    node = stack[NS::kStride * --sp];
   }
 }
 
 // any sphere but skip_sph occludes the shadow ray (Scene.cpp:129-141 restricted to the spheres)
-template <bool STATS>
+template <bool STATS, class NS>
 __device__ __forceinline__ bool occluded_spheres_bvh(const DevScene &S, v3 o, v3 ray, const RayConst &k, int skip_sph,
-                                                     Cnt &cnt)
+                                                     Cnt &cnt, const NS &ns)
 {
   const RayInv ri = ray_inv(S, o, ray);
-  BvhSlot *stack = s_bvh_stack + threadIdx.x;
+  BvhSlot *stack = ns.stack();
   int sp = 0, node = 0;
   float t, sq;
   for (;;)
   {
     if (node >= 0)
     {
-      const BvhNode n = S.bvh[node];
+      const BvhNode n = ns.node(S, node);
       float t0, t1;
       const bool h0 = bvh_box(n, 0, o, ri, t0), h1 = bvh_box(n, 1, o, ri, t1);
       if (h0 && h1)
       {
-        stack[kWgThreads * sp++] = n.child[1];
+        stack[NS::kStride * sp++] = n.child[1];
         node = n.child[0];
         continue;
       }
@@ -842,7 +874,7 @@ __device__ __forceinline__ bool occluded_spheres_bvh(const DevScene &S, v3 o, v3
         return true;
     }
     if (sp == 0) return false;
-    node = stack[kWgThreads * --sp];
+    node = stack[NS::kStride * --sp];
   }
 }
 
@@ -883,9 +915,9 @@ __device__ __forceinline__ bool occluded_planes(const DevScene &S, v3 o, v3 ray,
 // Large scenes: the spheres are stored in spatial order (recursive median splits), 64 to a chunk with a bounding sphere;
 // the bundle culls whole chunks (one lane per chunk), then the spheres of the surviving chunks.  The
 // visiting order is then not the insertion order, so spheres take the general (distance, object) rule.
-template <bool STATS, bool PLANES>
+template <bool STATS, bool PLANES, class NS = BvhGlobal>
 __device__ __forceinline__ void closest_hit(const DevScene &S, v3 origin, v3 ray, bool live, const Bundle *B, Hit &h,
-                                            Cnt &cnt)
+                                            Cnt &cnt, const NS &ns = NS{})
 {
   if (live) RFX_CNT(C_SEGMENTS);
   h.obj = -1; h.kind = 0; h.i = 0; h.t = 0.0f; h.u = 0.0f; h.v = 0.0f; h.sq = kNoHitKey;
@@ -898,7 +930,7 @@ __device__ __forceinline__ void closest_hit(const DevScene &S, v3 origin, v3 ray
   // a narrow bundle (the primary rays of a tile: one origin, a cone of ~0.1 degree) culls the spatial chunks and
   // their spheres for the whole wave at once; wider ones walk the BVH lane by lane
   const bool use_bvh = !STATS && S.bvh != nullptr && !(cull && B->cosa > kNarrowBundleCos);
-  if (use_bvh && live) closest_spheres_bvh<STATS>(S, origin, ray, k, h, cnt);
+  if (use_bvh && live) closest_spheres_bvh<STATS>(S, origin, ray, k, h, cnt, ns);
   for (int cfirst = 0; !use_bvh && cfirst < S.n_chunk; cfirst += 64)
   {
     uint64_t cm = cull ? cull_chunk(S.chunk_bound, cfirst, min(64, S.n_chunk - cfirst), *B)
@@ -1092,16 +1124,16 @@ __device__ __forceinline__ bool occluded_small(const DevScene &S, v3 o, v3 ray, 
 // lane has one.  (Spheres precede triangles, the reference's order for scenes whose objects are added
 // spheres-first -- then even the event counters match it: the second sphere of a pair is counted only
 // when the first did not occlude.)
-template <bool STATS, bool PLANES>
+template <bool STATS, bool PLANES, class NS = BvhGlobal>
 __device__ __forceinline__ bool occluded(const DevScene &S, v3 o, v3 ray, bool live, int skip_sph, int skip_tri,
-                                         int skip_pln, const Bundle *B, Cnt &cnt)
+                                         int skip_pln, const Bundle *B, Cnt &cnt, const NS &ns = NS{})
 {
   const RayConst k = ray_const(ray);
   const bool cull = B && B->ok;
   bool occ = false;
   float t, sq, u, v;
   const bool use_bvh = !STATS && S.bvh != nullptr;
-  if (use_bvh && live) occ = occluded_spheres_bvh<STATS>(S, o, ray, k, skip_sph, cnt);
+  if (use_bvh && live) occ = occluded_spheres_bvh<STATS>(S, o, ray, k, skip_sph, cnt, ns);
   for (int cfirst = 0; !use_bvh && cfirst < S.n_chunk; cfirst += 64)
   {
     if (__ballot(live && !occ) == 0) return occ;
@@ -1186,6 +1218,7 @@ struct Park {
   static constexpr bool kRefill = false;
   __device__ __forceinline__ void ids(uint32_t &t, uint32_t &o) const { t = trace; o = out; }
   __device__ __forceinline__ uint32_t *keys() const { return nullptr; }
+  __device__ __forceinline__ BvhGlobal bvh() const { return BvhGlobal{}; }
 };
 
 // Regroup sort key of a parked trace (RFX_QUEUE_SORT): its direction octant and the Morton index of its origin's cell
@@ -1253,7 +1286,7 @@ __device__ __forceinline__ col trace_from(const DevScene &S, v3 origin, v3 ray, 
     {
       Bundle B;
       if constexpr (CULL) B = make_bundle(origin, ray, alive);
-      closest_hit<STATS, PLANES>(S, origin, ray, alive, CULL ? &B : nullptr, h, cnt);
+      closest_hit<STATS, PLANES>(S, origin, ray, alive, CULL ? &B : nullptr, h, cnt, park.bvh());
     }
     const bool hit = alive && h.obj >= 0;
     // re-derive the winner's outputs with the reference's expressions
@@ -1334,7 +1367,7 @@ __device__ __forceinline__ col trace_from(const DevScene &S, v3 origin, v3 ray, 
             Bundle SB;
             if constexpr (CULL) SB = make_bundle(drop, sray, facing);
             const bool occ = occluded<STATS, PLANES>(S, drop, sray, facing, skip_sph, skip_tri, skip_pln,
-                                                     CULL ? &SB : nullptr, cnt);
+                                                     CULL ? &SB : nullptr, cnt, park.bvh());
             if (facing && !occ) lit |= 1u << q;
           }
         }
@@ -1542,6 +1575,7 @@ struct ParkTile {
   }
   static constexpr bool kRefill = false;
   __device__ __forceinline__ uint32_t *keys() const { return P.queue_key; }
+  __device__ __forceinline__ BvhGlobal bvh() const { return BvhGlobal{}; }
 };
 
 // trace i's randomInsideSphere draw (Vector3.cpp:176-188) from the LCG state before its accepted triple
@@ -1875,18 +1909,21 @@ __global__ RFX_TRACE_BOUNDS void prim_cull_kernel(DevScene S, FrameParams P, uin
 // run.
 __shared__ uint32_t s_refill_out[kWgWaves][64];  // per lane: the output pixel of its trace in flight (~0u: none)
 
+template <class NS = BvhGlobal>
 struct Refill {
   const FrameParams &P;
   uint32_t n;             // queue entries
-  uint32_t wv;            // the wave's slot in its workgroup
+  uint32_t *outs;         // LDS: the output pixel of each lane's trace in flight (~0u: none), 64 per wave
+  NS ns;                  // where the BVH walkers find the nodes
   mutable bool drained;   // wave-uniform: every entry has been claimed
   static constexpr bool kRefill = true;
   __device__ __forceinline__ void ids(uint32_t &t, uint32_t &o) const { t = o = 0u; }  // (never parks)
   __device__ __forceinline__ uint32_t *keys() const { return nullptr; }
+  __device__ __forceinline__ const NS &bvh() const { return ns; }
   __device__ __forceinline__ void refill(bool &alive, v3 &origin, v3 &ray, col &mulc, col &pix, int &refl, v3 &rd) const
   {
     const uint32_t lane = __lane_id();
-    uint32_t out = s_refill_out[wv][lane];
+    uint32_t out = outs[lane];
     if (!alive && out != ~0u)
     {
       const col o = cadd(mkc(0.0f, 0.0f, 0.0f), pix);                               // Render.cpp:185
@@ -1918,7 +1955,7 @@ struct Refill {
         alive = refl < P.depth;
       }
     }
-    s_refill_out[wv][lane] = out;
+    outs[lane] = out;
   }
 };
 
@@ -1935,7 +1972,7 @@ __global__ RFX_TRACE_BOUNDS void bounce_kernel(DevScene S, FrameParams P)
   Cnt cnt;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   s_refill_out[wv][__lane_id()] = ~0u;
-  const Refill rf{P, *P.queue_count, wv, false};
+  const Refill<> rf{P, *P.queue_count, s_refill_out[wv], BvhGlobal{}, false};
   bool alive = false;
   v3 origin = mk(0.0f, 0.0f, 0.0f), ray = origin, rd = origin;
   col mulc = mkc(0.0f, 0.0f, 0.0f), pix = mulc;
@@ -1946,6 +1983,54 @@ __global__ RFX_TRACE_BOUNDS void bounce_kernel(DevScene S, FrameParams P)
   (void)trace_from<false, CULL, MANYL, SMALL, PLANES, false>(S, origin, ray, mulc, pix, refl, P.depth, rd, lut, cnt, alive,
                                                              rf, parked);
   RFX_WAVE_T1(kBounceTimeBase + kWgWaves * blockIdx.x + wv);
+}
+
+// The bounce kernel with the BVH staged in LDS (RFX_LDS_BVH; large scenes whose nodes fit): one workgroup of
+// kLdsBvhThreads threads per CU copies the node boxes (48 B each) and links + margin terms (8 B, DevScene::bvh_aux)
+// into its LDS, then its 16 waves take parked traces as bounce_kernel's do -- the walkers' node fetches become LDS
+// reads instead of L2 round trips.  Dynamic LDS: lds_bvh_bytes(n_bvh).
+__host__ __device__ constexpr size_t lds_bvh_bytes(int n_bvh)
+{
+  return (size_t)n_bvh * 56 + sizeof(BvhSlot) * kBvhStack * kLdsBvhThreads + 4 * 64 * (kLdsBvhThreads / 64);
+}
+template <int CFG>
+__global__ __launch_bounds__(kLdsBvhThreads) __attribute__((amdgpu_waves_per_eu(4)))
+void bounce_kernel_lds(DevScene S, FrameParams P)
+{
+  constexpr bool CULL = (CFG & kCfgCull) != 0, MANYL = (CFG & kCfgManyLights) != 0, SMALL = (CFG & kCfgSmall) != 0;
+  constexpr bool PLANES = (CFG & kCfgPlanes) != 0;
+  static_assert(!SMALL, "large scenes only");
+  extern __shared__ float4 s_dyn[];
+  const int nn = S.n_bvh;
+  float4 *box = s_dyn;
+  uint2 *aux = reinterpret_cast<uint2 *>(box + 3 * nn);
+  BvhSlot *stk = reinterpret_cast<BvhSlot *>(aux + nn);
+  uint32_t *outs = reinterpret_cast<uint32_t *>(stk + kBvhStack * kLdsBvhThreads);
+  __shared__ float lut[256];
+  for (uint32_t i = threadIdx.x; i < 256; i += kLdsBvhThreads) lut[i] = (float)i / 255.0f;  // Color.cpp:11-13
+  stage_powf_tables();
+  const float4 *gb = reinterpret_cast<const float4 *>(S.bvh);
+  const uint2 *ga = reinterpret_cast<const uint2 *>(S.bvh_aux);
+  for (int i = (int)threadIdx.x; i < nn; i += kLdsBvhThreads)
+  {
+    box[3 * i] = gb[4 * i];
+    box[3 * i + 1] = gb[4 * i + 1];
+    box[3 * i + 2] = gb[4 * i + 2];
+    aux[i] = ga[i];
+  }
+  __syncthreads();
+  Cnt cnt;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  outs[64 * wv + __lane_id()] = ~0u;
+  const Refill<BvhLds> rf{P, *P.queue_count, outs + 64 * wv, BvhLds{box, aux, stk, S.bvh_mstep}, false};
+  bool alive = false;
+  v3 origin = mk(0.0f, 0.0f, 0.0f), ray = origin, rd = origin;
+  col mulc = mkc(0.0f, 0.0f, 0.0f), pix = mulc;
+  int refl = 0;
+  rf.refill(alive, origin, ray, mulc, pix, refl, rd);
+  bool parked;
+  (void)trace_from<false, CULL, MANYL, SMALL, PLANES, false>(S, origin, ray, mulc, pix, refl, P.depth, rd, lut, cnt, alive,
+                                                             rf, parked);
 }
 
 // ------------------------------------------------------------- launch of one family (the rfx_trace_*.hip TUs)

@@ -34,6 +34,30 @@ static void launch_bounce_one(dim3 grid, const DevScene &S, const FrameParams &P
   hipLaunchKernelGGL((bounce_kernel<CFG>), grid, dim3(kWgThreads), 0, st, S, P);
 }
 
+// the LDS-staged bounce kernel (large scenes, rfx_trace.h bounce_kernel_lds): one workgroup per CU
+template <int CFG>
+static hipError_t launch_bounce_lds_one(uint32_t groups, const DevScene &S, const FrameParams &P, hipStream_t st)
+{
+  const size_t lds = lds_bvh_bytes(S.n_bvh);
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&bounce_kernel_lds<CFG>),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((bounce_kernel_lds<CFG>), dim3(groups), dim3(kLdsBvhThreads), lds, st, S, P);
+  return hipGetLastError();
+}
+
+hipError_t launch_bounce_lds(int cfg, uint32_t groups, const DevScene &S, const FrameParams &P, hipStream_t st)
+{
+  switch (cfg)
+  {
+    case 1: return launch_bounce_lds_one<1>(groups, S, P, st);
+    case 3: return launch_bounce_lds_one<3>(groups, S, P, st);
+    case 9: return launch_bounce_lds_one<9>(groups, S, P, st);
+    case 11: return launch_bounce_lds_one<11>(groups, S, P, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
 void launch_bounce(int cfg, dim3 grid, const DevScene &S, const FrameParams &P, hipStream_t st)
 {
   switch (cfg)

@@ -90,6 +90,9 @@ struct DevScene {
   float key_lx, key_ly, key_lz;  // regroup sort keys: origin cell = (o - key_l) * key_s in [0, 8) per axis (the BVH
   float key_sx, key_sy, key_sz;  // root box; 0 scale without a BVH: one cell)
   int32_t n_chunk;            // (n_sph + 63) / 64
+  const uint32_t *bvh_aux;    // per node: child indices as two int16 (lo, hi), margin terms as two uint16 * bvh_mstep
+  float bvh_mstep;            //   (rounded up) -- the 8-B record the LDS-staged bounce kernel keeps beside the boxes
+  int32_t n_bvh;              // nodes of the BVH
   float amb_r, amb_g, amb_b;  // diffLightColor * diffLightPower (Scene.cpp:186, host-folded)
   float env_r, env_g, env_b;  // envColor (Scene.cpp:12,55)
   float half_tile_w, half_tile_h;  // Skybox.cpp:21-37

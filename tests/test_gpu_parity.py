@@ -464,6 +464,20 @@ def test_stress_band_other_regrouping(key, regroup, qsort):
     r.close()
 
 
+@pytest.mark.parametrize("n_spheres", [4096, 4600])
+def test_regrouped_large_scene_equals_unregrouped(n_spheres):
+    """The bounce kernel's two forms on large scenes: with the BVH staged in LDS (4096 spheres: 2,047 nodes fit) and
+    walking it in global memory (4600 spheres: 2,299 nodes do not).  Regrouped frames (park after 1 and 2) equal the
+    frame traced without regrouping, bit for bit, over two frames of the random stream."""
+    desc = scenes.stress_scene(n_spheres)
+    ref, _, r0 = gpu_render(desc, 320, 180, 12, frames=2, regroup=0)
+    r0.close()
+    for park in (1, 2):
+        rgb, _, r = gpu_render(desc, 320, 180, 12, frames=2, regroup=park)
+        assert rgb.tobytes() == ref.tobytes(), (n_spheres, park)
+        r.close()
+
+
 @pytest.mark.parametrize("key", ["hash_synth16_3840x2160_d8", "hash_default_640x480_d4", "hash_synth16_7680x4320_d8"])
 def test_primary_masks_match_reference_hash(key):
     """Precomputed primary-bundle cull masks (rfx_renderer_set_prim_masks 2: built before the launch, so the
