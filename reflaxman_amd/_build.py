@@ -41,12 +41,27 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found: cannot build librfx.so")
 
 
+def _sources_digest() -> str:
+    """SHA-256 over the compiler flags and the contents of every source and header the library is built from."""
+    import hashlib
+    h = hashlib.sha256(" ".join(FLAGS).encode())
+    for d in [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(INCLUDE, "rfx.h")]:
+        h.update(os.path.basename(d).encode())
+        with open(d, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
+DIGEST = LIB + ".src.sha256"  # the digest of the sources the in-tree librfx.so was built from
+
+
 def _stale() -> bool:
-    if not os.path.exists(LIB):
+    """Content-based: the library is stale when it is missing or was built from other sources (file times are not
+    compared -- a copied tree, e.g. on a GPU box, keeps the library it came with)."""
+    if not os.path.exists(LIB) or not os.path.exists(DIGEST):
         return True
-    t = os.path.getmtime(LIB)
-    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(INCLUDE, "rfx.h")]
-    return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
+    with open(DIGEST) as f:
+        return f.read().strip() != _sources_digest()
 
 
 def _compile_link(out: str, extra, objdir: str) -> str:
@@ -55,8 +70,13 @@ def _compile_link(out: str, extra, objdir: str) -> str:
 
     def one(src):
         obj = os.path.join(objdir, os.path.splitext(src)[0] + ".o")
-        cmd = [hipcc(), *FLAGS, *extra, "-c", os.path.join(CSRC, src), "-o", obj]
-        r = subprocess.run(cmd, capture_output=True, text=True)
+        # compiled from inside csrc/ by relative name, with the tree's root mapped to '.' and a fixed compilation-unit
+        # id (HIP derives the default from the input path): the code objects carry nothing of the build directory, so
+        # the device code -- and its hash, _lib.device_sha256, which keys profiles/pmc -- is the same wherever the tree
+        # is built
+        cmd = [hipcc(), *FLAGS, *extra, f"-ffile-prefix-map={ROOT}=.", f"-cuid=rfx_{os.path.splitext(src)[0]}", "-c", src,
+               "-o", os.path.abspath(obj)]
+        r = subprocess.run(cmd, capture_output=True, text=True, cwd=CSRC)
         if r.returncode != 0:
             raise RuntimeError("build failed:\n" + " ".join(cmd) + "\n" + r.stdout + r.stderr)
         return obj, r.stderr
@@ -83,7 +103,7 @@ def build_variant(name: str, defines, verbose: bool = False) -> str:
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
-    """Compile librfx.so if missing or older than its sources; return its path."""
+    """Compile librfx.so if missing or built from other sources; return its path."""
     if not force and not _stale():
         return LIB
     os.makedirs(LIBDIR, exist_ok=True)
@@ -92,6 +112,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if verbose:
         print(err)
     os.replace(tmp, LIB)
+    with open(DIGEST, "w") as f:
+        f.write(_sources_digest() + "\n")
     return LIB
 
 
