@@ -45,9 +45,6 @@ size_t tile_order_scratch();
 hipError_t launch_tile_order(const uint32_t *cost, uint32_t n, uint32_t *order, uint32_t *scratch, hipStream_t st);
 void launch_bounce(int cfg, dim3 grid, const DevScene &S, const FrameParams &P, hipStream_t st);
 hipError_t launch_bounce_lds(int cfg, uint32_t groups, const DevScene &S, const FrameParams &P, hipStream_t st);
-constexpr int kLdsBvhWaves = 16;  // rfx_trace.h kLdsBvhThreads / 64
-// rfx_trace.h lds_bvh_bytes: 56 B per node, 16 int16 stack slots per lane, 64 output slots per wave
-constexpr size_t lds_bvh_bytes_host(int n_bvh) { return (size_t)n_bvh * 56 + 2 * 16 * 64 * kLdsBvhWaves + 4 * 64 * kLdsBvhWaves; }
 hipError_t launch_kat(int what, const DevScene &S, int tex, const void *in, const int32_t *objs, uint32_t n, void *out,
                       hipStream_t st);
 hipError_t launch_kat_powf_cube(uint32_t first, uint32_t n, unsigned long long *counts, hipStream_t st);
@@ -1418,13 +1415,12 @@ static int trace_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *rd, float
     // a BVH whose nodes fit the workgroup's LDS (56 B each beside the stacks: up to ~2,100 nodes, i.e. 4,200 spheres):
     // the LDS-staged bounce kernel, one 16-wave workgroup per CU (C5 trace + bounce -4..6%, tools/ab.py); else the
     // two-wave workgroups walking the nodes in global memory
-    if (!small && r->dev.n_bvh > 0 && lds_bvh_bytes_host(r->dev.n_bvh) + 4096 <= 160 * 1024)
+    const uint32_t lgroups = (uint32_t)std::min<uint64_t>((waves + kLdsBvhWaves - 1) / kLdsBvhWaves, (uint64_t)r->cus);
+    if (small || !lds_bvh_fits(r->dev.n_bvh) || launch_bounce_lds(cfg, lgroups, r->dev, P, st) != hipSuccess)
     {
-      const uint32_t lgroups = (uint32_t)std::min<uint64_t>((waves + kLdsBvhWaves - 1) / kLdsBvhWaves, (uint64_t)r->cus);
-      HIP_CHECK(launch_bounce_lds(cfg, lgroups, r->dev, P, st));
-    }
-    else
+      (void)hipGetLastError();  // an LDS launch the runtime refused: the global-memory form instead
       launch_bounce(cfg, dim3(groups), r->dev, P, st);
+    }
     HIP_CHECK(hipGetLastError());
   }
   if (record)

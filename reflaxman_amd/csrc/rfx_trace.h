@@ -722,7 +722,8 @@ __shared__ BvhSlot s_bvh_stack[kBvhStack * kWgThreads];
 // Where the BVH walkers read nodes and keep their per-lane stacks: the scene's node array in global memory and the
 // workgroup's LDS stack (kernels of kWgThreads threads), or -- the LDS-staged bounce kernel (RFX_LDS_BVH) -- node
 // boxes and links staged in the workgroup's LDS by its kLdsBvhThreads threads.
-constexpr int kLdsBvhThreads = 1024;
+constexpr int kLdsBvhThreads = 64 * kLdsBvhWaves;
+static_assert(kLdsBvhStackSlots == kBvhStack, "rfx_types.h lds_bvh_bytes sizes the stacks");
 struct BvhGlobal {
   static constexpr int kStride = kWgThreads;
   __device__ __forceinline__ BvhNode node(const DevScene &S, int i) const { return S.bvh[i]; }
@@ -1988,11 +1989,7 @@ __global__ RFX_TRACE_BOUNDS void bounce_kernel(DevScene S, FrameParams P)
 // The bounce kernel with the BVH staged in LDS (RFX_LDS_BVH; large scenes whose nodes fit): one workgroup of
 // kLdsBvhThreads threads per CU copies the node boxes (48 B each) and links + margin terms (8 B, DevScene::bvh_aux)
 // into its LDS, then its 16 waves take parked traces as bounce_kernel's do -- the walkers' node fetches become LDS
-// reads instead of L2 round trips.  Dynamic LDS: lds_bvh_bytes(n_bvh).
-__host__ __device__ constexpr size_t lds_bvh_bytes(int n_bvh)
-{
-  return (size_t)n_bvh * 56 + sizeof(BvhSlot) * kBvhStack * kLdsBvhThreads + 4 * 64 * (kLdsBvhThreads / 64);
-}
+// reads instead of L2 round trips.  Dynamic LDS: lds_bvh_bytes(n_bvh) (rfx_types.h).
 template <int CFG>
 __global__ __launch_bounds__(kLdsBvhThreads) __attribute__((amdgpu_waves_per_eu(4)))
 void bounce_kernel_lds(DevScene S, FrameParams P)

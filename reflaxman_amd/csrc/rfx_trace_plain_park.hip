@@ -38,11 +38,11 @@ static void launch_bounce_one(dim3 grid, const DevScene &S, const FrameParams &P
 template <int CFG>
 static hipError_t launch_bounce_lds_one(uint32_t groups, const DevScene &S, const FrameParams &P, hipStream_t st)
 {
-  const size_t lds = lds_bvh_bytes(S.n_bvh);
-  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void *>(&bounce_kernel_lds<CFG>),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((bounce_kernel_lds<CFG>), dim3(groups), dim3(kLdsBvhThreads), lds, st, S, P);
+  // the kernel may take the whole CU's LDS: raise its dynamic limit once (every size lds_bvh_fits accepts)
+  static const hipError_t limit = hipFuncSetAttribute(reinterpret_cast<const void *>(&bounce_kernel_lds<CFG>),
+                                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 4096);
+  if (limit != hipSuccess) return limit;
+  hipLaunchKernelGGL((bounce_kernel_lds<CFG>), dim3(groups), dim3(kLdsBvhThreads), lds_bvh_bytes(S.n_bvh), st, S, P);
   return hipGetLastError();
 }
 

@@ -98,6 +98,17 @@ struct DevScene {
   float half_tile_w, half_tile_h;  // Skybox.cpp:21-37
 };
 
+// The bounce kernel with the BVH staged in LDS (rfx_trace.h bounce_kernel_lds): one workgroup of kLdsBvhWaves waves
+// per CU; its dynamic LDS holds the node boxes (48 B each), DevScene::bvh_aux (8 B each), the lanes' traversal stacks
+// (kLdsBvhStackSlots int16 each) and one output slot (u32) per lane.
+constexpr int kLdsBvhWaves = 16, kLdsBvhStackSlots = 16;
+constexpr size_t lds_bvh_bytes(int n_bvh)
+{
+  return (size_t)n_bvh * 56 + sizeof(int16_t) * kLdsBvhStackSlots * 64 * kLdsBvhWaves + 4 * 64 * kLdsBvhWaves;
+}
+// whether a BVH of n_bvh nodes fits beside the kernel's static LDS (the colour table and powf's tables, < 4 KB)
+constexpr bool lds_bvh_fits(int n_bvh) { return n_bvh > 0 && lds_bvh_bytes(n_bvh) + 4096 <= 160 * 1024; }
+
 // A trace parked between bounce segments (large scenes, plain pixels): the state Scene::trace carries from
 // one segment to the next (Scene.cpp:80-234: origin, ray, mulColor, pixelColor, refl), the trace index of its
 // randDir and the output pixel.  64 B: one lane stores / loads it with four 16-B accesses.
