@@ -3,7 +3,11 @@
 // waves -- its own TU so it compiles in parallel with the other families (reflaxman_amd/_build.py).
 #include "rfx_trace.h"
 
+#include <atomic>
+
 namespace rfx {
+
+constexpr int kLdsLimitDevices = 64;  // devices whose LDS-limit attribute is cached (others: set at every launch)
 
 template <int CFG>
 static void launch_park_one(dim3 grid, const DevScene &S, const FrameParams &P, hipStream_t st)
@@ -38,10 +42,19 @@ static void launch_bounce_one(dim3 grid, const DevScene &S, const FrameParams &P
 template <int CFG>
 static hipError_t launch_bounce_lds_one(uint32_t groups, const DevScene &S, const FrameParams &P, hipStream_t st)
 {
-  // the kernel may take the whole CU's LDS: raise its dynamic limit once (every size lds_bvh_fits accepts)
-  static const hipError_t limit = hipFuncSetAttribute(reinterpret_cast<const void *>(&bounce_kernel_lds<CFG>),
-                                                      hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 4096);
-  if (limit != hipSuccess) return limit;
+  // the kernel may take the whole CU's LDS: raise its dynamic limit (every size lds_bvh_fits accepts) once per device
+  // -- the attribute belongs to the current device, and a device group drives several from one process
+  static std::atomic<int> limit_set[kLdsLimitDevices];  // 0 not yet, 1 raised, 2 refused
+  int dev = 0;
+  const bool cached = hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < kLdsLimitDevices;
+  int state = cached ? limit_set[dev].load(std::memory_order_relaxed) : 0;
+  if (state == 0)
+  {
+    state = hipFuncSetAttribute(reinterpret_cast<const void *>(&bounce_kernel_lds<CFG>),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 4096) == hipSuccess ? 1 : 2;
+    if (cached) limit_set[dev].store(state, std::memory_order_relaxed);
+  }
+  if (state != 1) return hipErrorInvalidValue;
   hipLaunchKernelGGL((bounce_kernel_lds<CFG>), dim3(groups), dim3(kLdsBvhThreads), lds_bvh_bytes(S.n_bvh), st, S, P);
   return hipGetLastError();
 }
