@@ -61,17 +61,21 @@ def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
 
-# BASELINE.json configs: scene, width, height, depth, description
+# BASELINE.json configs (and the reference's screenshot workload): scene, width, height, depth, samples per pixel
+# (ss x ss), description
 CONFIGS = {
-    "c1": ("default", 640, 480, 4, "C1 default scene (Render::loadScene, textures absent -> checker)"),
-    "c2": ("default", 1920, 1080, 4, "C2 default scene"),
-    "c3": ("synth16", 3840, 2160, 8, "C3 synth16: 16 spheres + 4 textured triangles + sun"),
-    "c4": ("synth16", 7680, 4320, 8, "C4 synth16 (the C3 scene: 16 spheres + 4 textured triangles + sun)"),
-    "c5": ("stress4096", 3840, 2160, 12, "C5 stress4096: 4096 spheres + ground quad + sun"),
+    "c1": ("default", 640, 480, 4, 1, "C1 default scene (Render::loadScene, textures absent -> checker)"),
+    "c2": ("default", 1920, 1080, 4, 1, "C2 default scene"),
+    "c3": ("synth16", 3840, 2160, 8, 1, "C3 synth16: 16 spheres + 4 textured triangles + sun"),
+    "c4": ("synth16", 7680, 4320, 8, 1, "C4 synth16 (the C3 scene: 16 spheres + 4 textured triangles + sun)"),
+    "c5": ("stress4096", 3840, 2160, 12, 1, "C5 stress4096: 4096 spheres + ground quad + sun"),
+    "shot": ("default", 1920, 1080, 20, 4, "screenshot: Render's default scene, Full HD, 4x4 SSAA, depth 20 "
+                                           "(Pulse.cpp:156-178, defaults.h:9)"),
 }
 # cpu_baseline row strides: about 5 s of the reference's single-core trace time per config (C5's CPU rate is
-# 0.0064 Mrays/s: every 270th row)
+# 0.0064 Mrays/s: every 270th row); SSAA configs time a centred band of this many rows instead
 CPU_STRIDE = {"c1": 1, "c2": 4, "c3": 2, "c4": 16, "c5": 270}
+CPU_BAND_ROWS = {"shot": 64}
 
 
 def frame_size(n: int, w0: int, h0: int, scaling: str):
@@ -117,6 +121,36 @@ def cpu_model() -> str:
 def u8_diff(a: np.ndarray, b: np.ndarray) -> int:
     ch = lambda x, s: ((x >> s) & 0xFF).astype(np.int32)
     return int(max(np.abs(ch(a, s) - ch(b, s)).max() for s in (0, 8, 16))) if a.size else 0
+
+
+def cpu_baseline_band(desc, W, H, depth, ss, gpu_rgb, gpu_argb, rows):
+    """SSAA frames: the reference's CPU path (oracle/_ref/refharness bandss, Render::renderNext's pixel loop over the
+    unmodified sources) on a centred band of `rows` rows of the same frame, one host core; the band is also compared
+    with the GPU frame's."""
+    harness = os.path.join(ROOT, "oracle", "_ref", "refharness")
+    if not os.path.exists(harness):
+        return None, None
+    y0 = (H - rows) // 2
+    with tempfile.TemporaryDirectory() as tmp:
+        scene_path = desc.write(tmp)
+        out = os.path.join(tmp, "band")
+        r = subprocess.run([harness, "bandss", scene_path, str(W), str(H), str(depth), str(ss), "0", str(y0), str(rows),
+                            out], env={**os.environ, "RFX_SPHERE_SEED": str(SEED)}, capture_output=True, text=True,
+                           timeout=600)
+        if r.returncode != 0:
+            raise RuntimeError("refharness failed: " + r.stderr)
+        info = json.loads(r.stdout.strip().splitlines()[-1])
+        rgb = np.fromfile(out + ".f32", np.float32).reshape(rows, W, 3)
+        argb = np.fromfile(out + ".argb", np.uint32).reshape(rows, W)
+    secs, n = info["trace_seconds"], info["traced_samples"]
+    g_rgb, g_argb = gpu_rgb[y0:y0 + rows], gpu_argb[y0:y0 + rows]
+    return {
+        "value": round(n / secs / 1e6, 4), "unit": "Mrays/s", "cores": 1, "kind": "reference",
+        "sample": f"rows {y0}..{y0 + rows - 1} ({rows} x {W} px x {ss * ss} samples) of the first frame; {secs:.1f} s "
+                  f"of single-thread trace time; {cpu_model()}; "
+                  f"{subprocess.run(['nproc'], capture_output=True, text=True).stdout.strip()} host CPUs visible",
+    }, {"max_u8": u8_diff(g_argb, argb), "max_f32_ulp": ulp_diff(g_rgb, rgb), "f32_ulp_histogram": ulp_hist(g_rgb, rgb),
+        "pixels": int(W * rows)}
 
 
 def cpu_baseline(desc, W, H, depth, gpu_rgb, gpu_argb, stride):
@@ -262,13 +296,15 @@ def main():
     ap.add_argument("--prewarm-ms", type=float, default=250.0,
                     help="untimed frames for about this long before the warmup steps (GPU clock ramp); 0: none")
     ap.add_argument("--config", choices=sorted(CONFIGS), default=None,
-                    help="BASELINE config (default: c3 on one GPU, c4 on more)")
+                    help="BASELINE config (default: c3 on one GPU, c4 on more; shot: the reference's screenshot)")
     ap.add_argument("--scaling", choices=["strong", "weak"], default="strong",
                     help="N > 1: the config's fixed frame (strong) or a frame grown with N at its aspect (weak)")
     ap.add_argument("--scene", default=None)
     ap.add_argument("--width", type=int, default=None)
     ap.add_argument("--height", type=int, default=None)
     ap.add_argument("--depth", type=int, default=None)
+    ap.add_argument("--ss", type=int, default=None, help="samples per pixel ss x ss (SSAA; default: the config's)")
+    ap.add_argument("--no-first-view", action="store_true", help="N = 1: skip the first-view timing")
     ap.add_argument("--gather-rgb", action="store_true", help="N > 1: gather the float RGB strips to rank 0 too")
     ap.add_argument("--regroup", type=int, default=None,
                     help="ray regrouping: park traces after n segments (0 off; default: the library's choice)")
@@ -292,12 +328,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     cfg_name = args.config or ("c3" if world == 1 else "c4")
-    c_scene, c_w, c_h, c_depth, c_desc = CONFIGS[cfg_name]
-    custom = any(v is not None for v in (args.scene, args.width, args.height, args.depth))
+    c_scene, c_w, c_h, c_depth, c_ss, c_desc = CONFIGS[cfg_name]
+    custom = any(v is not None for v in (args.scene, args.width, args.height, args.depth, args.ss))
     args.scene = args.scene or c_scene
     args.width = args.width or c_w
     args.height = args.height or c_h
     args.depth = args.depth or c_depth
+    args.ss = args.ss or c_ss
     local = 0 if args.one_device else int(os.environ.get("LOCAL_RANK", str(rank)))
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
@@ -317,7 +354,9 @@ def main():
     L = _lib.load()
 
     W, H = frame_size(world, args.width, args.height, args.scaling)
-    depth, rb = args.depth, args.row_block
+    depth, rb, ss = args.depth, args.row_block, args.ss
+    if world > 1 and ss != 1:
+        raise SystemExit("bench.py: N > 1 renders one-sample frames (the SSAA screenshot is a single-GPU line)")
     desc = scenes.get_scene(args.scene)
     scene, cam = build_scene(desc)
     rr = Renderer(device=local, sphere_seed=SEED)
@@ -331,8 +370,8 @@ def main():
     rr.set_stream(stream.cuda_stream)
 
     bands = world > 1 and args.partition == "bands"
-    frame = make_frame(cam, W, H, depth, 1, row_block=rb if world > 1 and not bands else 0, rank=rank, nranks=world)
-    traces = W * H
+    frame = make_frame(cam, W, H, depth, ss, row_block=rb if world > 1 and not bands else 0, rank=rank, nranks=world)
+    traces = W * H * ss * ss  # one Scene::trace per sample (Render.cpp:181-187)
     if world > 1:
         # sliced RNG pre-pass (count own slice -> all-gather block counts -> emit own strips), trace of
         # the own strips, ARGB8 strip gather to rank 0 + device un-interleave (reflaxman_amd/dist.py)
@@ -382,7 +421,7 @@ def main():
         first_rgb = img.view(H, W, 3).cpu().numpy()
         first_argb = argb[: H * W].view(H, W).cpu().numpy().view(np.uint32)
         man = json.load(open(os.path.join(ROOT, "tests", "golden", "manifest.json")))["cases"]
-        key = f"hash_{args.scene}_{W}x{H}_d{depth}"
+        key = f"hash_{args.scene}_{W}x{H}_d{depth}" + (f"_ss{ss}" if ss != 1 else "")
         if key in man:
             ok_f = sha(first_rgb.tobytes()) == man[key]["sha_f32"]
             ok_a = sha(first_argb.tobytes()) == man[key]["sha_argb"]
@@ -522,13 +561,70 @@ def main():
             h_argb1.copy_(argb, non_blocking=True)
             torch.cuda.current_stream().synchronize()
         e2e_s = (time.perf_counter() - t1) / n_e2e
-        e2e = {"ms_per_frame": round(ovl_s * 1e3, 4), "Mrays_per_s": round(traces / ovl_s / 1e6, 2),
-               "d2h_bytes_per_frame": int(argb.numel() * 4), "frames": n_e2e,
-               "kind": "ARGB8 plane to pinned host memory, frame i's copy overlapped with frame i+1's render",
-               "serial_both_planes": {"ms_per_frame": round(e2e_s * 1e3, 4),
-                                      "Mrays_per_s": round(traces / e2e_s / 1e6, 2),
-                                      "d2h_bytes_per_frame": int(img.numel() * 4 + argb.numel() * 4)}}
+        # the r01/r02 keys keep their meaning (both planes, serial); the overlapped display path has its own key
+        e2e = {"ms_per_frame": round(e2e_s * 1e3, 4), "Mrays_per_s": round(traces / e2e_s / 1e6, 2),
+               "d2h_bytes_per_frame": int(img.numel() * 4 + argb.numel() * 4), "frames": n_e2e,
+               "kind": "both planes (f32 RGB + ARGB8) to pinned host memory after each frame, serially",
+               "overlapped_argb8": {"ms_per_frame": round(ovl_s * 1e3, 4), "Mrays_per_s": round(traces / ovl_s / 1e6, 2),
+                                    "d2h_bytes_per_frame": int(argb.numel() * 4),
+                                    "kind": "ARGB8 plane to pinned host memory, frame i's copy overlapped with frame "
+                                            "i+1's render (the display path)"}}
         del sets
+
+    first_view = None
+    if world == 1 and not args.no_first_view:
+        # what a view pays before the per-view state exists (the headline value is a still camera's steady state):
+        # per-view primary masks off (a camera that moves every frame never has them), then also the tile schedule
+        # reset to raster order (the very first frame of a grid, before any tile cost was measured)
+        def rate(n):
+            for _ in range(3):
+                step()
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            for _ in range(n):
+                step()
+            torch.cuda.synchronize()
+            el = (time.perf_counter() - t1) / n
+            return {"ms_per_step": round(el * 1e3, 4), "value": round(traces / el / 1e6, 2)}
+        n_fv = max(5, min(args.steps, 20))
+        rr.set_prim_masks(0)
+        moving = rate(n_fv)
+        rr.set_tile_order(0)
+        cold = rate(n_fv)
+        rr.set_tile_order(1)
+        rr.set_prim_masks(1)
+        first_view = {"unit": "Mrays/s", "frames": n_fv,
+                      "moving_camera": {**moving, "kind": "no per-view primary masks (built only when a view repeats); "
+                                                          "tile schedule learned from earlier frames of the grid"},
+                      "cold": {**cold, "kind": "no per-view masks and raster tile order: a view's first frame before "
+                                               "any per-view or per-grid state exists"},
+                      "note": "value (above) is the steady state of a still camera: masks built on its second frame, "
+                              "longest-first schedule from earlier frames' tile costs"}
+
+    rgb_gather = None
+    if world > 1 and bands and not args.gather_rgb:
+        # the drop-in's path reads the float image (Render::imagePixel): the same bands with the f32 RGB plane sent to
+        # rank 0 too (16 B/px instead of 4), timed the same way, reported beside the ARGB8-only value
+        sf.set_gather_rgb(True)
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        dist.barrier()
+        el = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device=dev)
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        el = float(el.item())
+        sf.set_gather_rgb(False)
+        rgb_gather = {"value": round(traces * args.steps / el / 1e6, 2), "unit": "Mrays/s",
+                      "ms_per_step": round(el / args.steps * 1e3, 4), "steps": args.steps,
+                      "bytes_to_rank0_per_px": 16,
+                      "kind": "bands with the f32 RGB plane gathered to rank 0 as well as ARGB8 (what a caller that "
+                              "reads Render::imagePixel needs); same bands, same timing bracket"}
 
     if rank != 0:
         dist.destroy_process_group()
@@ -550,19 +646,20 @@ def main():
     traffic = pmc["hbm_bytes_per_launch"] if pmc else None
     executed = metrics.executed_work(pmc, trace_avg)
     roofline = metrics.roofline(executed, traffic, flops_launch, trace_avg, px_launch)
-    roofline["kernel"] = "rfx::trace_kernel (plain pixel mode, wave-bundle culling)"
+    roofline["kernel"] = ("rfx::trace_kernel (plain pixel mode, wave-bundle culling)" if ss == 1 else
+                          "rfx::trace_kernel (SSAA pixel mode, wave-bundle culling)")
     if baseline is not None:
         baseline["efficiency"] = round(mrays / (world * baseline["value"]), 4)
-    workload = (c_desc if not custom else f"{args.scene} scene") + f", {W}x{H}, depth {depth}, 1 spp"
+    workload = (c_desc if not custom else f"{args.scene} scene") + f", {W}x{H}, depth {depth}, {ss * ss} spp"
     if world > 1:
         workload += f", {world} GPUs, fixed frame (strong scaling)" if args.scaling == "strong" else \
             f", {world} GPUs, frame grown with N (weak scaling)"
     out = {
         "metric": METRIC, "value": round(mrays, 2), "unit": "Mrays/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "prewarm_frames": prewarm, "ms_per_step": round(ms_step, 4), "higher_is_better": True,
-        "scaling": args.scaling if world > 1 else "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "scaling": args.scaling, "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "config": {"workload": workload, "name": None if custom else cfg_name.upper(),
-                   "scene": args.scene, "width": W, "height": H, "depth": depth, "spp": 1,
+                   "scene": args.scene, "width": W, "height": H, "depth": depth, "spp": ss * ss,
                    "parallelism": ((f"balanced-bands-x{world}" if bands else f"row-strips{rb}x{world}")
                                    + ("+pipelined-gather" if sf.pipeline else "")
                                    + ("+count-ahead" if sf.count_ahead else "")
@@ -577,6 +674,8 @@ def main():
         "secondary_Msegments_per_s": round((work["segments_per_ray"] + work["shadow_rays_per_ray"]) * traces
                                            * args.steps / elapsed / 1e6, 1),
         "end_to_end_incl_d2h": e2e,
+        **({"first_view": first_view} if first_view else {}),
+        **({"with_rgb_gather": rgb_gather} if rgb_gather else {}),
         "parity": parity,
         **({"band_bounds": sf.bounds} if bands else {}),
         **({"steady_state_parity": steady,
@@ -588,13 +687,18 @@ def main():
     }
     if world == 1 and not args.no_cpu_baseline:
         log("cpu_baseline: reference CPU path on a row sample of the same frame ...")
-        stride = args.cpu_stride or (2 if custom else CPU_STRIDE[cfg_name])
-        cb, delta = cpu_baseline(desc, W, H, depth, first_rgb, first_argb, stride)
-        out["cpu_baseline"] = cb
-        out["parity"]["sample_vs_cpu_reference"] = delta
-        out["max_abs_delta"] = {"u8": delta["max_u8"], "f32_ulp": delta["max_f32_ulp"]}
-        out["speedup_vs_cpu_1core"] = round(mrays / cb["value"], 1)
-        if not args.no_cpu_allcore:
+        if ss != 1:
+            cb, delta = cpu_baseline_band(desc, W, H, depth, ss, first_rgb, first_argb,
+                                          CPU_BAND_ROWS.get(cfg_name, 16) if not custom else 16)
+        else:
+            stride = args.cpu_stride or (2 if custom else CPU_STRIDE[cfg_name])
+            cb, delta = cpu_baseline(desc, W, H, depth, first_rgb, first_argb, stride)
+        out["cpu_baseline"] = cb  # None: an SSAA frame on a host without the reference build
+        if cb is not None:
+            out["parity"]["sample_vs_cpu_reference"] = delta
+            out["max_abs_delta"] = {"u8": delta["max_u8"], "f32_ulp": delta["max_f32_ulp"]}
+            out["speedup_vs_cpu_1core"] = round(mrays / cb["value"], 1)
+        if cb is not None and not args.no_cpu_allcore and ss == 1:
             log("cpu_allcore: the C restatement on every host thread (context row) ...")
             out["cpu_allcore"] = cpu_allcore(desc, W, H, depth, first_rgb, first_argb, cb["value"])
     print(json.dumps(out), flush=True)

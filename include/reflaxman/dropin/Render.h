@@ -15,8 +15,11 @@
 //     would have.  Policy "span" (RFX_DROPIN_POLICY=span, or setRenderPolicy) renders each call's span as it
 //     comes.  Any chunk pattern gives the reference's images and random streams under either policy;
 //   * several GPUs of this process (RFX_DEVICES=0,1,... in the environment): frames rendered ahead with
-//     sampleNum > 0 (still frames, screenshots) are cut into row bands over the devices (rfx_group_render_frame);
-//     block previews and spans stay on the first device, which carries the random streams;
+//     sampleNum > 0 (still frames, screenshots), and frames rendered by one renderNext(W*H) call under either policy,
+//     are cut into row bands over the devices (rfx_group_render_frame); block previews and partial spans stay on
+//     the first device, which carries the random streams.  Groups of distinct devices are unverified on hardware
+//     so far (every group test ran its members on one GPU; tests/test_gpu_group.py skips the multi-device test
+//     when only one device is visible);
 //   * the float framebuffer (std::vector<Color> image, Render.h:10) lives in HBM and is read back on demand;
 //     imagePixel / copyImage then apply the caller's own Color::operator/ and Color::argb, as the reference.
 // Random streams: the reference seeds its two per-TU LCG streams from rand() at static init (trace_math.h:34),
@@ -299,7 +302,10 @@ class Render {
     else if (!spec_active)
     {
       const rfx_frame f = frame_of(p0, p1);
-      rfx_dropin::check(rfx_render_frame(r, &f, (float *)d_image, nullptr, nullptr, nullptr), "Render::renderNext");
+      if (group && p0 == 0 && p1 == total && renderSampleNum > 0)  // one call for the whole frame (renderNext(W*H))
+        rfx_dropin::check(rfx_group_render_frame(group, &f, (float *)d_image, nullptr, nullptr), "Render::renderNext");
+      else
+        rfx_dropin::check(rfx_render_frame(r, &f, (float *)d_image, nullptr, nullptr, nullptr), "Render::renderNext");
     }
     host_valid = false;  // the reference's image has changed (a read mid-frame settles the frame rendered ahead)
     curx = (unsigned int)(p1 % imageWidth);

@@ -121,6 +121,9 @@ int rfx_renderer_set_regroup(rfx_renderer *r, int park_after);
  * kernel takes them, 0 (default) = taken in park order (a tile's survivors together: faster on C5).
  * Changes the schedule, never a value. */
 int rfx_renderer_set_regroup_sort(rfx_renderer *r, int on);
+/* Which bounce kernel the last trace launch ran: 0 = none (not regrouped), 1 = the global-memory BVH form, 2 = the
+ * LDS-staged BVH form (large scenes whose BVH fits the LDS; 1 when the runtime refused its LDS size). */
+int rfx_renderer_bounce_form(const rfx_renderer *r);
 /* Primary-bundle cull masks of small-scene plain frames (no pixel changes): the first segment's cull mask of every
  * 8x8 wave tile, computed by one extra launch for a view (camera, frame geometry, scene) and reused while the
  * view stays.  1 (default) = built when a view repeats (the second frame of a still camera on), so a camera that
@@ -234,7 +237,9 @@ int rfx_group_set_bands(rfx_group *g, uint32_t height, const uint32_t *bounds);
 int rfx_group_get_bands(const rfx_group *g, uint32_t *bounds);     /* the bands of the last frame (n + 1 rows) */
 /* One whole frame (sample_num > 0; SSAA, additive and accumulation included; the partition fields of `frame` must be
  * rank 0 of 1 and the span the whole frame) into d_rgb / d_argb (W*H*3 floats / W*H words, or NULL) on member 0's
- * device, ordered after and before the caller's work on `stream` (member 0's stream; NULL = its renderer's). */
+ * device, ordered after and before the caller's work on `stream` (member 0's stream; NULL = its renderer's).
+ * d_rgb NULL (d_argb given, no accumulation): an ARGB8-only frame -- the members copy 4 B/px to member 0 instead of
+ * 16 B/px, for a display that never reads the float image. */
 int rfx_group_render_frame(rfx_group *g, const rfx_frame *frame, float *d_rgb, uint32_t *d_argb, void *stream);
 
 /* Optional per-phase timing of rfx_render_frame with HIP events recorded on the launch stream:

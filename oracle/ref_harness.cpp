@@ -220,6 +220,59 @@ int main(int argc, char **argv)
     write_file(std::string(argv[8]) + ".argb", &argb[0], argb.size() * 4);
     return 0;
   }
+  if (mode == "bandss")
+  {
+    // bandss SCENE W H DEPTH SS FRAME Y0 ROWS OUT : rows [Y0, Y0+ROWS) of frame FRAME (0-based) of a sequence of
+    // non-additive frames with SS x SS samples per pixel (SS >= 1), the stream advanced over every draw before the
+    // band: FRAME whole frames and Y0 rows, SS*SS draws per pixel (one Scene::trace per sample, Scene.cpp:75).
+    // Each pixel is computed exactly as Render::renderNext's renderSampleNum > 0 branch (Render.cpp:146-194) with
+    // renderAdditive false: the reference's own Vector3/Matrix33/Color operators, in its order.  Bands of one frame
+    // rendered by separate processes concatenate to the frame Render::renderNext produces (tools/gen_golden.py).
+    if (argc != 11) die("bandss SCENE W H DEPTH SS FRAME Y0 ROWS OUT");
+    load_scene(r, argv[2]);
+    const unsigned W = atoi(argv[3]), H = atoi(argv[4]);
+    const int depth = atoi(argv[5]), ss = atoi(argv[6]);
+    const unsigned frame = atoi(argv[7]), y0 = atoi(argv[8]), rows = atoi(argv[9]);
+    if (ss < 1 || y0 + (size_t)rows > H) die("bandss: bad ss or rows");
+    const size_t spp = (size_t)ss * ss;
+    const size_t skip = ((size_t)frame * W * H + (size_t)y0 * W) * spp;
+    for (size_t i = 0; i < skip; ++i) Vector3::randomInsideSphere(1.0f);
+    const Vector3 origin = r.camera.eye;
+    const Matrix33 view = r.camera.view;
+    const float sqRenderSampleNum = float(ss * ss);
+    const float rz = float(W) / 2.0f / tanf(r.camera.fov / 2.0f);
+    const float wh = W / 2.0f, hh = H / 2.0f;
+    const float rndx = 0, rndy = 0;
+    std::vector<float> rgb((size_t)W * rows * 3);
+    std::vector<ARGB> argb((size_t)W * rows);
+    timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (unsigned y = y0; y < y0 + rows; ++y)
+      for (unsigned x = 0; x < W; ++x)
+      {
+        const float rx = float(x) - wh;
+        const float ry = float(y) - hh;
+        Color finColor = Color(0.0f, 0.0f, 0.0f);
+        for (int ssx = 0; ssx < ss; ssx++)
+          for (int ssy = 0; ssy < ss; ssy++)
+          {
+            Vector3 ray = Vector3(rx + float(ssx) / ss + rndx, ry + float(ssy) / ss + rndy, rz);
+            ray = view * ray;
+            finColor += r.scene.trace(origin, ray, depth);
+          }
+        finColor /= sqRenderSampleNum;
+        const size_t i = (size_t)(y - y0) * W + x;
+        rgb[i * 3 + 0] = finColor.r; rgb[i * 3 + 1] = finColor.g; rgb[i * 3 + 2] = finColor.b;
+        argb[i] = finColor.argb();
+      }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    write_file(std::string(argv[10]) + ".f32", &rgb[0], rgb.size() * 4);
+    write_file(std::string(argv[10]) + ".argb", &argb[0], argb.size() * 4);
+    // the band's trace time (the stream advance before it excluded): the timed CPU baseline of SSAA configs
+    printf("{\"traced_samples\": %llu, \"trace_seconds\": %.6f}\n", (unsigned long long)W * rows * spp,
+           (t1.tv_sec - t0.tv_sec) + 1e-9 * (t1.tv_nsec - t0.tv_nsec));
+    return 0;
+  }
   if (mode == "rows")
   {
     // rows SCENE W H DEPTH Y0 STRIDE COUNT OUT : rows Y0, Y0+STRIDE, ... of an ss=1 frame (bounded,

@@ -107,13 +107,16 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if not force and not _stale():
         return LIB
     os.makedirs(LIBDIR, exist_ok=True)
+    # the digest of the sources as they are when compilation starts: a file edited during the build leaves the
+    # library recorded under the older digest, so the next build() sees it stale
+    digest = _sources_digest()
     tmp = LIB + ".tmp"
     err = _compile_link(tmp, [], os.path.join(LIBDIR, "obj"))
     if verbose:
         print(err)
     os.replace(tmp, LIB)
     with open(DIGEST, "w") as f:
-        f.write(_sources_digest() + "\n")
+        f.write(digest + "\n")
     return LIB
 
 

@@ -96,6 +96,7 @@ SIGNATURES = [
     ("rfx_renderer_set_prim_masks", C.c_int, [C.c_void_p, C.c_int]),
     ("rfx_renderer_set_regroup", C.c_int, [C.c_void_p, C.c_int]),
     ("rfx_renderer_set_regroup_sort", C.c_int, [C.c_void_p, C.c_int]),
+    ("rfx_renderer_bounce_form", C.c_int, [C.c_void_p]),
     ("rfx_renderer_get_timing", C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double), _u64p]),
     ("rfx_device_alloc", C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p)]),
     ("rfx_device_free", C.c_int, [C.c_void_p, C.c_void_p]),

@@ -112,6 +112,8 @@ struct rfx_group {
   std::vector<float *> rgb;                      // members 1..n-1: whole-frame scratch (their band rows written)
   std::vector<uint32_t *> argb;
   size_t px_cap = 0;
+  float *rgb0 = nullptr;                         // member 0's float frame of ARGB8-only frames (d_rgb NULL)
+  size_t rgb0_cap = 0;
   std::vector<hipEvent_t> ev_start, ev_cnt, ev_emit[2], ev_t1, ev_done;
   std::vector<uint32_t> bounds;
   bool fixed = false;
@@ -141,6 +143,11 @@ static void destroy(rfx_group *g)
     for (std::vector<hipEvent_t> *v : {&g->ev_start, &g->ev_cnt, &g->ev_emit[0], &g->ev_emit[1], &g->ev_t1, &g->ev_done})
       if (i < v->size() && (*v)[i]) (void)hipEventDestroy((*v)[i]);
     if (i < g->own.size() && g->own[i]) (void)hipStreamDestroy(g->own[i]);
+  }
+  if (g->rgb0)
+  {
+    (void)hipSetDevice(g->dev[0]);
+    (void)hipFree(g->rgb0);
   }
   for (rfx_renderer *r : g->r) rfx_renderer_destroy(r);
   delete g;
@@ -323,16 +330,30 @@ static int ensure_buffers(rfx_group *g, const rfx_frame &f0)
 
 extern "C" int rfx_group_render_frame(rfx_group *g, const rfx_frame *f, float *d_rgb, uint32_t *d_argb, void *stream)
 {
-  if (!g || !f || !d_rgb) return rfx_detail_fail(RFX_ERR_ARG, "group_render_frame: bad args");
+  if (!g || !f || (!d_rgb && !d_argb)) return rfx_detail_fail(RFX_ERR_ARG, "group_render_frame: bad args");
   const size_t n = g->n();
   const uint32_t W = f->width, H = f->height;
   const uint64_t npx = (uint64_t)W * H;
+  // ARGB8-only frames (a display that never reads the float image): only the 4-B/px plane crosses to member 0
+  const bool argb_only = d_rgb == nullptr;
+  if (argb_only && f->additive_counter > 1)
+    return rfx_detail_fail(RFX_ERR_ARG, "group_render_frame: an accumulating frame needs the float frame (d_rgb)");
   if (f->sample_num <= 0 || (f->nranks > 1) || !((f->pixel_begin == 0 && f->pixel_end == 0) ||
                                                   (f->pixel_begin == 0 && f->pixel_end == npx)))
     return rfx_detail_fail(RFX_ERR_ARG, "group_render_frame: a whole frame with sample_num > 0 (no partition fields)");
   hipStream_t s0 = stream ? (hipStream_t)stream : rfx_detail_stream(g->r[0]);
+  if (argb_only && npx > g->rgb0_cap)
+  {
+    GCHECK(hipSetDevice(g->dev[0]));
+    GCHECK(hipStreamSynchronize(s0));
+    (void)hipFree(g->rgb0);
+    g->rgb0 = nullptr;
+    g->rgb0_cap = 0;
+    GCHECK(hipMalloc(&g->rgb0, npx * 3 * sizeof(float)));
+    g->rgb0_cap = npx;
+  }
   if (n == 1 || H < n)
-    return rfx_render_frame(g->r[0], f, d_rgb, d_argb, nullptr, s0);
+    return rfx_render_frame(g->r[0], f, argb_only ? g->rgb0 : d_rgb, d_argb, nullptr, s0);
   if (W != g->W || H != g->H || g->bounds.size() != n + 1)
   {
     if (g->fixed && H != g->H) return rfx_detail_fail(RFX_ERR_ARG, "group_render_frame: fixed bands of another height");
@@ -391,7 +412,7 @@ extern "C" int rfx_group_render_frame(rfx_group *g, const rfx_frame *f, float *d
     for (size_t j = 0; j < n; ++j)
       if (j != i) GCHECK(hipStreamWaitEvent(st[i], g->ev_cnt[j], 0));
     const uint64_t y0 = g->bounds[i], rows = g->bounds[i + 1] - y0;
-    float *img = i ? g->rgb[i] : d_rgb;
+    float *img = i ? g->rgb[i] : (argb_only ? g->rgb0 : d_rgb);
     uint32_t *a = i ? (d_argb ? g->argb[i] : nullptr) : d_argb;
     if (accumulate && i)  // the accumulated rows this member adds to (Render.cpp:191-194)
       GCHECK(hipMemcpyPeerAsync(img + y0 * W * 3, g->dev[i], d_rgb + y0 * W * 3, g->dev[0], rows * W * 12, st[i]));
@@ -403,7 +424,8 @@ extern "C" int rfx_group_render_frame(rfx_group *g, const rfx_frame *f, float *d
     GCHECK(hipEventRecord(g->ev_t1[i], st[i]));
     if (i)
     {
-      GCHECK(hipMemcpyPeerAsync(d_rgb + y0 * W * 3, g->dev[0], img + y0 * W * 3, g->dev[i], rows * W * 12, st[i]));
+      if (!argb_only)
+        GCHECK(hipMemcpyPeerAsync(d_rgb + y0 * W * 3, g->dev[0], img + y0 * W * 3, g->dev[i], rows * W * 12, st[i]));
       if (d_argb)
         GCHECK(hipMemcpyPeerAsync(d_argb + y0 * W, g->dev[0], a + y0 * W, g->dev[i], rows * W * 4, st[i]));
       GCHECK(hipEventRecord(g->ev_done[i], st[i]));

@@ -480,7 +480,7 @@ struct rfx_renderer {
   uint32_t *d_rd_alt = nullptr; uint64_t rd_alt_cap = 0;  // emit-ahead: the second randDir buffer
   int emit_pending = -1;  // emit-ahead: buffer (0 d_rd, 1 d_rd_alt) of an emitted, untraced frame, or -1
   int trace_buf = 0;      // buffer the last enqueued trace read
-  uint64_t emit_key[8] = {};  // the emitted frame's plan (traces, band, geometry): rfx_render_frame_emitted must match it
+  uint64_t emit_key[10] = {};  // the emitted frame's plan (traces, band, geometry): rfx_render_frame_emitted must match it
   // rfx_frame_rng_rewind: the last call was an rfx_render_frame; its start states (the sphere stream's is the other
   // seed word while rewind_flip) can be restored
   bool rewind_ok = false, rewind_flip = false;
@@ -514,6 +514,7 @@ struct rfx_renderer {
   std::vector<uint8_t> prim_seen;  // the view of the last plain small-scene launch
   uint64_t scene_gen = 0;  // bumped by every set_scene
   int prim_mode = 1;       // rfx_renderer_set_prim_masks
+  int bounce_form = 0;     // the last trace launch's bounce kernel: 0 none, 1 global-memory BVH, 2 LDS-staged BVH
   QRay *d_queue = nullptr;
   uint64_t queue_cap = 0;
   uint32_t *d_qctr = nullptr;   // count, claim counter, then the sort's kQueueBuckets histogram words
@@ -665,6 +666,12 @@ extern "C" int rfx_renderer_set_prim_masks(rfx_renderer *r, int mode)
   r->prim_key.clear();
   r->prim_seen.clear();
   return RFX_OK;
+}
+
+extern "C" int rfx_renderer_bounce_form(const rfx_renderer *r)
+{
+  if (!r) return fail(RFX_ERR_ARG, "renderer_bounce_form: null renderer");
+  return r->bounce_form;
 }
 
 extern "C" int rfx_renderer_set_regroup(rfx_renderer *r, int park_after)
@@ -1404,6 +1411,7 @@ static int trace_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *rd, float
     if (!r->prim_key.empty()) P.prim_mask = r->d_prim_mask;
   }
   if (P.grid_rows) HIP_CHECK(launch_trace(r->dev, P, d_counters != nullptr, st));
+  r->bounce_form = 0;
   if (park)
   {
     // packed waves over the queue, as many as the chip holds at once (RFX_BOUNCE_GROUPS_PER_CU workgroups of two waves
@@ -1416,10 +1424,12 @@ static int trace_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *rd, float
     // the LDS-staged bounce kernel, one 16-wave workgroup per CU (C5 trace + bounce -4..6%, tools/ab.py); else the
     // two-wave workgroups walking the nodes in global memory
     const uint32_t lgroups = (uint32_t)std::min<uint64_t>((waves + kLdsBvhWaves - 1) / kLdsBvhWaves, (uint64_t)r->cus);
+    r->bounce_form = 2;
     if (small || !lds_bvh_fits(r->dev.n_bvh) || launch_bounce_lds(cfg, lgroups, r->dev, P, st) != hipSuccess)
     {
       (void)hipGetLastError();  // an LDS launch the runtime refused: the global-memory form instead
       launch_bounce(cfg, dim3(groups), r->dev, P, st);
+      r->bounce_form = 1;  // visible through rfx_renderer_bounce_form, so a silent fall-back shows in the tests
     }
     HIP_CHECK(hipGetLastError());
   }
@@ -1465,7 +1475,7 @@ extern "C" int rfx_render_frame_counted_ev(rfx_renderer *r, const rfx_frame *f, 
 
 // What an emitted frame's randDirs depend on: the traces and their band, and the frame geometry that maps pixels to
 // trace indices.  rfx_render_frame_emitted refuses a frame whose plan differs (its rows' randDirs were never written).
-static void plan_key(const FramePlan &pl, uint64_t key[8])
+static void plan_key(const FramePlan &pl, uint64_t key[10])
 {
   const FrameParams &P = pl.P;
   key[0] = pl.traces;
@@ -1475,7 +1485,9 @@ static void plan_key(const FramePlan &pl, uint64_t key[8])
   key[4] = ((uint64_t)(uint32_t)P.ss << 32) | P.row_block;
   key[5] = ((uint64_t)P.rank << 32) | P.nranks;
   key[6] = ((uint64_t)P.row0 << 32) | P.grid_rows;
-  key[7] = P.p_begin ^ (P.p_end << 1) ^ (P.trace_base << 2);
+  key[7] = P.p_begin;  // the span and its first trace index in words of their own: no two spans share a key
+  key[8] = P.p_end;
+  key[9] = P.trace_base;
 }
 
 // Emit-ahead (multi-GPU): the emit of frame i + 1 on a side stream while frame i traces.  Two randDir buffers: an emit
@@ -1517,7 +1529,7 @@ extern "C" int rfx_render_frame_emitted(rfx_renderer *r, const rfx_frame *f, flo
   if (!d_rgb) return fail(RFX_ERR_ARG, "render_frame_emitted: null framebuffer");
   if (pl.traces == 0) return RFX_OK;
   if (r->emit_pending < 0) return fail(RFX_ERR_STATE, "render_frame_emitted: no emitted frame (rfx_frame_rng_emit)");
-  uint64_t key[8];
+  uint64_t key[10];
   plan_key(pl, key);
   if (memcmp(key, r->emit_key, sizeof(key)) != 0)
     return fail(RFX_ERR_STATE, "render_frame_emitted: the frame differs from the emitted one (band, geometry or traces); "

@@ -505,6 +505,25 @@ class BandFrame(_CountedFrame):
         self.rows = self.y1 - self.y0
         self.ops.set_rows(self.y0, self.y1)
 
+    def set_gather_rgb(self, on: bool):
+        """Send the f32 RGB plane to rank 0 as well (on) or the ARGB8 plane only (off) from the next frame on; waits
+        for the transfers in flight (bench.py times the bands both ways).  Every rank must call it alike."""
+        on = bool(on) and self.gather_to_root
+        if on == self.gather_rgb:
+            return
+        for ws in self.works:
+            for w in ws:
+                w.wait()
+        self.works = [[] for _ in self.works]
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+        nbuf = len(self.argb_bufs)
+        if on and len(self.img_bufs) < nbuf:
+            self.img_bufs += [torch.zeros_like(self.img_bufs[0]) for _ in range(nbuf - len(self.img_bufs))]
+        self.gather_rgb = on
+        if not on:
+            self.rgb_full = None
+
     def _sends(self, k: int):
         """(tensor, peer, is_send) of frame buffer set k: every band to rank 0."""
         W, ops = self.W, []

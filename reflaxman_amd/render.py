@@ -321,6 +321,11 @@ class Renderer:
         by direction octant and origin cell, or in park order (default).  No pixel changes."""
         check(_lib.load().rfx_renderer_set_regroup_sort(self._h, int(bool(on))), "set_regroup_sort")
 
+    def bounce_form(self) -> int:
+        """The last trace launch's bounce kernel (rfx.h rfx_renderer_bounce_form): 0 none, 1 global-memory BVH, 2 the
+        LDS-staged BVH."""
+        return _lib.load().rfx_renderer_bounce_form(self._h)
+
     def set_timing(self, enable):
         """HIP-event timing of the frames (rfx.h rfx_renderer_set_timing): True / 1 every frame, n > 1 every n-th
         frame, False / 0 off."""

@@ -17,6 +17,9 @@
 //       calls, R that of the window's first pixel read (which waits for the frame and copies it to the host).
 //       The fake clock advances TICK_US per reading, so Pulse's chunk doubling and sample adaptation are the same
 //       in both builds.
+//   pulse_headless OUT frames W H DEPTH SS ADDITIVE N
+//       no Pulse: N frames of Render's default scene, each rendered by one renderNext(W*H) call; writes OUT.f32
+//       (imagePixel) and OUT.argb (copyImage).
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -136,8 +139,44 @@ static int session(const std::string &dir, unsigned w, unsigned h, uint64_t tick
   return 0;
 }
 
+// A caller that renders each frame in one call, as Render::renderNext(W*H) allows (Render.cpp:136-215): N frames of
+// the default scene (Render's own loadScene), then the image read back as imagePixel (OUT.f32, row 0 first) and
+// copyImage (OUT.argb).  No Pulse: this is any non-interactive program's use of the renderer.
+static int frames(const std::string &out, unsigned w, unsigned h, int depth, int ss, bool additive, int n)
+{
+  Render render((out + ".").c_str());  // textures absent -> the checker fallback, as the goldens
+  render.setImageSize(w, h);
+  for (int i = 0; i < n; ++i)
+  {
+    render.renderBegin(depth, ss, additive);
+    if (render.renderNext(w * h)) return 3;  // one call covers the frame
+  }
+  FILE *f = fopen((out + ".f32").c_str(), "wb");
+  if (!f) return 4;
+  for (unsigned y = 0; y < h; ++y)
+    for (unsigned x = 0; x < w; ++x)
+    {
+      const Color c = render.imagePixel(x, y);
+      fwrite(&c.r, 4, 1, f);
+      fwrite(&c.g, 4, 1, f);
+      fwrite(&c.b, 4, 1, f);
+    }
+  fclose(f);
+  Texture t(w, h);
+  render.copyImage(t);
+  f = fopen((out + ".argb").c_str(), "wb");
+  if (!f) return 4;
+  fwrite(t.getColorBuffer(), 4, (size_t)w * h, f);
+  fclose(f);
+  printf("ok\n");
+  return 0;
+}
+
 int main(int argc, char **argv)
 {
+  if (argc == 9 && !strcmp(argv[2], "frames"))
+    return frames(argv[1], (unsigned)atoi(argv[3]), (unsigned)atoi(argv[4]), atoi(argv[5]), atoi(argv[6]),
+                  atoi(argv[7]) != 0, atoi(argv[8]));
   if (argc >= 6 && !strcmp(argv[2], "session"))
     return session(argv[1], (unsigned)atoi(argv[3]), (unsigned)atoi(argv[4]), (uint64_t)strtoull(argv[5], nullptr, 0),
                    !(argc > 6 && !strcmp(argv[6], "nohash")));

@@ -16,7 +16,10 @@ def test_strong_scaling_baseline_is_the_committed_one_gpu_c4_line():
 
 
 def test_cpu_sample_strides_cover_every_config():
-    assert set(bench.CPU_STRIDE) == set(bench.CONFIGS)
+    """Every config has a bounded CPU sample: a row stride (one-sample frames) or a band of rows (SSAA frames)."""
+    one = {k for k, c in bench.CONFIGS.items() if c[4] == 1}
+    assert set(bench.CPU_STRIDE) == one
+    assert set(bench.CPU_BAND_ROWS) == set(bench.CONFIGS) - one
 
 
 def test_weak_and_strong_frame_sizes():

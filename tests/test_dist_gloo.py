@@ -133,7 +133,7 @@ def test_strip_helpers_match_library():
                         assert rdist.strip_row_to_y(i, rb, r, world) == L.rfx_strip_row_to_y(i, rb, r, world)
 
 
-def _band_worker(rank, world, port, W, H, pipeline, q, gather_rgb, count_ahead):
+def _band_worker(rank, world, port, W, H, pipeline, q, gather_rgb, count_ahead, toggle=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -148,6 +148,9 @@ def _band_worker(rank, world, port, W, H, pipeline, q, gather_rgb, count_ahead):
                 # re-cut the bands from fake per-rank times (rank r's rows cost r + 1 each): the frames stay whole
                 nb = sf.balance(rounds=2, timer=lambda step: (step(), sf.rows * (sf.rank + 1))[1])
                 bounds.append(nb)
+            if toggle and frame == 3:  # bench.py's second timing: the f32 plane sent too, from the next frame on
+                sf.set_gather_rgb(not gather_rgb)
+                gather_rgb = not gather_rgb
             out = sf.step()
             fno = ops.frame - 1
             if rank == 0:
@@ -163,13 +166,18 @@ def _band_worker(rank, world, port, W, H, pipeline, q, gather_rgb, count_ahead):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("pipeline,gather_rgb,count_ahead", [(False, False, False), (True, True, True)])
+@pytest.mark.parametrize("pipeline,gather_rgb,count_ahead,toggle", [(False, False, False, False),
+                                                                     (True, True, True, False),
+                                                                     (True, False, True, True),
+                                                                     (False, True, False, True)])
 @pytest.mark.parametrize("world,W,H", [(2, 16, 37), (3, 8, 64)])
-def test_band_frame_gloo(world, W, H, pipeline, gather_rgb, count_ahead):
+def test_band_frame_gloo(world, W, H, pipeline, gather_rgb, count_ahead, toggle):
+    """Bands over gloo: whole frames on rank 0, re-balanced mid-run; with `toggle`, the f32 RGB plane's transfer is
+    switched on (or off) after frame 3 (BandFrame.set_gather_rgb, bench.py's with_rgb_gather timing)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_band_worker, args=(r, world, port, W, H, pipeline, q, gather_rgb, count_ahead))
+    procs = [ctx.Process(target=_band_worker, args=(r, world, port, W, H, pipeline, q, gather_rgb, count_ahead, toggle))
              for r in range(world)]
     for p in procs:
         p.start()

@@ -88,6 +88,47 @@ def test_pulse_screenshot_on_a_device_group(tmp_path):
     assert hashlib.sha256(data).hexdigest() == c["sha_bmp"]
 
 
+def run_frames(tmp_path, c, devices=None, policy="frame"):
+    """A non-Pulse caller of the drop-in Render: each frame of case c in one renderNext(W*H) call."""
+    if not os.path.exists(DROPIN):
+        pytest.fail("tests/native/_build/pulse_dropin missing: run __graft_entry__.build() where /root/reference exists")
+    env = {k: v for k, v in os.environ.items() if k != "RFX_DEVICES"}
+    env.update({"RFX_SPHERE_SEED": str(c["sphere_seed"]), "RFX_JITTER_SEED": str(c.get("jitter_seed", 0)),
+                "RFX_DROPIN_POLICY": policy, **({"RFX_DEVICES": devices} if devices else {})})
+    out = str(tmp_path / "frame")
+    r = subprocess.run([DROPIN, out, "frames", str(c["W"]), str(c["H"]), str(c["depth"]), str(c["ss"]),
+                        str(int(c["additive"])), str(c["frames"])], capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip() == "ok", r.stdout + r.stderr
+    f32 = open(out + ".f32", "rb").read()
+    argb = open(out + ".argb", "rb").read()
+    return hashlib.sha256(f32).hexdigest(), hashlib.sha256(argb).hexdigest()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("devices,policy", [(None, "frame"), ("0,0", "frame"), ("0,0,0", "span")])
+def test_single_call_screenshot_frame(tmp_path, devices, policy):
+    """The reference's screenshot workload (Full HD, 4x4 SSAA, depth 20: Pulse.cpp:156-178, defaults.h:9) rendered by
+    a caller that covers the frame with one renderNext(W*H) -- on one device, and cut into row bands over a device
+    group (RFX_DEVICES; all members on device 0 on the one-GPU box) under either policy: SHA-256 of imagePixel's floats
+    and of copyImage's ARGB8 equal the reference's full frame (tools/gen_golden.py, banded refharness)."""
+    c = manifest()["cases"]["hash_default_1920x1080_d20_ss4"]
+    assert run_frames(tmp_path, c, devices, policy) == (c["sha_f32"], c["sha_argb"])
+
+
+@pytest.mark.gpu
+def test_single_call_additive_frames_on_a_device_group(tmp_path):
+    """Two additive SSAA-2 frames, each in one renderNext(W*H) call, over a 2-member group: the second frame
+    accumulates onto the first across the members' bands; equal to the reference's stored golden."""
+    import numpy as np
+    from helpers import GOLDEN
+    key = "render_default_96x64_d4_ss2_add2"
+    c = manifest()["cases"][key]
+    g = np.load(os.path.join(GOLDEN, key + ".npz"))
+    # imagePixel divides by additiveCounter, as the reference (Render.cpp:103-114); the golden was read the same way
+    assert run_frames(tmp_path, c, "0,0") == (hashlib.sha256(g["rgb"].tobytes()).hexdigest(),
+                                               hashlib.sha256(g["argb"].tobytes()).hexdigest())
+
+
 def run_session(tmp_path, c, policy, hash_frames=True, devices=None):
     """The interactive session of tests/native/pulse_headless.cpp through the drop-in; returns the parsed frame lines."""
     if not os.path.exists(DROPIN):

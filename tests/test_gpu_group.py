@@ -17,10 +17,10 @@ SEED = 1350490027
 
 
 class Group:
-    def __init__(self, n, scene):
+    def __init__(self, n, scene, devices=None):
         self.L = _lib.load()
         self.g = C.c_void_p()
-        devs = (C.c_int * n)(*([0] * n))
+        devs = (C.c_int * n)(*(devices or [0] * n))
         _lib.check(self.L.rfx_group_create(C.byref(self.g), devs, n), "group_create")
         _lib.check(self.L.rfx_group_set_scene(self.g, scene._h), "group_set_scene")
         self.r0 = C.c_void_p(self.L.rfx_group_renderer(self.g, 0))
@@ -28,7 +28,7 @@ class Group:
         self.n = n
 
     def render(self, f, rgb, argb):
-        _lib.check(self.L.rfx_group_render_frame(self.g, C.byref(f), C.c_void_p(rgb.data_ptr()),
+        _lib.check(self.L.rfx_group_render_frame(self.g, C.byref(f), C.c_void_p(rgb.data_ptr() if rgb is not None else 0),
                                                  C.c_void_p(argb.data_ptr()), None), "group_render_frame")
 
     def bands(self):
@@ -149,3 +149,49 @@ def test_group_rejects_block_preview_and_partitions():
               make_frame(cam, 64, 48, 4, 1, row_block=8, rank=0, nranks=2)):
         assert g.L.rfx_group_render_frame(g.g, C.byref(f), C.c_void_p(rgb.data_ptr()), None, None) == -1
     g.close()
+
+
+def test_group_argb_only_frames():
+    """ARGB8-only group frames (d_rgb NULL: the members send 4 B/px to member 0, not 16): equal to the single renderer's
+    ARGB8 frames over a run with a re-cut; an accumulating frame without the float frame is refused."""
+    import torch
+    from reflaxman_amd.render import build_scene, make_frame
+    scene, cam = build_scene(scenes.get_scene("synth16"))
+    W, H = 1280, 720
+    g, one = Group(3, scene), _single(scene)
+    f = make_frame(cam, W, H, 8, 1)
+    _, argb = _bufs(torch, W, H)
+    rgb1, argb1 = _bufs(torch, W, H)
+    for i in range(10):
+        g.render(f, None, argb)
+        one.render_frame(f, rgb1.data_ptr(), argb1.data_ptr())
+        torch.cuda.synchronize()
+        assert torch.equal(argb, argb1), i
+    fa = make_frame(cam, W, H, 4, 1, additive=True, additive_counter=2)
+    assert g.L.rfx_group_render_frame(g.g, C.byref(fa), None, C.c_void_p(argb.data_ptr()), None) != 0
+    g.close()
+    one.close()
+
+
+def test_group_on_distinct_devices():
+    """The group over distinct devices (peer access, cross-device event waits, peer count and band copies): frames
+    equal the single renderer's.  Needs two or more visible GPUs: the one-GPU box skips it, so distinct-device groups
+    stay unverified there (README)."""
+    import torch
+    n = min(torch.cuda.device_count(), 4)
+    if n < 2:
+        pytest.skip("one visible GPU: distinct-device groups need two or more")
+    from reflaxman_amd.render import build_scene, make_frame
+    scene, cam = build_scene(scenes.get_scene("synth16"))
+    W, H = 1920, 1080
+    g, one = Group(n, scene, devices=list(range(n))), _single(scene)
+    f = make_frame(cam, W, H, 8, 1)
+    rgb, argb = _bufs(torch, W, H)
+    rgb1, argb1 = _bufs(torch, W, H)
+    for i in range(10):
+        g.render(f, rgb, argb)
+        one.render_frame(f, rgb1.data_ptr(), argb1.data_ptr())
+        torch.cuda.synchronize()
+        assert torch.equal(rgb, rgb1) and torch.equal(argb, argb1), i
+    g.close()
+    one.close()

@@ -43,16 +43,42 @@ def test_golden_bitexact(key):
     r.close()
 
 
-@pytest.mark.parametrize("key", ["hash_default_640x480_d4", "hash_default_1920x1080_d4",
+@pytest.mark.parametrize("key", ["hash_default_640x480_d4", "hash_default_1920x1080_d1", "hash_default_1920x1080_d4",
                                  "hash_synth16_3840x2160_d8", "hash_default_3840x2160_d8",
-                                 "hash_synth16_7680x4320_d8"])
+                                 "hash_synth16_7680x4320_d8", "hash_stress4096_3840x2160_d12",
+                                 "hash_stress4096_3840x2160_d12_f2", "hash_default_1920x1080_d20_ss4"])
 def test_full_size_hash(key):
-    """BASELINE configs C1, C2, C3, C4 (and the default scene at 4K d8) at full size, bit-exact by SHA-256."""
+    """BASELINE configs C1, C2 (depth 1 and 4), C3, C4, C5 (frame 0, and frame 1 with the stream continued: the
+    image after two frames) and the reference's screenshot workload (Full HD, 4x4 SSAA, depth 20), plus the default
+    scene at 4K d8, at full size and the library defaults, bit-exact by SHA-256.  C5 runs the large-scene path as
+    shipped: park after 2 segments, the LDS-staged bounce kernel, the longest-first schedule (learned from frame 0 on
+    frame 1)."""
     c = CASES[key]
     rgb, argb, r = run_case(c)
+    if c["scene"] == "stress4096":
+        assert r._r.bounce_form() == 2, key  # the regrouped frame's LDS-staged bounce kernel ran
     assert sha(argb) == c["sha_argb"], key
     assert sha(rgb) == c["sha_f32"], key
     r.close()
+
+
+def test_c5_full_frames_steady_state():
+    """C5 over three frames at the defaults, per-view state included: frame 0 (first view: per-launch bundles, raster
+    tile order), frame 1 (the view repeats: the large-scene path has no primary masks, the schedule is sorted from
+    frame 0's costs) hash to the reference's frames 0 and 1; frame 2 equals a frame rendered without regrouping and
+    without a schedule from the same stream state."""
+    c0, c1 = CASES["hash_stress4096_3840x2160_d12"], CASES["hash_stress4096_3840x2160_d12_f2"]
+    got = []
+    _, _, r = gpu_render(scene("stress4096"), 3840, 2160, 12, frames=3, sphere_seed=c0["sphere_seed"],
+                         each_frame=lambda rgb, argb: got.append((sha(rgb), sha(argb))))
+    r.close()
+    assert got[0] == (c0["sha_f32"], c0["sha_argb"])
+    assert got[1] == (c1["sha_f32"], c1["sha_argb"])
+    plain = []
+    _, _, r = gpu_render(scene("stress4096"), 3840, 2160, 12, frames=3, sphere_seed=c0["sphere_seed"], regroup=0,
+                         tile_order=0, prim_masks=0, each_frame=lambda rgb, argb: plain.append((sha(rgb), sha(argb))))
+    r.close()
+    assert plain == got
 
 
 @pytest.mark.parametrize("key", sorted(k for k, c in CASES.items() if c["kind"] == "band"))
@@ -471,10 +497,13 @@ def test_regrouped_large_scene_equals_unregrouped(n_spheres):
     frame traced without regrouping, bit for bit, over two frames of the random stream."""
     desc = scenes.stress_scene(n_spheres)
     ref, _, r0 = gpu_render(desc, 320, 180, 12, frames=2, regroup=0)
+    assert r0._r.bounce_form() == 0
     r0.close()
     for park in (1, 2):
         rgb, _, r = gpu_render(desc, 320, 180, 12, frames=2, regroup=park)
         assert rgb.tobytes() == ref.tobytes(), (n_spheres, park)
+        # the form the test is about ran (a refused LDS launch falls back to the global form silently otherwise)
+        assert r._r.bounce_form() == (2 if n_spheres == 4096 else 1), (n_spheres, park)
         r.close()
 
 

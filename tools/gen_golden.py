@@ -59,6 +59,32 @@ def band_case(tmp, scene_arg, W, H, depth, y0, rows, sphere_seed):
     return rgb, argb
 
 
+def banded_frame(tmp, scene_arg, W, H, depth, ss, frame, sphere_seed, workers=None, band_rows=None):
+    """Frame `frame` (0-based, non-additive frames, ss x ss samples) of the reference, rendered as row bands by
+    parallel `refharness bandss` processes (each advances the random stream over every draw before its band) and
+    concatenated.  Used for the full-size hashes the single-threaded reference would take tens of minutes for."""
+    from concurrent.futures import ThreadPoolExecutor
+    workers = workers or os.cpu_count() or 8
+    band_rows = band_rows or max(1, -(-H // (workers * 4)))  # ~4 bands per worker: the cost varies along y
+    bands = [(y, min(band_rows, H - y)) for y in range(0, H, band_rows)]
+    env = dict(os.environ, RFX_SPHERE_SEED=str(sphere_seed))
+
+    def one(b):
+        y0, rows = b
+        out = os.path.join(tmp, f"bss_{frame}_{y0}")
+        subprocess.run([HARNESS, "bandss", scene_arg, str(W), str(H), str(depth), str(ss), str(frame), str(y0),
+                        str(rows), out], check=True, env=env, capture_output=True)
+        rgb = np.fromfile(out + ".f32", dtype=np.float32).reshape(rows, W, 3)
+        argb = np.fromfile(out + ".argb", dtype=np.uint32).reshape(rows, W)
+        os.remove(out + ".f32")
+        os.remove(out + ".argb")
+        return rgb, argb
+
+    with ThreadPoolExecutor(workers) as ex:
+        parts = list(ex.map(one, bands))
+    return np.concatenate([p[0] for p in parts]), np.concatenate([p[1] for p in parts])
+
+
 def kat_io(tmp, mode, inp, extra=(), out_dtype=np.float32):
     fi = os.path.join(tmp, "kat.in")
     fo = os.path.join(tmp, "kat.out")
@@ -284,6 +310,36 @@ def main():
         save_render("hash_default_1920x1080_d4", "default", 1920, 1080, 4, store=False, use_file=False)
         # C4: the C3 scene at 7680x4320 d8 (BASELINE configs[3])
         save_render("hash_synth16_7680x4320_d8", "synth16", 7680, 4320, 8, store=False)
+
+        # C2's depth-1 leg (BASELINE configs[1], "primary rays only")
+        save_render("hash_default_1920x1080_d1", "default", 1920, 1080, 1, store=False, use_file=False)
+
+        # Full frames the single-threaded reference needs tens of CPU-minutes for, rendered as parallel row bands
+        # (refharness bandss) and concatenated.  First the band path is checked against Render::renderNext itself
+        # (the render mode) on small frames: SSAA, a second frame of the stream, the large-scene path.
+        def save_banded(key, scene, W, H, depth, ss, frames, use_file=True):
+            if not want(key):
+                return
+            arg = scene_files[scene] if (use_file or scene != "default") else "default"
+            for (sW, sH, sd, sss, sfr) in ((96, 64, 4, ss, frames), (64, 36, min(depth, 12), 1, 2)):
+                rr, ra = render_case(tmp, arg, sW, sH, sd, sss, False, sfr, DEFAULT_SEED, 0)
+                br, ba = banded_frame(tmp, arg, sW, sH, sd, sss, sfr - 1, DEFAULT_SEED, band_rows=7)
+                assert rr.tobytes() == br.tobytes() and np.array_equal(ra, ba), (key, "bandss != renderNext")
+            t0 = time.time()
+            rgb, argb = banded_frame(tmp, arg, W, H, depth, ss, frames - 1, DEFAULT_SEED)
+            cases[key] = dict(kind="render", scene=scene, W=W, H=H, depth=depth, ss=ss, additive=False, frames=frames,
+                              sphere_seed=DEFAULT_SEED, jitter_seed=0, sha_f32=sha(rgb.tobytes()),
+                              sha_argb=sha(argb.tobytes()), stored=False,
+                              generated="refharness bandss: parallel row bands of Render::renderNext's pixel loop, "
+                                        "concatenated; checked equal to the render mode on small frames",
+                              cpu_wall_s=round(time.time() - t0, 1))
+            print(f"{key}: {time.time() - t0:.1f}s", flush=True)
+
+        # C5 (BASELINE configs[4]) frame 0 and frame 1 (the stream continued), full size
+        save_banded("hash_stress4096_3840x2160_d12", "stress4096", 3840, 2160, 12, 1, 1)
+        save_banded("hash_stress4096_3840x2160_d12_f2", "stress4096", 3840, 2160, 12, 1, 2)
+        # the reference's screenshot workload (Pulse.cpp:156-178: renderBegin(20, ss, false), Full HD, 4x4 SSAA)
+        save_banded("hash_default_1920x1080_d20_ss4", "default", 1920, 1080, 20, 4, 1, use_file=False)
 
         # C4 band: 4 rows at the middle of the 8K frame (stream advanced over the 2160 rows above)
         key = "band_synth16_7680x4320_d8_y2160_r4"
