@@ -75,7 +75,7 @@ CONFIGS = {
 # cpu_baseline row strides: about 5 s of the reference's single-core trace time per config (C5's CPU rate is
 # 0.0064 Mrays/s: every 270th row); SSAA configs time a centred band of this many rows instead
 CPU_STRIDE = {"c1": 1, "c2": 4, "c3": 2, "c4": 16, "c5": 270}
-CPU_BAND_ROWS = {"shot": 64}
+CPU_BAND_ROWS = {"shot": 160}
 
 
 def frame_size(n: int, w0: int, h0: int, scaling: str):

@@ -1244,11 +1244,44 @@ __shared__ __attribute__((aligned(16))) uint32_t s_out[kWgWaves][256];
 
 // Scene::trace from a mid-trace state (mulc, pix after `refl` segments); park: see Park.  *parked: this lane's
 // trace was queued and its returned colour is not final.
-template <bool STATS, bool CULL, bool MANYL, bool SMALL, bool PLANES, bool PARK, class PK>
-__device__ __forceinline__ col trace_from(const DevScene &S, v3 origin, v3 ray, col mulc, col pix, int refl, int depth,
-                                          v3 rd, const float *lut, Cnt &cnt, bool valid, const PK &park, bool &parked,
-                                          const uint64_t *pm_tile = nullptr)
+#ifdef RFX_LAUNDER_SCENE
+typedef const __attribute__((address_space(4))) DevScene *ConstScenePtr;
+// The record is read through the kernarg segment pointer: every kernel that reaches trace_from (trace_kernel,
+// bounce_kernel, bounce_kernel_lds) takes the DevScene as its first argument, at offset 0.  (Taking the address of
+// the by-value parameter instead makes the compiler copy it to scratch, and a constant-space pointer to that copy
+// faults.)
+template <bool ON>
+__device__ __forceinline__ const DevScene &launder_scene(const DevScene &S)
 {
+  if constexpr (!ON) return S;
+  ConstScenePtr p = (ConstScenePtr)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return *(const DevScene *)p;
+}
+#define RFX_SCENE_PARAM S_in
+#else
+#define RFX_SCENE_PARAM S
+#endif
+// The frame parameters (the kernels' second argument, after the DevScene) read through the kernarg segment pointer, laundered
+// by an empty asm: every use reloads them with scalar loads where it stands, so their values are not held in SGPRs
+// across a bounce loop (the SSAA sample loop; with RFX_LAUNDER_PARAMS also the plain epilogue and park ids)
+constexpr size_t kParamsOff = (sizeof(DevScene) + alignof(FrameParams) - 1) / alignof(FrameParams) * alignof(FrameParams);
+__device__ __forceinline__ const FrameParams &kernarg_params()
+{
+  typedef const __attribute__((address_space(4))) char *KP;
+  KP p = (KP)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(p));
+  return *(const FrameParams *)(const __attribute__((address_space(4))) FrameParams *)(p + kParamsOff);
+}
+
+template <bool STATS, bool CULL, bool MANYL, bool SMALL, bool PLANES, bool PARK, class PK>
+__device__ __forceinline__ col trace_from(const DevScene &RFX_SCENE_PARAM, v3 origin, v3 ray, col mulc, col pix, int refl,
+                                          int depth, v3 rd, const float *lut, Cnt &cnt, bool valid, const PK &park,
+                                          bool &parked, const uint64_t *pm_tile = nullptr)
+{
+#ifdef RFX_LAUNDER_SCENE
+  const DevScene &S = S_in;
+#endif
   // the first segment of a plain small-scene trace: this tile's per-view masks (prim_cull_kernel) -- the closest
   // hit's, then one per light for its shadow rays
   bool seg0 = pm_tile != nullptr;
@@ -1264,6 +1297,12 @@ __device__ __forceinline__ col trace_from(const DevScene &S, v3 origin, v3 ray, 
   {
 #ifdef RFX_DEBUG_SEGS
     if (alive) ++nseg;
+#endif
+#ifdef RFX_LAUNDER_SCENE
+    // experiment: the scene record re-read (scalar loads from the kernarg segment) in every segment instead of its
+    // fields held in SGPRs across the bounce loop, where they spill to VGPR lanes
+    const DevScene &S = launder_scene<!SMALL>(S_in);  // large scenes only: the small-scene kernel spills VGPRs with it
+    const Tabs<SMALL> T{S};
 #endif
     Hit h;
     if constexpr (SMALL)
@@ -1568,6 +1607,9 @@ struct ParkTile {
     const uint32_t t8 = ((volatile uint32_t *)s_tile8)[wv];
     uint32_t le = __lane_id();
     asm volatile("" : "+v"(le));
+#ifdef RFX_LAUNDER_PARAMS
+    const FrameParams &P = kernarg_params();
+#endif
     const uint32_t gx = (t8 % w8) * 8u + (le & 7u), gy = (t8 / w8) * 8u + (le >> 3);
     const uint32_t y = P.nranks > 1 ? strip_row_to_y(gy, P) : gy + P.row0;
     const uint32_t orow = P.nranks > 1 ? gy : y;
@@ -1759,27 +1801,56 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
     }
     else
     {
-      float rndx = 0.0f, rndy = 0.0f;
+      // SSAA / additive (Render.cpp:174-194).  The per-lane state that outlives each sample's bounce loop -- the
+      // running sum and the additive jitter -- waits in the wave's epilogue staging slot (s_out: 192 words of sum, 64
+      // of jitter), and the pixel's coordinates are re-derived from the tile index in LDS for every sample, so the
+      // bounce loop runs with the plain kernel's live state (round 4: 22 -> 0 VGPR spills in the small-scene kernel).
+      uint32_t *slot = s_out[wv];
+      uint32_t jit = 0;
       if (P.additive && valid)                                                     // Render.cpp:177-178
       {
         const uint32_t s1 = lcg_jump(P.jitter_seed, 2 * pr + 1);
-        rndx = (float)lcg_out(s1) / (float)0x7FFF;
-        rndy = (float)lcg_out(lcg_step(s1)) / (float)0x7FFF;
+        jit = lcg_out(s1) | lcg_out(lcg_step(s1)) << 16;  // two 15-bit draws
       }
+      slot[192 + lane] = jit;
+      slot[3 * lane] = 0u;  // +0.0f: Color finColor(0, 0, 0)
+      slot[3 * lane + 1] = 0u;
+      slot[3 * lane + 2] = 0u;
       const int ss = P.ss;
       const float ssf = (float)ss;
-      col fin = mkc(0.0f, 0.0f, 0.0f);
       for (int sx = 0; sx < ss; ++sx)                                              // Render.cpp:181-187
         for (int sy = 0; sy < ss; ++sy)
         {
+          const FrameParams &P = kernarg_params();  // shadows the by-value parameter: reloaded per sample
+          m33 view;
+          view.m11 = P.v11; view.m12 = P.v12; view.m13 = P.v13;
+          view.m21 = P.v21; view.m22 = P.v22; view.m23 = P.v23;
+          view.m31 = P.v31; view.m32 = P.v32; view.m33 = P.v33;
+          const v3 eye = mk(P.eye_x, P.eye_y, P.eye_z);
+          const uint32_t t8s = ((volatile uint32_t *)s_tile8)[wv];
+          uint32_t ls = lane;
+          asm volatile("" : "+v"(ls));  // a fresh lane value: the coordinates are recomputed, not kept live
+          const uint32_t sgx = (t8s % w8) * 8u + (ls & 7u), sgy = (t8s / w8) * 8u + (ls >> 3);
+          const uint32_t sy_ = P.nranks > 1 ? strip_row_to_y(sgy, P) : sgy + P.row0;
+          const uint64_t sp = (uint64_t)sy_ * P.W + sgx;
+          const bool svalid = sgx < P.W && sgy < P.grid_rows && sp >= P.p_begin && sp < P.p_end;
+          const uint32_t jw = ((volatile uint32_t *)slot)[192 + ls];
+          const float rndx = P.additive ? (float)(jw & 0xFFFFu) / (float)0x7FFF : 0.0f;
+          const float rndy = P.additive ? (float)(jw >> 16) / (float)0x7FFF : 0.0f;
           // float(0) / ss == +0 exactly, so the first sample's offsets need no division
           const float ox = sx ? (float)sx / ssf : 0.0f, oy = sy ? (float)sy / ssf : 0.0f;
-          v3 ray = mk(rx + ox + rndx, ry + oy + rndy, P.rz);
+          v3 ray = mk((float)sgx - P.wh + ox + rndx, (float)sy_ - P.hh + oy + rndy, P.rz);
           ray = mmul(view, ray);
           v3 rd = mk(0.0f, 0.0f, 0.0f);
-          if (valid) rd = load_rd(P, pr * (uint64_t)(ss * ss) + (uint64_t)(sx * ss + sy));
-          fin = cadd(fin, trace<STATS, CULL, MANYL, SMALL, PLANES>(S, eye, ray, P.depth, rd, lut, cnt, valid));
+          if (svalid) rd = load_rd(P, (sp - P.p_begin) * (uint64_t)(ss * ss) + (uint64_t)(sx * ss + sy));
+          const col c = trace<STATS, CULL, MANYL, SMALL, PLANES>(S, eye, ray, P.depth, rd, lut, cnt, svalid);
+          float *f = reinterpret_cast<float *>(slot) + 3 * ls;
+          f[0] = f[0] + c.r;
+          f[1] = f[1] + c.g;
+          f[2] = f[2] + c.b;
         }
+      const float *f = reinterpret_cast<const float *>(slot) + 3 * lane;
+      col fin = mkc(f[0], f[1], f[2]);
       if (ss != 1)                                                                 // Render.cpp:189 (x / 1.0f == x)
       {
         const float sq = (float)(ss * ss);
@@ -1788,6 +1859,9 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
       out = fin;
     }
     // output coordinates again, from the tile index in LDS (volatile: re-read, not kept live)
+#ifdef RFX_LAUNDER_PARAMS
+    const FrameParams &P = kernarg_params();  // shadows the by-value parameter: re-read after the bounce loop
+#endif
     const uint32_t t8e = ((volatile uint32_t *)s_tile8)[wv];
     uint32_t le = lane;
     asm volatile("" : "+v"(le));  // a fresh lane value: its row/column are recomputed, not kept live

@@ -56,6 +56,10 @@ VARIANTS = {
     "lpt4k": ["RFX_TILE_ORDER_MIN_TILES=4096"],
     "bg16": ["RFX_BOUNCE_GROUPS_PER_CU=16"],
     "bg8": ["RFX_BOUNCE_GROUPS_PER_CU=8"],
+    "launder": ["RFX_LAUNDER_SCENE"],
+    "launderp": ["RFX_LAUNDER_PARAMS"],
+    "launder2": ["RFX_LAUNDER_SCENE", "RFX_LAUNDER_PARAMS"],
+    "ssaa2": [],  # (built from a newer source than base: the A/B of a source change)
 }
 
 
@@ -94,7 +98,7 @@ def build_scene_with(L, desc):
 
 
 class Runner:
-    def __init__(self, name, path, desc, W, H, depth, seed, tile_order=None, regroup=None, prim=None):
+    def __init__(self, name, path, desc, W, H, depth, seed, tile_order=None, regroup=None, prim=None, ss=1):
         self.name = name
         L = self.L = _lib.bind(path, partial=True)
         self.scene, eye, view, fov = build_scene_with(L, desc)
@@ -117,7 +121,7 @@ class Runner:
         f.eye[:] = eye
         f.view[:] = view
         f.fov = fov
-        f.width, f.height, f.reflect_num, f.sample_num, f.nranks = W, H, depth, 1, 1
+        f.width, f.height, f.reflect_num, f.sample_num, f.nranks = W, H, depth, ss, 1
         self.frame = f
 
     def render(self, n=1):
@@ -162,7 +166,7 @@ def cmd_build(names):
 
 def cmd_run(args):
     man = json.load(open(os.path.join(ROOT, "tests", "golden", "manifest.json")))["cases"]
-    key = f"hash_{args.scene}_{args.width}x{args.height}_d{args.depth}"
+    key = f"hash_{args.scene}_{args.width}x{args.height}_d{args.depth}" + (f"_ss{args.ss}" if args.ss != 1 else "")
     desc = scenes.get_scene(args.scene)
     paths = sorted(glob.glob(os.path.join(_build.LIBDIR, "variants", "librfx_*.so")))
     names = [os.path.basename(p)[len("librfx_"):-3] for p in paths]
@@ -173,13 +177,13 @@ def cmd_run(args):
     regroups = [None] if not args.regroup else [int(v) for v in args.regroup.split(",")]
     prims = [None] if not args.prim else [int(v) for v in args.prim.split(",")]
     runners = [Runner(n + ("" if g is None else f"@park{g}") + ("" if q is None else f"@prim{q}"), p, desc, args.width,
-                      args.height, args.depth, 1350490027, regroup=g, prim=q)
+                      args.height, args.depth, 1350490027, regroup=g, prim=q, ss=args.ss)
                for n, p in zip(names, paths) for g in regroups for q in prims]
     # parity of every variant: frame 1 against the reference's full-frame hash (when the manifest has one), and
     # frame 1 + LATER frames (rendered in the learned longest-tile-first order, after the tile sorts) against
     # the product build rendering the same frames in raster order
     later = max(2, args.later_frame)
-    ref = Runner("raster", _build.LIB, desc, args.width, args.height, args.depth, 1350490027, tile_order=0)
+    ref = Runner("raster", _build.LIB, desc, args.width, args.height, args.depth, 1350490027, tile_order=0, ss=args.ss)
     ref_first = ref.frame_hashes(1)
     ref_later = ref.frame_hashes(later - 1)
     ref.close()
@@ -211,7 +215,7 @@ def cmd_run(args):
                     "prepass_ms_median": round(statistics.median(pre[r.name]), 4),
                     "frame_ms_median": round(statistics.median(wall[r.name]), 4),
                     "vs_first": round(med / base, 4),
-                    "mrays_trace_only": round(args.width * args.height / (med * 1e-3) / 1e6, 1)})
+                    "mrays_trace_only": round(args.width * args.height * args.ss ** 2 / (med * 1e-3) / 1e6, 1)})
     for o in out:
         print(json.dumps(o))
 
@@ -225,6 +229,7 @@ def main():
     ap.add_argument("--width", type=int, default=3840)
     ap.add_argument("--height", type=int, default=2160)
     ap.add_argument("--depth", type=int, default=8)
+    ap.add_argument("--ss", type=int, default=1, help="samples per pixel ss x ss (SSAA frames)")
     ap.add_argument("--rounds", type=int, default=12)
     ap.add_argument("--frames", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
