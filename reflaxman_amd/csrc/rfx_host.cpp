@@ -443,7 +443,8 @@ extern "C" uint32_t rfx_strip_row_to_y(uint32_t r, uint32_t rb, uint32_t rank, u
 // trace 0.41 ms unsorted vs 0.34 at N = 4 per eighth of the frame, tools/root_overhead.py)
 #define RFX_TILE_ORDER_MIN_TILES 49152
 #endif
-constexpr size_t kPrimWords = 5;  // per wave tile (rfx_trace.h kPrimStride)
+constexpr size_t kPrimWords = 5;        // per wave tile, small scenes (rfx_trace.h kPrimStride)
+constexpr size_t kPrimLargeWords = 12;  // per wave tile, large scenes (rfx_trace.h kPrimLargeStride)
 #ifndef RFX_BOUNCE_GROUPS_PER_CU
 #define RFX_BOUNCE_GROUPS_PER_CU 14
 #endif
@@ -1371,11 +1372,12 @@ static int trace_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *rd, float
   uint64_t key = 0;
   bool record = false;
   if (sched && (rc = tile_schedule(r, P, st, key, record)) != RFX_OK) return rc;
-  // primary-bundle cull masks: small scenes, plain frames, culling launches; recomputed only when the camera,
-  // the frame geometry or the scene changed (the bench's frames all reuse one set)
-  if (small && plain && !d_counters && !park && P.grid_rows && r->prim_mode)
+  // primary-bundle cull masks: small scenes, plain and SSAA frames (not block previews), culling launches; large scenes,
+  // plain frames: the primary bundles' chunk lists.  Recomputed only when the camera, the frame geometry, the sampling
+  // or the scene changed (the bench's frames all reuse one set)
+  if (((small && P.ss >= 1 && !park) || (!small && plain)) && !d_counters && P.grid_rows && r->prim_mode)
   {
-    struct Key { float cam[15]; uint32_t W, H, grid_rows, row0, row_block, rank, nranks; int32_t depth;
+    struct Key { float cam[15]; uint32_t W, H, grid_rows, row0, row_block, rank, nranks; int32_t depth, ss, additive;
                  uint64_t p_begin, p_end, gen; } k;
     memset(&k, 0, sizeof(k));  // padding bytes too: the key is compared bytewise
     const float cam[15] = {P.eye_x, P.eye_y, P.eye_z, P.v11, P.v12, P.v13, P.v21, P.v22, P.v23,
@@ -1383,15 +1385,16 @@ static int trace_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *rd, float
     memcpy(k.cam, cam, sizeof(cam));
     k.W = P.W; k.H = P.H; k.grid_rows = P.grid_rows; k.row0 = P.row0; k.row_block = P.row_block; k.rank = P.rank;
     k.nranks = P.nranks; k.depth = P.depth > 0 ? 1 : 0; k.p_begin = P.p_begin; k.p_end = P.p_end; k.gen = r->scene_gen;
-    const size_t ntiles = trace_tiles(P);
+    k.ss = P.ss; k.additive = P.additive ? 1 : 0;
+    const size_t nwords = trace_tiles(P) * (small ? kPrimWords : kPrimLargeWords);
     std::vector<uint8_t> kb((const uint8_t *)&k, (const uint8_t *)&k + sizeof(k));
-    if (ntiles > r->prim_cap)
+    if (nwords > r->prim_cap)
     {
       (void)hipFree(r->d_prim_mask);
       r->d_prim_mask = nullptr;
       r->prim_cap = 0;
-      HIP_CHECK(hipMalloc(&r->d_prim_mask, ntiles * kPrimWords * sizeof(uint64_t)));
-      r->prim_cap = ntiles;
+      HIP_CHECK(hipMalloc(&r->d_prim_mask, nwords * sizeof(uint64_t)));
+      r->prim_cap = nwords;
       r->prim_key.clear();
       r->prim_seen.clear();
     }
@@ -1408,7 +1411,11 @@ static int trace_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *rd, float
         r->prim_key = kb;
       }
     }
-    if (!r->prim_key.empty()) P.prim_mask = r->d_prim_mask;
+    if (!r->prim_key.empty())
+    {
+      P.prim_mask = r->d_prim_mask;
+      P.prim_shadow = P.additive ? 0 : 1;  // jittered frames: closest-hit masks only (prim_cull_kernel)
+    }
   }
   if (P.grid_rows) HIP_CHECK(launch_trace(r->dev, P, d_counters != nullptr, st));
   r->bounce_form = 0;

@@ -479,6 +479,11 @@ constexpr float kCullRel = 2e-3f;
 // per-view primary masks (prim_cull_kernel): per wave tile, the closest hit's mask and the shadow masks of the
 // first kPrimLights lights
 constexpr int kPrimLights = 4, kPrimStride = 1 + kPrimLights;
+// Large scenes (prim_cull_large_kernel): per wave tile, the chunk cull of its primary bundle -- [0] the number of kept
+// 64-sphere chunks (at most kPrimLargeChunks; kPrimLargeNone: no list, the tile culls per launch), [1] the triangle mask,
+// [2] the chunk mask (scenes of at most 64 chunks), [4..] the kept chunks' sphere masks in chunk order
+constexpr int kPrimLargeChunks = 8, kPrimLargeStride = 4 + kPrimLargeChunks;
+constexpr uint64_t kPrimLargeNone = ~0ull;
 
 struct Bundle {
   float cx, cy, cz, rw;
@@ -554,6 +559,40 @@ __device__ __forceinline__ Bundle make_bundle_ball(v3 o, v3 d, float R, bool liv
   const float cosl = ca * cb - sa * sb;
   const float dev = 1.0f - cosl;
   const bool bad = live && !(e2 <= 1.0e30f && dev >= -0.5f && dev <= 2.5f && sb < 0.5f);
+  const float e2m = wave_max_nonneg(live ? e2 : 0.0f);
+  const float devm = wave_max_nonneg(live ? fmaxf(dev, 0.0f) : 0.0f);
+  B.rw = __builtin_amdgcn_sqrtf(e2m) * 1.0001f;
+  B.cosa = 1.0f - devm - 4e-6f;                                                // approximate cosines: widen
+  B.sina = __builtin_amdgcn_sqrtf(fmaxf(1.0f - B.cosa * B.cosa, 0.0f) + 1e-7f) * 1.001f;
+  B.ok = __ballot(bad) == 0 && B.cosa > 0.1f && B.rw <= 1.0e15f;
+  return B;
+}
+
+// Bundle of every ray from o with a direction in the quadrilateral d[0..3] of each `live` lane (the sample rays of an SSAA
+// pixel: the directions are a linear image of the pixel's sample rectangle, and the cone is convex, so a cone
+// holding the four corners holds every ray between them).  For the per-view masks of SSAA frames (prim_cull_kernel).
+__device__ __forceinline__ Bundle make_bundle_quad(v3 o, const v3 (&d)[4], bool live)
+{
+  Bundle B;
+  const int ref = __ffsll((long long)__ballot(live)) - 1;
+  B.cx = lane_bcast(o.x, ref); B.cy = lane_bcast(o.y, ref); B.cz = lane_bcast(o.z, ref);
+  const float dx = lane_bcast(d[0].x, ref), dy = lane_bcast(d[0].y, ref), dz = lane_bcast(d[0].z, ref);
+  const float inv = __builtin_amdgcn_rsqf(dx * dx + dy * dy + dz * dz);
+  B.ax = dx * inv; B.ay = dy * inv; B.az = dz * inv;
+  const float ex = o.x - B.cx, ey = o.y - B.cy, ez = o.z - B.cz;
+  const float e2 = ex * ex + ey * ey + ez * ez;
+  float dev = 0.0f;
+  bool bad = false;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+  {
+    const v3 v = d[k];
+    const float cosl = (v.x * B.ax + v.y * B.ay + v.z * B.az) * __builtin_amdgcn_rsqf(v.x * v.x + v.y * v.y + v.z * v.z);
+    const float dk = 1.0f - cosl;
+    bad = bad || !(dk >= -0.5f && dk <= 2.5f);
+    dev = fmaxf(dev, dk);
+  }
+  bad = live && (bad || !(e2 <= 1.0e30f));
   const float e2m = wave_max_nonneg(live ? e2 : 0.0f);
   const float devm = wave_max_nonneg(live ? fmaxf(dev, 0.0f) : 0.0f);
   B.rw = __builtin_amdgcn_sqrtf(e2m) * 1.0001f;
@@ -918,7 +957,7 @@ __device__ __forceinline__ bool occluded_planes(const DevScene &S, v3 o, v3 ray,
 // visiting order is then not the insertion order, so spheres take the general (distance, object) rule.
 template <bool STATS, bool PLANES, class NS = BvhGlobal>
 __device__ __forceinline__ void closest_hit(const DevScene &S, v3 origin, v3 ray, bool live, const Bundle *B, Hit &h,
-                                            Cnt &cnt, const NS &ns = NS{})
+                                            Cnt &cnt, const NS &ns = NS{}, const uint64_t *pl = nullptr)
 {
   if (live) RFX_CNT(C_SEGMENTS);
   h.obj = -1; h.kind = 0; h.i = 0; h.t = 0.0f; h.u = 0.0f; h.v = 0.0f; h.sq = kNoHitKey;
@@ -930,21 +969,25 @@ __device__ __forceinline__ void closest_hit(const DevScene &S, v3 origin, v3 ray
   RFX_PROF_BEGIN(P_SPH);
   // a narrow bundle (the primary rays of a tile: one origin, a cone of ~0.1 degree) culls the spatial chunks and
   // their spheres for the whole wave at once; wider ones walk the BVH lane by lane
-  const bool use_bvh = !STATS && S.bvh != nullptr && !(cull && B->cosa > kNarrowBundleCos);
+  // a per-view list (the tile's primary rays, prim_cull_large_kernel): the kept chunks and their sphere masks as listed
+  const bool listed = pl != nullptr;
+  const bool use_bvh = !listed && !STATS && S.bvh != nullptr && !(cull && B->cosa > kNarrowBundleCos);
   if (use_bvh && live) closest_spheres_bvh<STATS>(S, origin, ray, k, h, cnt, ns);
   for (int cfirst = 0; !use_bvh && cfirst < S.n_chunk; cfirst += 64)
   {
-    uint64_t cm = cull ? cull_chunk(S.chunk_bound, cfirst, min(64, S.n_chunk - cfirst), *B)
-                       : all_bits(min(64, S.n_chunk - cfirst));
+    uint64_t cm = listed ? pl[2]
+                         : cull ? cull_chunk(S.chunk_bound, cfirst, min(64, S.n_chunk - cfirst), *B)
+                                : all_bits(min(64, S.n_chunk - cfirst));
 #ifdef RFX_DEBUG_PROF
     st_chunks += __popcll(cm);
 #endif
+    int e = 4;
     while (cm)
     {
       const int first = 64 * (cfirst + __builtin_ctzll(cm));
       cm &= cm - 1ull;
       const int n = min(64, S.n_sph - first);
-      const uint64_t m = cull ? cull_chunk(S.bound, first, n, *B) : all_bits(n);
+      const uint64_t m = listed ? pl[e++] : cull ? cull_chunk(S.bound, first, n, *B) : all_bits(n);
       uint32_t pm = pair_bits(m);
 #ifdef RFX_DEBUG_PROF
       st_sph += __popcll(m);
@@ -983,7 +1026,7 @@ __device__ __forceinline__ void closest_hit(const DevScene &S, v3 origin, v3 ray
   for (int first = 0; first < S.n_tri; first += 64)
   {
     const int n = min(64, S.n_tri - first);
-    uint64_t m = (B && B->ok) ? cull_chunk(S.bound, S.n_sph + first, n, *B) : all_bits(n);
+    uint64_t m = listed ? pl[1] : (B && B->ok) ? cull_chunk(S.bound, S.n_sph + first, n, *B) : all_bits(n);
     while (m)
     {
       const int i = first + __builtin_ctzll(m);
@@ -1277,7 +1320,7 @@ __device__ __forceinline__ const FrameParams &kernarg_params()
 template <bool STATS, bool CULL, bool MANYL, bool SMALL, bool PLANES, bool PARK, class PK>
 __device__ __forceinline__ col trace_from(const DevScene &RFX_SCENE_PARAM, v3 origin, v3 ray, col mulc, col pix, int refl,
                                           int depth, v3 rd, const float *lut, Cnt &cnt, bool valid, const PK &park,
-                                          bool &parked, const uint64_t *pm_tile = nullptr)
+                                          bool &parked, const uint64_t *pm_tile = nullptr, bool pm_shadow = true)
 {
 #ifdef RFX_LAUNDER_SCENE
   const DevScene &S = S_in;
@@ -1324,9 +1367,11 @@ __device__ __forceinline__ col trace_from(const DevScene &RFX_SCENE_PARAM, v3 or
     }
     else
     {
+      // the first segment of a plain trace: the tile's per-view chunk list (prim_cull_large_kernel), when it has one
+      const uint64_t *pl = CULL && seg0 && pm_tile[0] != kPrimLargeNone ? pm_tile : nullptr;
       Bundle B;
       if constexpr (CULL) B = make_bundle(origin, ray, alive);
-      closest_hit<STATS, PLANES>(S, origin, ray, alive, CULL ? &B : nullptr, h, cnt, park.bvh());
+      closest_hit<STATS, PLANES>(S, origin, ray, alive, CULL ? &B : nullptr, h, cnt, park.bvh(), pl);
     }
     const bool hit = alive && h.obj >= 0;
     // re-derive the winner's outputs with the reference's expressions
@@ -1390,7 +1435,7 @@ __device__ __forceinline__ col trace_from(const DevScene &RFX_SCENE_PARAM, v3 or
             uint64_t om = S.cull_valid;
             if constexpr (CULL)
             {
-              if (!MANYL && seg0 && q < kPrimLights)
+              if (!MANYL && seg0 && pm_shadow && q < kPrimLights)
                 om = pm_tile[1 + q];  // the primary hits' shadow mask for light q, precomputed for the view
               else
               {
@@ -1559,12 +1604,12 @@ __device__ __forceinline__ col trace_from(const DevScene &RFX_SCENE_PARAM, v3 or
 
 template <bool STATS, bool CULL, bool MANYL, bool SMALL, bool PLANES>
 __device__ __forceinline__ col trace(const DevScene &S, v3 origin, v3 ray, int depth, v3 rd, const float *lut,
-                                     Cnt &cnt, bool valid)
+                                     Cnt &cnt, bool valid, const uint64_t *pm_tile = nullptr, bool pm_shadow = true)
 {
   bool parked;
   return trace_from<STATS, CULL, MANYL, SMALL, PLANES, false>(S, origin, ray, mkc(1.0f, 1.0f, 1.0f), mkc(0.0f, 0.0f, 0.0f), 0,
                                                        depth, rd, lut, cnt, valid, Park{0, nullptr, nullptr, 0, 0},
-                                                       parked);
+                                                       parked, pm_tile, pm_shadow);
 }
 
 template <bool STATS>
@@ -1793,7 +1838,8 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
       v3 rd = mk(0.0f, 0.0f, 0.0f);
       if (valid) rd = load_rd(P, pr);
       const ParkTile park{P.park_after, P.queue, P.queue_count, P, wv, w8};
-      const uint64_t *pm_tile = SMALL && CULL && !STATS && P.prim_mask ? P.prim_mask + (size_t)kPrimStride * t8 : nullptr;
+      const uint64_t *pm_tile = CULL && !STATS && P.prim_mask
+                                    ? P.prim_mask + (size_t)(SMALL ? kPrimStride : kPrimLargeStride) * t8 : nullptr;
       const col c = trace_from<STATS, CULL, MANYL, SMALL, PLANES, PARK>(S, eye, ray, mkc(1.0f, 1.0f, 1.0f),
                                                                   mkc(0.0f, 0.0f, 0.0f), 0, P.depth, rd, lut, cnt,
                                                                   valid, park, parked, pm_tile);
@@ -1843,7 +1889,10 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
           ray = mmul(view, ray);
           v3 rd = mk(0.0f, 0.0f, 0.0f);
           if (svalid) rd = load_rd(P, (sp - P.p_begin) * (uint64_t)(ss * ss) + (uint64_t)(sx * ss + sy));
-          const col c = trace<STATS, CULL, MANYL, SMALL, PLANES>(S, eye, ray, P.depth, rd, lut, cnt, svalid);
+          // the tile's per-view masks cover every sample's primary rays (prim_cull_kernel)
+          const uint64_t *pm = SMALL && CULL && !STATS && P.prim_mask ? P.prim_mask + (size_t)kPrimStride * t8s : nullptr;
+          const col c = trace<STATS, CULL, MANYL, SMALL, PLANES>(S, eye, ray, P.depth, rd, lut, cnt, svalid, pm,
+                                                                 P.prim_shadow != 0);
           float *f = reinterpret_cast<float *>(slot) + 3 * ls;
           f[0] = f[0] + c.r;
           f[1] = f[1] + c.g;
@@ -1893,7 +1942,7 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
 
 }
 
-// Per-view masks of a small scene's plain frame (FrameParams::prim_mask), kPrimStride words per wave tile t8:
+// Per-view masks of a small scene's plain or SSAA frame (FrameParams::prim_mask), kPrimStride words per wave tile t8:
 // [0] the cull mask of the tile's primary bundle, [1 + q] that of its primary hits' shadow rays toward light q
 // for every randDir (q < kPrimLights).  Wave t8 builds its tile's primary rays exactly as trace_kernel does (same
 // tile mapping, same validity), their bundle (one origin: the eye) and cull mask -- with the triangle footprint
@@ -1921,54 +1970,137 @@ __global__ RFX_TRACE_BOUNDS void prim_cull_kernel(DevScene S, FrameParams P, uin
   view.m31 = P.v31; view.m32 = P.v32; view.m33 = P.v33;
   const v3 eye = mk(P.eye_x, P.eye_y, P.eye_z);
   const float rx = (float)x - P.wh, ry = (float)y - P.hh;                       // Render.cpp:152-153
-  const v3 ray = mmul(view, mk(rx + 0.0f + 0.0f, ry + 0.0f + 0.0f, P.rz));     // as trace_kernel (plain)
   uint64_t *out = masks + (size_t)kPrimStride * t8;
+  // one sample per pixel without jitter: the plain rays themselves; SSAA and jittered (additive) frames: every ray of
+  // the pixel's sample rectangle [rx, rx + omax] x [ry, ry + omax] (Render.cpp:177-183: offsets (ss - 1) / ss at most,
+  // plus a jitter of at most 1 in additive frames), through its four corners
+  const int ss = P.ss;
+  const bool exact = ss == 1 && !P.additive;
   uint64_t om = 0;
   if (__ballot(valid))
   {
-    const Bundle B = make_bundle(eye, ray, valid);
+    Bundle B;
+    if (exact)
+      B = make_bundle(eye, mmul(view, mk(rx + 0.0f + 0.0f, ry + 0.0f + 0.0f, P.rz)), valid);  // as trace_kernel (plain)
+    else
+    {
+      const float omax = (float)(ss - 1) / (float)ss + (P.additive ? 1.0f : 0.0f);
+      const v3 q[4] = {mmul(view, mk(rx, ry, P.rz)), mmul(view, mk(rx + omax, ry, P.rz)),
+                       mmul(view, mk(rx, ry + omax, P.rz)), mmul(view, mk(rx + omax, ry + omax, P.rz))};
+      B = make_bundle_quad(eye, q, valid);
+    }
     om = B.ok ? cull_small<true>(T.cull(), S.cull_valid, B, S.cull_tri) : S.cull_valid;
   }
   if (lane == 0) out[0] = om;
-  // the primary hits, as trace_from's first segment finds them with this mask (Scene.cpp:86-106)
-  Cnt cnt;
-  Hit h;
-  if (valid) closest_hit_small<false, PLANES>(S, eye, ray, om, h, cnt);
-  else h.obj = -1;
-  const bool hit = valid && h.obj >= 0;
-  v3 drop = eye, norm = mk(0.0f, 0.0f, 0.0f);
-  if (hit)
+  // the primary hits of every sample, as trace_from's first segment finds them with this mask (Scene.cpp:86-106), and
+  // per light the union of their shadow bundles' masks.  Jittered frames: the hits are not known ahead, no shadow masks
+  // (FrameParams::prim_shadow; the trace kernel builds those bundles itself).
+  const int nl = P.additive ? 0 : min(S.n_light, kPrimLights);
+  uint64_t sm[kPrimLights] = {0, 0, 0, 0};
+  const float ssf = (float)ss;
+  for (int sx = 0; nl > 0 && sx < ss; ++sx)
+    for (int sy = 0; sy < ss; ++sy)
+    {
+      // the sample's ray exactly as trace_kernel forms it (plain: rx + 0 + 0; SSAA: rx + float(sx) / ss + 0)
+      const float ox = sx ? (float)sx / ssf : 0.0f, oy = sy ? (float)sy / ssf : 0.0f;
+      const v3 ray = mmul(view, mk(rx + ox + 0.0f, ry + oy + 0.0f, P.rz));
+      Cnt cnt;
+      Hit h;
+      if (valid) closest_hit_small<false, PLANES>(S, eye, ray, om, h, cnt);
+      else h.obj = -1;
+      const bool hit = valid && h.obj >= 0;
+      v3 drop = eye, norm = mk(0.0f, 0.0f, 0.0f);
+      if (hit)
+      {
+        drop = add(eye, mul(ray, h.t));
+        if (h.kind == 0)
+        {
+          const SphereGeo g = T.sph_geo(h.i);
+          norm = sub(drop, mk(g.cx, g.cy, g.cz));                                // Sphere.cpp:67
+        }
+        else if (!PLANES || h.kind == 1)
+        {
+          const TriShade sh = T.tri_shade(h.i);
+          norm = mk(sh.nx, sh.ny, sh.nz);
+        }
+        else
+        {
+          const PlaneGeo g = S.pln_geo[h.i];
+          norm = mk(g.nx, g.ny, g.nz);                                           // Plane.cpp:58-59
+        }
+      }
+      for (int q = 0; q < nl; ++q)
+      {
+        const LightRec L = S.lights[q];
+        const v3 dtl = sub(mk(L.ox, L.oy, L.oz), drop);
+        const bool facing = hit && dot(dtl, norm) > kVerySmall;                  // Scene.cpp:125
+        if (__ballot(facing))
+        {
+          const Bundle SB = make_bundle_ball(drop, dtl, L.radius, facing);
+          sm[q] |= SB.ok ? cull_small(T.cull(), S.cull_valid, SB) : S.cull_valid;
+        }
+      }
+    }
+  for (int q = 0; q < nl; ++q)
+    if (lane == 0) out[1 + q] = sm[q];
+}
+
+// Per-view chunk lists of a large scene's plain frame (FrameParams::prim_mask, kPrimLargeStride words per wave tile t8):
+// the primary bundle of the tile -- the same rays, validity and bundle as trace_from's first segment -- and, when it is
+// narrow enough for the chunk path (closest_hit), its chunk cull and the sphere cull of each kept chunk, stored as a
+// list the trace kernel walks instead of culling again; the triangle cull too.  More than kPrimLargeChunks kept chunks,
+// more than 64 triangles, or a bundle the chunk path would not take: kPrimLargeNone (the tile culls per launch).
+template <int UNUSED = 0>  // a template, as every kernel this header defines: one definition across the TUs
+__global__ RFX_TRACE_BOUNDS void prim_cull_large_kernel(DevScene S, FrameParams P, uint64_t *masks)
+{
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(wave);
+  const uint32_t w8 = kTileWavesX * gridDim.x;
+  const uint32_t t8 = (blockIdx.y * kTileWavesY + wv / kTileWavesX) * w8 + blockIdx.x * kTileWavesX + wv % kTileWavesX;
+  const uint32_t gx = (t8 % w8) * 8u + (lane & 7u), gy = (t8 / w8) * 8u + (lane >> 3);
+  const uint32_t x = gx;
+  const uint32_t y = P.nranks > 1 ? strip_row_to_y(gy, P) : gy + P.row0;
+  const uint64_t p = (uint64_t)y * P.W + x;
+  const bool valid = gx < P.W && gy < P.grid_rows && p >= P.p_begin && p < P.p_end && P.depth > 0;
+  m33 view;
+  view.m11 = P.v11; view.m12 = P.v12; view.m13 = P.v13;
+  view.m21 = P.v21; view.m22 = P.v22; view.m23 = P.v23;
+  view.m31 = P.v31; view.m32 = P.v32; view.m33 = P.v33;
+  const v3 eye = mk(P.eye_x, P.eye_y, P.eye_z);
+  const float rx = (float)x - P.wh, ry = (float)y - P.hh;                       // Render.cpp:152-153
+  const v3 ray = mmul(view, mk(rx + 0.0f + 0.0f, ry + 0.0f + 0.0f, P.rz));     // as trace_kernel (plain)
+  uint64_t *out = masks + (size_t)kPrimLargeStride * t8;
+  uint64_t w[kPrimLargeStride];
+#pragma unroll
+  for (int i = 0; i < kPrimLargeStride; ++i) w[i] = 0;
+  bool listed = false;
+  if (__ballot(valid) && S.n_tri <= 64 && S.n_chunk <= 64)
   {
-    drop = add(eye, mul(ray, h.t));
-    if (h.kind == 0)
+    const Bundle B = make_bundle(eye, ray, valid);
+    // the bundles closest_hit takes through the chunk path (the others walk the BVH per lane)
+    if (B.ok && (S.bvh == nullptr || B.cosa > kNarrowBundleCos))
     {
-      const SphereGeo g = T.sph_geo(h.i);
-      norm = sub(drop, mk(g.cx, g.cy, g.cz));                                    // Sphere.cpp:67
-    }
-    else if (!PLANES || h.kind == 1)
-    {
-      const TriShade sh = T.tri_shade(h.i);
-      norm = mk(sh.nx, sh.ny, sh.nz);
-    }
-    else
-    {
-      const PlaneGeo g = S.pln_geo[h.i];
-      norm = mk(g.nx, g.ny, g.nz);                                               // Plane.cpp:58-59
+      const uint64_t cm = cull_chunk(S.chunk_bound, 0, S.n_chunk, B);
+      listed = __popcll(cm) <= kPrimLargeChunks;
+      if (listed)
+      {
+        w[0] = (uint64_t)__popcll(cm);
+        w[2] = cm;
+        int e = 4;
+        for (uint64_t c = cm; c; c &= c - 1ull)
+        {
+          const int first = 64 * __builtin_ctzll(c);
+          w[e++] = cull_chunk(S.bound, first, min(64, S.n_sph - first), B);
+        }
+        if (S.n_tri > 0) w[1] = cull_chunk(S.bound, S.n_sph, S.n_tri, B);
+      }
     }
   }
-  const int nl = min(S.n_light, kPrimLights);
-  for (int q = 0; q < nl; ++q)
+  if (!listed) w[0] = kPrimLargeNone;
+  if (lane == 0)
   {
-    const LightRec L = S.lights[q];
-    const v3 dtl = sub(mk(L.ox, L.oy, L.oz), drop);
-    const bool facing = hit && dot(dtl, norm) > kVerySmall;                      // Scene.cpp:125
-    uint64_t sm = 0;
-    if (__ballot(facing))
-    {
-      const Bundle SB = make_bundle_ball(drop, dtl, L.radius, facing);
-      sm = SB.ok ? cull_small(T.cull(), S.cull_valid, SB) : S.cull_valid;
-    }
-    if (lane == 0) out[1 + q] = sm;
+#pragma unroll
+    for (int i = 0; i < kPrimLargeStride; ++i) out[i] = w[i];
   }
 }
 

@@ -151,8 +151,11 @@ struct FrameParams {
   // time; queue_order lists the entries bucket by bucket, and the bounce kernel claims them in that order
   uint32_t *queue_key;
   const uint32_t *queue_order;
-  // small scenes, plain pixels: per wave tile, the cull mask of its primary bundle (prim_cull_kernel), or null
+  // small scenes, plain and SSAA pixels: per wave tile, the cull mask of its primary bundle and of its primary hits'
+  // shadow rays (prim_cull_kernel), or null; prim_shadow: the shadow masks hold (not for jittered additive frames,
+  // whose primary hits are not known ahead)
   const uint64_t *prim_mask;
+  int32_t prim_shadow;
 };
 
 }  // namespace rfx

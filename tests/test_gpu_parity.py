@@ -64,9 +64,9 @@ def test_full_size_hash(key):
 
 def test_c5_full_frames_steady_state():
     """C5 over three frames at the defaults, per-view state included: frame 0 (first view: per-launch bundles, raster
-    tile order), frame 1 (the view repeats: the large-scene path has no primary masks, the schedule is sorted from
-    frame 0's costs) hash to the reference's frames 0 and 1; frame 2 equals a frame rendered without regrouping and
-    without a schedule from the same stream state."""
+    tile order), frame 1 (the view repeats: the primary bundles' chunk lists are built, the schedule is sorted from
+    frame 0's costs) hash to the reference's frames 0 and 1; frame 2 equals a frame rendered without regrouping,
+    lists or schedule from the same stream state."""
     c0, c1 = CASES["hash_stress4096_3840x2160_d12"], CASES["hash_stress4096_3840x2160_d12_f2"]
     got = []
     _, _, r = gpu_render(scene("stress4096"), 3840, 2160, 12, frames=3, sphere_seed=c0["sphere_seed"],
@@ -490,6 +490,19 @@ def test_stress_band_other_regrouping(key, regroup, qsort):
     r.close()
 
 
+@pytest.mark.parametrize("key", sorted(k for k, c in CASES.items() if c["kind"] == "band" and c["scene"] == "stress4096"))
+def test_stress_band_chunk_lists(key):
+    """C5 with the per-view chunk lists of the primary bundles built before the first frame (prim_masks 2,
+    prim_cull_large_kernel): the reference's bands."""
+    c = CASES[key]
+    rgb, argb, r = gpu_render(scene(c["scene"]), c["W"], c["H"], c["depth"], sphere_seed=c["sphere_seed"], prim_masks=2)
+    g = np.load(os.path.join(GOLDEN, key + ".npz"))
+    y0, rows = c["y0"], c["rows"]
+    assert np.array_equal(argb[y0:y0 + rows], g["argb"])
+    assert rgb[y0:y0 + rows].tobytes() == g["rgb"].tobytes()
+    r.close()
+
+
 @pytest.mark.parametrize("n_spheres", [4096, 4600])
 def test_regrouped_large_scene_equals_unregrouped(n_spheres):
     """The bounce kernel's two forms on large scenes: with the BVH staged in LDS (4096 spheres: 2,047 nodes fit) and
@@ -507,7 +520,8 @@ def test_regrouped_large_scene_equals_unregrouped(n_spheres):
         r.close()
 
 
-@pytest.mark.parametrize("key", ["hash_synth16_3840x2160_d8", "hash_default_640x480_d4", "hash_synth16_7680x4320_d8"])
+@pytest.mark.parametrize("key", ["hash_synth16_3840x2160_d8", "hash_default_640x480_d4", "hash_synth16_7680x4320_d8",
+                                 "hash_default_1920x1080_d20_ss4"])
 def test_primary_masks_match_reference_hash(key):
     """Precomputed primary-bundle cull masks (rfx_renderer_set_prim_masks 2: built before the launch, so the
     very first frame uses them): the full frame still hashes to the reference's."""
@@ -519,10 +533,12 @@ def test_primary_masks_match_reference_hash(key):
 
 
 @pytest.mark.parametrize("key", sorted(k for k, c in CASES.items()
-                                       if c["kind"] == "render" and c.get("stored") and c["ss"] == 1
-                                       and not c["additive"] and c["W"] * c["H"] > 1))
+                                       if c["kind"] == "render" and c.get("stored") and c["ss"] >= 1
+                                       and c["W"] * c["H"] > 1))
 def test_primary_masks_on_goldens(key):
-    """Every stored one-sample golden with the masks built before the launch."""
+    """Every stored golden but the block previews with the masks built before every launch: one-sample frames, SSAA
+    frames (masks over each pixel's sample rectangle, shadow masks from every sample's primary hit) and additive
+    frames (the rectangle widened by the jitter; closest-hit masks only)."""
     c = CASES[key]
     rgb, argb, r = run_case(c, prim_masks=2)
     g = np.load(os.path.join(GOLDEN, key + ".npz"))
@@ -531,15 +547,16 @@ def test_primary_masks_on_goldens(key):
     r.close()
 
 
-def test_primary_masks_over_repeated_views():
-    """A still camera over 4 frames (masks built on the second and reused) and a camera that alternates between
-    two views: every frame equals the frame rendered without masks."""
+@pytest.mark.parametrize("ss,additive", [(1, False), (2, False), (1, True), (3, True)])
+def test_primary_masks_over_repeated_views(ss, additive):
+    """A still camera over 4 frames (masks built on the second and reused), one-sample, SSAA and additive (jittered,
+    accumulating) frames: every frame equals the frame rendered without masks."""
     desc = scene("synth16")
-    W, H, depth = 640, 360, 8
+    W, H, depth = (640, 360, 8) if ss == 1 else (320, 184, 8)
     frames = {}
     for mode in (0, 1):
         out = []
-        _, _, r = gpu_render(desc, W, H, depth, frames=4, prim_masks=mode,
+        _, _, r = gpu_render(desc, W, H, depth, ss=ss, additive=additive, frames=4, prim_masks=mode, jitter_seed=99,
                              each_frame=lambda rgb, argb: out.append((rgb.tobytes(), argb.tobytes())))
         r.close()
         frames[mode] = out

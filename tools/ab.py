@@ -60,6 +60,9 @@ VARIANTS = {
     "launderp": ["RFX_LAUNDER_PARAMS"],
     "launder2": ["RFX_LAUNDER_SCENE", "RFX_LAUNDER_PARAMS"],
     "ssaa2": [],  # (built from a newer source than base: the A/B of a source change)
+    "ssaa3": [],
+    "list": [],
+    "listl2": ["RFX_LAUNDER_SCENE", "RFX_LAUNDER_PARAMS"],
 }
 
 
