@@ -445,6 +445,13 @@ extern "C" uint32_t rfx_strip_row_to_y(uint32_t r, uint32_t rb, uint32_t rank, u
 #endif
 constexpr size_t kPrimWords = 5;        // per wave tile, small scenes (rfx_trace.h kPrimStride)
 constexpr size_t kPrimLargeWords = 12;  // per wave tile, large scenes (rfx_trace.h kPrimLargeStride)
+// per-view masks of SSAA frames / chunk lists of large scenes: measured slower, compiled out (rfx_trace.h)
+#ifndef RFX_PRIM_SSAA
+#define RFX_PRIM_SSAA 0
+#endif
+#ifndef RFX_PRIM_LARGE
+#define RFX_PRIM_LARGE 0
+#endif
 #ifndef RFX_BOUNCE_GROUPS_PER_CU
 #define RFX_BOUNCE_GROUPS_PER_CU 14
 #endif
@@ -1375,7 +1382,8 @@ static int trace_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *rd, float
   // primary-bundle cull masks: small scenes, plain and SSAA frames (not block previews), culling launches; large scenes,
   // plain frames: the primary bundles' chunk lists.  Recomputed only when the camera, the frame geometry, the sampling
   // or the scene changed (the bench's frames all reuse one set)
-  if (((small && P.ss >= 1 && !park) || (!small && plain)) && !d_counters && P.grid_rows && r->prim_mode)
+  if (((small && (plain || (RFX_PRIM_SSAA && P.ss >= 1)) && !park) || (RFX_PRIM_LARGE && !small && plain)) &&
+      !d_counters && P.grid_rows && r->prim_mode)
   {
     struct Key { float cam[15]; uint32_t W, H, grid_rows, row0, row_block, rank, nranks; int32_t depth, ss, additive;
                  uint64_t p_begin, p_end, gen; } k;

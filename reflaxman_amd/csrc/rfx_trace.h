@@ -479,6 +479,15 @@ constexpr float kCullRel = 2e-3f;
 // per-view primary masks (prim_cull_kernel): per wave tile, the closest hit's mask and the shadow masks of the
 // first kPrimLights lights
 constexpr int kPrimLights = 4, kPrimStride = 1 + kPrimLights;
+// Per-view masks of SSAA / additive frames (RFX_PRIM_SSAA) and per-view chunk lists of large scenes (RFX_PRIM_LARGE):
+// built, parity-tested and measured slower in round 4 (the screenshot frame +4.3%, C5 +3.3%; interleaved A/B,
+// profiles/r04/ab/), so compiled out by default
+#ifndef RFX_PRIM_SSAA
+#define RFX_PRIM_SSAA 0
+#endif
+#ifndef RFX_PRIM_LARGE
+#define RFX_PRIM_LARGE 0
+#endif
 // Large scenes (prim_cull_large_kernel): per wave tile, the chunk cull of its primary bundle -- [0] the number of kept
 // 64-sphere chunks (at most kPrimLargeChunks; kPrimLargeNone: no list, the tile culls per launch), [1] the triangle mask,
 // [2] the chunk mask (scenes of at most 64 chunks), [4..] the kept chunks' sphere masks in chunk order
@@ -1287,6 +1296,14 @@ __shared__ __attribute__((aligned(16))) uint32_t s_out[kWgWaves][256];
 
 // Scene::trace from a mid-trace state (mulc, pix after `refl` segments); park: see Park.  *parked: this lane's
 // trace was queued and its returned colour is not final.
+// Kernel arguments re-read where they are used (round 4, on by default; RFX_NO_LAUNDER turns it off): the DevScene in
+// every bounce segment of the large-scene kernels, the FrameParams after the bounce loop.  Kept in SGPRs across the loops, they
+// spilled to VGPR lanes (C5 trace kernel: 102 -> 25 SGPR spills, C5 trace + bounce -1.6%; C3: 23 -> 8, -0.3%;
+// interleaved A/B, profiles/r04/ab/).
+#ifndef RFX_NO_LAUNDER
+#define RFX_LAUNDER_SCENE
+#define RFX_LAUNDER_PARAMS
+#endif
 #ifdef RFX_LAUNDER_SCENE
 typedef const __attribute__((address_space(4))) DevScene *ConstScenePtr;
 // The record is read through the kernarg segment pointer: every kernel that reaches trace_from (trace_kernel,
@@ -1307,7 +1324,7 @@ __device__ __forceinline__ const DevScene &launder_scene(const DevScene &S)
 #endif
 // The frame parameters (the kernels' second argument, after the DevScene) read through the kernarg segment pointer, laundered
 // by an empty asm: every use reloads them with scalar loads where it stands, so their values are not held in SGPRs
-// across a bounce loop (the SSAA sample loop; with RFX_LAUNDER_PARAMS also the plain epilogue and park ids)
+// across a bounce loop (with RFX_LAUNDER_PARAMS: the epilogue and the park ids; the RFX_SSAA_LDS_STATE sample loop)
 constexpr size_t kParamsOff = (sizeof(DevScene) + alignof(FrameParams) - 1) / alignof(FrameParams) * alignof(FrameParams);
 __device__ __forceinline__ const FrameParams &kernarg_params()
 {
@@ -1368,7 +1385,7 @@ __device__ __forceinline__ col trace_from(const DevScene &RFX_SCENE_PARAM, v3 or
     else
     {
       // the first segment of a plain trace: the tile's per-view chunk list (prim_cull_large_kernel), when it has one
-      const uint64_t *pl = CULL && seg0 && pm_tile[0] != kPrimLargeNone ? pm_tile : nullptr;
+      const uint64_t *pl = RFX_PRIM_LARGE && CULL && seg0 && pm_tile[0] != kPrimLargeNone ? pm_tile : nullptr;
       Bundle B;
       if constexpr (CULL) B = make_bundle(origin, ray, alive);
       closest_hit<STATS, PLANES>(S, origin, ray, alive, CULL ? &B : nullptr, h, cnt, park.bvh(), pl);
@@ -1838,7 +1855,7 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
       v3 rd = mk(0.0f, 0.0f, 0.0f);
       if (valid) rd = load_rd(P, pr);
       const ParkTile park{P.park_after, P.queue, P.queue_count, P, wv, w8};
-      const uint64_t *pm_tile = CULL && !STATS && P.prim_mask
+      const uint64_t *pm_tile = (SMALL || RFX_PRIM_LARGE) && CULL && !STATS && P.prim_mask
                                     ? P.prim_mask + (size_t)(SMALL ? kPrimStride : kPrimLargeStride) * t8 : nullptr;
       const col c = trace_from<STATS, CULL, MANYL, SMALL, PLANES, PARK>(S, eye, ray, mkc(1.0f, 1.0f, 1.0f),
                                                                   mkc(0.0f, 0.0f, 0.0f), 0, P.depth, rd, lut, cnt,
@@ -1847,10 +1864,12 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
     }
     else
     {
-      // SSAA / additive (Render.cpp:174-194).  The per-lane state that outlives each sample's bounce loop -- the
-      // running sum and the additive jitter -- waits in the wave's epilogue staging slot (s_out: 192 words of sum, 64
-      // of jitter), and the pixel's coordinates are re-derived from the tile index in LDS for every sample, so the
-      // bounce loop runs with the plain kernel's live state (round 4: 22 -> 0 VGPR spills in the small-scene kernel).
+      // SSAA / additive (Render.cpp:174-194): each lane runs its pixel's ss x ss traces in turn
+#ifdef RFX_SSAA_LDS_STATE
+      // Experiment (round 4, off: +3.7% on the screenshot frame, interleaved A/B).  The per-lane state that outlives
+      // each sample's bounce loop -- the running sum and the additive jitter -- waits in the wave's epilogue staging
+      // slot (s_out: 192 words of sum, 64 of jitter), and the pixel's coordinates are re-derived from the tile index in
+      // LDS for every sample, so the bounce loop runs with fewer live values (22 -> 9 VGPR spills, small scenes).
       uint32_t *slot = s_out[wv];
       uint32_t jit = 0;
       if (P.additive && valid)                                                     // Render.cpp:177-178
@@ -1890,7 +1909,8 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
           v3 rd = mk(0.0f, 0.0f, 0.0f);
           if (svalid) rd = load_rd(P, (sp - P.p_begin) * (uint64_t)(ss * ss) + (uint64_t)(sx * ss + sy));
           // the tile's per-view masks cover every sample's primary rays (prim_cull_kernel)
-          const uint64_t *pm = SMALL && CULL && !STATS && P.prim_mask ? P.prim_mask + (size_t)kPrimStride * t8s : nullptr;
+          const uint64_t *pm = RFX_PRIM_SSAA && SMALL && CULL && !STATS && P.prim_mask
+                                   ? P.prim_mask + (size_t)kPrimStride * t8s : nullptr;
           const col c = trace<STATS, CULL, MANYL, SMALL, PLANES>(S, eye, ray, P.depth, rd, lut, cnt, svalid, pm,
                                                                  P.prim_shadow != 0);
           float *f = reinterpret_cast<float *>(slot) + 3 * ls;
@@ -1906,6 +1926,38 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
         if (fabsf(sq) > kVerySmall) fin = mkc(fin.r / sq, fin.g / sq, fin.b / sq);
       }
       out = fin;
+#else
+      float rndx = 0.0f, rndy = 0.0f;
+      if (P.additive && valid)                                                     // Render.cpp:177-178
+      {
+        const uint32_t s1 = lcg_jump(P.jitter_seed, 2 * pr + 1);
+        rndx = (float)lcg_out(s1) / (float)0x7FFF;
+        rndy = (float)lcg_out(lcg_step(s1)) / (float)0x7FFF;
+      }
+      const int ss = P.ss;
+      const float ssf = (float)ss;
+      col fin = mkc(0.0f, 0.0f, 0.0f);
+      for (int sx = 0; sx < ss; ++sx)                                              // Render.cpp:181-187
+        for (int sy = 0; sy < ss; ++sy)
+        {
+          // float(0) / ss == +0 exactly, so the first sample's offsets need no division
+          const float ox = sx ? (float)sx / ssf : 0.0f, oy = sy ? (float)sy / ssf : 0.0f;
+          v3 ray = mk(rx + ox + rndx, ry + oy + rndy, P.rz);
+          ray = mmul(view, ray);
+          v3 rd = mk(0.0f, 0.0f, 0.0f);
+          if (valid) rd = load_rd(P, pr * (uint64_t)(ss * ss) + (uint64_t)(sx * ss + sy));
+          const uint64_t *pm = RFX_PRIM_SSAA && SMALL && CULL && !STATS && P.prim_mask
+                                   ? P.prim_mask + (size_t)kPrimStride * t8 : nullptr;
+          fin = cadd(fin, trace<STATS, CULL, MANYL, SMALL, PLANES>(S, eye, ray, P.depth, rd, lut, cnt, valid, pm,
+                                                                   P.prim_shadow != 0));
+        }
+      if (ss != 1)                                                                 // Render.cpp:189 (x / 1.0f == x)
+      {
+        const float sq = (float)(ss * ss);
+        if (fabsf(sq) > kVerySmall) fin = mkc(fin.r / sq, fin.g / sq, fin.b / sq);
+      }
+      out = fin;
+#endif
     }
     // output coordinates again, from the tile index in LDS (volatile: re-read, not kept live)
 #ifdef RFX_LAUNDER_PARAMS

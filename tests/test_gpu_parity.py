@@ -64,9 +64,8 @@ def test_full_size_hash(key):
 
 def test_c5_full_frames_steady_state():
     """C5 over three frames at the defaults, per-view state included: frame 0 (first view: per-launch bundles, raster
-    tile order), frame 1 (the view repeats: the primary bundles' chunk lists are built, the schedule is sorted from
-    frame 0's costs) hash to the reference's frames 0 and 1; frame 2 equals a frame rendered without regrouping,
-    lists or schedule from the same stream state."""
+    tile order), frame 1 (the view repeats: the schedule is sorted from frame 0's costs) hash to the reference's
+    frames 0 and 1; frame 2 equals a frame rendered without regrouping or schedule from the same stream state."""
     c0, c1 = CASES["hash_stress4096_3840x2160_d12"], CASES["hash_stress4096_3840x2160_d12_f2"]
     got = []
     _, _, r = gpu_render(scene("stress4096"), 3840, 2160, 12, frames=3, sphere_seed=c0["sphere_seed"],
@@ -492,8 +491,8 @@ def test_stress_band_other_regrouping(key, regroup, qsort):
 
 @pytest.mark.parametrize("key", sorted(k for k, c in CASES.items() if c["kind"] == "band" and c["scene"] == "stress4096"))
 def test_stress_band_chunk_lists(key):
-    """C5 with the per-view chunk lists of the primary bundles built before the first frame (prim_masks 2,
-    prim_cull_large_kernel): the reference's bands."""
+    """C5 with prim_masks 2: the per-view chunk lists of the primary bundles (prim_cull_large_kernel) in an
+    RFX_PRIM_LARGE build (compiled out by default, measured slower); either way the reference's bands."""
     c = CASES[key]
     rgb, argb, r = gpu_render(scene(c["scene"]), c["W"], c["H"], c["depth"], sphere_seed=c["sphere_seed"], prim_masks=2)
     g = np.load(os.path.join(GOLDEN, key + ".npz"))
@@ -536,9 +535,9 @@ def test_primary_masks_match_reference_hash(key):
                                        if c["kind"] == "render" and c.get("stored") and c["ss"] >= 1
                                        and c["W"] * c["H"] > 1))
 def test_primary_masks_on_goldens(key):
-    """Every stored golden but the block previews with the masks built before every launch: one-sample frames, SSAA
-    frames (masks over each pixel's sample rectangle, shadow masks from every sample's primary hit) and additive
-    frames (the rectangle widened by the jitter; closest-hit masks only)."""
+    """Every stored golden but the block previews with the masks built before every launch (prim_masks 2): one-sample
+    frames use them; SSAA and additive frames use them only in an RFX_PRIM_SSAA build (compiled out by default, measured
+    slower), so there the test pins that the setting changes nothing."""
     c = CASES[key]
     rgb, argb, r = run_case(c, prim_masks=2)
     g = np.load(os.path.join(GOLDEN, key + ".npz"))
@@ -550,7 +549,8 @@ def test_primary_masks_on_goldens(key):
 @pytest.mark.parametrize("ss,additive", [(1, False), (2, False), (1, True), (3, True)])
 def test_primary_masks_over_repeated_views(ss, additive):
     """A still camera over 4 frames (masks built on the second and reused), one-sample, SSAA and additive (jittered,
-    accumulating) frames: every frame equals the frame rendered without masks."""
+    accumulating) frames: every frame equals the frame rendered without masks (SSAA frames take masks only in an
+    RFX_PRIM_SSAA build)."""
     desc = scene("synth16")
     W, H, depth = (640, 360, 8) if ss == 1 else (320, 184, 8)
     frames = {}

@@ -56,13 +56,12 @@ VARIANTS = {
     "lpt4k": ["RFX_TILE_ORDER_MIN_TILES=4096"],
     "bg16": ["RFX_BOUNCE_GROUPS_PER_CU=16"],
     "bg8": ["RFX_BOUNCE_GROUPS_PER_CU=8"],
-    "launder": ["RFX_LAUNDER_SCENE"],
-    "launderp": ["RFX_LAUNDER_PARAMS"],
-    "launder2": ["RFX_LAUNDER_SCENE", "RFX_LAUNDER_PARAMS"],
-    "ssaa2": [],  # (built from a newer source than base: the A/B of a source change)
-    "ssaa3": [],
-    "list": [],
-    "listl2": ["RFX_LAUNDER_SCENE", "RFX_LAUNDER_PARAMS"],
+    "nolaunder": ["RFX_NO_LAUNDER"],
+    "launderscene": ["RFX_NO_LAUNDER", "RFX_LAUNDER_SCENE"],
+    "launderparams": ["RFX_NO_LAUNDER", "RFX_LAUNDER_PARAMS"],
+    "primssaa": ["RFX_PRIM_SSAA=1"],
+    "primlarge": ["RFX_PRIM_LARGE=1"],
+    "ssaalds": ["RFX_SSAA_LDS_STATE"],
 }
 
 
