@@ -697,6 +697,7 @@ static void launch_mode_cfg(bool stats, int mode, int cfg, dim3 grid, const DevS
     else if (P.park_after > 0) launch_trace_plain_park(cfg, grid, S, P, st);
     else launch_trace_plain_fast(cfg, grid, S, P, st);
   }
+  else if (mode == kModeSsaaLanes) (stats ? launch_trace_lanes_stats : launch_trace_lanes_fast)(cfg, grid, S, P, st);
   else (stats ? launch_trace_ssaa_stats : launch_trace_ssaa_fast)(cfg, grid, S, P, st);
 }
 
@@ -723,8 +724,21 @@ hipError_t launch_kat_powf_cube(uint32_t first, uint32_t n, unsigned long long *
   return hipGetLastError();
 }
 
+// the mode of a trace launch (rfx_trace.h TraceMode)
+static int trace_mode(const FrameParams &P)
+{
+  if (P.ss < 0) return kModeBlock;
+  if (P.ss == 1 && !P.additive && !P.accumulate) return kModePlain;
+  return RFX_SSAA_LANES && ss_lane_block(P.ss) ? kModeSsaaLanes : kModeSsaa;
+}
+
 static dim3 trace_grid(const FrameParams &P)
 {
+  if (trace_mode(P) == kModeSsaaLanes)  // waves of bw x bw pixels (their samples in the lanes), two side by side
+  {
+    const uint32_t bw = ss_lane_block(P.ss);
+    return dim3((P.W + kTileWavesX * bw - 1) / (kTileWavesX * bw), (P.grid_rows + kTileWavesY * bw - 1) / (kTileWavesY * bw));
+  }
   const uint32_t cols = P.ss < 0 ? (P.W + (uint32_t)(-P.ss) - 1) / (uint32_t)(-P.ss) : P.W;
   return dim3((cols + kTileW - 1) / kTileW, (P.grid_rows + kTileH - 1) / kTileH);
 }
@@ -755,7 +769,7 @@ hipError_t launch_trace(const DevScene &S, const FrameParams &P, bool stats, hip
   const dim3 grid = trace_grid(P);
   FrameParams Pt = P;
   Pt.tiles_x = kTileWavesX * grid.x;  // wave tiles per row (the schedule's unit)
-  const int mode = P.ss < 0 ? kModeBlock : (P.ss == 1 && !P.additive && !P.accumulate) ? kModePlain : kModeSsaa;
+  const int mode = trace_mode(P);
   // the stats build counts the reference's every test, so it never culls
   const int cfg = (S.n_light > 32 ? kCfgManyLights : 0) | (stats ? 0 : kCfgCull) |
                   (S.n_sph <= 32 && S.n_tri <= 32 ? kCfgSmall : 0) | (S.n_pln > 0 ? kCfgPlanes : 0);

@@ -1761,7 +1761,14 @@ __device__ __forceinline__ void store_wave_tile(const FrameParams &P, uint32_t x
 // Pixel loop variants of Render::renderNext: block preview (sampleNum < 0), one plain trace per pixel
 // (sampleNum == 1, no jitter, no accumulation -- the benchmark frame), and the general SSAA / additive
 // loop.  The plain variant drops the sample loops and their live state (no spills before the bounce loop).
-enum TraceMode { kModeSsaa = 0, kModeBlock = 1, kModePlain = 2 };
+enum TraceMode { kModeSsaa = 0, kModeBlock = 1, kModePlain = 2, kModeSsaaLanes = 3 };
+// kModeSsaaLanes (sampleNum 2, 4 or 8): one lane per sample -- a wave is a bw x bw block of pixels (ss_lane_block), each
+// pixel's ss x ss samples in consecutive lanes, and the wave sums each pixel's samples in the reference's order
+// afterwards; the other sampleNums run kModeSsaa (one lane per pixel, its samples in turn)
+__host__ __device__ constexpr uint32_t ss_lane_block(int ss) { return ss == 2 ? 4u : ss == 4 ? 2u : ss == 8 ? 1u : 0u; }
+#ifndef RFX_SSAA_LANES
+#define RFX_SSAA_LANES 1
+#endif
 // CFG bits: kCfgCull -- wave-bundle culling (every non-stats launch); kCfgManyLights -- more than 32 lights;
 // kCfgSmall -- at most 32 spheres and 32 triangles (one lane-layout cull mask for the whole scene)
 // kCfgPlanes -- the scene holds planes (Scene::addPlane extension); kCfgPark -- plain pixels park their traces
@@ -1811,7 +1818,60 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
   view.m31 = P.v31; view.m32 = P.v32; view.m33 = P.v33;
   const v3 eye = mk(P.eye_x, P.eye_y, P.eye_z);
 
-  if constexpr (MODE == kModeBlock)
+  if constexpr (MODE == kModeSsaaLanes)
+  {
+    // Render.cpp:174-194 with the sample loops (181-187) across lanes: lane = ss*ss q + (ss sx + sy) of pixel q of the
+    // wave's block -- trace index (pixel - p_begin) ss^2 + ss sx + sy, as the reference draws them
+    const uint32_t ss = (uint32_t)P.ss, ss2 = ss * ss, bw = ss_lane_block(P.ss);
+    const uint32_t q = lane / ss2, kk = lane - q * ss2, sx = kk / ss, sy = kk - sx * ss;
+    const uint32_t lx = (t8 % w8) * bw + q % bw, ly = (t8 / w8) * bw + q / bw;
+    const uint32_t x = lx;
+    const uint32_t y = P.nranks > 1 ? strip_row_to_y(ly, P) : ly + P.row0;
+    const uint64_t p = (uint64_t)y * P.W + x;
+    const bool valid = lx < P.W && ly < P.grid_rows && p >= P.p_begin && p < P.p_end;
+    const uint64_t pr = p - P.p_begin;
+    float rndx = 0.0f, rndy = 0.0f;
+    if (P.additive && valid)                                                       // Render.cpp:177-178
+    {
+      const uint32_t s1 = lcg_jump(P.jitter_seed, 2 * pr + 1);
+      rndx = (float)lcg_out(s1) / (float)0x7FFF;
+      rndy = (float)lcg_out(lcg_step(s1)) / (float)0x7FFF;
+    }
+    const float ssf = (float)(int)ss;
+    // float(0) / ss == +0 exactly, so the first sample's offsets need no division
+    const float ox = sx ? (float)(int)sx / ssf : 0.0f, oy = sy ? (float)(int)sy / ssf : 0.0f;
+    const float rx = (float)x - P.wh, ry = (float)y - P.hh;                       // Render.cpp:152-153
+    const v3 ray = mmul(view, mk(rx + ox + rndx, ry + oy + rndy, P.rz));           // Render.cpp:183-184
+    v3 rd = mk(0.0f, 0.0f, 0.0f);
+    if (valid) rd = load_rd(P, pr * (uint64_t)ss2 + kk);
+    const col c = trace<STATS, CULL, MANYL, SMALL, PLANES>(S, eye, ray, P.depth, rd, lut, cnt, valid);
+#ifdef RFX_LAUNDER_PARAMS
+    const FrameParams &P = kernarg_params();  // shadows the by-value parameter: re-read after the bounce loop
+#endif
+    // the pixel's samples summed in the reference's order (finColor += trace, Render.cpp:181-187) through the wave's
+    // LDS slot, by the pixel's first lane
+    float *sm = reinterpret_cast<float *>(s_out[wv]);
+    sm[3 * lane] = c.r;
+    sm[3 * lane + 1] = c.g;
+    sm[3 * lane + 2] = c.b;
+    __builtin_amdgcn_wave_barrier();
+    if (kk == 0 && valid)
+    {
+      col fin = mkc(0.0f, 0.0f, 0.0f);
+      for (uint32_t j = 0; j < ss2; ++j)
+        fin = cadd(fin, mkc(sm[3 * (lane + j)], sm[3 * (lane + j) + 1], sm[3 * (lane + j) + 2]));
+      const float sq = (float)(int)ss2;                                            // Render.cpp:189
+      if (fabsf(sq) > kVerySmall) fin = mkc(fin.r / sq, fin.g / sq, fin.b / sq);
+      const size_t o = (size_t)(P.nranks > 1 ? ly : y) * P.W + x;
+      float *d = P.img + o * 3;
+      if (P.accumulate) fin = mkc(d[0] + fin.r, d[1] + fin.g, d[2] + fin.b);      // Render.cpp:191-194
+      d[0] = fin.r; d[1] = fin.g; d[2] = fin.b;
+      if (P.argb) P.argb[o] = argb(fin);                                             // Render::copyImage
+    }
+    if (P.tile_cost && __lane_id() == 0) P.tile_cost[t8] = clock32() - s_clk0;
+    RFX_WAVE_T1(t8);
+  }
+  else if constexpr (MODE == kModeBlock)
   {
     // block preview (Render.cpp:158-172): only block corners inside the cursor span are traced;
     // trace order = raster order of corners, so corner (cx, cy) is trace cy * bw + cx.
@@ -2327,6 +2387,8 @@ RFX_DECLARE_TRACE_FAMILY(launch_trace_plain_fast);
 RFX_DECLARE_TRACE_FAMILY(launch_trace_plain_stats);
 RFX_DECLARE_TRACE_FAMILY(launch_trace_ssaa_fast);
 RFX_DECLARE_TRACE_FAMILY(launch_trace_ssaa_stats);
+RFX_DECLARE_TRACE_FAMILY(launch_trace_lanes_fast);
+RFX_DECLARE_TRACE_FAMILY(launch_trace_lanes_stats);
 RFX_DECLARE_TRACE_FAMILY(launch_trace_block_fast);
 RFX_DECLARE_TRACE_FAMILY(launch_trace_block_stats);
 RFX_DECLARE_TRACE_FAMILY(launch_trace_plain_park);

@@ -62,6 +62,7 @@ VARIANTS = {
     "primssaa": ["RFX_PRIM_SSAA=1"],
     "primlarge": ["RFX_PRIM_LARGE=1"],
     "ssaalds": ["RFX_SSAA_LDS_STATE"],
+    "nolanes": ["RFX_SSAA_LANES=0"],
 }
 
 
