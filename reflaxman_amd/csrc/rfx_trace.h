@@ -1845,31 +1845,44 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
     v3 rd = mk(0.0f, 0.0f, 0.0f);
     if (valid) rd = load_rd(P, pr * (uint64_t)ss2 + kk);
     const col c = trace<STATS, CULL, MANYL, SMALL, PLANES>(S, eye, ray, P.depth, rd, lut, cnt, valid);
-#ifdef RFX_LAUNDER_PARAMS
-    const FrameParams &P = kernarg_params();  // shadows the by-value parameter: re-read after the bounce loop
-#endif
-    // the pixel's samples summed in the reference's order (finColor += trace, Render.cpp:181-187) through the wave's
-    // LDS slot, by the pixel's first lane
-    float *sm = reinterpret_cast<float *>(s_out[wv]);
-    sm[3 * lane] = c.r;
-    sm[3 * lane + 1] = c.g;
-    sm[3 * lane + 2] = c.b;
-    __builtin_amdgcn_wave_barrier();
-    if (kk == 0 && valid)
     {
-      col fin = mkc(0.0f, 0.0f, 0.0f);
-      for (uint32_t j = 0; j < ss2; ++j)
-        fin = cadd(fin, mkc(sm[3 * (lane + j)], sm[3 * (lane + j) + 1], sm[3 * (lane + j) + 2]));
-      const float sq = (float)(int)ss2;                                            // Render.cpp:189
-      if (fabsf(sq) > kVerySmall) fin = mkc(fin.r / sq, fin.g / sq, fin.b / sq);
-      const size_t o = (size_t)(P.nranks > 1 ? ly : y) * P.W + x;
-      float *d = P.img + o * 3;
-      if (P.accumulate) fin = mkc(d[0] + fin.r, d[1] + fin.g, d[2] + fin.b);      // Render.cpp:191-194
-      d[0] = fin.r; d[1] = fin.g; d[2] = fin.b;
-      if (P.argb) P.argb[o] = argb(fin);                                             // Render::copyImage
+#ifdef RFX_LAUNDER_PARAMS
+      const FrameParams &P = kernarg_params();  // shadows the by-value parameter: re-read after the bounce loop
+#endif
+      // the lane's pixel again, from the tile index in LDS and a fresh lane id (not kept live across the bounce loop)
+      const uint32_t t8e = ((volatile uint32_t *)s_tile8)[wv];
+      uint32_t le = lane;
+      asm volatile("" : "+v"(le));
+      const uint32_t ss = (uint32_t)P.ss, ss2 = ss * ss, bw = ss_lane_block(P.ss);
+      const uint32_t q = le / ss2, kk = le - q * ss2;
+      const uint32_t lx = (t8e % w8) * bw + q % bw, ly = (t8e / w8) * bw + q / bw;
+      const uint32_t x = lx;
+      const uint32_t y = P.nranks > 1 ? strip_row_to_y(ly, P) : ly + P.row0;
+      const uint64_t p = (uint64_t)y * P.W + x;
+      const bool valid = lx < P.W && ly < P.grid_rows && p >= P.p_begin && p < P.p_end;
+      // the pixel's samples summed in the reference's order (finColor += trace, Render.cpp:181-187) through the wave's
+      // LDS slot, by the pixel's first lane
+      float *sm = reinterpret_cast<float *>(s_out[wv]);
+      sm[3 * le] = c.r;
+      sm[3 * le + 1] = c.g;
+      sm[3 * le + 2] = c.b;
+      __builtin_amdgcn_wave_barrier();
+      if (kk == 0 && valid)
+      {
+        col fin = mkc(0.0f, 0.0f, 0.0f);
+        for (uint32_t j = 0; j < ss2; ++j)
+          fin = cadd(fin, mkc(sm[3 * (le + j)], sm[3 * (le + j) + 1], sm[3 * (le + j) + 2]));
+        const float sq = (float)(int)ss2;                                            // Render.cpp:189
+        if (fabsf(sq) > kVerySmall) fin = mkc(fin.r / sq, fin.g / sq, fin.b / sq);
+        const size_t o = (size_t)(P.nranks > 1 ? ly : y) * P.W + x;
+        float *d = P.img + o * 3;
+        if (P.accumulate) fin = mkc(d[0] + fin.r, d[1] + fin.g, d[2] + fin.b);      // Render.cpp:191-194
+        d[0] = fin.r; d[1] = fin.g; d[2] = fin.b;
+        if (P.argb) P.argb[o] = argb(fin);                                             // Render::copyImage
+      }
+      if (P.tile_cost && __lane_id() == 0) P.tile_cost[t8e] = clock32() - s_clk0;
+      RFX_WAVE_T1(t8e);
     }
-    if (P.tile_cost && __lane_id() == 0) P.tile_cost[t8] = clock32() - s_clk0;
-    RFX_WAVE_T1(t8);
   }
   else if constexpr (MODE == kModeBlock)
   {
