@@ -20,7 +20,7 @@ INCLUDE = os.path.join(ROOT, "include")
 
 # the trace kernel families compile as separate TUs in parallel (one hipcc per source), then link
 SOURCES = ["rfx_kernels.hip", "rfx_host.cpp", "rfx_group.cpp", "rfx_trace_plain_park.hip"] + [
-    f"rfx_trace_{m}_{s}.hip" for m in ("plain", "ssaa", "lanes", "block") for s in ("fast", "stats")]
+    f"rfx_trace_{m}_{s}.hip" for m in ("plain", "ssaa", "lanes", "chunks", "block") for s in ("fast", "stats")]
 HEADERS = ["rfx_math.h", "rfx_powf.h", "rfx_types.h", "rfx_trace.h", "rfx_internal.h"]
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0] or "gfx950"
 

@@ -698,6 +698,7 @@ static void launch_mode_cfg(bool stats, int mode, int cfg, dim3 grid, const DevS
     else launch_trace_plain_fast(cfg, grid, S, P, st);
   }
   else if (mode == kModeSsaaLanes) (stats ? launch_trace_lanes_stats : launch_trace_lanes_fast)(cfg, grid, S, P, st);
+  else if (mode == kModeSsaaChunks) (stats ? launch_trace_chunks_stats : launch_trace_chunks_fast)(cfg, grid, S, P, st);
   else (stats ? launch_trace_ssaa_stats : launch_trace_ssaa_fast)(cfg, grid, S, P, st);
 }
 
@@ -729,13 +730,15 @@ static int trace_mode(const FrameParams &P)
 {
   if (P.ss < 0) return kModeBlock;
   if (P.ss == 1 && !P.additive && !P.accumulate) return kModePlain;
-  return RFX_SSAA_LANES && ss_lane_block(P.ss) ? kModeSsaaLanes : kModeSsaa;
+  if (!RFX_SSAA_LANES || !ss_lane_block(P.ss)) return kModeSsaa;
+  return P.ss > 8 ? kModeSsaaChunks : kModeSsaaLanes;
 }
 
 static dim3 trace_grid(const FrameParams &P)
 {
-  if (trace_mode(P) == kModeSsaaLanes)  // waves of bw x bw pixels (their samples in the lanes), two side by side
-  {
+  const int mode = trace_mode(P);
+  if (mode == kModeSsaaLanes || mode == kModeSsaaChunks)  // waves of bw x bw pixels (their samples in the lanes), two
+  {                                                       // side by side
     const uint32_t bw = ss_lane_block(P.ss);
     return dim3((P.W + kTileWavesX * bw - 1) / (kTileWavesX * bw), (P.grid_rows + kTileWavesY * bw - 1) / (kTileWavesY * bw));
   }

@@ -1326,11 +1326,12 @@ __device__ __forceinline__ const DevScene &launder_scene(const DevScene &S)
 // by an empty asm: every use reloads them with scalar loads where it stands, so their values are not held in SGPRs
 // across a bounce loop (with RFX_LAUNDER_PARAMS: the epilogue and the park ids; the RFX_SSAA_LDS_STATE sample loop)
 constexpr size_t kParamsOff = (sizeof(DevScene) + alignof(FrameParams) - 1) / alignof(FrameParams) * alignof(FrameParams);
+template <bool LAUNDER = true>  // false: the plain kernarg reference, which the compiler may keep in registers
 __device__ __forceinline__ const FrameParams &kernarg_params()
 {
   typedef const __attribute__((address_space(4))) char *KP;
   KP p = (KP)__builtin_amdgcn_kernarg_segment_ptr();
-  asm volatile("" : "+s"(p));
+  if constexpr (LAUNDER) asm volatile("" : "+s"(p));
   return *(const FrameParams *)(const __attribute__((address_space(4))) FrameParams *)(p + kParamsOff);
 }
 
@@ -1761,11 +1762,13 @@ __device__ __forceinline__ void store_wave_tile(const FrameParams &P, uint32_t x
 // Pixel loop variants of Render::renderNext: block preview (sampleNum < 0), one plain trace per pixel
 // (sampleNum == 1, no jitter, no accumulation -- the benchmark frame), and the general SSAA / additive
 // loop.  The plain variant drops the sample loops and their live state (no spills before the bounce loop).
-enum TraceMode { kModeSsaa = 0, kModeBlock = 1, kModePlain = 2, kModeSsaaLanes = 3 };
-// kModeSsaaLanes (sampleNum 2, 4 or 8): one lane per sample -- a wave is a bw x bw block of pixels (ss_lane_block), each
+enum TraceMode { kModeSsaa = 0, kModeBlock = 1, kModePlain = 2, kModeSsaaLanes = 3, kModeSsaaChunks = 4 };
+// kModeSsaaLanes (sampleNum 2, 4, 8): one lane per sample -- a wave is a bw x bw block of pixels (ss_lane_block), each
 // pixel's ss x ss samples in consecutive lanes, and the wave sums each pixel's samples in the reference's order
-// afterwards; the other sampleNums run kModeSsaa (one lane per pixel, its samples in turn)
-__host__ __device__ constexpr uint32_t ss_lane_block(int ss) { return ss == 2 ? 4u : ss == 4 ? 2u : ss == 8 ? 1u : 0u; }
+// afterwards; kModeSsaaChunks (sampleNum > 8): the same with the wave on one pixel, its samples 64 at a time (a separate
+// mode: the chunk loop around the bounce loop costs registers); sampleNum 1 (additive frames), 3, 5, 6, 7 run kModeSsaa
+// (one lane per pixel, its samples in turn)
+__host__ __device__ constexpr uint32_t ss_lane_block(int ss) { return ss == 2 ? 4u : ss == 4 ? 2u : ss >= 8 ? 1u : 0u; }
 #ifndef RFX_SSAA_LANES
 #define RFX_SSAA_LANES 1
 #endif
@@ -1818,70 +1821,99 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
   view.m31 = P.v31; view.m32 = P.v32; view.m33 = P.v33;
   const v3 eye = mk(P.eye_x, P.eye_y, P.eye_z);
 
-  if constexpr (MODE == kModeSsaaLanes)
+  if constexpr (MODE == kModeSsaaLanes || MODE == kModeSsaaChunks)
   {
-    // Render.cpp:174-194 with the sample loops (181-187) across lanes: lane = ss*ss q + (ss sx + sy) of pixel q of the
-    // wave's block -- trace index (pixel - p_begin) ss^2 + ss sx + sy, as the reference draws them
-    const uint32_t ss = (uint32_t)P.ss, ss2 = ss * ss, bw = ss_lane_block(P.ss);
-    const uint32_t q = lane / ss2, kk = lane - q * ss2, sx = kk / ss, sy = kk - sx * ss;
-    const uint32_t lx = (t8 % w8) * bw + q % bw, ly = (t8 / w8) * bw + q / bw;
-    const uint32_t x = lx;
-    const uint32_t y = P.nranks > 1 ? strip_row_to_y(ly, P) : ly + P.row0;
-    const uint64_t p = (uint64_t)y * P.W + x;
-    const bool valid = lx < P.W && ly < P.grid_rows && p >= P.p_begin && p < P.p_end;
-    const uint64_t pr = p - P.p_begin;
-    float rndx = 0.0f, rndy = 0.0f;
-    if (P.additive && valid)                                                       // Render.cpp:177-178
+    // Render.cpp:174-194 with the sample loops (181-187) across lanes.  sampleNum 2 / 4: lane = ss^2 q + (ss sx + sy) of
+    // pixel q of the wave's bw x bw block; sampleNum >= 8: the wave is one pixel, its ss^2 samples taken 64 at a time
+    // (lane = sample - 64 chunk).  Trace index (pixel - p_begin) ss^2 + ss sx + sy, as the reference draws them; the
+    // pixel's samples are summed in the reference's order (finColor += trace) through the wave's LDS slot, chunk by
+    // chunk onto a running sum kept there (s_out words 192-194).
+    constexpr bool CHUNKS = MODE == kModeSsaaChunks;
+    const uint32_t ss = (uint32_t)P.ss, ss2 = ss * ss, bw = CHUNKS ? 1u : ss_lane_block(P.ss);
+    const uint32_t nchunk = CHUNKS ? (ss2 + 63) / 64 : 1;
+    float *sm = reinterpret_cast<float *>(s_out[wv]);
+    for (uint32_t chunk = 0; chunk < nchunk; ++chunk)
     {
-      const uint32_t s1 = lcg_jump(P.jitter_seed, 2 * pr + 1);
-      rndx = (float)lcg_out(s1) / (float)0x7FFF;
-      rndy = (float)lcg_out(lcg_step(s1)) / (float)0x7FFF;
-    }
-    const float ssf = (float)(int)ss;
-    // float(0) / ss == +0 exactly, so the first sample's offsets need no division
-    const float ox = sx ? (float)(int)sx / ssf : 0.0f, oy = sy ? (float)(int)sy / ssf : 0.0f;
-    const float rx = (float)x - P.wh, ry = (float)y - P.hh;                       // Render.cpp:152-153
-    const v3 ray = mmul(view, mk(rx + ox + rndx, ry + oy + rndy, P.rz));           // Render.cpp:183-184
-    v3 rd = mk(0.0f, 0.0f, 0.0f);
-    if (valid) rd = load_rd(P, pr * (uint64_t)ss2 + kk);
-    const col c = trace<STATS, CULL, MANYL, SMALL, PLANES>(S, eye, ray, P.depth, rd, lut, cnt, valid);
-    {
+      // every chunk derives its lanes' state afresh (a laundered lane id and frame parameters), so nothing of it is
+      // hoisted out of the chunk loop and held across the bounce loop
+      uint32_t lane = threadIdx.x & 63u;
+      if constexpr (CHUNKS) asm volatile("" : "+v"(lane));
 #ifdef RFX_LAUNDER_PARAMS
-      const FrameParams &P = kernarg_params();  // shadows the by-value parameter: re-read after the bounce loop
+      const FrameParams &P = kernarg_params<CHUNKS>();
 #endif
-      // the lane's pixel again, from the tile index in LDS and a fresh lane id (not kept live across the bounce loop)
-      const uint32_t t8e = ((volatile uint32_t *)s_tile8)[wv];
-      uint32_t le = lane;
-      asm volatile("" : "+v"(le));
-      const uint32_t ss = (uint32_t)P.ss, ss2 = ss * ss, bw = ss_lane_block(P.ss);
-      const uint32_t q = le / ss2, kk = le - q * ss2;
-      const uint32_t lx = (t8e % w8) * bw + q % bw, ly = (t8e / w8) * bw + q / bw;
+      const uint32_t q = bw == 1 ? 0 : lane / ss2, kk = bw == 1 ? 64 * chunk + lane : lane - q * ss2;
+      const uint32_t sx = kk / ss, sy = kk - sx * ss;
+      const uint32_t lx = (t8 % w8) * bw + q % bw, ly = (t8 / w8) * bw + q / bw;
       const uint32_t x = lx;
       const uint32_t y = P.nranks > 1 ? strip_row_to_y(ly, P) : ly + P.row0;
       const uint64_t p = (uint64_t)y * P.W + x;
-      const bool valid = lx < P.W && ly < P.grid_rows && p >= P.p_begin && p < P.p_end;
-      // the pixel's samples summed in the reference's order (finColor += trace, Render.cpp:181-187) through the wave's
-      // LDS slot, by the pixel's first lane
-      float *sm = reinterpret_cast<float *>(s_out[wv]);
-      sm[3 * le] = c.r;
-      sm[3 * le + 1] = c.g;
-      sm[3 * le + 2] = c.b;
-      __builtin_amdgcn_wave_barrier();
-      if (kk == 0 && valid)
+      const bool valid = lx < P.W && ly < P.grid_rows && p >= P.p_begin && p < P.p_end && kk < ss2;
+      const uint64_t pr = p - P.p_begin;
+      float rndx = 0.0f, rndy = 0.0f;
+      if (P.additive && valid)                                                     // Render.cpp:177-178
       {
-        col fin = mkc(0.0f, 0.0f, 0.0f);
-        for (uint32_t j = 0; j < ss2; ++j)
-          fin = cadd(fin, mkc(sm[3 * (le + j)], sm[3 * (le + j) + 1], sm[3 * (le + j) + 2]));
-        const float sq = (float)(int)ss2;                                            // Render.cpp:189
-        if (fabsf(sq) > kVerySmall) fin = mkc(fin.r / sq, fin.g / sq, fin.b / sq);
-        const size_t o = (size_t)(P.nranks > 1 ? ly : y) * P.W + x;
-        float *d = P.img + o * 3;
-        if (P.accumulate) fin = mkc(d[0] + fin.r, d[1] + fin.g, d[2] + fin.b);      // Render.cpp:191-194
-        d[0] = fin.r; d[1] = fin.g; d[2] = fin.b;
-        if (P.argb) P.argb[o] = argb(fin);                                             // Render::copyImage
+        const uint32_t s1 = lcg_jump(P.jitter_seed, 2 * pr + 1);
+        rndx = (float)lcg_out(s1) / (float)0x7FFF;
+        rndy = (float)lcg_out(lcg_step(s1)) / (float)0x7FFF;
       }
-      if (P.tile_cost && __lane_id() == 0) P.tile_cost[t8e] = clock32() - s_clk0;
-      RFX_WAVE_T1(t8e);
+      const float ssf = (float)(int)ss;
+      // float(0) / ss == +0 exactly, so the first sample's offsets need no division
+      const float ox = sx ? (float)(int)sx / ssf : 0.0f, oy = sy ? (float)(int)sy / ssf : 0.0f;
+      const float rx = (float)x - P.wh, ry = (float)y - P.hh;                     // Render.cpp:152-153
+      const v3 ray = mmul(view, mk(rx + ox + rndx, ry + oy + rndy, P.rz));         // Render.cpp:183-184
+      v3 rd = mk(0.0f, 0.0f, 0.0f);
+      if (valid) rd = load_rd(P, pr * (uint64_t)ss2 + kk);
+      const col c = trace<STATS, CULL, MANYL, SMALL, PLANES>(S, eye, ray, P.depth, rd, lut, cnt, valid);
+      {
+#ifdef RFX_LAUNDER_PARAMS
+        const FrameParams &P = kernarg_params();  // shadows the by-value parameter: re-read after the bounce loop
+#endif
+        // the lane's pixel again, from the tile index in LDS and a fresh lane id (not kept live across the bounce loop)
+        const uint32_t t8e = ((volatile uint32_t *)s_tile8)[wv];
+        uint32_t le = lane;
+        asm volatile("" : "+v"(le));
+        const uint32_t ss = (uint32_t)P.ss, ss2 = ss * ss, bw = CHUNKS ? 1u : ss_lane_block(P.ss);
+        const uint32_t q = bw == 1 ? 0 : le / ss2, kk = bw == 1 ? 64 * chunk + le : le - q * ss2;
+        const uint32_t lx = (t8e % w8) * bw + q % bw, ly = (t8e / w8) * bw + q / bw;
+        const uint32_t x = lx;
+        const uint32_t y = P.nranks > 1 ? strip_row_to_y(ly, P) : ly + P.row0;
+        const uint64_t p = (uint64_t)y * P.W + x;
+        const bool pvalid = lx < P.W && ly < P.grid_rows && p >= P.p_begin && p < P.p_end;
+        sm[3 * le] = c.r;
+        sm[3 * le + 1] = c.g;
+        sm[3 * le + 2] = c.b;
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t first = bw == 1 ? 64 * chunk : 0;  // the pixel's sum starts at its sample 0
+        if (pvalid && (bw == 1 ? le == 0 : kk == 0))
+        {
+          col fin = first ? mkc(sm[192], sm[193], sm[194]) : mkc(0.0f, 0.0f, 0.0f);
+          const uint32_t n = min(ss2 - first, bw == 1 ? 64u : ss2);
+          for (uint32_t j = 0; j < n; ++j)
+            fin = cadd(fin, mkc(sm[3 * (le + j)], sm[3 * (le + j) + 1], sm[3 * (le + j) + 2]));
+          if (first + n < ss2)  // more chunks to come: the running sum waits in LDS
+          {
+            sm[192] = fin.r;
+            sm[193] = fin.g;
+            sm[194] = fin.b;
+          }
+          else
+          {
+            const float sq = (float)(int)ss2;                                      // Render.cpp:189
+            if (fabsf(sq) > kVerySmall) fin = mkc(fin.r / sq, fin.g / sq, fin.b / sq);
+            const size_t o = (size_t)(P.nranks > 1 ? ly : y) * P.W + x;
+            float *d = P.img + o * 3;
+            if (P.accumulate) fin = mkc(d[0] + fin.r, d[1] + fin.g, d[2] + fin.b);  // Render.cpp:191-194
+            d[0] = fin.r; d[1] = fin.g; d[2] = fin.b;
+            if (P.argb) P.argb[o] = argb(fin);                                       // Render::copyImage
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (chunk + 1 == nchunk)
+        {
+          if (P.tile_cost && __lane_id() == 0) P.tile_cost[t8e] = clock32() - s_clk0;
+          RFX_WAVE_T1(t8e);
+        }
+      }
     }
   }
   else if constexpr (MODE == kModeBlock)
@@ -2402,6 +2434,8 @@ RFX_DECLARE_TRACE_FAMILY(launch_trace_ssaa_fast);
 RFX_DECLARE_TRACE_FAMILY(launch_trace_ssaa_stats);
 RFX_DECLARE_TRACE_FAMILY(launch_trace_lanes_fast);
 RFX_DECLARE_TRACE_FAMILY(launch_trace_lanes_stats);
+RFX_DECLARE_TRACE_FAMILY(launch_trace_chunks_fast);
+RFX_DECLARE_TRACE_FAMILY(launch_trace_chunks_stats);
 RFX_DECLARE_TRACE_FAMILY(launch_trace_block_fast);
 RFX_DECLARE_TRACE_FAMILY(launch_trace_block_stats);
 RFX_DECLARE_TRACE_FAMILY(launch_trace_plain_park);

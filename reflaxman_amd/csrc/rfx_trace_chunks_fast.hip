@@ -1,0 +1,12 @@
+// One trace_kernel family of librfx.so: mode kModeSsaaChunks (SSAA frames of sampleNum > 8, one pixel per wave, its
+// samples 64 at a time), render -- its own TU so the families compile in parallel (reflaxman_amd/_build.py).
+#include "rfx_trace.h"
+
+namespace rfx {
+
+void launch_trace_chunks_fast(int cfg, dim3 grid, const DevScene &S, const FrameParams &P, hipStream_t st)
+{
+  launch_cfg<false, kModeSsaaChunks>(cfg, grid, S, P, st);
+}
+
+}  // namespace rfx

@@ -280,6 +280,14 @@ def main():
         save_render("render_default_160x120_d4_ss2", "default", 160, 120, 4, ss=2, use_file=False)
         save_render("render_default_161x121_d4_ssm4", "default", 161, 121, 4, ss=-4, use_file=False)
         save_render("render_default_160x120_d4_ssm3", "default", 160, 120, 4, ss=-3, use_file=False)
+        # SSAA rates of the screenshot menu (Pulse.cpp:24-34) beyond 2x2: the one-lane-per-sample modes (4, 8) and the
+        # 64-samples-per-chunk mode (16, 32), additive jitter among them; 3x3 (the per-pixel sample loop) with planes
+        save_render("render_default_64x40_d8_ss4", "default", 64, 40, 8, ss=4, use_file=False)
+        save_render("render_default_40x24_d6_ss8", "default", 40, 24, 6, ss=8, use_file=False)
+        save_render("render_default_17x9_d8_ss16_add2", "default", 17, 9, 8, ss=16, additive=True, frames=2, jseed=5150,
+                    use_file=False)
+        save_render("render_default_6x5_d4_ss32", "default", 6, 5, 4, ss=32, use_file=False)
+        save_render("render_planes_40x24_d6_ss3", "planes", 40, 24, 6, ss=3)
         # 3. additive progressive refinement (jitter stream explicit), 3 frames
         save_render("render_default_160x120_d15_add3", "default", 160, 120, 15, additive=True, frames=3,
                     jseed=987654321, use_file=False)
