@@ -1,5 +1,5 @@
 # One GPU call: the PMC passes (one counter group per run) of the trace kernel (+ its bounce kernel) at every
-# config bench.py reports -- C1, C2 depth 1 and 4, C3, the C4 frame on one GPU, C5 -- summarised into
+# config bench.py reports -- C1, C2 depth 1 and 4, C3, the C4 frame on one GPU, C5, the screenshot -- summarised into
 # profiles/pmc records keyed by the library's device-code hash.  Records land under gpurun_out/<outdir>/records
 # (copy them into profiles/pmc/ afterwards); with --lines, every config's bench line again so each carries
 # roofline.frac.  Any device-code change invalidates every record: re-run this after the last kernel change.
@@ -25,6 +25,7 @@ run_cfg c1_default_640x480_d4 default 640 480 4 --config c1 --steps 20 --warmup 
 run_cfg c2_default_1920x1080_d1 default 1920 1080 1 --config c2 --depth 1 --steps 10 --warmup 2 || exit $?
 run_cfg c2_default_1920x1080_d4 default 1920 1080 4 --config c2 --steps 10 --warmup 2 || exit $?
 run_cfg c4_synth16_7680x4320_d8 synth16 7680 4320 8 --config c4 --steps 3 --warmup 1 || exit $?
+run_cfg shot_default_1920x1080_d20 default 1920 1080 20 --config shot --steps 3 --warmup 1 || exit $?
 if [ "$2" = "--lines" ]; then
   cp $O/records/*.json $R/profiles/pmc/ || exit 12
   cd $R

@@ -1,6 +1,6 @@
 # One GPU call for a library build: the GPU tests, rocprofv3 kernel stats of the default bench (C3) and of C5, and the
 # PMC records of every config (tools/pmc_configs.sh).  Copy gpurun_out/<outdir>/records/*.json into profiles/pmc/
-# afterwards, then run tools/r03_lines.sh for the bench lines that read them.
+# afterwards, then run tools/lines_round.sh for the bench lines that read them.
 # Usage (repo root, via gpurun): bash tools/round_profile.sh <outdir under gpurun_out>
 R=$PWD
 O=$R/gpurun_out/${1:-round_profile}
