@@ -94,8 +94,10 @@ def test_stress_band(key):
 
 @pytest.mark.parametrize("chunks", [[1], [7, 1000, 13], [4096], [19200 - 1, 1]])
 def test_chunked_render_next(chunks):
-    """Pulse-style chunked renderNext (Pulse.cpp:131-145) gives the reference's image for any chunk pattern."""
-    for key in ("render_default_160x120_d4", "render_default_161x121_d4_ssm4", "render_default_160x120_d15_add3"):
+    """Pulse-style chunked renderNext (Pulse.cpp:131-145) gives the reference's image for any chunk pattern: plain,
+    block-preview and additive frames, and SSAA frames whose spans cut through the lanes modes' pixel blocks."""
+    for key in ("render_default_160x120_d4", "render_default_161x121_d4_ssm4", "render_default_160x120_d15_add3",
+                "render_default_160x120_d4_ss2", "render_default_64x40_d8_ss4", "render_default_17x9_d8_ss16_add2"):
         c = CASES[key]
         rgb, argb, r = run_case(c, chunks=chunks)
         g = np.load(os.path.join(GOLDEN, key + ".npz"))
