@@ -1763,12 +1763,15 @@ __device__ __forceinline__ void store_wave_tile(const FrameParams &P, uint32_t x
 // (sampleNum == 1, no jitter, no accumulation -- the benchmark frame), and the general SSAA / additive
 // loop.  The plain variant drops the sample loops and their live state (no spills before the bounce loop).
 enum TraceMode { kModeSsaa = 0, kModeBlock = 1, kModePlain = 2, kModeSsaaLanes = 3, kModeSsaaChunks = 4 };
-// kModeSsaaLanes (sampleNum 2, 4, 8): one lane per sample -- a wave is a bw x bw block of pixels (ss_lane_block), each
-// pixel's ss x ss samples in consecutive lanes, and the wave sums each pixel's samples in the reference's order
-// afterwards; kModeSsaaChunks (sampleNum > 8): the same with the wave on one pixel, its samples 64 at a time (a separate
-// mode: the chunk loop around the bounce loop costs registers); sampleNum 1 (additive frames), 3, 5, 6, 7 run kModeSsaa
+// kModeSsaaLanes (sampleNum 1 with jitter or accumulation, 2, 4, 8): one lane per sample -- a wave is a bw x bw block of
+// pixels (ss_lane_block), each pixel's ss x ss samples in consecutive lanes, and the wave sums each pixel's samples in the
+// reference's order afterwards; kModeSsaaChunks (sampleNum > 8): the same with the wave on one pixel, its samples 64 at
+// a time (a separate mode: the chunk loop around the bounce loop costs registers); sampleNum 3, 5, 6, 7 run kModeSsaa
 // (one lane per pixel, its samples in turn)
-__host__ __device__ constexpr uint32_t ss_lane_block(int ss) { return ss == 2 ? 4u : ss == 4 ? 2u : ss >= 8 ? 1u : 0u; }
+__host__ __device__ constexpr uint32_t ss_lane_block(int ss)
+{
+  return ss == 1 ? 8u : ss == 2 ? 4u : ss == 4 ? 2u : ss >= 8 ? 1u : 0u;
+}
 #ifndef RFX_SSAA_LANES
 #define RFX_SSAA_LANES 1
 #endif

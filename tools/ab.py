@@ -101,7 +101,7 @@ def build_scene_with(L, desc):
 
 
 class Runner:
-    def __init__(self, name, path, desc, W, H, depth, seed, tile_order=None, regroup=None, prim=None, ss=1):
+    def __init__(self, name, path, desc, W, H, depth, seed, tile_order=None, regroup=None, prim=None, ss=1, additive=0):
         self.name = name
         L = self.L = _lib.bind(path, partial=True)
         self.scene, eye, view, fov = build_scene_with(L, desc)
@@ -125,6 +125,7 @@ class Runner:
         f.view[:] = view
         f.fov = fov
         f.width, f.height, f.reflect_num, f.sample_num, f.nranks = W, H, depth, ss, 1
+        f.additive = additive  # jitter (Render.cpp:177-178); additive_counter 0: no accumulation
         self.frame = f
 
     def render(self, n=1):
@@ -169,7 +170,8 @@ def cmd_build(names):
 
 def cmd_run(args):
     man = json.load(open(os.path.join(ROOT, "tests", "golden", "manifest.json")))["cases"]
-    key = f"hash_{args.scene}_{args.width}x{args.height}_d{args.depth}" + (f"_ss{args.ss}" if args.ss != 1 else "")
+    key = f"hash_{args.scene}_{args.width}x{args.height}_d{args.depth}" + (f"_ss{args.ss}" if args.ss != 1 else "") + \
+        ("_jitter" if args.additive else "")
     desc = scenes.get_scene(args.scene)
     paths = sorted(glob.glob(os.path.join(_build.LIBDIR, "variants", "librfx_*.so")))
     names = [os.path.basename(p)[len("librfx_"):-3] for p in paths]
@@ -180,13 +182,14 @@ def cmd_run(args):
     regroups = [None] if not args.regroup else [int(v) for v in args.regroup.split(",")]
     prims = [None] if not args.prim else [int(v) for v in args.prim.split(",")]
     runners = [Runner(n + ("" if g is None else f"@park{g}") + ("" if q is None else f"@prim{q}"), p, desc, args.width,
-                      args.height, args.depth, 1350490027, regroup=g, prim=q, ss=args.ss)
+                      args.height, args.depth, 1350490027, regroup=g, prim=q, ss=args.ss, additive=args.additive)
                for n, p in zip(names, paths) for g in regroups for q in prims]
     # parity of every variant: frame 1 against the reference's full-frame hash (when the manifest has one), and
     # frame 1 + LATER frames (rendered in the learned longest-tile-first order, after the tile sorts) against
     # the product build rendering the same frames in raster order
     later = max(2, args.later_frame)
-    ref = Runner("raster", _build.LIB, desc, args.width, args.height, args.depth, 1350490027, tile_order=0, ss=args.ss)
+    ref = Runner("raster", _build.LIB, desc, args.width, args.height, args.depth, 1350490027, tile_order=0, ss=args.ss,
+                 additive=args.additive)
     ref_first = ref.frame_hashes(1)
     ref_later = ref.frame_hashes(later - 1)
     ref.close()
@@ -233,6 +236,7 @@ def main():
     ap.add_argument("--height", type=int, default=2160)
     ap.add_argument("--depth", type=int, default=8)
     ap.add_argument("--ss", type=int, default=1, help="samples per pixel ss x ss (SSAA frames)")
+    ap.add_argument("--additive", type=int, default=0, help="1: jittered frames (Render.cpp:177-178)")
     ap.add_argument("--rounds", type=int, default=12)
     ap.add_argument("--frames", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
