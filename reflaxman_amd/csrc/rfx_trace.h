@@ -546,6 +546,59 @@ __device__ __forceinline__ Bundle make_bundle(v3 o, v3 d, bool live)
   return B;
 }
 
+#ifdef RFX_HALF_BUNDLES
+// make_bundle for each half of the wave (lanes 0-31, 32-63): the DPP scan's row_bcast:15 step leaves each half's maximum
+// in its lane 31 / 63.  A half without a live lane gets ok = false (its lanes test nothing).
+__device__ __forceinline__ void make_bundle_halves(v3 o, v3 d, bool live, Bundle (&H)[2])
+{
+  const uint64_t lm = __ballot(live);
+  const bool hi = (threadIdx.x & 63u) >= 32u;
+  float ax[2], ay[2], az[2], cx[2], cy[2], cz[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+  {
+    const uint64_t hm = lm & (h ? 0xFFFFFFFF00000000ull : 0xFFFFFFFFull);
+    const int ref = hm ? __ffsll((long long)hm) - 1 : 0;
+    cx[h] = lane_bcast(o.x, ref); cy[h] = lane_bcast(o.y, ref); cz[h] = lane_bcast(o.z, ref);
+    const float dx = lane_bcast(d.x, ref), dy = lane_bcast(d.y, ref), dz = lane_bcast(d.z, ref);
+    const float inv = __builtin_amdgcn_rsqf(dx * dx + dy * dy + dz * dz);
+    ax[h] = dx * inv; ay[h] = dy * inv; az[h] = dz * inv;
+  }
+  const float ex = o.x - (hi ? cx[1] : cx[0]), ey = o.y - (hi ? cy[1] : cy[0]), ez = o.z - (hi ? cz[1] : cz[0]);
+  const float e2 = ex * ex + ey * ey + ez * ez;
+  const float cosl = (d.x * (hi ? ax[1] : ax[0]) + d.y * (hi ? ay[1] : ay[0]) + d.z * (hi ? az[1] : az[0])) *
+                     __builtin_amdgcn_rsqf(d.x * d.x + d.y * d.y + d.z * d.z);
+  const float dev = 1.0f - cosl;
+  const bool bad = live && !(e2 <= 1.0e30f && dev >= -0.5f && dev <= 2.5f);
+  const uint64_t badm = __ballot(bad);
+  const auto half_max = [](float v, float &lo, float &hi_) {
+    uint32_t u = __float_as_uint(v);
+    u = max(u, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x111, 0xf, 0xf, false));  // row_shr:1
+    u = max(u, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x112, 0xf, 0xf, false));  // row_shr:2
+    u = max(u, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x114, 0xf, 0xf, false));  // row_shr:4
+    u = max(u, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x118, 0xf, 0xf, false));  // row_shr:8
+    u = max(u, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)u, 0x142, 0xa, 0xf, false));  // row_bcast:15
+    lo = __int_as_float(__builtin_amdgcn_readlane((int)u, 31));
+    hi_ = __int_as_float(__builtin_amdgcn_readlane((int)u, 63));
+  };
+  float e2m[2], devm[2];
+  half_max(live ? e2 : 0.0f, e2m[0], e2m[1]);
+  half_max(live ? fmaxf(dev, 0.0f) : 0.0f, devm[0], devm[1]);
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+  {
+    Bundle &B = H[h];
+    B.cx = cx[h]; B.cy = cy[h]; B.cz = cz[h];
+    B.ax = ax[h]; B.ay = ay[h]; B.az = az[h];
+    B.rw = __builtin_amdgcn_sqrtf(e2m[h]) * 1.0001f;
+    B.cosa = 1.0f - devm[h] - 4e-6f;                                             // approximate cosines: widen
+    B.sina = __builtin_amdgcn_sqrtf(fmaxf(1.0f - B.cosa * B.cosa, 0.0f) + 1e-7f) * 1.001f;
+    const uint64_t hm = h ? 0xFFFFFFFF00000000ull : 0xFFFFFFFFull;
+    B.ok = (lm & hm) != 0 && (badm & hm) == 0 && B.cosa > 0.1f && B.rw <= 1.0e15f;
+  }
+}
+#endif
+
 // Bundle of every ray (o, d + rd R) with |rd| <= 1 of the `live` lanes (the shadow rays toward a light of radius R
 // for any randDir, Scene.cpp:128-129): make_bundle's cone widened per lane by the angular radius asin(R / |d|) of
 // the direction ball, cos(alpha + beta) = cos a cos b - sin a sin b.  A lane whose ball reaches its own origin's
@@ -1377,6 +1430,15 @@ __device__ __forceinline__ col trace_from(const DevScene &RFX_SCENE_PARAM, v3 or
         {
           const Bundle B = make_bundle(origin, ray, alive);
           if (B.ok) om = cull_small(T.cull(), S.cull_valid, B);
+#ifdef RFX_HALF_BUNDLES
+          else  // too wide for one cone: a cone per half wave, and the objects either half may hit
+          {
+            Bundle H[2];
+            make_bundle_halves(origin, ray, alive, H);
+            om = (H[0].ok ? cull_small(T.cull(), S.cull_valid, H[0]) : S.cull_valid) |
+                 (H[1].ok ? cull_small(T.cull(), S.cull_valid, H[1]) : S.cull_valid);
+          }
+#endif
           RFX_CULL_STAT(0, B.ok, __ballot(alive), om, S.cull_valid);
         }
       }

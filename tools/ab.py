@@ -63,6 +63,7 @@ VARIANTS = {
     "primlarge": ["RFX_PRIM_LARGE=1"],
     "ssaalds": ["RFX_SSAA_LDS_STATE"],
     "nolanes": ["RFX_SSAA_LANES=0"],
+    "halves": ["RFX_HALF_BUNDLES"],
 }
 
 
