@@ -775,7 +775,8 @@ hipError_t launch_trace(const DevScene &S, const FrameParams &P, bool stats, hip
   const int mode = trace_mode(P);
   // the stats build counts the reference's every test, so it never culls
   const int cfg = (S.n_light > 32 ? kCfgManyLights : 0) | (stats ? 0 : kCfgCull) |
-                  (S.n_sph <= 32 && S.n_tri <= 32 ? kCfgSmall : 0) | (S.n_pln > 0 ? kCfgPlanes : 0);
+                  (S.n_sph <= 32 && S.n_tri <= 32 ? kCfgSmall : 0) | (S.n_pln > 0 ? kCfgPlanes : 0) |
+                  (S.n_light == 1 && !stats && RFX_ONE_LIGHT ? kCfgOneLight : 0);
   launch_mode_cfg(stats, mode, cfg, grid, S, Pt, st);
   return hipGetLastError();
 }

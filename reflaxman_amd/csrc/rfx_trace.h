@@ -1388,7 +1388,7 @@ __device__ __forceinline__ const FrameParams &kernarg_params()
   return *(const FrameParams *)(const __attribute__((address_space(4))) FrameParams *)(p + kParamsOff);
 }
 
-template <bool STATS, bool CULL, bool MANYL, bool SMALL, bool PLANES, bool PARK, class PK>
+template <bool STATS, bool CULL, bool MANYL, bool SMALL, bool PLANES, bool PARK, class PK, bool ONEL = false>
 __device__ __forceinline__ col trace_from(const DevScene &RFX_SCENE_PARAM, v3 origin, v3 ray, col mulc, col pix, int refl,
                                           int depth, v3 rd, const float *lut, Cnt &cnt, bool valid, const PK &park,
                                           bool &parked, const uint64_t *pm_tile = nullptr, bool pm_shadow = true)
@@ -1491,7 +1491,7 @@ __device__ __forceinline__ col trace_from(const DevScene &RFX_SCENE_PARAM, v3 or
     {
       RFX_PROF_BEGIN(P_SHADOW);
       uint32_t lit = 0;
-      const int nl = min(32, S.n_light - base);
+      const int nl = ONEL ? 1 : min(32, S.n_light - base);  // ONEL: the scene has exactly one light
       for (int q = 0; q < nl; ++q)
       {
         const LightRec L = S.lights[base + q];
@@ -1682,12 +1682,12 @@ __device__ __forceinline__ col trace_from(const DevScene &RFX_SCENE_PARAM, v3 or
 #endif
 }
 
-template <bool STATS, bool CULL, bool MANYL, bool SMALL, bool PLANES>
+template <bool STATS, bool CULL, bool MANYL, bool SMALL, bool PLANES, bool ONEL = false>
 __device__ __forceinline__ col trace(const DevScene &S, v3 origin, v3 ray, int depth, v3 rd, const float *lut,
                                      Cnt &cnt, bool valid, const uint64_t *pm_tile = nullptr, bool pm_shadow = true)
 {
   bool parked;
-  return trace_from<STATS, CULL, MANYL, SMALL, PLANES, false>(S, origin, ray, mkc(1.0f, 1.0f, 1.0f), mkc(0.0f, 0.0f, 0.0f), 0,
+  return trace_from<STATS, CULL, MANYL, SMALL, PLANES, false, Park, ONEL>(S, origin, ray, mkc(1.0f, 1.0f, 1.0f), mkc(0.0f, 0.0f, 0.0f), 0,
                                                        depth, rd, lut, cnt, valid, Park{0, nullptr, nullptr, 0, 0},
                                                        parked, pm_tile, pm_shadow);
 }
@@ -1841,7 +1841,10 @@ __host__ __device__ constexpr uint32_t ss_lane_block(int ss)
 // kCfgSmall -- at most 32 spheres and 32 triangles (one lane-layout cull mask for the whole scene)
 // kCfgPlanes -- the scene holds planes (Scene::addPlane extension); kCfgPark -- plain pixels park their traces
 // for the bounce kernel (ray regrouping; rfx_trace_plain_park.hip)
-constexpr int kCfgCull = 1, kCfgManyLights = 2, kCfgSmall = 4, kCfgPlanes = 8, kCfgPark = 16;
+constexpr int kCfgCull = 1, kCfgManyLights = 2, kCfgSmall = 4, kCfgPlanes = 8, kCfgPark = 16, kCfgOneLight = 32;
+#ifndef RFX_ONE_LIGHT
+#define RFX_ONE_LIGHT 1
+#endif
 
 // one workgroup = kTileW x kTileH output pixels (block mode: block corners), one wave = an 8x8 tile (ray coherence).
 // Every lane of a wave reaches trace() -- lanes outside the frame or the cursor span as invalid -- so the
@@ -1851,6 +1854,7 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
 {
   constexpr bool CULL = (CFG & kCfgCull) != 0, MANYL = (CFG & kCfgManyLights) != 0, SMALL = (CFG & kCfgSmall) != 0;
   constexpr bool PLANES = (CFG & kCfgPlanes) != 0, PARK = MODE == kModePlain && !STATS && (CFG & kCfgPark) != 0;
+  constexpr bool ONEL = (CFG & kCfgOneLight) != 0;  // exactly one light: the light loops unrolled
   RFX_WAVE_T0();
   __shared__ float lut[256];
   for (uint32_t i = threadIdx.x; i < 256; i += kWgThreads) lut[i] = (float)i / 255.0f;  // Color.cpp:11-13
@@ -1928,7 +1932,7 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
       const v3 ray = mmul(view, mk(rx + ox + rndx, ry + oy + rndy, P.rz));         // Render.cpp:183-184
       v3 rd = mk(0.0f, 0.0f, 0.0f);
       if (valid) rd = load_rd(P, pr * (uint64_t)ss2 + kk);
-      const col c = trace<STATS, CULL, MANYL, SMALL, PLANES>(S, eye, ray, P.depth, rd, lut, cnt, valid);
+      const col c = trace<STATS, CULL, MANYL, SMALL, PLANES, ONEL>(S, eye, ray, P.depth, rd, lut, cnt, valid);
       {
 #ifdef RFX_LAUNDER_PARAMS
         const FrameParams &P = kernarg_params();  // shadows the by-value parameter: re-read after the bounce loop
@@ -1994,7 +1998,7 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
     const v3 ray = mmul(view, mk((float)x - P.wh, (float)y - P.hh, P.rz));
     v3 rd = mk(0.0f, 0.0f, 0.0f);
     if (valid) rd = load_rd(P, (uint64_t)cy * bw + cx - P.trace_base);
-    const col c = trace<STATS, CULL, MANYL, SMALL, PLANES>(S, eye, ray, P.depth, rd, lut, cnt, valid);
+    const col c = trace<STATS, CULL, MANYL, SMALL, PLANES, ONEL>(S, eye, ray, P.depth, rd, lut, cnt, valid);
     if (valid)
     {
       const uint32_t ex = min(P.W, x + n), ey = min(P.H, y + n);
@@ -2027,7 +2031,7 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
       const ParkTile park{P.park_after, P.queue, P.queue_count, P, wv, w8};
       const uint64_t *pm_tile = (SMALL || RFX_PRIM_LARGE) && CULL && !STATS && P.prim_mask
                                     ? P.prim_mask + (size_t)(SMALL ? kPrimStride : kPrimLargeStride) * t8 : nullptr;
-      const col c = trace_from<STATS, CULL, MANYL, SMALL, PLANES, PARK>(S, eye, ray, mkc(1.0f, 1.0f, 1.0f),
+      const col c = trace_from<STATS, CULL, MANYL, SMALL, PLANES, PARK, ParkTile, ONEL>(S, eye, ray, mkc(1.0f, 1.0f, 1.0f),
                                                                   mkc(0.0f, 0.0f, 0.0f), 0, P.depth, rd, lut, cnt,
                                                                   valid, park, parked, pm_tile);
       out = cadd(mkc(0.0f, 0.0f, 0.0f), c);                                      // Render.cpp:185 (/ 1.0f exact)
@@ -2469,6 +2473,17 @@ inline void launch_one(dim3 grid, const DevScene &S, const FrameParams &P, hipSt
 template <bool STATS, int MODE>
 inline void launch_cfg(int cfg, dim3 grid, const DevScene &S, const FrameParams &P, hipStream_t st)
 {
+  if (cfg & kCfgOneLight)  // scenes with exactly one light: the culling configurations have unrolled light loops
+  {
+    switch (cfg & ~kCfgOneLight)
+    {
+      case 1: launch_one<STATS, MODE, 1 | kCfgOneLight>(grid, S, P, st); return;
+      case 5: launch_one<STATS, MODE, 5 | kCfgOneLight>(grid, S, P, st); return;
+      case 9: launch_one<STATS, MODE, 9 | kCfgOneLight>(grid, S, P, st); return;
+      case 13: launch_one<STATS, MODE, 13 | kCfgOneLight>(grid, S, P, st); return;
+      default: cfg &= ~kCfgOneLight;
+    }
+  }
   switch (cfg)
   {
     case 0: launch_one<STATS, MODE, 0>(grid, S, P, st); break;

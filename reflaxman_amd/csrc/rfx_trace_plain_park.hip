@@ -19,6 +19,8 @@ void launch_trace_plain_park(int cfg, dim3 grid, const DevScene &S, const FrameP
 {
   switch (cfg & ~kCfgPark)
   {
+    case 1 | kCfgOneLight: launch_park_one<1 | kCfgOneLight>(grid, S, P, st); break;
+    case 5 | kCfgOneLight: launch_park_one<5 | kCfgOneLight>(grid, S, P, st); break;
     case 1: launch_park_one<1>(grid, S, P, st); break;
     case 3: launch_park_one<3>(grid, S, P, st); break;
     case 5: launch_park_one<5>(grid, S, P, st); break;
@@ -27,7 +29,9 @@ void launch_trace_plain_park(int cfg, dim3 grid, const DevScene &S, const FrameP
     case 11: launch_park_one<11>(grid, S, P, st); break;
     case 13: launch_park_one<13>(grid, S, P, st); break;
     case 15: launch_park_one<15>(grid, S, P, st); break;
-    default: break;
+    default:  // one light, other configurations: the general kernels
+      if (cfg & kCfgOneLight) launch_trace_plain_park(cfg & ~kCfgOneLight, grid, S, P, st);
+      break;
   }
 }
 

@@ -64,6 +64,7 @@ VARIANTS = {
     "ssaalds": ["RFX_SSAA_LDS_STATE"],
     "nolanes": ["RFX_SSAA_LANES=0"],
     "halves": ["RFX_HALF_BUNDLES"],
+    "nolight1": ["RFX_ONE_LIGHT=0"],
 }
 
 
