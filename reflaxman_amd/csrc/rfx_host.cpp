@@ -1433,7 +1433,8 @@ static int trace_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *rd, float
     // per CU: 7 waves per SIMD); a lane whose trace ends takes the next entry, so no wave waits for a slot
     const uint64_t waves = (pl.traces + 63) / 64;
     const uint32_t groups = (uint32_t)std::min<uint64_t>((waves + 1) / 2, (uint64_t)r->cus * RFX_BOUNCE_GROUPS_PER_CU);
-    const int cfg = 1 | (r->dev.n_light > 32 ? 2 : 0) | (small ? 4 : 0) | (r->dev.n_pln ? 8 : 0);  // rfx_trace.h kCfg*
+    const int cfg = 1 | (r->dev.n_light > 32 ? 2 : 0) | (small ? 4 : 0) | (r->dev.n_pln ? 8 : 0) |  // rfx_trace.h kCfg*
+                    (r->dev.n_light == 1 ? 32 : 0);  // kCfgOneLight (rfx_trace_plain_park.hip: else the general form)
     if (sort_queue) HIP_CHECK(launch_queue_sort(r->d_qctr, r->d_qkey, r->d_qctr + 2, r->d_qorder, st));
     // a BVH whose nodes fit the workgroup's LDS (56 B each beside the stacks: up to ~2,100 nodes, i.e. 4,200 spheres):
     // the LDS-staged bounce kernel, one 16-wave workgroup per CU (C5 trace + bounce -4..6%, tools/ab.py); else the

@@ -2413,8 +2413,8 @@ __global__ RFX_TRACE_BOUNDS void bounce_kernel(DevScene S, FrameParams P)
   rf.refill(alive, origin, ray, mulc, pix, refl, rd);  // the wave's first 64 traces
   RFX_WAVE_T0();
   bool parked;
-  (void)trace_from<false, CULL, MANYL, SMALL, PLANES, false>(S, origin, ray, mulc, pix, refl, P.depth, rd, lut, cnt, alive,
-                                                             rf, parked);
+  (void)trace_from<false, CULL, MANYL, SMALL, PLANES, false, decltype(rf), (CFG & kCfgOneLight) != 0>(
+      S, origin, ray, mulc, pix, refl, P.depth, rd, lut, cnt, alive, rf, parked);
   RFX_WAVE_T1(kBounceTimeBase + kWgWaves * blockIdx.x + wv);
 }
 
@@ -2458,8 +2458,8 @@ void bounce_kernel_lds(DevScene S, FrameParams P)
   int refl = 0;
   rf.refill(alive, origin, ray, mulc, pix, refl, rd);
   bool parked;
-  (void)trace_from<false, CULL, MANYL, SMALL, PLANES, false>(S, origin, ray, mulc, pix, refl, P.depth, rd, lut, cnt, alive,
-                                                             rf, parked);
+  (void)trace_from<false, CULL, MANYL, SMALL, PLANES, false, decltype(rf), (CFG & kCfgOneLight) != 0>(
+      S, origin, ray, mulc, pix, refl, P.depth, rd, lut, cnt, alive, rf, parked);
 }
 
 // ------------------------------------------------------------- launch of one family (the rfx_trace_*.hip TUs)

@@ -67,11 +67,14 @@ hipError_t launch_bounce_lds(int cfg, uint32_t groups, const DevScene &S, const 
 {
   switch (cfg)
   {
+    case 1 | kCfgOneLight: return launch_bounce_lds_one<1 | kCfgOneLight>(groups, S, P, st);
+    case 9 | kCfgOneLight: return launch_bounce_lds_one<9 | kCfgOneLight>(groups, S, P, st);
     case 1: return launch_bounce_lds_one<1>(groups, S, P, st);
     case 3: return launch_bounce_lds_one<3>(groups, S, P, st);
     case 9: return launch_bounce_lds_one<9>(groups, S, P, st);
     case 11: return launch_bounce_lds_one<11>(groups, S, P, st);
-    default: return hipErrorInvalidValue;
+    default:  // one light, other configurations: the general kernels
+      return (cfg & kCfgOneLight) ? launch_bounce_lds(cfg & ~kCfgOneLight, groups, S, P, st) : hipErrorInvalidValue;
   }
 }
 
@@ -79,6 +82,8 @@ void launch_bounce(int cfg, dim3 grid, const DevScene &S, const FrameParams &P, 
 {
   switch (cfg)
   {
+    case 1 | kCfgOneLight: launch_bounce_one<1 | kCfgOneLight>(grid, S, P, st); break;
+    case 5 | kCfgOneLight: launch_bounce_one<5 | kCfgOneLight>(grid, S, P, st); break;
     case 1: launch_bounce_one<1>(grid, S, P, st); break;
     case 3: launch_bounce_one<3>(grid, S, P, st); break;
     case 5: launch_bounce_one<5>(grid, S, P, st); break;
@@ -87,7 +92,9 @@ void launch_bounce(int cfg, dim3 grid, const DevScene &S, const FrameParams &P, 
     case 11: launch_bounce_one<11>(grid, S, P, st); break;
     case 13: launch_bounce_one<13>(grid, S, P, st); break;
     case 15: launch_bounce_one<15>(grid, S, P, st); break;
-    default: break;
+    default:  // one light, other configurations: the general kernels
+      if (cfg & kCfgOneLight) launch_bounce(cfg & ~kCfgOneLight, grid, S, P, st);
+      break;
   }
 }
 
