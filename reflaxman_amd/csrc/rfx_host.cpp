@@ -41,6 +41,7 @@ hipError_t launch_trace(const DevScene &S, const FrameParams &P, bool stats, hip
 hipError_t launch_prim_cull(const DevScene &S, const FrameParams &P, uint64_t *masks, hipStream_t st);
 hipError_t launch_queue_sort(const uint32_t *count, const uint32_t *key, uint32_t *hist, uint32_t *order, hipStream_t st);
 uint32_t trace_tiles(const FrameParams &P);
+bool trace_lanes(const FrameParams &P);
 size_t tile_order_scratch();
 hipError_t launch_tile_order(const uint32_t *cost, uint32_t n, uint32_t *order, uint32_t *scratch, hipStream_t st);
 void launch_bounce(int cfg, dim3 grid, const DevScene &S, const FrameParams &P, hipStream_t st);
@@ -448,6 +449,9 @@ constexpr size_t kPrimLargeWords = 12;  // per wave tile, large scenes (rfx_trac
 // per-view masks of SSAA frames / chunk lists of large scenes: measured slower, compiled out (rfx_trace.h)
 #ifndef RFX_PRIM_SSAA
 #define RFX_PRIM_SSAA 0
+#endif
+#ifndef RFX_PRIM_LANES
+#define RFX_PRIM_LANES 1  // masks of kModeSsaaLanes frames (the lanes' own small pixel blocks)
 #endif
 #ifndef RFX_PRIM_LARGE
 #define RFX_PRIM_LARGE 0
@@ -1382,7 +1386,8 @@ static int trace_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *rd, float
   // primary-bundle cull masks: small scenes, plain and SSAA frames (not block previews), culling launches; large scenes,
   // plain frames: the primary bundles' chunk lists.  Recomputed only when the camera, the frame geometry, the sampling
   // or the scene changed (the bench's frames all reuse one set)
-  if (((small && (plain || (RFX_PRIM_SSAA && P.ss >= 1)) && !park) || (RFX_PRIM_LARGE && !small && plain)) &&
+  if (((small && (plain || (RFX_PRIM_LANES && trace_lanes(P)) || (RFX_PRIM_SSAA && P.ss >= 1)) && !park) ||
+       (RFX_PRIM_LARGE && !small && plain)) &&
       !d_counters && P.grid_rows && r->prim_mode)
   {
     struct Key { float cam[15]; uint32_t W, H, grid_rows, row0, row_block, rank, nranks; int32_t depth, ss, additive;

@@ -753,6 +753,12 @@ uint32_t trace_tiles(const FrameParams &P)
   return kWgWaves * g.x * g.y;
 }
 
+// the frame runs kModeSsaaLanes (its per-view masks are prim_cull_kernel<., true>'s)
+bool trace_lanes(const FrameParams &P)
+{
+  return trace_mode(P) == kModeSsaaLanes;
+}
+
 // the per-view masks of a small scene's plain or SSAA frame (prim_cull_kernel, kPrimStride words per wave tile), or
 // a large scene's chunk lists (prim_cull_large_kernel, kPrimLargeStride words)
 hipError_t launch_prim_cull(const DevScene &S, const FrameParams &P, uint64_t *masks, hipStream_t st)
@@ -760,6 +766,13 @@ hipError_t launch_prim_cull(const DevScene &S, const FrameParams &P, uint64_t *m
   const dim3 grid = trace_grid(P);
   if (!(S.n_sph <= 32 && S.n_tri <= 32))  // large scenes: the primary bundles' chunk lists
     hipLaunchKernelGGL(prim_cull_large_kernel<0>, grid, dim3(kWgThreads), 0, st, S, P, masks);
+  else if (trace_lanes(P))
+  {
+    if (S.n_pln > 0)
+      hipLaunchKernelGGL((prim_cull_kernel<true, true>), grid, dim3(kWgThreads), 0, st, S, P, masks);
+    else
+      hipLaunchKernelGGL((prim_cull_kernel<false, true>), grid, dim3(kWgThreads), 0, st, S, P, masks);
+  }
   else if (S.n_pln > 0)
     hipLaunchKernelGGL(prim_cull_kernel<true>, grid, dim3(kWgThreads), 0, st, S, P, masks);
   else

@@ -485,6 +485,10 @@ constexpr int kPrimLights = 4, kPrimStride = 1 + kPrimLights;
 #ifndef RFX_PRIM_SSAA
 #define RFX_PRIM_SSAA 0
 #endif
+// per-view masks of kModeSsaaLanes frames (sampleNum 1 jittered, 2, 4, 8: the wave's own bw x bw pixels)
+#ifndef RFX_PRIM_LANES
+#define RFX_PRIM_LANES 1
+#endif
 #ifndef RFX_PRIM_LARGE
 #define RFX_PRIM_LARGE 0
 #endif
@@ -1932,7 +1936,11 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
       const v3 ray = mmul(view, mk(rx + ox + rndx, ry + oy + rndy, P.rz));         // Render.cpp:183-184
       v3 rd = mk(0.0f, 0.0f, 0.0f);
       if (valid) rd = load_rd(P, pr * (uint64_t)ss2 + kk);
-      const col c = trace<STATS, CULL, MANYL, SMALL, PLANES, ONEL>(S, eye, ray, P.depth, rd, lut, cnt, valid);
+      // the tile's per-view masks (prim_cull_kernel<., true>), not for the chunk loop
+      const uint64_t *pm = RFX_PRIM_LANES && !CHUNKS && SMALL && CULL && !STATS && P.prim_mask
+                               ? P.prim_mask + (size_t)kPrimStride * t8 : nullptr;
+      const col c = trace<STATS, CULL, MANYL, SMALL, PLANES, ONEL>(S, eye, ray, P.depth, rd, lut, cnt, valid, pm,
+                                                                  P.prim_shadow != 0);
       {
 #ifdef RFX_LAUNDER_PARAMS
         const FrameParams &P = kernarg_params();  // shadows the by-value parameter: re-read after the bounce loop
@@ -2175,7 +2183,10 @@ __global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
 // test, which the trace kernel could not afford per segment -- then the primary hits with the same closest-hit
 // code and that mask, and per light the bundle of all shadow rays of the facing lanes (make_bundle_ball).  The
 // masks depend only on the view (camera, frame geometry, scene), so the host builds them once per view.
-template <bool PLANES>
+// LANES: the tiles of a kModeSsaaLanes frame (sampleNum 1 jittered, 2, 4, 8): wave t8 covers bw x bw pixels, one sample
+// per lane, exactly as trace_kernel's lanes branch maps them; its masks cover the lanes' own rays (jittered: each lane's
+// unit jitter square), so the shadow masks need one primary hit per lane.
+template <bool PLANES, bool LANES = false>
 __global__ RFX_TRACE_BOUNDS void prim_cull_kernel(DevScene S, FrameParams P, uint64_t *masks)
 {
   stage_small_scene(S);
@@ -2185,11 +2196,30 @@ __global__ RFX_TRACE_BOUNDS void prim_cull_kernel(DevScene S, FrameParams P, uin
   const uint32_t wv = __builtin_amdgcn_readfirstlane(wave);
   const uint32_t w8 = kTileWavesX * gridDim.x;
   const uint32_t t8 = (blockIdx.y * kTileWavesY + wv / kTileWavesX) * w8 + blockIdx.x * kTileWavesX + wv % kTileWavesX;
-  const uint32_t gx = (t8 % w8) * 8u + (lane & 7u), gy = (t8 / w8) * 8u + (lane >> 3);
+  uint32_t gx, gy, kk = 0;
+  float lox = 0.0f, loy = 0.0f;  // LANES: the lane's sample offsets (Render.cpp:183), as trace_kernel forms them
+  if constexpr (LANES)
+  {
+    const uint32_t ss = (uint32_t)P.ss, ss2 = ss * ss, bw = ss_lane_block(P.ss);
+    const uint32_t q = bw == 1 ? 0 : lane / ss2;
+    kk = bw == 1 ? lane : lane - q * ss2;
+    const uint32_t sx = kk / ss, sy = kk - sx * ss;
+    gx = (t8 % w8) * bw + q % bw;
+    gy = (t8 / w8) * bw + q / bw;
+    const float ssf = (float)(int)ss;
+    lox = sx ? (float)(int)sx / ssf : 0.0f;
+    loy = sy ? (float)(int)sy / ssf : 0.0f;
+  }
+  else
+  {
+    gx = (t8 % w8) * 8u + (lane & 7u);
+    gy = (t8 / w8) * 8u + (lane >> 3);
+  }
   const uint32_t x = gx;
   const uint32_t y = P.nranks > 1 ? strip_row_to_y(gy, P) : gy + P.row0;
   const uint64_t p = (uint64_t)y * P.W + x;
-  const bool valid = gx < P.W && gy < P.grid_rows && p >= P.p_begin && p < P.p_end && P.depth > 0;
+  const bool valid = gx < P.W && gy < P.grid_rows && p >= P.p_begin && p < P.p_end && P.depth > 0 &&
+                     (!LANES || kk < (uint32_t)(P.ss * P.ss));
   m33 view;
   view.m11 = P.v11; view.m12 = P.v12; view.m13 = P.v13;
   view.m21 = P.v21; view.m22 = P.v22; view.m23 = P.v23;
@@ -2201,18 +2231,19 @@ __global__ RFX_TRACE_BOUNDS void prim_cull_kernel(DevScene S, FrameParams P, uin
   // the pixel's sample rectangle [rx, rx + omax] x [ry, ry + omax] (Render.cpp:177-183: offsets (ss - 1) / ss at most,
   // plus a jitter of at most 1 in additive frames), through its four corners
   const int ss = P.ss;
-  const bool exact = ss == 1 && !P.additive;
+  const bool exact = (LANES || ss == 1) && !P.additive;
   uint64_t om = 0;
   if (__ballot(valid))
   {
     Bundle B;
-    if (exact)
-      B = make_bundle(eye, mmul(view, mk(rx + 0.0f + 0.0f, ry + 0.0f + 0.0f, P.rz)), valid);  // as trace_kernel (plain)
+    if (exact)  // as trace_kernel (plain: rx + 0 + 0; lanes: rx + float(sx) / ss + 0)
+      B = make_bundle(eye, mmul(view, mk(rx + lox + 0.0f, ry + loy + 0.0f, P.rz)), valid);
     else
     {
-      const float omax = (float)(ss - 1) / (float)ss + (P.additive ? 1.0f : 0.0f);
-      const v3 q[4] = {mmul(view, mk(rx, ry, P.rz)), mmul(view, mk(rx + omax, ry, P.rz)),
-                       mmul(view, mk(rx, ry + omax, P.rz)), mmul(view, mk(rx + omax, ry + omax, P.rz))};
+      const float bx = rx + lox, by = ry + loy;  // LANES: the lane's jitter square; else the pixel's sample rectangle
+      const float omax = LANES ? 1.0f : (float)(ss - 1) / (float)ss + (P.additive ? 1.0f : 0.0f);
+      const v3 q[4] = {mmul(view, mk(bx, by, P.rz)), mmul(view, mk(bx + omax, by, P.rz)),
+                       mmul(view, mk(bx, by + omax, P.rz)), mmul(view, mk(bx + omax, by + omax, P.rz))};
       B = make_bundle_quad(eye, q, valid);
     }
     om = B.ok ? cull_small<true>(T.cull(), S.cull_valid, B, S.cull_tri) : S.cull_valid;
@@ -2224,11 +2255,12 @@ __global__ RFX_TRACE_BOUNDS void prim_cull_kernel(DevScene S, FrameParams P, uin
   const int nl = P.additive ? 0 : min(S.n_light, kPrimLights);
   uint64_t sm[kPrimLights] = {0, 0, 0, 0};
   const float ssf = (float)ss;
-  for (int sx = 0; nl > 0 && sx < ss; ++sx)
-    for (int sy = 0; sy < ss; ++sy)
+  const int nss = LANES ? 1 : ss;  // LANES: the lane's one sample
+  for (int sx = 0; nl > 0 && sx < nss; ++sx)
+    for (int sy = 0; sy < nss; ++sy)
     {
       // the sample's ray exactly as trace_kernel forms it (plain: rx + 0 + 0; SSAA: rx + float(sx) / ss + 0)
-      const float ox = sx ? (float)sx / ssf : 0.0f, oy = sy ? (float)sy / ssf : 0.0f;
+      const float ox = LANES ? lox : sx ? (float)sx / ssf : 0.0f, oy = LANES ? loy : sy ? (float)sy / ssf : 0.0f;
       const v3 ray = mmul(view, mk(rx + ox + 0.0f, ry + oy + 0.0f, P.rz));
       Cnt cnt;
       Hit h;

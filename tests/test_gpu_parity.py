@@ -538,7 +538,8 @@ def test_primary_masks_match_reference_hash(key):
                                        and c["W"] * c["H"] > 1))
 def test_primary_masks_on_goldens(key):
     """Every stored golden but the block previews with the masks built before every launch (prim_masks 2): one-sample
-    frames use them; SSAA and additive frames use them only in an RFX_PRIM_SSAA build (compiled out by default, measured
+    frames and the one-lane-per-sample frames (sampleNum 2, 4, 8, jittered sampleNum 1: prim_cull_kernel<., true>) use
+    them; sampleNum 3, 5, 6, 7 and > 8 use them only in an RFX_PRIM_SSAA build (compiled out by default, measured
     slower), so there the test pins that the setting changes nothing."""
     c = CASES[key]
     rgb, argb, r = run_case(c, prim_masks=2)
@@ -548,11 +549,11 @@ def test_primary_masks_on_goldens(key):
     r.close()
 
 
-@pytest.mark.parametrize("ss,additive", [(1, False), (2, False), (1, True), (3, True)])
+@pytest.mark.parametrize("ss,additive", [(1, False), (2, False), (1, True), (3, True), (4, False), (2, True), (8, False)])
 def test_primary_masks_over_repeated_views(ss, additive):
     """A still camera over 4 frames (masks built on the second and reused), one-sample, SSAA and additive (jittered,
-    accumulating) frames: every frame equals the frame rendered without masks (SSAA frames take masks only in an
-    RFX_PRIM_SSAA build)."""
+    accumulating) frames: every frame equals the frame rendered without masks (sampleNum 3 takes masks only in an
+    RFX_PRIM_SSAA build; 2, 4, 8 and jittered 1 take the lanes masks, jittered ones without the shadow masks)."""
     desc = scene("synth16")
     W, H, depth = (640, 360, 8) if ss == 1 else (320, 184, 8)
     frames = {}

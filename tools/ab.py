@@ -65,6 +65,7 @@ VARIANTS = {
     "nolanes": ["RFX_SSAA_LANES=0"],
     "halves": ["RFX_HALF_BUNDLES"],
     "nolight1": ["RFX_ONE_LIGHT=0"],
+    "noprimlanes": ["RFX_PRIM_LANES=0"],
 }
 
 
