@@ -124,9 +124,9 @@ int rfx_renderer_set_regroup_sort(rfx_renderer *r, int on);
 /* Which bounce kernel the last trace launch ran: 0 = none (not regrouped), 1 = the global-memory BVH form, 2 = the
  * LDS-staged BVH form (large scenes whose BVH fits the LDS; 1 when the runtime refused its LDS size). */
 int rfx_renderer_bounce_form(const rfx_renderer *r);
-/* Primary-bundle cull masks of small-scene plain frames (no pixel changes): the first segment's cull mask of every
- * 8x8 wave tile, computed by one extra launch for a view (camera, frame geometry, scene) and reused while the
- * view stays.  1 (default) = built when a view repeats (the second frame of a still camera on), so a camera that
+/* Primary-bundle cull masks of small-scene plain frames and of SSAA frames run one sample per lane (sampleNum 2, 4,
+ * 8, and jittered sampleNum 1) (no pixel changes): the first segment's cull masks of every wave tile, computed by one
+ * extra launch for a view (camera, frame geometry, sampling, scene) and reused while the view stays.  1 (default) = built when a view repeats (the second frame of a still camera on), so a camera that
  * moves every frame never pays for them; 2 = built before every launch; 0 = off (per-launch bundles). */
 int rfx_renderer_set_prim_masks(rfx_renderer *r, int mode);
 /* The reference's two LCG streams (trace_math.h:34-39): Vector3.cpp's (randomInsideSphere) and

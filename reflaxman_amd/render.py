@@ -307,7 +307,8 @@ class Renderer:
         check(_lib.load().rfx_renderer_set_tile_order(self._h, int(mode)), "set_tile_order")
 
     def set_prim_masks(self, mode: int):
-        """Primary-bundle cull masks of small-scene plain frames (rfx.h rfx_renderer_set_prim_masks): 1 built when
+        """Primary-bundle cull masks of small-scene plain and one-sample-per-lane SSAA frames
+        (rfx.h rfx_renderer_set_prim_masks): 1 built when
         a view repeats (default), 2 before every launch, 0 off.  No pixel changes."""
         check(_lib.load().rfx_renderer_set_prim_masks(self._h, int(mode)), "set_prim_masks")
 

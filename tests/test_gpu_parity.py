@@ -212,10 +212,13 @@ def test_strip_partition_assembles_to_whole_frame(nranks, row_block):
     assert np.array_equal(argb, whole_argb)
 
 
-@pytest.mark.parametrize("nranks,row_block,ss", [(2, 8, 1), (3, 5, 1), (4, 16, 2), (8, 8, 1)])
-def test_sliced_rng_prepass_multi_rank(nranks, row_block, ss):
+@pytest.mark.parametrize("nranks,row_block,ss,masks", [(2, 8, 1, 1), (3, 5, 1, 1), (4, 16, 2, 1), (8, 8, 1, 1),
+                                                       (3, 5, 2, 2), (2, 3, 4, 2), (2, 8, 1, 2)])
+def test_sliced_rng_prepass_multi_rank(nranks, row_block, ss, masks):
     """The multi-GPU pre-pass (slice counts -> all-gather -> filtered emit), emulated rank by rank in one
-    process: the assembled strips equal the 1-GPU frame and every rank carries the same stream state."""
+    process: the assembled strips equal the 1-GPU frame and every rank carries the same stream state.  masks 2: the
+    ranks build their per-view masks before the launch, over strips whose height is no multiple of the lanes mode's
+    pixel block (sampleNum 2: 4-row blocks over 5-row strips; 4: 2-row blocks over 3-row strips)."""
     import ctypes as C
     from reflaxman_amd import _lib
     from reflaxman_amd.render import Renderer, build_scene, make_frame
@@ -244,6 +247,7 @@ def test_sliced_rng_prepass_multi_rank(nranks, row_block, ss):
     for rank in range(nranks):
         rr = Renderer(sphere_seed=97531)
         rr.set_scene(s)
+        rr.set_prim_masks(masks)
         f = make_frame(cam, W, H, depth, ss, row_block=row_block, rank=rank, nranks=nranks)
         bps = C.c_uint64()
         _lib.check(L.rfx_frame_rng_blocks(rr._h, C.byref(f), nranks, C.byref(bps)))
