@@ -868,15 +868,32 @@ __device__ __forceinline__ RayInv ray_inv(const DevScene &S, v3 o, v3 ray)
 
 // child c of node n against the ray: hit (conservative), and the entry parameter t (>= 0) of the widened box.
 // Every decision is a comparison that a NaN fails in the keeping direction.
+#ifndef RFX_BVH_FMA
+#define RFX_BVH_FMA 0
+#endif
+#ifndef RFX_BVH_TLIM
+#define RFX_BVH_TLIM 0
+#endif
 __device__ __forceinline__ bool bvh_box(const BvhNode &n, int c, v3 o, const RayInv &ri, float &tn)
 {
   const float lx = n.lx[c], ly = n.ly[c], lz = n.lz[c], hx = n.hx[c], hy = n.hy[c], hz = n.hz[c];
   // |o - c|_2 + half-diagonal <= |o - ref|_2 + mt[c] (c the box centre): the margin is at least
   // kCullRel (|o - c|_2 + half-diagonal) + 1e-6, the per-box bound of the culling argument
+#if RFX_BVH_FMA
+  // The slab parameters as (bound - m) ix - o ix with one fused multiply-add each.  This is a cull decision with a
+  // margin, not a reference value: it rounds once where the unfused form rounds twice, so the margin covers it as
+  // before.  A 0 * inf NaN (axis-parallel ray, or bound - m and o on the same side) drops that axis: conservative.
+  const float m = __builtin_fmaf(kCullRel, n.mt[c], ri.dm);
+  const float oxi = o.x * ri.ix, oyi = o.y * ri.iy, ozi = o.z * ri.iz;
+  const float ax = __builtin_fmaf(lx - m, ri.ix, -oxi), bx = __builtin_fmaf(hx + m, ri.ix, -oxi);
+  const float ay = __builtin_fmaf(ly - m, ri.iy, -oyi), by = __builtin_fmaf(hy + m, ri.iy, -oyi);
+  const float az = __builtin_fmaf(lz - m, ri.iz, -ozi), bz = __builtin_fmaf(hz + m, ri.iz, -ozi);
+#else
   const float m = ri.dm + kCullRel * n.mt[c];
   const float ax = (lx - m - o.x) * ri.ix, bx = (hx + m - o.x) * ri.ix;
   const float ay = (ly - m - o.y) * ri.iy, by = (hy + m - o.y) * ri.iy;
   const float az = (lz - m - o.z) * ri.iz, bz = (hz + m - o.z) * ri.iz;
+#endif
   // fminf / fmaxf return the other operand for a NaN (0 * inf on an axis-parallel ray): that axis is ignored
   const float t0 = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), 0.0f));
   const float t1 = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
@@ -891,6 +908,13 @@ __device__ __forceinline__ void closest_spheres_bvh(const DevScene &S, v3 origin
 {
   const RayInv ri = ray_inv(S, origin, ray);
   const float a = 0.5f * k.a2;                // |ray|^2 (exact: a2 = 2a)
+#if RFX_BVH_TLIM
+  // the entry parameter beyond which a child cannot hold a closer (or tying) sphere, sqrt(1.001 best / a), kept per
+  // ray and re-derived on each new best hit: one compare per child instead of three multiplies.  Approximate rcp and
+  // sqrt (1 ulp each) under a 1e-4 widening keep it above the exact bound, so it skips no child the product form keeps.
+  const float ia = __builtin_amdgcn_rcpf(a);
+  float tlim = __builtin_amdgcn_sqrtf(h.sq * 1.001f * ia) * 1.0001f;
+#endif
   BvhSlot *stack = ns.stack();
   int sp = 0, node = 0;
   for (;;)
@@ -900,8 +924,13 @@ __device__ __forceinline__ void closest_spheres_bvh(const DevScene &S, v3 origin
       const BvhNode n = ns.node(S, node);
       float t0, t1;
       // a child entered beyond the best hit cannot hold a closer (or tying) sphere
+#if RFX_BVH_TLIM
+      const bool h0 = bvh_box(n, 0, origin, ri, t0) && !(t0 > tlim);
+      const bool h1 = bvh_box(n, 1, origin, ri, t1) && !(t1 > tlim);
+#else
       const bool h0 = bvh_box(n, 0, origin, ri, t0) && !(t0 * t0 * a > h.sq * 1.001f);
       const bool h1 = bvh_box(n, 1, origin, ri, t1) && !(t1 * t1 * a > h.sq * 1.001f);
+#endif
       if (h0 && h1)
       {
         const bool first0 = !(t1 < t0);
@@ -933,6 +962,9 @@ __device__ __forceinline__ void closest_spheres_bvh(const DevScene &S, v3 origin
           const int obj = S.sph_info[4 * j + 2];
           if (tri_takes(sq, h.sq, obj, h.obj)) { h.sq = sq; h.obj = obj; h.i = 2 * j + 1; h.t = t; }
         }
+#if RFX_BVH_TLIM
+        tlim = __builtin_amdgcn_sqrtf(h.sq * 1.001f * ia) * 1.0001f;
+#endif
       }
     }
     if (sp == 0) break;

@@ -66,6 +66,9 @@ VARIANTS = {
     "halves": ["RFX_HALF_BUNDLES"],
     "nolight1": ["RFX_ONE_LIGHT=0"],
     "noprimlanes": ["RFX_PRIM_LANES=0"],
+    "bvhfma": ["RFX_BVH_FMA=1"],
+    "tlim": ["RFX_BVH_TLIM=1"],
+    "bvhopt": ["RFX_BVH_FMA=1", "RFX_BVH_TLIM=1"],
 }
 
 
