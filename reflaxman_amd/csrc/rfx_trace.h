@@ -857,23 +857,30 @@ struct BvhLds {
   __device__ __forceinline__ BvhSlot *stack() const { return stk + threadIdx.x; }
 };
 
-// box margins from the node's stored term and one per-ray distance (round 2: C5 -8.5% against a margin per box)
-struct RayInv { float ix, iy, iz, dm; };  // dm: kCullRel |o - bvh_ref|_2 + 1e-6 (approximate root, widened 1e-4)
-__device__ __forceinline__ RayInv ray_inv(const DevScene &S, v3 o, v3 ray)
-{
-  const float ex = o.x - S.bvh_rx, ey = o.y - S.bvh_ry, ez = o.z - S.bvh_rz;
-  const float dm = kCullRel * (__builtin_amdgcn_sqrtf(ex * ex + ey * ey + ez * ez) * 1.0001f) + 1e-6f;
-  return RayInv{__builtin_amdgcn_rcpf(ray.x), __builtin_amdgcn_rcpf(ray.y), __builtin_amdgcn_rcpf(ray.z), dm};
-}
-
-// child c of node n against the ray: hit (conservative), and the entry parameter t (>= 0) of the widened box.
-// Every decision is a comparison that a NaN fails in the keeping direction.
 #ifndef RFX_BVH_FMA
 #define RFX_BVH_FMA 0
 #endif
 #ifndef RFX_BVH_TLIM
 #define RFX_BVH_TLIM 0
 #endif
+// box margins from the node's stored term and one per-ray distance (round 2: C5 -8.5% against a margin per box)
+struct RayInv { float ix, iy, iz, dm; };  // dm: kCullRel |o - bvh_ref|_2 + 1e-6 (approximate root, widened 1e-4)
+__device__ __forceinline__ RayInv ray_inv(const DevScene &S, v3 o, v3 ray)
+{
+  const float ex = o.x - S.bvh_rx, ey = o.y - S.bvh_ry, ez = o.z - S.bvh_rz;
+  const float dm = kCullRel * (__builtin_amdgcn_sqrtf(ex * ex + ey * ey + ez * ez) * 1.0001f) + 1e-6f;
+#if RFX_BVH_FMA
+  // finite reciprocals for the fused slabs: with rcp(0) = inf the fused form's inf - inf would leave one NaN slab end, and
+  // fminf / fmaxf would then take the other end for both (a false cull of an axis-parallel ray, tests/test_bvh_box_bound.py)
+  const auto fin = [](float v) { return fminf(fmaxf(v, -1e30f), 1e30f); };
+  return RayInv{fin(__builtin_amdgcn_rcpf(ray.x)), fin(__builtin_amdgcn_rcpf(ray.y)), fin(__builtin_amdgcn_rcpf(ray.z)), dm};
+#else
+  return RayInv{__builtin_amdgcn_rcpf(ray.x), __builtin_amdgcn_rcpf(ray.y), __builtin_amdgcn_rcpf(ray.z), dm};
+#endif
+}
+
+// child c of node n against the ray: hit (conservative), and the entry parameter t (>= 0) of the widened box.
+// Every decision is a comparison that a NaN fails in the keeping direction.
 __device__ __forceinline__ bool bvh_box(const BvhNode &n, int c, v3 o, const RayInv &ri, float &tn)
 {
   const float lx = n.lx[c], ly = n.ly[c], lz = n.lz[c], hx = n.hx[c], hy = n.hy[c], hz = n.hz[c];
