@@ -83,3 +83,18 @@ def test_box_test_keeps_every_box_a_reported_hit_lies_in(fused):
     lo, hi = (centre - size).astype(F), (centre + size).astype(F)
     k = kept(lo, hi, o.astype(F), d.astype(F), ref.astype(F), mt, rng, fused)
     assert k[inside].all(), int((~k[inside]).sum())
+
+
+def test_entry_limit_keeps_what_the_product_form_keeps():
+    """RFX_BVH_TLIM: a child is skipped when its entry parameter t0 exceeds tlim = sqrt(1.001 best / a) 1.0001 (approximate
+    rcp and sqrt); the product form skips it when t0^2 a > 1.001 best.  Every child the product form keeps, tlim keeps."""
+    rng = np.random.default_rng(7)
+    n = 1 << 20
+    a = np.exp(rng.uniform(np.log(1e-4), np.log(1e6), n)).astype(F)            # |ray|^2
+    best = np.exp(rng.uniform(np.log(1e-8), np.log(1e8), n)).astype(F)         # best |ray t|^2 so far
+    t0 = (np.sqrt(best.astype(np.float64) * 1.001 / a) * np.exp(rng.normal(0.0, 1e-5, n))).astype(F)
+    keep_product = ~(t0 * t0 * a > best * F(1.001))
+    tlim = approx(np.sqrt(best * F(1.001) * approx(F(1) / a, rng)), rng) * F(1.0001)
+    keep_tlim = ~(t0 > tlim)
+    assert keep_product.sum() > n // 4
+    assert not (keep_product & ~keep_tlim).any()
