@@ -858,7 +858,7 @@ struct BvhLds {
 };
 
 #ifndef RFX_BVH_FMA
-#define RFX_BVH_FMA 0
+#define RFX_BVH_FMA 1
 #endif
 #ifndef RFX_BVH_TLIM
 #define RFX_BVH_TLIM 0

@@ -66,9 +66,8 @@ VARIANTS = {
     "halves": ["RFX_HALF_BUNDLES"],
     "nolight1": ["RFX_ONE_LIGHT=0"],
     "noprimlanes": ["RFX_PRIM_LANES=0"],
-    "bvhfma": ["RFX_BVH_FMA=1"],
+    "nobvhfma": ["RFX_BVH_FMA=0"],
     "tlim": ["RFX_BVH_TLIM=1"],
-    "bvhopt": ["RFX_BVH_FMA=1", "RFX_BVH_TLIM=1"],
 }
 
 
