@@ -822,6 +822,21 @@ int build_pair_bvh(std::vector<BvhNode> &nodes, std::vector<uint32_t> &pairs, si
     double l[3] = {INFINITY, INFINITY, INFINITY}, h[3] = {-INFINITY, -INFINITY, -INFINITY};
     for (size_t i = range[c][0]; i < range[c][1]; ++i)
       for (int k = 0; k < 3; ++k) { l[k] = fmin(l[k], box[pairs[i]].lo[k]); h[k] = fmax(h[k], box[pairs[i]].hi[k]); }
+#if RFX_BVH_PREWIDE
+    {
+      // the box grown by the node part of the kernel's margin, kCullRel mt[c] (rfx_trace.h kCullRel = 2e-3), from the
+      // float mt the kernel would have used, with a relative 1e-6 on top
+      double cd = 0.0, hd = 0.0;
+      for (int k = 0; k < 3; ++k)
+      {
+        const double dc = ref[k] - 0.5 * (l[k] + h[k]), dh = 0.5 * (h[k] - l[k]);
+        cd += dc * dc;
+        hd += dh * dh;
+      }
+      const double w = 2e-3 * (double)nextafterf((float)((sqrt(cd) + sqrt(hd)) * 1.0001), INFINITY) * (1.0 + 1e-6);
+      for (int k = 0; k < 3; ++k) { l[k] -= w; h[k] += w; }
+    }
+#endif
     // round outwards to float
     n.lx[c] = nextafterf((float)l[0], -INFINITY); n.ly[c] = nextafterf((float)l[1], -INFINITY);
     n.lz[c] = nextafterf((float)l[2], -INFINITY);

@@ -850,8 +850,12 @@ struct BvhLds {
     const uint2 x = aux[i];
     n.child[0] = (int32_t)(int16_t)(x.x & 0xFFFFu);
     n.child[1] = (int32_t)(int16_t)(x.x >> 16);
+#if RFX_BVH_PREWIDE
+    n.mt[0] = n.mt[1] = 0.0f;  // the boxes are stored grown by their node margin
+#else
     n.mt[0] = (float)(x.y & 0xFFFFu) * mstep;
     n.mt[1] = (float)(x.y >> 16) * mstep;
+#endif
     return n;
   }
   __device__ __forceinline__ BvhSlot *stack() const { return stk + threadIdx.x; }
@@ -864,7 +868,15 @@ struct BvhLds {
 #define RFX_BVH_TLIM 0
 #endif
 // box margins from the node's stored term and one per-ray distance (round 2: C5 -8.5% against a margin per box)
+#if RFX_BVH_PREWIDE
+#if !RFX_BVH_FMA
+#error "RFX_BVH_PREWIDE needs RFX_BVH_FMA (finite reciprocals)"
+#endif
+// the per-ray slab constants: (o + dm) rcp(d) for the low ends, (o - dm) rcp(d) for the high ends
+struct RayInv { float ix, iy, iz, dm, lx, ly, lz, hx, hy, hz; };
+#else
 struct RayInv { float ix, iy, iz, dm; };  // dm: kCullRel |o - bvh_ref|_2 + 1e-6 (approximate root, widened 1e-4)
+#endif
 __device__ __forceinline__ RayInv ray_inv(const DevScene &S, v3 o, v3 ray)
 {
   const float ex = o.x - S.bvh_rx, ey = o.y - S.bvh_ry, ez = o.z - S.bvh_rz;
@@ -873,7 +885,14 @@ __device__ __forceinline__ RayInv ray_inv(const DevScene &S, v3 o, v3 ray)
   // finite reciprocals for the fused slabs: with rcp(0) = inf the fused form's inf - inf would leave one NaN slab end, and
   // fminf / fmaxf would then take the other end for both (a false cull of an axis-parallel ray, tests/test_bvh_box_bound.py)
   const auto fin = [](float v) { return fminf(fmaxf(v, -1e30f), 1e30f); };
+#if RFX_BVH_PREWIDE
+  const float ix = fin(__builtin_amdgcn_rcpf(ray.x)), iy = fin(__builtin_amdgcn_rcpf(ray.y)),
+              iz = fin(__builtin_amdgcn_rcpf(ray.z));
+  return RayInv{ix, iy, iz, dm, (o.x + dm) * ix, (o.y + dm) * iy, (o.z + dm) * iz,
+                (o.x - dm) * ix, (o.y - dm) * iy, (o.z - dm) * iz};
+#else
   return RayInv{fin(__builtin_amdgcn_rcpf(ray.x)), fin(__builtin_amdgcn_rcpf(ray.y)), fin(__builtin_amdgcn_rcpf(ray.z)), dm};
+#endif
 #else
   return RayInv{__builtin_amdgcn_rcpf(ray.x), __builtin_amdgcn_rcpf(ray.y), __builtin_amdgcn_rcpf(ray.z), dm};
 #endif
@@ -886,7 +905,12 @@ __device__ __forceinline__ bool bvh_box(const BvhNode &n, int c, v3 o, const Ray
   const float lx = n.lx[c], ly = n.ly[c], lz = n.lz[c], hx = n.hx[c], hy = n.hy[c], hz = n.hz[c];
   // |o - c|_2 + half-diagonal <= |o - ref|_2 + mt[c] (c the box centre): the margin is at least
   // kCullRel (|o - c|_2 + half-diagonal) + 1e-6, the per-box bound of the culling argument
-#if RFX_BVH_FMA
+#if RFX_BVH_PREWIDE
+  // boxes grown by kCullRel mt[c] on the host; the per-ray margin dm sits in the slab constants
+  const float ax = __builtin_fmaf(lx, ri.ix, -ri.lx), bx = __builtin_fmaf(hx, ri.ix, -ri.hx);
+  const float ay = __builtin_fmaf(ly, ri.iy, -ri.ly), by = __builtin_fmaf(hy, ri.iy, -ri.hy);
+  const float az = __builtin_fmaf(lz, ri.iz, -ri.lz), bz = __builtin_fmaf(hz, ri.iz, -ri.hz);
+#elif RFX_BVH_FMA
   // The slab parameters as (bound - m) ix - o ix with one fused multiply-add each.  This is a cull decision with a
   // margin, not a reference value: it rounds once where the unfused form rounds twice, so the margin covers it as
   // before.  A 0 * inf NaN (axis-parallel ray, or bound - m and o on the same side) drops that axis: conservative.

@@ -28,13 +28,25 @@ def fmaf(a, b, c):
 
 
 def kept(lo, hi, o, d, ref, mt, rng, fused):
-    """rfx_trace.h ray_inv + bvh_box for one child, in float32."""
+    """rfx_trace.h ray_inv + bvh_box for one child, in float32 (fused: False, True or "prewide")."""
     e = o - ref
     dm = K_CULL_REL * (approx(np.sqrt((e * e).sum(1, dtype=F)), rng) * F(1.0001)) + F(1e-6)
     with np.errstate(divide="ignore", invalid="ignore", over="ignore"):
         inv = approx(F(1) / d, rng)
-        if fused:  # ray_inv clamps the reciprocals to +-1e30 for the fused form
+        if fused:  # ray_inv clamps the reciprocals to +-1e30 for the fused forms
             inv = np.clip(inv, F(-1e30), F(1e30))
+        if fused == "prewide":
+            # rfx_host.cpp: the box grown by kCullRel mt (x (1 + 1e-6)) and rounded outward; the kernel's slab
+            # constants (o + dm) rcp(d) and (o - dm) rcp(d)
+            w = 2e-3 * mt.astype(np.float64) * (1.0 + 1e-6)
+            lo = np.nextafter((lo.astype(np.float64) - w[:, None]).astype(F), F(-np.inf))
+            hi = np.nextafter((hi.astype(np.float64) + w[:, None]).astype(F), F(np.inf))
+            a = fmaf(lo, inv, -((o + dm[:, None]) * inv))
+            b = fmaf(hi, inv, -((o - dm[:, None]) * inv))
+            mn, mx = np.fmin(a, b), np.fmax(a, b)
+            t0 = np.fmax(np.fmax(mn[:, 0], mn[:, 1]), np.fmax(mn[:, 2], F(0)))
+            t1 = np.fmin(np.fmin(mx[:, 0], mx[:, 1]), mx[:, 2])
+            return ~(t0 > t1 * F(1.00001) + F(1e-30))
             m = fmaf(np.full_like(mt, K_CULL_REL), mt, dm)
             oi = o * inv
             a = fmaf(lo - m[:, None], inv, -oi)
@@ -50,9 +62,9 @@ def kept(lo, hi, o, d, ref, mt, rng, fused):
         return ~(t0 > t1 * F(1.00001) + F(1e-30))
 
 
-@pytest.mark.parametrize("fused", [False, True])
+@pytest.mark.parametrize("fused", [False, True, "prewide"])
 def test_box_test_keeps_every_box_a_reported_hit_lies_in(fused):
-    rng = np.random.default_rng(20261017 + fused)
+    rng = np.random.default_rng(20261017 + [False, True, "prewide"].index(fused))
     n = 1 << 19
     size = np.exp(rng.uniform(np.log(0.02), np.log(5.0), (n, 3)))         # half extents
     centre = rng.uniform(-20.0, 20.0, (n, 3))
