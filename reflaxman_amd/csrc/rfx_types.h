@@ -57,10 +57,10 @@ struct alignas(16) CullTri { float v0x, v0y, v0z, nu, gux, guy, guz, nv, gvx, gv
 // node, c < 0 the leaf pair ~c (spheres 2(~c), 2(~c) + 1 of the device arrays, which are in spatial order).
 // mt[c]: |ref - centre of child c|_2 + its half-diagonal (ref: DevScene::bvh_ref), so that kCullRel (|o - ref|_2 + mt[c])
 // bounds the kernel's per-ray box margin from above with one add per child (triangle inequality)
-// RFX_BVH_PREWIDE (experiment): the host stores each child box already grown by kCullRel mt[c] (rounded outward), so the
-// kernel adds only the per-ray part of the margin, folded into per-ray slab constants.
+// RFX_BVH_PREWIDE (round 4, kept: C5 trace + bounce -4.0%): the host stores each child box already grown by kCullRel
+// mt[c] (rounded outward), so the kernel adds only the per-ray part of the margin, folded into per-ray slab constants.
 #ifndef RFX_BVH_PREWIDE
-#define RFX_BVH_PREWIDE 0
+#define RFX_BVH_PREWIDE 1
 #endif
 struct alignas(16) BvhNode { float lx[2], ly[2], lz[2], hx[2], hy[2], hz[2]; int32_t child[2]; float mt[2]; };
 // Plane(pos, norm, material) (Plane.h:6-14): the normal as given (the reference never normalises it)

@@ -68,7 +68,7 @@ VARIANTS = {
     "noprimlanes": ["RFX_PRIM_LANES=0"],
     "nobvhfma": ["RFX_BVH_FMA=0"],
     "tlim": ["RFX_BVH_TLIM=1"],
-    "prewide": ["RFX_BVH_PREWIDE=1"],
+    "noprewide": ["RFX_BVH_PREWIDE=0"],
 }
 
 
