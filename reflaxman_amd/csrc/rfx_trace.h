@@ -872,8 +872,15 @@ struct BvhLds {
 #if !RFX_BVH_FMA
 #error "RFX_BVH_PREWIDE needs RFX_BVH_FMA (finite reciprocals)"
 #endif
+#ifndef RFX_BVH_PREWIDE_KEEP
+#define RFX_BVH_PREWIDE_KEEP 1  // 1: the six slab constants live across the walk; 0: re-derived per node (fewer registers)
+#endif
+#if RFX_BVH_PREWIDE_KEEP
 // the per-ray slab constants: (o + dm) rcp(d) for the low ends, (o - dm) rcp(d) for the high ends
 struct RayInv { float ix, iy, iz, dm, lx, ly, lz, hx, hy, hz; };
+#else
+struct RayInv { float ix, iy, iz, dm; };
+#endif
 #else
 struct RayInv { float ix, iy, iz, dm; };  // dm: kCullRel |o - bvh_ref|_2 + 1e-6 (approximate root, widened 1e-4)
 #endif
@@ -888,8 +895,12 @@ __device__ __forceinline__ RayInv ray_inv(const DevScene &S, v3 o, v3 ray)
 #if RFX_BVH_PREWIDE
   const float ix = fin(__builtin_amdgcn_rcpf(ray.x)), iy = fin(__builtin_amdgcn_rcpf(ray.y)),
               iz = fin(__builtin_amdgcn_rcpf(ray.z));
+#if RFX_BVH_PREWIDE_KEEP
   return RayInv{ix, iy, iz, dm, (o.x + dm) * ix, (o.y + dm) * iy, (o.z + dm) * iz,
                 (o.x - dm) * ix, (o.y - dm) * iy, (o.z - dm) * iz};
+#else
+  return RayInv{ix, iy, iz, dm};
+#endif
 #else
   return RayInv{fin(__builtin_amdgcn_rcpf(ray.x)), fin(__builtin_amdgcn_rcpf(ray.y)), fin(__builtin_amdgcn_rcpf(ray.z)), dm};
 #endif
@@ -907,9 +918,15 @@ __device__ __forceinline__ bool bvh_box(const BvhNode &n, int c, v3 o, const Ray
   // kCullRel (|o - c|_2 + half-diagonal) + 1e-6, the per-box bound of the culling argument
 #if RFX_BVH_PREWIDE
   // boxes grown by kCullRel mt[c] on the host; the per-ray margin dm sits in the slab constants
-  const float ax = __builtin_fmaf(lx, ri.ix, -ri.lx), bx = __builtin_fmaf(hx, ri.ix, -ri.hx);
-  const float ay = __builtin_fmaf(ly, ri.iy, -ri.ly), by = __builtin_fmaf(hy, ri.iy, -ri.hy);
-  const float az = __builtin_fmaf(lz, ri.iz, -ri.lz), bz = __builtin_fmaf(hz, ri.iz, -ri.hz);
+#if RFX_BVH_PREWIDE_KEEP
+  const float olx = ri.lx, oly = ri.ly, olz = ri.lz, ohx = ri.hx, ohy = ri.hy, ohz = ri.hz;
+#else
+  const float olx = (o.x + ri.dm) * ri.ix, oly = (o.y + ri.dm) * ri.iy, olz = (o.z + ri.dm) * ri.iz;
+  const float ohx = (o.x - ri.dm) * ri.ix, ohy = (o.y - ri.dm) * ri.iy, ohz = (o.z - ri.dm) * ri.iz;
+#endif
+  const float ax = __builtin_fmaf(lx, ri.ix, -olx), bx = __builtin_fmaf(hx, ri.ix, -ohx);
+  const float ay = __builtin_fmaf(ly, ri.iy, -oly), by = __builtin_fmaf(hy, ri.iy, -ohy);
+  const float az = __builtin_fmaf(lz, ri.iz, -olz), bz = __builtin_fmaf(hz, ri.iz, -ohz);
 #elif RFX_BVH_FMA
   // The slab parameters as (bound - m) ix - o ix with one fused multiply-add each.  This is a cull decision with a
   // margin, not a reference value: it rounds once where the unfused form rounds twice, so the margin covers it as

@@ -69,6 +69,7 @@ VARIANTS = {
     "nobvhfma": ["RFX_BVH_FMA=0"],
     "tlim": ["RFX_BVH_TLIM=1"],
     "noprewide": ["RFX_BVH_PREWIDE=0"],
+    "pwlite": ["RFX_BVH_PREWIDE_KEEP=0"],
 }
 
 
