@@ -5,8 +5,8 @@ lane and occupancy, from the compiler's kernel-resource-usage remarks, for every
     python tools/resource_usage.py [TU ...]      # default: the plain-mode translation units
     python tools/resource_usage.py --json OUT    # also write the table as JSON
 
-Kernel names are shortened to trace<STATS,MODE,CFG> / bounce<CFG>; CFG bits (rfx_trace.h kCfg*): 1 cull,
-2 >32 lights, 4 small scene, 8 planes, 16 park.
+Kernel names are shortened to trace<STATS,MODE,CFG> / bounce<CFG> / bounce_lds<CFG> (the LDS-staged BVH form); CFG bits
+(rfx_trace.h kCfg*): 1 cull, 2 >32 lights, 4 small scene, 8 planes, 16 park, 32 one light.
 """
 from __future__ import annotations
 
@@ -34,6 +34,9 @@ def short(name: str) -> str:
     m = re.match(r"_ZN3rfx13bounce_kernelILi(\d+)EEEv", name)
     if m:
         return f"bounce<{m.group(1)}>"
+    m = re.match(r"_ZN3rfx17bounce_kernel_ldsILi(\d+)EEEv", name)
+    if m:
+        return f"bounce_lds<{m.group(1)}>"
     return name
 
 
@@ -56,7 +59,7 @@ def usage(tu: str):
             out.append(cur)
         elif cur is not None and key in FIELDS:
             cur[FIELDS[key]] = int(val)
-    return [k for k in out if k["kernel"].startswith(("trace<", "bounce<"))]
+    return [k for k in out if k["kernel"].startswith(("trace<", "bounce<", "bounce_lds<"))]
 
 
 def main():
