@@ -311,6 +311,13 @@ def main():
         save_render("render_planes_160x90_d8", "planes", 160, 90, 8)
         save_render("render_planes_64x36_d6_ss2_add2", "planes", 64, 36, 6, ss=2, additive=True, frames=2, jseed=77)
         save_render("render_planes300_96x54_d8", "planes300", 96, 54, 8)
+        # large scenes (pair BVH, > 64 triangles) in the one-lane-per-sample and 64-samples-per-chunk SSAA modes
+        save_render("render_stress4096_48x27_d12_ss2", "stress4096", 48, 27, 12, ss=2)
+        save_render("render_stress4096_24x14_d8_ss4_add2", "stress4096", 24, 14, 8, ss=4, additive=True, frames=2,
+                    jseed=31337)
+        save_render("render_stress4096_6x4_d8_ss16", "stress4096", 6, 4, 8, ss=16)
+        save_render("render_planes300_40x24_d6_ss2", "planes300", 40, 24, 6, ss=2)
+        save_render("render_mesh100_40x24_d6_ss2_add2", "mesh100", 40, 24, 6, ss=2, additive=True, frames=2, jseed=9)
         # full-size hashes only (C1, C3; the default 4K d8 too -- SURVEY Appendix B)
         save_render("hash_default_640x480_d4", "default", 640, 480, 4, store=False, use_file=False)
         save_render("hash_synth16_3840x2160_d8", "synth16", 3840, 2160, 8, store=False)
