@@ -70,6 +70,7 @@ VARIANTS = {
     "tlim": ["RFX_BVH_TLIM=1"],
     "noprewide": ["RFX_BVH_PREWIDE=0"],
     "pwlite": ["RFX_BVH_PREWIDE_KEEP=0"],
+    "tlimlite": ["RFX_BVH_TLIM=1", "RFX_BVH_PREWIDE_KEEP=0"],
 }
 
 
