@@ -525,6 +525,20 @@ __device__ __forceinline__ float wave_max_nonneg(float v)
   return __int_as_float(__builtin_amdgcn_readlane((int)u, 63));
 }
 
+// Sums of products in the bundle and cull bounds (RFX_CULL_FMA): these are conservative decisions with margins far above
+// a rounding, not reference values, so they may fuse their multiply-adds.
+#ifndef RFX_CULL_FMA
+#define RFX_CULL_FMA 1
+#endif
+__device__ __forceinline__ float cdot(float ax, float ay, float az, float bx, float by, float bz)
+{
+#if RFX_CULL_FMA
+  return __builtin_fmaf(az, bz, __builtin_fmaf(ay, by, ax * bx));
+#else
+  return ax * bx + ay * by + az * bz;
+#endif
+}
+
 // Bundle of the rays (o, d) of the `live` lanes.  Call with every lane of the wave active and at least
 // one live lane.  Approximate square roots are fine here: every bound is widened well past their error.
 __device__ __forceinline__ Bundle make_bundle(v3 o, v3 d, bool live)
@@ -533,11 +547,11 @@ __device__ __forceinline__ Bundle make_bundle(v3 o, v3 d, bool live)
   const int ref = __ffsll((long long)__ballot(live)) - 1;
   B.cx = lane_bcast(o.x, ref); B.cy = lane_bcast(o.y, ref); B.cz = lane_bcast(o.z, ref);
   const float dx = lane_bcast(d.x, ref), dy = lane_bcast(d.y, ref), dz = lane_bcast(d.z, ref);
-  const float inv = __builtin_amdgcn_rsqf(dx * dx + dy * dy + dz * dz);
+  const float inv = __builtin_amdgcn_rsqf(cdot(dx, dy, dz, dx, dy, dz));
   B.ax = dx * inv; B.ay = dy * inv; B.az = dz * inv;
   const float ex = o.x - B.cx, ey = o.y - B.cy, ez = o.z - B.cz;
-  const float e2 = ex * ex + ey * ey + ez * ez;
-  const float cosl = (d.x * B.ax + d.y * B.ay + d.z * B.az) * __builtin_amdgcn_rsqf(d.x * d.x + d.y * d.y + d.z * d.z);
+  const float e2 = cdot(ex, ey, ez, ex, ey, ez);
+  const float cosl = cdot(d.x, d.y, d.z, B.ax, B.ay, B.az) * __builtin_amdgcn_rsqf(cdot(d.x, d.y, d.z, d.x, d.y, d.z));
   const float dev = 1.0f - cosl;
   // a live lane with a non-finite or degenerate ray disables the bound for the whole wave
   const bool bad = live && !(e2 <= 1.0e30f && dev >= -0.5f && dev <= 2.5f);
@@ -680,11 +694,17 @@ __device__ __forceinline__ uint64_t cull_chunk(const Bound *bound, int first, in
   {
     const Bound g = bound[first + l];
     const float vx = g.x - B.cx, vy = g.y - B.cy, vz = g.z - B.cz;
-    const float L2 = vx * vx + vy * vy + vz * vz;
+    const float L2 = cdot(vx, vy, vz, vx, vy, vz);
     const float L = __builtin_amdgcn_sqrtf(L2);
+#if RFX_CULL_FMA
+    const float rp = __builtin_fmaf(kCullRel, L + B.rw, g.r + B.rw);
+    const float va = cdot(vx, vy, vz, B.ax, B.ay, B.az);
+    const float lim = __builtin_fmaf(B.cosa, __builtin_amdgcn_sqrtf(fmaxf(__builtin_fmaf(-rp, rp, L2), 0.0f)), -(B.sina * rp));
+#else
     const float rp = g.r + B.rw + kCullRel * (L + B.rw);
-    const float va = vx * B.ax + vy * B.ay + vz * B.az;
+    const float va = cdot(vx, vy, vz, B.ax, B.ay, B.az);
     const float lim = B.cosa * __builtin_amdgcn_sqrtf(fmaxf(L2 - rp * rp, 0.0f)) - B.sina * rp;
+#endif
     keep = !(L > rp && va < lim);
   }
   return __ballot(keep);
@@ -734,13 +754,19 @@ __device__ __forceinline__ uint64_t cull_small(const CullRec *tab, uint64_t vali
 {
   const CullRec g = tab[threadIdx.x & 63u];
   const float vx = g.x - B.cx, vy = g.y - B.cy, vz = g.z - B.cz;
-  const float L2 = vx * vx + vy * vy + vz * vz;
+  const float L2 = cdot(vx, vy, vz, vx, vy, vz);
   const float L = __builtin_amdgcn_sqrtf(L2);
+#if RFX_CULL_FMA
+  const float rp = __builtin_fmaf(kCullRel, L + B.rw, g.r + B.rw);
+  const float va = cdot(vx, vy, vz, B.ax, B.ay, B.az);
+  const float lim = __builtin_fmaf(B.cosa, __builtin_amdgcn_sqrtf(fmaxf(__builtin_fmaf(-rp, rp, L2), 0.0f)), -(B.sina * rp));
+#else
   const float rp = g.r + B.rw + kCullRel * (L + B.rw);
-  const float va = vx * B.ax + vy * B.ay + vz * B.az;
+  const float va = cdot(vx, vy, vz, B.ax, B.ay, B.az);
   const float lim = B.cosa * __builtin_amdgcn_sqrtf(fmaxf(L2 - rp * rp, 0.0f)) - B.sina * rp;
-  const float side = g.nx * B.cx + g.ny * B.cy + g.nz * B.cz - g.d;
-  const float an = g.nx * B.ax + g.ny * B.ay + g.nz * B.az;
+#endif
+  const float side = cdot(g.nx, g.ny, g.nz, B.cx, B.cy, B.cz) - g.d;
+  const float an = cdot(g.nx, g.ny, g.nz, B.ax, B.ay, B.az);
   const float ms = B.rw + 1e-3f * (L + g.r + B.rw) + 1e-6f, ma = B.sina + 1e-3f;
   const bool away = (side > ms && an > ma) || (side < -ms && an < -ma);
   bool keep = !(L > rp && va < lim) && !away;

@@ -71,6 +71,7 @@ VARIANTS = {
     "noprewide": ["RFX_BVH_PREWIDE=0"],
     "pwlite": ["RFX_BVH_PREWIDE_KEEP=0"],
     "tlimlite": ["RFX_BVH_TLIM=1", "RFX_BVH_PREWIDE_KEEP=0"],
+    "nocullfma": ["RFX_CULL_FMA=0"],
 }
 
 
