@@ -72,6 +72,7 @@ VARIANTS = {
     "pwlite": ["RFX_BVH_PREWIDE_KEEP=0"],
     "tlimlite": ["RFX_BVH_TLIM=1", "RFX_BVH_PREWIDE_KEEP=0"],
     "nocullfma": ["RFX_CULL_FMA=0"],
+    "lanes8": ["RFX_LANES_WAVES_PER_EU=8"],
 }
 
 
