@@ -725,6 +725,10 @@ hipError_t launch_kat_powf_cube(uint32_t first, uint32_t n, unsigned long long *
   return hipGetLastError();
 }
 
+#ifndef RFX_NOCULL_MAX_TILES
+#define RFX_NOCULL_MAX_TILES 0
+#endif
+
 // the mode of a trace launch (rfx_trace.h TraceMode)
 static int trace_mode(const FrameParams &P)
 {
@@ -786,8 +790,12 @@ hipError_t launch_trace(const DevScene &S, const FrameParams &P, bool stats, hip
   FrameParams Pt = P;
   Pt.tiles_x = kTileWavesX * grid.x;  // wave tiles per row (the schedule's unit)
   const int mode = trace_mode(P);
-  // the stats build counts the reference's every test, so it never culls
-  const int cfg = (S.n_light > 32 ? kCfgManyLights : 0) | (stats ? 0 : kCfgCull) |
+  // the stats build counts the reference's every test, so it never culls.  RFX_NOCULL_MAX_TILES (experiment): small
+  // scenes in frames of at most that many wave tiles -- all waves resident at once, the launch as long as its slowest
+  // tile -- skip the bundle cull, trading tests for the cull's serial latency
+  const bool cull = !stats && !(RFX_NOCULL_MAX_TILES > 0 && S.n_sph <= 32 && S.n_tri <= 32 &&
+                                trace_tiles(P) <= (uint32_t)RFX_NOCULL_MAX_TILES);
+  const int cfg = (S.n_light > 32 ? kCfgManyLights : 0) | (cull ? kCfgCull : 0) |
                   (S.n_sph <= 32 && S.n_tri <= 32 ? kCfgSmall : 0) | (S.n_pln > 0 ? kCfgPlanes : 0) |
                   (S.n_light == 1 && !stats && RFX_ONE_LIGHT ? kCfgOneLight : 0);
   launch_mode_cfg(stats, mode, cfg, grid, S, Pt, st);

@@ -73,9 +73,8 @@ VARIANTS = {
     "tlimlite": ["RFX_BVH_TLIM=1", "RFX_BVH_PREWIDE_KEEP=0"],
     "nocullfma": ["RFX_CULL_FMA=0"],
     "lanes8": ["RFX_LANES_WAVES_PER_EU=8"],
-    "nb99999": ["RFX_NARROW_BUNDLE_COS=0.99999f"],
     "nb999": ["RFX_NARROW_BUNDLE_COS=0.999f"],
-    "nbbvh": ["RFX_NARROW_BUNDLE_COS=2.0f"],
+    "nocullsmall": ["RFX_NOCULL_MAX_TILES=8192"],
 }
 
 
