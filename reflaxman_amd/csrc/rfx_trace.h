@@ -1959,8 +1959,12 @@ constexpr int kCfgCull = 1, kCfgManyLights = 2, kCfgSmall = 4, kCfgPlanes = 8, k
 // one workgroup = kTileW x kTileH output pixels (block mode: block corners), one wave = an 8x8 tile (ray coherence).
 // Every lane of a wave reaches trace() -- lanes outside the frame or the cursor span as invalid -- so the
 // bounce loop can use wave-wide bundles.
+#ifndef RFX_WAVES_PER_EU_LARGE
+#define RFX_WAVES_PER_EU_LARGE RFX_WAVES_PER_EU  // large-scene (BVH) trace kernels' occupancy target (experiment)
+#endif
 template <bool STATS, int MODE, int CFG>
-__global__ RFX_TRACE_BOUNDS void trace_kernel(DevScene S, FrameParams P)
+__global__ __launch_bounds__(kWgThreads) __attribute__((amdgpu_waves_per_eu(
+    (CFG & kCfgSmall) ? RFX_WAVES_PER_EU : RFX_WAVES_PER_EU_LARGE))) void trace_kernel(DevScene S, FrameParams P)
 {
   constexpr bool CULL = (CFG & kCfgCull) != 0, MANYL = (CFG & kCfgManyLights) != 0, SMALL = (CFG & kCfgSmall) != 0;
   constexpr bool PLANES = (CFG & kCfgPlanes) != 0, PARK = MODE == kModePlain && !STATS && (CFG & kCfgPark) != 0;

@@ -75,6 +75,8 @@ VARIANTS = {
     "lanes8": ["RFX_LANES_WAVES_PER_EU=8"],
     "nb999": ["RFX_NARROW_BUNDLE_COS=0.999f"],
     "nocullsmall": ["RFX_NOCULL_MAX_TILES=8192"],
+    "large6": ["RFX_WAVES_PER_EU_LARGE=6"],
+    "large5": ["RFX_WAVES_PER_EU_LARGE=5"],
 }
 
 
