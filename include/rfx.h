@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define RFX_ABI_VERSION 2
+#define RFX_ABI_VERSION 3
 
 typedef enum {
   RFX_OK = 0,
@@ -151,6 +151,9 @@ typedef struct {
    * the W x H frame into whole-frame buffers (d_rgb W*H*3, d_argb W*H; only the band's rows are written), with the
    * frame's random stream sliced nranks ways as for strips (rfx_frame_rng_count / rfx_render_frame_counted).  Rank 0
    * can then receive each band straight into its rows of the frame (reflaxman_amd/dist.py BandFrame). */
+  uint64_t span_begin;      /* band partition only: the random stream covers the whole rows [span_begin, span_end) / W */
+  uint64_t span_end;        /* of the frame (0, 0 = the whole frame) and the band lies within them -- a frame of 2^32 */
+                            /* traces or more is rendered as consecutive row spans (rfx_group_render_frame) */
 } rfx_frame;
 
 /* rows of `frame` that `rank` owns under the block-cyclic strip partition */
@@ -164,10 +167,17 @@ uint32_t rfx_strip_row_to_y(uint32_t r, uint32_t row_block, uint32_t rank, uint3
  *   d_rgb  : device float RGB, strip_rows x W x 3 (read-modify-write when additive_counter > 1)
  *   d_argb : device uint32, strip_rows x W, Color::argb of the stored value (copyImage), or NULL
  *   d_counters : device uint64[RFX_NCOUNTERS] accumulated event counters (stats kernel), or NULL
+ * Any sample count (Pulse's menu reaches 7680x4320 at 256x256 samples, 2.2e12 traces): a span of more traces than the
+ * launch limit (rfx_renderer_set_launch_traces) is rendered as consecutive pixel spans (whole rows where a row fits),
+ * each its own pre-pass and trace launch, alternating between two streams so one span's tail overlaps the next span's
+ * start; the random streams run on from span to span exactly as the reference's cursor does (Render.cpp:136-215).
  */
 #define RFX_NCOUNTERS 40
 int rfx_render_frame(rfx_renderer *r, const rfx_frame *frame, float *d_rgb, uint32_t *d_argb,
                      uint64_t *d_counters, void *stream);
+/* The most traces one rfx_render_frame launch takes (default 2^30: 4 GB of randDir state per buffer, two buffers);
+ * 0 = the default.  Splitting changes no pixel (tests/test_gpu_parity.py forces small limits). */
+int rfx_renderer_set_launch_traces(rfx_renderer *r, uint64_t max_traces);
 
 /*
  * Multi-GPU form of the RNG pre-pass, around ONE exchange step.  The trace-ordered

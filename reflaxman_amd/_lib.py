@@ -13,7 +13,7 @@ from . import _build
 
 RFX_OK = 0
 RFX_NCOUNTERS = 40
-RFX_ABI_VERSION = 2
+RFX_ABI_VERSION = 3
 METAL, DIELECTRIC = 0, 1
 
 _fp = C.POINTER(C.c_float)
@@ -34,6 +34,7 @@ class Frame(C.Structure):
         ("additive", C.c_int32), ("additive_counter", C.c_int32),
         ("row_block", C.c_uint32), ("rank", C.c_uint32), ("nranks", C.c_uint32),
         ("pixel_begin", C.c_uint64), ("pixel_end", C.c_uint64),
+        ("span_begin", C.c_uint64), ("span_end", C.c_uint64),
     ]
 
 
@@ -96,6 +97,7 @@ SIGNATURES = [
     ("rfx_renderer_set_prim_masks", C.c_int, [C.c_void_p, C.c_int]),
     ("rfx_renderer_set_regroup", C.c_int, [C.c_void_p, C.c_int]),
     ("rfx_renderer_set_regroup_sort", C.c_int, [C.c_void_p, C.c_int]),
+    ("rfx_renderer_set_launch_traces", C.c_int, [C.c_void_p, C.c_uint64]),
     ("rfx_renderer_bounce_form", C.c_int, [C.c_void_p]),
     ("rfx_renderer_get_timing", C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double), _u64p]),
     ("rfx_device_alloc", C.c_int, [C.c_void_p, C.c_size_t, C.POINTER(C.c_void_p)]),

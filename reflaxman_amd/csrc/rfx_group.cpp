@@ -290,13 +290,13 @@ static int collect_times(rfx_group *g)
   return RFX_OK;
 }
 
-static int ensure_buffers(rfx_group *g, const rfx_frame &f0)
+static int ensure_buffers(rfx_group *g, const rfx_frame &f0, size_t m)
 {
   const size_t n = g->n();
   uint64_t bps = 0;
-  RCHECK(rfx_frame_rng_blocks(g->r[0], &f0, (uint32_t)n, &bps));
+  RCHECK(rfx_frame_rng_blocks(g->r[0], &f0, (uint32_t)m, &bps));
   g->bps = bps;
-  if (bps * n > g->cnt_words)
+  if (bps * m > g->cnt_words)
   {
     for (size_t i = 0; i < n; ++i)
     {
@@ -306,10 +306,10 @@ static int ensure_buffers(rfx_group *g, const rfx_frame &f0)
       {
         (void)hipFree(g->cnt[b][i]);
         g->cnt[b][i] = nullptr;
-        GCHECK(hipMalloc(&g->cnt[b][i], bps * n * sizeof(uint32_t)));
+        GCHECK(hipMalloc(&g->cnt[b][i], bps * m * sizeof(uint32_t)));
       }
     }
-    g->cnt_words = bps * n;
+    g->cnt_words = bps * m;
   }
   const size_t px = (size_t)f0.width * f0.height;
   if (px > g->px_cap)
@@ -328,6 +328,89 @@ static int ensure_buffers(rfx_group *g, const rfx_frame &f0)
   return RFX_OK;
 }
 
+// One pass of the group over the rows [y0, y1) of the frame: members 0..m-1 take the bands bd[i] .. bd[i + 1] (whole rows
+// within [y0, y1)), the random stream runs over the pass's rows (rfx_frame span_begin / span_end).  A frame is one pass
+// over all rows, or -- 2^31 traces or more -- consecutive passes of row spans (the stream continues from pass to pass on
+// every member, as Render.cpp:136-215's cursor does).
+static int group_pass(rfx_group *g, const rfx_frame *f, uint32_t y0, uint32_t y1, const std::vector<uint32_t> &bd,
+                      float *d_rgb, uint32_t *d_argb, float *img0, hipStream_t s0)
+{
+  const size_t m = bd.size() - 1;
+  const uint32_t W = f->width;
+  std::vector<rfx_frame> fr(m, *f);
+  for (size_t i = 0; i < m; ++i)
+  {
+    fr[i].row_block = 0;
+    fr[i].rank = (uint32_t)i;
+    fr[i].nranks = (uint32_t)m;
+    fr[i].pixel_begin = (uint64_t)bd[i] * W;
+    fr[i].pixel_end = (uint64_t)bd[i + 1] * W;
+    fr[i].span_begin = (uint64_t)y0 * W;
+    fr[i].span_end = (uint64_t)y1 * W;
+  }
+  RCHECK(ensure_buffers(g, fr[0], m));
+  const int b = (int)(g->frames & 1);
+  const bool accumulate = f->additive_counter > 1;
+  std::vector<hipStream_t> st(m);
+  for (size_t i = 0; i < m; ++i) st[i] = i ? g->own[i] : s0;
+  // 0. after the caller's work on its stream; member 0's stream state is the group's
+  GCHECK(hipSetDevice(g->dev[0]));
+  GCHECK(hipEventRecord(g->ev_start[0], s0));
+  const uint32_t jitter = rfx_detail_jitter(g->r[0]);
+  for (size_t i = 1; i < m; ++i)
+  {
+    GCHECK(hipSetDevice(g->dev[i]));
+    GCHECK(hipStreamWaitEvent(st[i], g->ev_start[0], 0));
+    GCHECK(hipMemcpyPeerAsync(rfx_detail_seed_word(g->r[i]), g->dev[i], rfx_detail_seed_word(g->r[0]), g->dev[0],
+                              sizeof(uint32_t), st[i]));
+    rfx_detail_set_jitter(g->r[i], jitter);
+  }
+  // 1. each member counts its slice of the pass's random stream and pushes it to every other member
+  const size_t sl = g->bps * sizeof(uint32_t);
+  for (size_t i = 0; i < m; ++i)
+  {
+    RCHECK(rfx_frame_rng_count(g->r[i], &fr[i], (uint32_t)i, (uint32_t)m, g->cnt[b][i], st[i]));
+    GCHECK(hipSetDevice(g->dev[i]));
+    for (size_t j = 0; j < m; ++j)
+    {
+      if (j == i) continue;
+      GCHECK(hipStreamWaitEvent(st[i], g->ev_emit[b][j], 0));  // j's emit of two passes ago read this array
+      GCHECK(hipMemcpyPeerAsync(g->cnt[b][j] + i * g->bps, g->dev[j], g->cnt[b][i] + i * g->bps, g->dev[i], sl, st[i]));
+    }
+    GCHECK(hipEventRecord(g->ev_cnt[i], st[i]));
+  }
+  // 2. every slice arrived: emit the band's randDirs and trace the band; 3. bands to the caller's frame
+  for (size_t i = 0; i < m; ++i)
+  {
+    GCHECK(hipSetDevice(g->dev[i]));
+    for (size_t j = 0; j < m; ++j)
+      if (j != i) GCHECK(hipStreamWaitEvent(st[i], g->ev_cnt[j], 0));
+    const uint64_t r0 = bd[i], rows = bd[i + 1] - r0;
+    float *img = i ? g->rgb[i] : img0;
+    uint32_t *a = i ? (d_argb ? g->argb[i] : nullptr) : d_argb;
+    if (accumulate && i)  // the accumulated rows this member adds to (Render.cpp:191-194)
+      GCHECK(hipMemcpyPeerAsync(img + r0 * W * 3, g->dev[i], d_rgb + r0 * W * 3, g->dev[0], rows * W * 12, st[i]));
+    const uint32_t j0 = rfx_detail_jitter(g->r[i]);
+    RCHECK(rfx_render_frame_counted_ev(g->r[i], &fr[i], (uint32_t)m, g->cnt[b][i], img, a, nullptr, st[i],
+                                       g->ev_emit[b][i]));
+    rfx_detail_set_rewindable(g->r[i], j0);
+    GCHECK(hipSetDevice(g->dev[i]));
+    GCHECK(hipEventRecord(g->ev_t1[i], st[i]));
+    if (i)
+    {
+      if (d_rgb)
+        GCHECK(hipMemcpyPeerAsync(d_rgb + r0 * W * 3, g->dev[0], img + r0 * W * 3, g->dev[i], rows * W * 12, st[i]));
+      if (d_argb)
+        GCHECK(hipMemcpyPeerAsync(d_argb + r0 * W, g->dev[0], a + r0 * W, g->dev[i], rows * W * 4, st[i]));
+      GCHECK(hipEventRecord(g->ev_done[i], st[i]));
+    }
+  }
+  GCHECK(hipSetDevice(g->dev[0]));
+  for (size_t i = 1; i < m; ++i) GCHECK(hipStreamWaitEvent(s0, g->ev_done[i], 0));
+  ++g->frames;
+  return RFX_OK;
+}
+
 extern "C" int rfx_group_render_frame(rfx_group *g, const rfx_frame *f, float *d_rgb, uint32_t *d_argb, void *stream)
 {
   if (!g || !f || (!d_rgb && !d_argb)) return rfx_detail_fail(RFX_ERR_ARG, "group_render_frame: bad args");
@@ -338,22 +421,45 @@ extern "C" int rfx_group_render_frame(rfx_group *g, const rfx_frame *f, float *d
   const bool argb_only = d_rgb == nullptr;
   if (argb_only && f->additive_counter > 1)
     return rfx_detail_fail(RFX_ERR_ARG, "group_render_frame: an accumulating frame needs the float frame (d_rgb)");
-  if (f->sample_num <= 0 || (f->nranks > 1) || !((f->pixel_begin == 0 && f->pixel_end == 0) ||
-                                                  (f->pixel_begin == 0 && f->pixel_end == npx)))
+  if (f->sample_num <= 0 || f->sample_num > 256 || (f->nranks > 1) ||
+      !((f->pixel_begin == 0 && f->pixel_end == 0) || (f->pixel_begin == 0 && f->pixel_end == npx)))
     return rfx_detail_fail(RFX_ERR_ARG, "group_render_frame: a whole frame with sample_num > 0 (no partition fields)");
   hipStream_t s0 = stream ? (hipStream_t)stream : rfx_detail_stream(g->r[0]);
   if (argb_only && npx > g->rgb0_cap)
   {
     GCHECK(hipSetDevice(g->dev[0]));
-    GCHECK(hipStreamSynchronize(s0));
+    GCHECK(hipDeviceSynchronize());  // any earlier frame on any stream may still write the old buffer
     (void)hipFree(g->rgb0);
     g->rgb0 = nullptr;
     g->rgb0_cap = 0;
     GCHECK(hipMalloc(&g->rgb0, npx * 3 * sizeof(float)));
     g->rgb0_cap = npx;
   }
-  if (n == 1 || H < n)
-    return rfx_render_frame(g->r[0], f, argb_only ? g->rgb0 : d_rgb, d_argb, nullptr, s0);
+  float *img0 = argb_only ? g->rgb0 : d_rgb;
+  if (n == 1 || H < n) return rfx_render_frame(g->r[0], f, img0, d_argb, nullptr, s0);  // (splits a large frame itself)
+  // a frame of more traces than one pass takes -- every member's band at most its launch limit, the pass under the band
+  // scan's 2^31 -- runs as passes over consecutive row spans, each cut into equal bands (no balancing)
+  const uint64_t spp = (uint64_t)f->sample_num * (uint64_t)f->sample_num;
+  const uint64_t cap = std::min<uint64_t>((uint64_t)n * rfx_detail_launch_traces(g->r[0]), 1ull << 31);
+  if (npx * spp > cap)
+  {
+    const uint64_t per = cap / ((uint64_t)W * spp);  // rows per pass
+    if (!per) return rfx_detail_fail(RFX_ERR_ARG, "group_render_frame: one row exceeds 2^31 traces");
+    GCHECK(hipSetDevice(g->dev[0]));
+    const uint32_t jitter0 = rfx_detail_jitter(g->r[0]);
+    RCHECK(rfx_detail_save_start(g->r[0], s0));
+    for (uint64_t y = 0; y < H; y += per)
+    {
+      const uint32_t y0 = (uint32_t)y, y1 = (uint32_t)std::min<uint64_t>(H, y + per);
+      const size_t m = std::min<size_t>(n, y1 - y0);
+      std::vector<uint32_t> bd(m + 1);
+      for (size_t i = 0; i <= m; ++i) bd[i] = y0 + (uint32_t)(((uint64_t)(y1 - y0) * i) / m);
+      RCHECK(group_pass(g, f, y0, y1, bd, d_rgb, d_argb, img0, s0));
+    }
+    g->timing_pending = false;  // the bands of a split frame are not the frame's bands
+    rfx_detail_set_rewindable_saved(g->r[0], jitter0, s0);
+    return RFX_OK;
+  }
   if (W != g->W || H != g->H || g->bounds.size() != n + 1)
   {
     if (g->fixed && H != g->H) return rfx_detail_fail(RFX_ERR_ARG, "group_render_frame: fixed bands of another height");
@@ -365,76 +471,9 @@ extern "C" int rfx_group_render_frame(rfx_group *g, const rfx_frame *f, float *d
     g->timing_pending = false;
   }
   RCHECK(collect_times(g));
-  std::vector<rfx_frame> fr(n, *f);
-  for (size_t i = 0; i < n; ++i)
-  {
-    fr[i].row_block = 0;
-    fr[i].rank = (uint32_t)i;
-    fr[i].nranks = (uint32_t)n;
-    fr[i].pixel_begin = (uint64_t)g->bounds[i] * W;
-    fr[i].pixel_end = (uint64_t)g->bounds[i + 1] * W;
-  }
-  RCHECK(ensure_buffers(g, fr[0]));
-  const int b = (int)(g->frames & 1);
-  const bool accumulate = f->additive_counter > 1;
-  std::vector<hipStream_t> st(n);
-  for (size_t i = 0; i < n; ++i) st[i] = i ? g->own[i] : s0;
-  // 0. after the caller's work on its stream; member 0's stream state is the group's
-  GCHECK(hipSetDevice(g->dev[0]));
-  GCHECK(hipEventRecord(g->ev_start[0], s0));
-  const uint32_t jitter = rfx_detail_jitter(g->r[0]);
-  for (size_t i = 1; i < n; ++i)
-  {
-    GCHECK(hipSetDevice(g->dev[i]));
-    GCHECK(hipStreamWaitEvent(st[i], g->ev_start[0], 0));
-    GCHECK(hipMemcpyPeerAsync(rfx_detail_seed_word(g->r[i]), g->dev[i], rfx_detail_seed_word(g->r[0]), g->dev[0],
-                              sizeof(uint32_t), st[i]));
-    rfx_detail_set_jitter(g->r[i], jitter);
-  }
-  // 1. each member counts its slice of the frame's random stream and pushes it to every other member
-  const size_t sl = g->bps * sizeof(uint32_t);
-  for (size_t i = 0; i < n; ++i)
-  {
-    RCHECK(rfx_frame_rng_count(g->r[i], &fr[i], (uint32_t)i, (uint32_t)n, g->cnt[b][i], st[i]));
-    GCHECK(hipSetDevice(g->dev[i]));
-    for (size_t j = 0; j < n; ++j)
-    {
-      if (j == i) continue;
-      GCHECK(hipStreamWaitEvent(st[i], g->ev_emit[b][j], 0));  // j's emit of two frames ago read this array
-      GCHECK(hipMemcpyPeerAsync(g->cnt[b][j] + i * g->bps, g->dev[j], g->cnt[b][i] + i * g->bps, g->dev[i], sl, st[i]));
-    }
-    GCHECK(hipEventRecord(g->ev_cnt[i], st[i]));
-  }
-  // 2. every slice arrived: emit the band's randDirs and trace the band; 3. bands to the caller's frame
-  for (size_t i = 0; i < n; ++i)
-  {
-    GCHECK(hipSetDevice(g->dev[i]));
-    for (size_t j = 0; j < n; ++j)
-      if (j != i) GCHECK(hipStreamWaitEvent(st[i], g->ev_cnt[j], 0));
-    const uint64_t y0 = g->bounds[i], rows = g->bounds[i + 1] - y0;
-    float *img = i ? g->rgb[i] : (argb_only ? g->rgb0 : d_rgb);
-    uint32_t *a = i ? (d_argb ? g->argb[i] : nullptr) : d_argb;
-    if (accumulate && i)  // the accumulated rows this member adds to (Render.cpp:191-194)
-      GCHECK(hipMemcpyPeerAsync(img + y0 * W * 3, g->dev[i], d_rgb + y0 * W * 3, g->dev[0], rows * W * 12, st[i]));
-    const uint32_t j0 = rfx_detail_jitter(g->r[i]);
-    RCHECK(rfx_render_frame_counted_ev(g->r[i], &fr[i], (uint32_t)n, g->cnt[b][i], img, a, nullptr, st[i],
-                                       g->ev_emit[b][i]));
-    rfx_detail_set_rewindable(g->r[i], j0);
-    GCHECK(hipSetDevice(g->dev[i]));
-    GCHECK(hipEventRecord(g->ev_t1[i], st[i]));
-    if (i)
-    {
-      if (!argb_only)
-        GCHECK(hipMemcpyPeerAsync(d_rgb + y0 * W * 3, g->dev[0], img + y0 * W * 3, g->dev[i], rows * W * 12, st[i]));
-      if (d_argb)
-        GCHECK(hipMemcpyPeerAsync(d_argb + y0 * W, g->dev[0], a + y0 * W, g->dev[i], rows * W * 4, st[i]));
-      GCHECK(hipEventRecord(g->ev_done[i], st[i]));
-    }
-  }
-  GCHECK(hipSetDevice(g->dev[0]));
-  for (size_t i = 1; i < n; ++i) GCHECK(hipStreamWaitEvent(s0, g->ev_done[i], 0));
-  g->timing_parity = b;
+  const int parity = (int)(g->frames & 1);
+  RCHECK(group_pass(g, f, 0, H, g->bounds, d_rgb, d_argb, img0, s0));
+  g->timing_parity = parity;
   g->timing_pending = true;
-  ++g->frames;
   return RFX_OK;
 }

@@ -34,9 +34,9 @@ hipError_t launch_rng_finish(const uint32_t *d_seed, const uint32_t *d_jump, uin
                              uint32_t *d_rd_state, int *d_err, uint64_t ss2, uint64_t W, uint32_t row_block,
                              uint32_t rank, uint32_t nranks, hipStream_t st);
 hipError_t launch_rng_finish_band(const uint32_t *d_seed, const uint32_t *d_jump, uint32_t *d_next_seed,
-                                  const uint32_t *d_blk_cnt, uint64_t nblk, uint64_t traces, uint32_t *d_rd_state,
-                                  int *d_err, uint64_t lo, uint64_t hi, uint64_t *d_off, uint32_t *d_range,
-                                  hipStream_t st);
+                                  const uint32_t *d_blk_cnt, const uint16_t *d_masks, uint64_t nblk, uint64_t traces,
+                                  uint32_t *d_rd_state, int *d_err, uint64_t lo, uint64_t hi, uint64_t *d_off,
+                                  uint32_t *d_range, hipStream_t st);
 hipError_t launch_trace(const DevScene &S, const FrameParams &P, bool stats, hipStream_t st);
 hipError_t launch_prim_cull(const DevScene &S, const FrameParams &P, uint64_t *masks, hipStream_t st);
 hipError_t launch_queue_sort(const uint32_t *count, const uint32_t *key, uint32_t *hist, uint32_t *order, hipStream_t st);
@@ -472,6 +472,15 @@ constexpr size_t kPrimLargeWords = 12;  // per wave tile, large scenes (rfx_trac
 #ifndef RFX_TILE_SORT_EVERY
 #define RFX_TILE_SORT_EVERY 4  // tools/ab.py, C3: every launch -7.5% trace time vs raster order, every 4th -9.4%, every 16th -9.8%
 #endif
+#ifndef RFX_LAUNCH_TRACES
+#define RFX_LAUNCH_TRACES (1ull << 30)  // traces per launch of a split frame (rfx_renderer_set_launch_traces)
+#endif
+constexpr uint64_t kMaxLaunchTraces = 1ull << 31;  // the band scan's 32-bit offsets (rfx_kernels.hip rng_band_range)
+#ifndef RFX_SCAN_EMIT_BLOCKS
+// one-device emits of more RNG blocks than this scan the counts first (rng_band_range) instead of summing them per
+// block (rng_emit: O(nblk^2) reads); C3 has 4,054 blocks, the 4x4 screenshot frame 16,219
+#define RFX_SCAN_EMIT_BLOCKS 16384
+#endif
 struct rfx_renderer {
   int device = 0;
   int cus = 256;  // compute units of the device (the bounce kernel's grid: one resident wave per slot)
@@ -494,9 +503,16 @@ struct rfx_renderer {
   int trace_buf = 0;      // buffer the last enqueued trace read
   uint64_t emit_key[10] = {};  // the emitted frame's plan (traces, band, geometry): rfx_render_frame_emitted must match it
   // rfx_frame_rng_rewind: the last call was an rfx_render_frame; its start states (the sphere stream's is the other
-  // seed word while rewind_flip) can be restored
-  bool rewind_ok = false, rewind_flip = false;
+  // seed word while rewind_flip, or the saved word d_seed[2] while rewind_saved: a frame of several launches) can be
+  // restored
+  bool rewind_ok = false, rewind_flip = false, rewind_saved = false;
   uint32_t rewind_jitter = 0;
+  hipStream_t rewind_stream = nullptr;
+  // frames of more traces than launch_traces: consecutive spans alternate between the caller's stream and split_stream
+  // (randDirs in d_rd / d_rd_alt); split_ev[k] marks span k's emit (the next span's pre-pass starts from its state)
+  uint64_t launch_traces = RFX_LAUNCH_TRACES;
+  hipStream_t split_stream = nullptr;
+  hipEvent_t split_ev[3] = {nullptr, nullptr, nullptr};
   uint32_t *d_blk_cnt = nullptr; uint64_t blk_cap = 0;
   uint64_t *d_blk_off = nullptr;     // band emits: the scanned block offsets ...
   uint32_t *d_rng_range = nullptr;   // ... and the band's first / last / final block
@@ -614,7 +630,7 @@ extern "C" int rfx_renderer_create(rfx_renderer **out, int device)
   int rc;
   if ((rc = set_dev(r)) != RFX_OK) { delete r; return rc; }
   if (hipStreamCreateWithFlags(&r->own_stream, hipStreamNonBlocking) != hipSuccess ||
-      hipMalloc(&r->d_seed, 2 * sizeof(uint32_t)) != hipSuccess || hipMalloc(&r->d_err, sizeof(int)) != hipSuccess)
+      hipMalloc(&r->d_seed, 3 * sizeof(uint32_t)) != hipSuccess || hipMalloc(&r->d_err, sizeof(int)) != hipSuccess)
   {
     delete r;
     return fail(RFX_ERR_HIP, "renderer_create: HIP allocation failed");
@@ -658,8 +674,22 @@ extern "C" void rfx_renderer_destroy(rfx_renderer *r)
   if (r->tile_fork) (void)hipEventDestroy(r->tile_fork);
   if (r->tile_join) (void)hipEventDestroy(r->tile_join);
   if (r->tile_stream) (void)hipStreamDestroy(r->tile_stream);
+  if (r->split_stream)
+  {
+    (void)hipStreamSynchronize(r->split_stream);
+    (void)hipStreamDestroy(r->split_stream);
+  }
+  for (hipEvent_t e : r->split_ev)
+    if (e) (void)hipEventDestroy(e);
   if (r->own_stream) (void)hipStreamDestroy(r->own_stream);
   delete r;
+}
+
+extern "C" int rfx_renderer_set_launch_traces(rfx_renderer *r, uint64_t max_traces)
+{
+  if (!r) return fail(RFX_ERR_ARG, "renderer_set_launch_traces: null renderer");
+  r->launch_traces = max_traces ? std::min(max_traces, kMaxLaunchTraces) : (uint64_t)RFX_LAUNCH_TRACES;
+  return RFX_OK;
 }
 
 extern "C" int rfx_renderer_device(const rfx_renderer *r) { return r ? r->device : -1; }
@@ -1189,6 +1219,20 @@ static uint64_t rng_layout(uint64_t traces, uint32_t nslices, uint64_t *per_slic
   return bps * nslices;
 }
 
+// the second randDir buffer (emit-ahead frames, the odd spans of a split frame)
+static int ensure_rd_alt(rfx_renderer *r, uint64_t traces)
+{
+  if (r->rd_alt_cap < traces)
+  {
+    (void)hipFree(r->d_rd_alt);
+    r->d_rd_alt = nullptr;
+    r->rd_alt_cap = 0;
+    HIP_CHECK(hipMalloc(&r->d_rd_alt, traces * sizeof(uint32_t)));
+    r->rd_alt_cap = traces;
+  }
+  return RFX_OK;
+}
+
 static int ensure_rng_workspace(rfx_renderer *r, uint64_t traces, uint64_t nblk)
 {
   if (traces > r->rd_cap)
@@ -1236,9 +1280,14 @@ struct FramePlan {
   FrameParams P;
   uint64_t traces = 0;
   hipStream_t st = nullptr;
-  // band partition (rfx.h: nranks > 1, row_block 0): the emit writes the randDirs of traces [band_lo, band_hi) only
+  // band partition (rfx.h: nranks > 1, row_block 0): the emit writes the randDirs of traces [band_lo, band_hi) only,
+  // into a buffer of the band's size (its base pointer offset by band_lo)
   bool band = false;
   uint64_t band_lo = 0, band_hi = UINT64_MAX;
+  // one span of a split frame (rfx_render_frame): launches on two streams overlap, so the per-renderer state of
+  // single launches (tile schedule, per-view masks, regroup queue) stays out
+  bool split = false;
+  uint64_t rd_traces() const { return band ? band_hi - band_lo : traces; }  // randDir words the plan writes and reads
 };
 
 static int plan_frame(rfx_renderer *r, const rfx_frame *f, void *stream, FramePlan &plan);
@@ -1262,7 +1311,7 @@ extern "C" int rfx_frame_rng_count(rfx_renderer *r, const rfx_frame *f, uint32_t
   if (!d_blk_counts || !nslices || slice >= nslices) return fail(RFX_ERR_ARG, "frame_rng_count: bad slice");
   uint64_t bps = 0;
   const uint64_t nblk = rng_layout(pl.traces, nslices, &bps);
-  if ((rc = ensure_rng_workspace(r, pl.traces, nblk)) != RFX_OK) return rc;
+  if ((rc = ensure_rng_workspace(r, pl.rd_traces(), nblk)) != RFX_OK) return rc;
   HIP_CHECK(launch_rng_count(seed_cur(r), r->d_jump, d_blk_counts, (uint64_t)slice * bps, bps, nullptr, pl.st));
   return RFX_OK;
 }
@@ -1318,9 +1367,12 @@ static int emit_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *d_counts, 
   const FrameParams &P = pl.P;
   const hipStream_t st = pl.st;
   const uint64_t ss2 = P.ss > 0 ? (uint64_t)(P.ss * P.ss) : 1;
-  if (pl.band)
-    HIP_CHECK(launch_rng_finish_band(seed_cur(r), r->d_jump, seed_next(r), d_counts, nblk, pl.traces, rd, r->d_err,
-                                     pl.band_lo, pl.band_hi, r->d_blk_off, r->d_rng_range, st));
+  if (pl.band)  // the band's randDirs into a buffer of the band's size: index trace - band_lo
+    HIP_CHECK(launch_rng_finish_band(seed_cur(r), r->d_jump, seed_next(r), d_counts, nullptr, nblk, pl.traces,
+                                     rd - pl.band_lo, r->d_err, pl.band_lo, pl.band_hi, r->d_blk_off, r->d_rng_range, st));
+  else if (P.nranks <= 1 && nblk > RFX_SCAN_EMIT_BLOCKS)
+    HIP_CHECK(launch_rng_finish_band(seed_cur(r), r->d_jump, seed_next(r), d_counts, d_masks, nblk, pl.traces, rd,
+                                     r->d_err, 0, pl.traces, r->d_blk_off, r->d_rng_range, st));
   else
     HIP_CHECK(launch_rng_finish(seed_cur(r), r->d_jump, seed_next(r), d_counts, d_masks, nblk, pl.traces, rd,
                                 r->d_err, ss2, P.W, P.row_block, P.rank, P.nranks, st));
@@ -1361,7 +1413,7 @@ static int trace_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *rd, float
   const bool small = r->dev.n_sph <= 32 && r->dev.n_tri <= 32;
   const bool plain = P.ss == 1 && !P.additive && !P.accumulate;
   const int park_after = r->park_after < 0 ? (small ? 0 : RFX_PARK_AFTER) : r->park_after;
-  const bool park = park_after > 0 && plain && !d_counters && P.depth > park_after && P.grid_rows;
+  const bool park = park_after > 0 && plain && !d_counters && P.depth > park_after && P.grid_rows && !pl.split;
   const bool sort_queue = park && r->queue_sort;
   if (park)
   {
@@ -1389,11 +1441,11 @@ static int trace_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *rd, float
       P.queue_order = r->d_qorder;
     }
   }
-  P.rd_state = rd;
+  P.rd_state = pl.band ? rd - pl.band_lo : rd;  // a band's randDirs are stored from its first trace on (emit_frame)
   P.counters = (unsigned long long *)d_counters;
   // mode 1 schedules only launches of at least RFX_TILE_ORDER_MIN_TILES tiles: on shorter ones the sort's
   // latency (three small launches and a cross-stream wait, ~15 us) is not hidden by the RNG pre-pass
-  const bool sched = P.grid_rows && r->tile_mode && !d_counters && P.ss >= 0 &&
+  const bool sched = P.grid_rows && r->tile_mode && !d_counters && P.ss >= 0 && !pl.split &&
                      (r->tile_mode != 1 || trace_tiles(P) >= RFX_TILE_ORDER_MIN_TILES);
   uint64_t key = 0;
   bool record = false;
@@ -1403,7 +1455,7 @@ static int trace_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *rd, float
   // or the scene changed (the bench's frames all reuse one set)
   if (((small && (plain || (RFX_PRIM_LANES && trace_lanes(P)) || (RFX_PRIM_SSAA && P.ss >= 1)) && !park) ||
        (RFX_PRIM_LARGE && !small && plain)) &&
-      !d_counters && P.grid_rows && r->prim_mode)
+      !d_counters && P.grid_rows && r->prim_mode && !pl.split)
   {
     struct Key { float cam[15]; uint32_t W, H, grid_rows, row0, row_block, rank, nranks; int32_t depth, ss, additive;
                  uint64_t p_begin, p_end, gen; } k;
@@ -1504,7 +1556,7 @@ extern "C" int rfx_render_frame_counted_ev(rfx_renderer *r, const rfx_frame *f, 
   if (!d_rgb || !d_blk_counts || !nslices) return fail(RFX_ERR_ARG, "render_frame_counted: bad args");
   if (pl.traces == 0) return RFX_OK;
   const uint64_t nblk = rng_layout(pl.traces, nslices, nullptr);
-  if ((rc = ensure_rng_workspace(r, pl.traces, nblk)) != RFX_OK) return rc;
+  if ((rc = ensure_rng_workspace(r, pl.rd_traces(), nblk)) != RFX_OK) return rc;
   if ((rc = timing_start(r, pl.st)) != RFX_OK) return rc;
   return finish_frame(r, pl, d_blk_counts, nullptr, nblk, d_rgb, d_argb, d_counters, (hipEvent_t)emitted_event);
 }
@@ -1538,15 +1590,8 @@ extern "C" int rfx_frame_rng_emit(rfx_renderer *r, const rfx_frame *f, uint32_t 
   if (r->emit_pending >= 0) return fail(RFX_ERR_STATE, "frame_rng_emit: the last emitted frame has not been traced");
   if (pl.traces == 0) return RFX_OK;
   const uint64_t nblk = rng_layout(pl.traces, nslices, nullptr);
-  if ((rc = ensure_rng_workspace(r, pl.traces, nblk)) != RFX_OK) return rc;
-  if (r->rd_alt_cap < pl.traces)
-  {
-    (void)hipFree(r->d_rd_alt);
-    r->d_rd_alt = nullptr;
-    r->rd_alt_cap = 0;
-    HIP_CHECK(hipMalloc(&r->d_rd_alt, pl.traces * sizeof(uint32_t)));
-    r->rd_alt_cap = pl.traces;
-  }
+  if ((rc = ensure_rng_workspace(r, pl.rd_traces(), nblk)) != RFX_OK) return rc;
+  if ((rc = ensure_rd_alt(r, pl.rd_traces())) != RFX_OK) return rc;
   const int buf = r->trace_buf == 0 ? 1 : 0;  // not the buffer of the last enqueued trace
   if ((rc = emit_frame(r, pl, d_blk_counts, nullptr, nblk, buf ? r->d_rd_alt : r->d_rd,
                        (hipEvent_t)emitted_event)) != RFX_OK)
@@ -1604,14 +1649,26 @@ extern "C" int rfx_frame_rng_pending(rfx_renderer *r, uint32_t *frame_start)
   return r->emit_pending >= 0 ? 1 : 0;
 }
 
+static int render_split(rfx_renderer *r, const rfx_frame *f, uint64_t p0, uint64_t p1, float *d_rgb, uint32_t *d_argb,
+                        uint64_t *d_counters, void *stream);
+
 extern "C" int rfx_render_frame(rfx_renderer *r, const rfx_frame *f, float *d_rgb, uint32_t *d_argb,
                                 uint64_t *d_counters, void *stream)
 {
   FramePlan pl;
   int rc;
   if (!d_rgb) return fail(RFX_ERR_ARG, "render_frame: null framebuffer");
+  if (r && f && f->sample_num > 0 && f->sample_num <= 256 && f->nranks <= 1 && f->width && f->height)
+  {
+    // a span of more traces than one launch takes: consecutive pixel spans (Render.cpp:136-215 walks the same cursor)
+    const uint64_t npx = (uint64_t)f->width * f->height;
+    const uint64_t p0 = f->pixel_begin, p1 = (f->pixel_begin == 0 && f->pixel_end == 0) ? npx : f->pixel_end;
+    if (p0 < p1 && p1 <= npx && (p1 - p0) * (uint64_t)(f->sample_num * f->sample_num) > r->launch_traces)
+      return render_split(r, f, p0, p1, d_rgb, d_argb, d_counters, stream);
+  }
   if ((rc = plan_frame(r, f, stream, pl)) != RFX_OK) return rc;
   const uint32_t jitter0 = r->jitter_seed;
+  r->rewind_saved = false;
   if (pl.traces == 0)  // a span with no block corner traces nothing (and draws no randDir)
   {
     r->rewind_ok = true;
@@ -1633,15 +1690,97 @@ extern "C" int rfx_render_frame(rfx_renderer *r, const rfx_frame *f, float *d_rg
   return RFX_OK;
 }
 
+// The stream state a frame of several launches starts from, kept in d_seed[2] for rfx_frame_rng_rewind (the seed words
+// ping-pong once per launch, so flipping back would restore only the last span's start).
+static int save_rewind_state(rfx_renderer *r, hipStream_t st)
+{
+  HIP_CHECK(hipMemcpyAsync(r->d_seed + 2, seed_cur(r), sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
+  return RFX_OK;
+}
+
+// Pixel spans [p0, p1) of more than r->launch_traces traces: launches of at most that many traces each, whole rows where
+// a row fits.  Span k runs on the caller's stream (k even) or the renderer's split stream (k odd) with its randDirs in
+// d_rd / d_rd_alt; its pre-pass waits for span k - 1's emit, whose end state it starts from, so span k's trace overlaps
+// span k - 1's tail.  Every span is a cursor span of the reference's loop: trace indices and the additive jitter run
+// from the span's first pixel (Render.cpp:136-215), so the pixels and both streams equal one launch over [p0, p1).
+static int render_split(rfx_renderer *r, const rfx_frame *f, uint64_t p0, uint64_t p1, float *d_rgb, uint32_t *d_argb,
+                        uint64_t *d_counters, void *stream)
+{
+  int rc;
+  if ((rc = set_dev(r)) != RFX_OK) return rc;
+  if (r->emit_pending >= 0)
+    return fail(RFX_ERR_STATE, "render_frame: an emitted frame awaits rfx_render_frame_emitted (or rfx_frame_rng_discard)");
+  const uint64_t W = f->width, spp = (uint64_t)(f->sample_num * f->sample_num);
+  uint64_t per = std::max<uint64_t>(1, r->launch_traces / spp);  // pixels per launch
+  const bool rows = per >= W;
+  if (rows) per = per / W * W;
+  const uint64_t cap = per * spp;
+  const hipStream_t st[2] = {stream ? (hipStream_t)stream : r->stream, nullptr};
+  if (!r->split_stream) HIP_CHECK(hipStreamCreateWithFlags(&r->split_stream, hipStreamNonBlocking));
+  for (hipEvent_t &e : r->split_ev)
+    if (!e) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  hipStream_t s2[2] = {st[0], r->split_stream};
+  // workspaces for the largest span before any launch (no re-allocation while spans are in flight)
+  if ((rc = ensure_rng_workspace(r, cap, rng_layout(cap, 1, nullptr))) != RFX_OK) return rc;
+  if ((rc = ensure_rd_alt(r, cap)) != RFX_OK) return rc;
+  const uint32_t jitter0 = r->jitter_seed;
+  if ((rc = save_rewind_state(r, s2[0])) != RFX_OK) return rc;
+  // the split stream starts after the caller's earlier work (its first span also waits for span 0's emit)
+  HIP_CHECK(hipEventRecord(r->split_ev[2], s2[0]));
+  HIP_CHECK(hipStreamWaitEvent(s2[1], r->split_ev[2], 0));
+  uint64_t k = 0;
+  for (uint64_t a = p0; a < p1; ++k)
+  {
+    const uint64_t b = std::min(p1, rows ? (a / W) * W + per : a + per);
+    rfx_frame fk = *f;
+    fk.pixel_begin = a;
+    fk.pixel_end = b;
+    const int side = (int)(k & 1);
+    FramePlan pl;
+    if ((rc = plan_frame(r, &fk, s2[side], pl)) != RFX_OK) return rc;
+    pl.split = true;
+    const uint64_t nblk = rng_layout(pl.traces, 1, nullptr);
+    if (k > 0) HIP_CHECK(hipStreamWaitEvent(s2[side], r->split_ev[side ^ 1], 0));  // span k - 1's end state
+    if ((rc = timing_start(r, pl.st)) != RFX_OK) return rc;
+    HIP_CHECK(launch_rng_count(seed_cur(r), r->d_jump, r->d_blk_cnt, 0, nblk, r->d_rng_masks, pl.st));
+    uint32_t *rd = side ? r->d_rd_alt : r->d_rd;
+    if ((rc = emit_frame(r, pl, r->d_blk_cnt, r->d_rng_masks, nblk, rd, r->split_ev[side])) != RFX_OK) return rc;
+    if ((rc = timing_event(r, pl.st)) != RFX_OK) return rc;
+    if ((rc = trace_frame(r, pl, rd, d_rgb, d_argb, d_counters)) != RFX_OK) return rc;
+    a = b;
+  }
+  // the caller's stream continues after every span
+  if (k > 1)
+  {
+    HIP_CHECK(hipEventRecord(r->split_ev[2], s2[1]));
+    HIP_CHECK(hipStreamWaitEvent(s2[0], r->split_ev[2], 0));
+  }
+  r->trace_buf = 0;
+  r->rewind_ok = true;
+  r->rewind_flip = false;
+  r->rewind_saved = true;
+  r->rewind_stream = s2[0];
+  r->rewind_jitter = jitter0;
+  return RFX_OK;
+}
+
 // Undo the random-stream advance of the last rfx_render_frame (its pixels stay as written): the pre-pass read the
-// frame's start state from one seed word and wrote the end state to the other, so flipping back restores the start.
+// frame's start state from one seed word and wrote the end state to the other, so flipping back restores the start
+// (a frame of several launches: its start state is copied back from d_seed[2]).
 extern "C" int rfx_frame_rng_rewind(rfx_renderer *r)
 {
   if (!r) return fail(RFX_ERR_ARG, "frame_rng_rewind: null renderer");
   if (!r->rewind_ok) return fail(RFX_ERR_STATE, "frame_rng_rewind: the last call was not rfx_render_frame");
   if (r->rewind_flip) r->seed_idx ^= 1u;
+  if (r->rewind_saved)
+  {
+    int rc;
+    if ((rc = set_dev(r)) != RFX_OK) return rc;
+    HIP_CHECK(hipMemcpyAsync(seed_cur(r), r->d_seed + 2, sizeof(uint32_t), hipMemcpyDeviceToDevice, r->rewind_stream));
+  }
   r->jitter_seed = r->rewind_jitter;
   r->rewind_ok = false;
+  r->rewind_saved = false;
   return RFX_OK;
 }
 
@@ -1667,19 +1806,23 @@ static int plan_frame(rfx_renderer *r, const rfx_frame *f, void *stream, FramePl
   uint64_t p0 = f->pixel_begin, p1 = f->pixel_end;
   if (band)
   {
-    // the band's rows; the frame (random stream, trace indices, output rows) stays the whole W x H frame
+    // the band's rows; the random stream and the trace indices run over the span [span_begin, span_end) of whole rows
+    // (the whole W x H frame by default), output rows stay the frame's
+    const uint64_t s0 = f->span_begin, s1 = (f->span_begin == 0 && f->span_end == 0) ? npx : f->span_end;
     if (p0 >= p1 || p1 > npx || p0 % W || p1 % W)
       return fail(RFX_ERR_ARG, "render_frame: a band is whole rows [pixel_begin, pixel_end) / W of the frame");
+    if (s0 >= s1 || s1 > npx || s0 % W || s1 % W || p0 < s0 || p1 > s1)
+      return fail(RFX_ERR_ARG, "render_frame: a band's span is whole rows [span_begin, span_end) / W around the band");
     plan.band = true;
-    plan.band_lo = p0 * (uint64_t)(f->sample_num * f->sample_num);
-    plan.band_hi = p1 * (uint64_t)(f->sample_num * f->sample_num);
-    p0 = 0;
-    p1 = npx;
+    plan.band_lo = (p0 - s0) * (uint64_t)(f->sample_num * f->sample_num);
+    plan.band_hi = (p1 - s0) * (uint64_t)(f->sample_num * f->sample_num);
+    p0 = s0;
+    p1 = s1;
   }
   if (p0 == 0 && p1 == 0) p1 = npx;
   if (p0 >= p1 || p1 > npx) return fail(RFX_ERR_ARG, "render_frame: pixel span [%llu, %llu) outside frame",
                                         (unsigned long long)p0, (unsigned long long)p1);
-  if (nranks > 1 && (p0 != 0 || p1 != npx)) return fail(RFX_ERR_ARG, "render_frame: strips need the whole frame");
+  if (nranks > 1 && !band && (p0 != 0 || p1 != npx)) return fail(RFX_ERR_ARG, "render_frame: strips need the whole frame");
   const uint32_t y0 = (uint32_t)(p0 / W), y1 = (uint32_t)((p1 - 1) / W);
   uint64_t traces, trace_base = 0;
   uint32_t grid_rows, row0;
@@ -1708,7 +1851,10 @@ static int plan_frame(rfx_renderer *r, const rfx_frame *f, void *stream, FramePl
       grid_rows = (uint32_t)((f->pixel_end - f->pixel_begin) / W);
     }
   }
-  if (traces >= (1ull << 32)) return fail(RFX_ERR_ARG, "render_frame: %llu traces exceed 2^32", (unsigned long long)traces);
+  // one launch (rfx_render_frame splits larger spans before planning them; a band's span must stay within this)
+  if (traces > kMaxLaunchTraces)
+    return fail(RFX_ERR_ARG, "render_frame: %llu traces in one launch exceed 2^31 (partitions: a smaller span)",
+                (unsigned long long)traces);
   plan.traces = traces;
   plan.st = st;
   FrameParams &P = plan.P;
@@ -1943,5 +2089,21 @@ void rfx_detail_set_rewindable(rfx_renderer *r, uint32_t jitter0)
 {
   r->rewind_ok = true;
   r->rewind_flip = true;
+  r->rewind_saved = false;
   r->rewind_jitter = jitter0;
 }
+int rfx_detail_save_start(rfx_renderer *r, hipStream_t st)
+{
+  int rc;
+  if ((rc = set_dev(r)) != RFX_OK) return rc;
+  return save_rewind_state(r, st);
+}
+void rfx_detail_set_rewindable_saved(rfx_renderer *r, uint32_t jitter0, hipStream_t st)
+{
+  r->rewind_ok = true;
+  r->rewind_flip = false;
+  r->rewind_saved = true;
+  r->rewind_stream = st;
+  r->rewind_jitter = jitter0;
+}
+uint64_t rfx_detail_launch_traces(const rfx_renderer *r) { return r->launch_traces; }

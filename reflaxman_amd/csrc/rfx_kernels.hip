@@ -443,9 +443,10 @@ __global__ __launch_bounds__(kScanThreads) void rng_band_range(const uint32_t *b
 }
 
 __global__ __launch_bounds__(kRngBlock) void rng_emit_band(const uint32_t *seed, const uint32_t *jump,
-                                                           const uint32_t *blk_cnt, const uint64_t *off,
-                                                           const uint32_t *range, uint64_t nblk, uint64_t need,
-                                                           uint32_t *rd_state, uint32_t *next_seed, EmitFilter flt)
+                                                           const uint32_t *blk_cnt, const uint16_t *masks,
+                                                           const uint64_t *off, const uint32_t *range, uint64_t nblk,
+                                                           uint64_t need, uint32_t *rd_state, uint32_t *next_seed,
+                                                           EmitFilter flt)
 {
   __shared__ uint32_t sst[kTriplesPerBlock];
   __shared__ uint32_t wsum[kRngBlock / 64];
@@ -455,7 +456,7 @@ __global__ __launch_bounds__(kRngBlock) void rng_emit_band(const uint32_t *seed,
   {
     const uint32_t b = j <= last - first ? first + j : fin;
     if (b >= nblk) break;  // (a stream too short for the frame leaves the range unset: the error flag is raised)
-    emit_block(b, off[b], seed, jump, blk_cnt, nullptr, need, rd_state, next_seed, flt, sst, wsum);
+    emit_block(b, off[b], seed, jump, blk_cnt, masks, need, rd_state, next_seed, flt, sst, wsum);
     __syncthreads();  // sst / wsum are reused by the next block
   }
 }
@@ -670,11 +671,12 @@ hipError_t launch_rng_finish(const uint32_t *d_seed, const uint32_t *d_jump, uin
 }
 
 // the band partition's emit: traces [lo, hi) (and the frame's last trace's stream state); scratch: nblk offsets and
-// 3 range words
+// 3 range words.  Also the one-device emit of launches with many blocks (lo = 0, hi = traces, the count kernel's
+// accept flags in d_masks): rng_emit's per-block prefix sums cost O(nblk^2) reads, this scan O(nblk).
 hipError_t launch_rng_finish_band(const uint32_t *d_seed, const uint32_t *d_jump, uint32_t *d_next_seed,
-                                  const uint32_t *d_blk_cnt, uint64_t nblk, uint64_t traces, uint32_t *d_rd_state,
-                                  int *d_err, uint64_t lo, uint64_t hi, uint64_t *d_off, uint32_t *d_range,
-                                  hipStream_t st)
+                                  const uint32_t *d_blk_cnt, const uint16_t *d_masks, uint64_t nblk, uint64_t traces,
+                                  uint32_t *d_rd_state, int *d_err, uint64_t lo, uint64_t hi, uint64_t *d_off,
+                                  uint32_t *d_range, hipStream_t st)
 {
   const EmitFilter flt{1, 1, 1, 0, 1, lo, hi};
   hipLaunchKernelGGL(rng_band_range, dim3(1), dim3(kScanThreads), 0, st, d_blk_cnt, nblk, traces, lo, hi, d_off, d_range,
@@ -682,8 +684,8 @@ hipError_t launch_rng_finish_band(const uint32_t *d_seed, const uint32_t *d_jump
   // about (hi - lo) / (accept rate pi/6 x 4096) blocks hold the band; the workgroups loop over however many there are
   const uint64_t est = (hi - lo) / 2048 + 4;
   hipLaunchKernelGGL(rng_emit_band, dim3((uint32_t)std::min<uint64_t>(est, nblk)), dim3(kRngBlock), 0, st, d_seed, d_jump,
-                     d_blk_cnt, (const uint64_t *)d_off, (const uint32_t *)d_range, nblk, traces, d_rd_state, d_next_seed,
-                     flt);
+                     d_blk_cnt, d_masks, (const uint64_t *)d_off, (const uint32_t *)d_range, nblk, traces, d_rd_state,
+                     d_next_seed, flt);
   return hipGetLastError();
 }
 

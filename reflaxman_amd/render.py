@@ -322,6 +322,11 @@ class Renderer:
         by direction octant and origin cell, or in park order (default).  No pixel changes."""
         check(_lib.load().rfx_renderer_set_regroup_sort(self._h, int(bool(on))), "set_regroup_sort")
 
+    def set_launch_traces(self, max_traces: int):
+        """The most traces one launch takes (rfx.h rfx_renderer_set_launch_traces; 0 = the default 2^30): larger spans
+        render as consecutive launches.  No pixel changes."""
+        check(_lib.load().rfx_renderer_set_launch_traces(self._h, int(max_traces)), "set_launch_traces")
+
     def bounce_form(self) -> int:
         """The last trace launch's bounce kernel (rfx.h rfx_renderer_bounce_form): 0 none, 1 global-memory BVH, 2 the
         LDS-staged BVH."""

@@ -20,7 +20,7 @@ def sha(a) -> str:
 
 def gpu_render(desc, W, H, depth, ss=1, additive=False, frames=1, sphere_seed=1350490027, jitter_seed=0,
                chunks=None, device=0, tile_order=None, each_frame=None, regroup=None, prim_masks=None,
-               regroup_sort=None):
+               regroup_sort=None, launch_traces=None):
     """Render through the Python mirror of Render (reflaxman_amd.render.Render) on the GPU.
 
     chunks: None -> one renderNext(W*H) per frame; else a list of renderNext sizes cycled until done.
@@ -37,6 +37,8 @@ def gpu_render(desc, W, H, depth, ss=1, additive=False, frames=1, sphere_seed=13
         r._r.set_regroup_sort(regroup_sort)
     if prim_masks is not None:
         r._r.set_prim_masks(prim_masks)
+    if launch_traces is not None:
+        r._r.set_launch_traces(launch_traces)
     for _ in range(frames):
         r.renderBegin(depth, ss, additive)
         if chunks is None:

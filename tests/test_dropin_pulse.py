@@ -88,6 +88,27 @@ def test_pulse_screenshot_on_a_device_group(tmp_path):
     assert hashlib.sha256(data).hexdigest() == c["sha_bmp"]
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("devices,policy", [(None, "frame"), (None, "span"), ("0,0,0", "frame")])
+def test_pulse_screenshot_128x128_samples(tmp_path, devices, policy):
+    """Pulse's screenshot at 800x600 with 128x128 SSAA (menu keys 1 and 8; Pulse.cpp:10-34): 7.9e9 samples, more than
+    2^32, which the renderer splits into launches (rfx_render_frame) or row-span passes (a device group).  The BMP equals,
+    byte for byte, the reference's frame written by the reference's Texture::saveToFile (tools/gen_golden.py
+    pulse_screenshot_800x600_ss128; the route is pinned to the reference Pulse's own BMP at 2x2)."""
+    c = manifest()["cases"]["pulse_screenshot_800x600_ss128"]
+    if not os.path.exists(DROPIN):
+        pytest.fail("tests/native/_build/pulse_dropin missing: run __graft_entry__.build() where /root/reference exists")
+    env = {k: v for k, v in os.environ.items() if k != "RFX_DEVICES"}
+    env.update({"RFX_SPHERE_SEED": str(c["RFX_SPHERE_SEED"]), "RFX_JITTER_SEED": str(c["RFX_JITTER_SEED"]),
+                "RFX_DROPIN_POLICY": policy, **({"RFX_DEVICES": devices} if devices else {})})
+    r = subprocess.run([DROPIN, str(tmp_path) + "/", str(c["res_key"]), str(c["ss_key"])], capture_output=True,
+                       text=True, env=env, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    data = open(r.stdout.strip(), "rb").read()
+    assert len(data) == c["bytes"]
+    assert hashlib.sha256(data).hexdigest() == c["sha_bmp"]
+
+
 def run_frames(tmp_path, c, devices=None, policy="frame"):
     """A non-Pulse caller of the drop-in Render: each frame of case c in one renderNext(W*H) call."""
     if not os.path.exists(DROPIN):

@@ -1,0 +1,153 @@
+"""Frames of any sample count: spans of more traces than one launch takes render as consecutive launches
+(rfx_render_frame, include/rfx.h) and a device group's frame as consecutive row-span passes (rfx_group_render_frame).
+
+The reference traces every sample of every pixel serially with no trace count (Render.cpp:136-215, Pulse.cpp:10-34 offers
+SSAA up to 256x256 at up to 7680x4320), so a frame's pixels and both random streams must come out the same whatever the
+launch size.  Small frames are forced through the split with tiny launch limits and compared with the reference's
+stored frames (SSAA 2..256, additive jitter, accumulation, the per-pixel sample loop, a large scene); the full-size case
+is a 800x600 128x128 screenshot (7.9e9 samples, over 2^32) hashed against the reference's banded frame.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+from helpers import GOLDEN, gpu_render, manifest, sha
+from reflaxman_amd import _lib, scenes
+
+pytestmark = pytest.mark.gpu
+CASES = manifest()["cases"]
+
+
+def _golden(key):
+    return np.load(os.path.join(GOLDEN, key + ".npz"))
+
+
+@pytest.mark.parametrize("key,limit,chunks", [
+    ("render_default_160x120_d4", 5000, None),             # whole-row launches (31 rows)
+    ("render_default_160x120_d4", 100, None),              # launches of 100 pixels: spans start mid-row
+    ("render_default_160x120_d15_add3", 3000, None),       # additive jitter, accumulation over 3 frames
+    ("render_default_160x120_d4_ss2", 4 * 700, None),      # one lane per sample, 2x2
+    ("render_default_64x40_d8_ss4", 16 * 50, None),        # 4x4, spans cutting the lanes' pixel blocks
+    ("render_default_40x24_d6_ss8", 64 * 30, None),        # 8x8
+    ("render_default_17x9_d8_ss16_add2", 256 * 5, None),   # 64-sample chunks, additive over 2 frames
+    ("render_default_6x5_d4_ss32", 1024 * 4, None),
+    ("render_planes_40x24_d6_ss3", 9 * 100, None),         # the per-pixel sample loop, planes
+    ("render_default_3x2_d20_ss64", 4096, None),           # one pixel per launch
+    ("render_default_2x2_d20_ss128", 1, None),             # a limit below one pixel: still one pixel per launch
+    ("render_default_1x1_d20_ss256", 1, None),
+    ("render_default_2x1_d8_ss64_add2", 4096, None),
+    ("render_stress4096_48x27_d12_ss2", 4 * 200, None),    # the pair BVH per lane
+    ("render_default_160x120_d4_ss2", 4 * 700, [7, 1000, 13]),  # Pulse-style chunks, each split again
+])
+def test_split_launches_equal_reference(key, limit, chunks):
+    c = CASES[key]
+    rgb, argb, r = gpu_render(scenes.get_scene(c["scene"]), c["W"], c["H"], c["depth"], c["ss"], c["additive"],
+                              c["frames"], c["sphere_seed"], c.get("jitter_seed", 0), chunks=chunks, launch_traces=limit)
+    g = _golden(key)
+    assert np.array_equal(argb, g["argb"]), key
+    assert rgb.tobytes() == g["rgb"].tobytes(), key
+    r.close()
+
+
+@pytest.mark.parametrize("key", ["render_default_3x2_d20_ss64", "render_default_2x2_d20_ss128",
+                                 "render_default_1x1_d20_ss256", "render_default_2x1_d8_ss64_add2"])
+def test_top_menu_rates_chunked(key):
+    """SSAA 64/128/256 (the top of Pulse's menu) one renderNext pixel at a time, at the default launch limit."""
+    c = CASES[key]
+    rgb, argb, r = gpu_render(scenes.get_scene(c["scene"]), c["W"], c["H"], c["depth"], c["ss"], c["additive"],
+                              c["frames"], c["sphere_seed"], c.get("jitter_seed", 0), chunks=[1])
+    g = _golden(key)
+    assert np.array_equal(argb, g["argb"]) and rgb.tobytes() == g["rgb"].tobytes(), key
+    r.close()
+
+
+def _renderer(scene, seed=1350490027, jitter=99):
+    from reflaxman_amd.render import Renderer
+    r = Renderer(sphere_seed=seed, jitter_seed=jitter)
+    r.set_scene(scene)
+    return r
+
+
+def test_split_streams_counters_and_rewind():
+    """A split frame leaves both random streams where one launch leaves them, counts the same events (stats kernel),
+    and rfx_frame_rng_rewind returns both streams to the frame's start (the saved start state, not a seed flip)."""
+    import torch
+    from reflaxman_amd.render import build_scene, make_frame
+    scene, cam = build_scene(scenes.get_scene("default"))
+    W, H = 96, 64
+    f = make_frame(cam, W, H, 6, 4, additive=True, additive_counter=1)
+    out = {}
+    for limit in (0, 16 * 333):
+        r = _renderer(scene)
+        r.set_launch_traces(limit)
+        start = r.get_rng()
+        rgb = torch.zeros(H * W * 3, dtype=torch.float32, device="cuda")
+        argb = torch.zeros(H * W, dtype=torch.int32, device="cuda")
+        cnt = torch.zeros(_lib.RFX_NCOUNTERS, dtype=torch.int64, device="cuda")
+        r.render_frame(f, rgb.data_ptr(), argb.data_ptr(), cnt.data_ptr())
+        r.synchronize()
+        end = r.get_rng()
+        assert end != start
+        _lib.check(_lib.load().rfx_frame_rng_rewind(r._h))
+        assert r.get_rng() == start, limit
+        # the rewound frame renders again to the same pixels
+        rgb2 = torch.zeros_like(rgb)
+        r.render_frame(f, rgb2.data_ptr(), 0)
+        r.synchronize()
+        assert torch.equal(rgb, rgb2) and r.get_rng() == end
+        out[limit] = (rgb.cpu().numpy().tobytes(), argb.cpu().numpy().tobytes(), end, cnt.cpu().numpy().tolist())
+        r.close()
+    assert out[0] == out[16 * 333]
+
+
+def test_split_frame_on_a_device_group():
+    """A device group's frame of more traces than one pass takes (3 members on device 0, launch limit forced low):
+    consecutive row-span passes with the random stream continued, equal to the single renderer's frames over 3 frames
+    (4x4 SSAA, additive accumulation), then rewound on member 0 and rendered again."""
+    import torch
+    from reflaxman_amd.render import build_scene, make_frame
+    scene, cam = build_scene(scenes.get_scene("default"))
+    W, H = 200, 150
+    L = _lib.load()
+    g = C.c_void_p()
+    devs = (C.c_int * 3)(0, 0, 0)
+    _lib.check(L.rfx_group_create(C.byref(g), devs, 3), "group_create")
+    _lib.check(L.rfx_group_set_scene(g, scene._h))
+    r0 = C.c_void_p(L.rfx_group_renderer(g, 0))
+    _lib.check(L.rfx_renderer_set_rng(r0, 1350490027, 99))
+    _lib.check(L.rfx_renderer_set_launch_traces(r0, 16 * 200 * 7))  # passes of 3 x 7 rows, the last one shorter
+    one = _renderer(scene)
+    rgb, argb = torch.zeros(H * W * 3, device="cuda"), torch.zeros(H * W, dtype=torch.int32, device="cuda")
+    rgb1, argb1 = torch.zeros_like(rgb), torch.zeros_like(argb)
+    for k in range(1, 4):
+        f = make_frame(cam, W, H, 5, 4, additive=True, additive_counter=k)
+        _lib.check(L.rfx_group_render_frame(g, C.byref(f), C.c_void_p(rgb.data_ptr()), C.c_void_p(argb.data_ptr()),
+                                            None), "group_render_frame")
+        one.render_frame(f, rgb1.data_ptr(), argb1.data_ptr())
+        torch.cuda.synchronize()
+        assert torch.equal(rgb, rgb1) and torch.equal(argb, argb1), k
+    # rewind the last group frame on member 0 (the saved start state) and render a fresh non-additive frame from it
+    _lib.check(L.rfx_frame_rng_rewind(r0))
+    _lib.check(L.rfx_frame_rng_rewind(one._h))
+    f = make_frame(cam, W, H, 5, 4)
+    _lib.check(L.rfx_group_render_frame(g, C.byref(f), C.c_void_p(rgb.data_ptr()), C.c_void_p(argb.data_ptr()), None))
+    one.render_frame(f, rgb1.data_ptr(), argb1.data_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(rgb, rgb1) and torch.equal(argb, argb1)
+    L.rfx_group_destroy(g)
+    one.close()
+
+
+def test_screenshot_over_2_32_samples():
+    """800x600 at 128x128 samples, depth 20 (Pulse's menu keys 1 and 8): 7.9e9 samples in one rfx_render_frame, split
+    into launches at the default limit; SHA-256 of the floats and the ARGB8 image equal the reference's frame
+    (tools/gen_golden.py, banded refharness)."""
+    c = CASES["pulse_screenshot_800x600_ss128"]
+    assert c["samples"] >= 1 << 32
+    rgb, argb, r = gpu_render(scenes.get_scene("default"), c["W"], c["H"], c["depth"], c["ss"],
+                              sphere_seed=c["RFX_SPHERE_SEED"])
+    assert sha(argb) == c["sha_argb"]
+    assert sha(rgb) == c["sha_f32"]
+    r.close()

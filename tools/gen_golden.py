@@ -287,6 +287,13 @@ def main():
         save_render("render_default_17x9_d8_ss16_add2", "default", 17, 9, 8, ss=16, additive=True, frames=2, jseed=5150,
                     use_file=False)
         save_render("render_default_6x5_d4_ss32", "default", 6, 5, 4, ss=32, use_file=False)
+        # the top of the menu (64, 128, 256 per axis: 4096 .. 65536 samples per pixel) at the screenshot depth, and 64
+        # with additive jitter over two frames
+        save_render("render_default_3x2_d20_ss64", "default", 3, 2, 20, ss=64, use_file=False)
+        save_render("render_default_2x2_d20_ss128", "default", 2, 2, 20, ss=128, use_file=False)
+        save_render("render_default_1x1_d20_ss256", "default", 1, 1, 20, ss=256, use_file=False)
+        save_render("render_default_2x1_d8_ss64_add2", "default", 2, 1, 8, ss=64, additive=True, frames=2, jseed=2718,
+                    use_file=False)
         save_render("render_planes_40x24_d6_ss3", "planes", 40, 24, 6, ss=3)
         # 3. additive progressive refinement (jitter stream explicit), 3 frames
         save_render("render_default_160x120_d15_add3", "default", 160, 120, 15, additive=True, frames=3,
@@ -355,6 +362,40 @@ def main():
         save_banded("hash_stress4096_3840x2160_d12_f2", "stress4096", 3840, 2160, 12, 1, 2)
         # the reference's screenshot workload (Pulse.cpp:156-178: renderBegin(20, ss, false), Full HD, 4x4 SSAA)
         save_banded("hash_default_1920x1080_d20_ss4", "default", 1920, 1080, 20, 4, 1, use_file=False)
+
+        # Screenshots of 2^32 samples and more (the renderer splits them into launches of fewer traces).  The
+        # reference's own Pulse would take hours on one core for these, so the frame is banded as above and its BMP is
+        # written by the reference's Texture::saveToFile (refharness savetex) from the frame's Color::argb words, which
+        # is what Pulse::screenshotRenderSave does (Pulse.cpp:200-205).  The route is first checked against the BMP the
+        # reference's Pulse itself wrote at 800x600 2x2 (pulse_screenshot_800x600_ss2).
+        def shot_bmp(argb, W, H):
+            src, fn = os.path.join(tmp, "shot.u32"), os.path.join(tmp, "shot.bmp")
+            np.ascontiguousarray(argb, np.uint32).tofile(src)
+            subprocess.run([HARNESS, "savetex", str(W), str(H), src, fn], check=True, capture_output=True)
+            return open(fn, "rb").read()
+
+        def save_shot(key, res_key, ss_key, W, H, ss):
+            if not want(key):
+                return
+            ref = cases["pulse_screenshot_800x600_ss2"]
+            _, a2 = banded_frame(tmp, "default", 800, 600, 20, 2, 0, ref["RFX_SPHERE_SEED"])
+            assert sha(shot_bmp(a2, 800, 600)) == ref["sha_bmp"], "banded frame + savetex != the reference Pulse's BMP"
+            t0 = time.time()
+            rgb, argb = banded_frame(tmp, "default", W, H, 20, ss, 0, ref["RFX_SPHERE_SEED"])
+            data = shot_bmp(argb, W, H)
+            cases[key] = dict(kind="pulse", res_key=res_key, ss_key=ss_key, W=W, H=H, ss=ss, depth=20, bytes=len(data),
+                              sha_bmp=sha(data), file=ref["file"], RFX_SPHERE_SEED=ref["RFX_SPHERE_SEED"],
+                              RFX_JITTER_SEED=ref["RFX_JITTER_SEED"], sha_f32=sha(rgb.tobytes()),
+                              sha_argb=sha(argb.tobytes()), samples=W * H * ss * ss,
+                              generated="refharness bandss (parallel row bands of Render::renderNext's pixel loop) + "
+                                        "refharness savetex; route checked against pulse_screenshot_800x600_ss2",
+                              cpu_wall_s=round(time.time() - t0, 1))
+            print(f"{key}: {time.time() - t0:.1f}s", flush=True)
+
+        # 800x600 at 128x128 (menu keys 1 and 8): 7.9e9 samples
+        save_shot("pulse_screenshot_800x600_ss128", 1, 8, 800, 600, 128)
+        # the screenshot the reference's ReadMe shows (ReadMe.md:30-32): Full HD (key 8) at 128x128 (key 8), 3.4e10 samples
+        save_shot("pulse_screenshot_1920x1080_ss128", 8, 8, 1920, 1080, 128)
 
         # C4 band: 4 rows at the middle of the 8K frame (stream advanced over the 2160 rows above)
         key = "band_synth16_7680x4320_d8_y2160_r4"
