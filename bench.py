@@ -1,8 +1,11 @@
 #!/usr/bin/env python3
 """bench.py -- Mrays/s of ReflaxMan's per-pixel trace loop on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1..c5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c1..c5|shot|shot128]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+`--gpus N` (N > 1) without a launcher starts the N ranks itself (a torch.distributed.run child job, rendezvous on
+127.0.0.1) and exits with its code; under a launcher, --gpus must equal WORLD_SIZE (else exit 2).
 
 Workload (BASELINE.json metric "Mrays/sec at 3840x2160 depth-8"): at N = 1 config
 C3 -- the synth16 scene (16 spheres, ground + back-wall quads = 4 textured
@@ -71,11 +74,20 @@ CONFIGS = {
     "c5": ("stress4096", 3840, 2160, 12, 1, "C5 stress4096: 4096 spheres + ground quad + sun"),
     "shot": ("default", 1920, 1080, 20, 4, "screenshot: Render's default scene, Full HD, 4x4 SSAA, depth 20 "
                                            "(Pulse.cpp:156-178, defaults.h:9)"),
+    "shot128": ("default", 1920, 1080, 20, 128, "the reference's ReadMe screenshot (ReadMe.md:30-32): Render's default "
+                                                "scene, Full HD, 128x128 SSAA, depth 20 (Pulse.cpp:10-34,156-178): "
+                                                "3.4e10 samples per frame, rendered as launches of 2^30 traces"),
 }
 # cpu_baseline row strides: about 5 s of the reference's single-core trace time per config (C5's CPU rate is
-# 0.0064 Mrays/s: every 270th row); SSAA configs time a centred band of this many rows instead
+# 0.0064 Mrays/s: every 270th row); SSAA configs time a band of rows instead: (first row or None = centred, rows).
+# shot128's band is its first row (31.5 M samples, ~28 s on one core): a centred band would first advance the random
+# stream over 1.7e10 draws.
 CPU_STRIDE = {"c1": 1, "c2": 4, "c3": 2, "c4": 16, "c5": 270}
-CPU_BAND_ROWS = {"shot": 160}
+CPU_BAND_ROWS = {"shot": (None, 160), "shot128": (0, 1)}
+# full-frame parity keys of configs whose manifest case is not named hash_<scene>_<W>x<H>_d<depth>_ss<ss>
+PARITY_CASE = {"shot128": "pulse_screenshot_1920x1080_ss128"}
+# steps / warmup when not given: a shot128 frame takes ~1.5 s
+DEFAULT_STEPS = {"shot128": (3, 1)}
 
 
 def frame_size(n: int, w0: int, h0: int, scaling: str):
@@ -123,14 +135,14 @@ def u8_diff(a: np.ndarray, b: np.ndarray) -> int:
     return int(max(np.abs(ch(a, s) - ch(b, s)).max() for s in (0, 8, 16))) if a.size else 0
 
 
-def cpu_baseline_band(desc, W, H, depth, ss, gpu_rgb, gpu_argb, rows):
+def cpu_baseline_band(desc, W, H, depth, ss, gpu_rgb, gpu_argb, rows, y0=None):
     """SSAA frames: the reference's CPU path (oracle/_ref/refharness bandss, Render::renderNext's pixel loop over the
-    unmodified sources) on a centred band of `rows` rows of the same frame, one host core; the band is also compared
-    with the GPU frame's."""
+    unmodified sources) on a band of `rows` rows of the same frame (centred unless y0 is given), one host core; the
+    band is also compared with the GPU frame's."""
     harness = os.path.join(ROOT, "oracle", "_ref", "refharness")
     if not os.path.exists(harness):
         return None, None
-    y0 = (H - rows) // 2
+    y0 = (H - rows) // 2 if y0 is None else y0
     with tempfile.TemporaryDirectory() as tmp:
         scene_path = desc.write(tmp)
         out = os.path.join(tmp, "band")
@@ -288,11 +300,33 @@ class SingleGpu:
         self.r.close()
 
 
-def main():
+def launcher_command(n: int, argv: list, port: int) -> list:
+    """The command that runs this bench as n ranks of one node (torch.distributed.run, rendezvous on 127.0.0.1)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+
+
+def launch_ranks(n: int, argv: list) -> int:
+    """`bench.py --gpus N` (N > 1) started without a launcher: run the N ranks as a child torch.distributed.run job and
+    return its exit code; rank 0's JSON line reaches this process's stdout directly.  Nothing in this process has
+    touched the GPU (torch is not even imported here), so the ranks own their devices."""
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = launcher_command(n, argv, port)
+    log("launching", n, "ranks:", " ".join(cmd))
+    return subprocess.run(cmd).returncode
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (GPUs of one node); N > 1 without WORLD_SIZE in the environment starts the N ranks "
+                         "itself (torch.distributed.run)")
+    ap.add_argument("--steps", type=int, default=None, help="timed frames (default 50; shot128: 3)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed frames before them (default 5; shot128: 1)")
     ap.add_argument("--prewarm-ms", type=float, default=250.0,
                     help="untimed frames for about this long before the warmup steps (GPU clock ramp); 0: none")
     ap.add_argument("--config", choices=sorted(CONFIGS), default=None,
@@ -323,11 +357,20 @@ def main():
                     help="N > 1: emit each frame's randDirs on its critical path, not during the last trace")
     ap.add_argument("--no-count-ahead", action="store_true",
                     help="N > 1: count and all-gather each frame's RNG blocks on its critical path, not during the last trace")
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world_env = os.environ.get("WORLD_SIZE")
+    if args.gpus is not None and args.gpus > 1 and world_env is None:
+        return launch_ranks(args.gpus, argv)
+    world = int(world_env or "1")
+    if args.gpus is not None and args.gpus != world:
+        log(f"--gpus {args.gpus} but WORLD_SIZE {world}: refusing to measure another number of GPUs than asked")
+        return 2
     rank = int(os.environ.get("RANK", "0"))
     cfg_name = args.config or ("c3" if world == 1 else "c4")
+    d_steps, d_warmup = DEFAULT_STEPS.get(cfg_name, (50, 5))
+    args.steps = d_steps if args.steps is None else args.steps
+    args.warmup = d_warmup if args.warmup is None else args.warmup
     c_scene, c_w, c_h, c_depth, c_ss, c_desc = CONFIGS[cfg_name]
     custom = any(v is not None for v in (args.scene, args.width, args.height, args.depth, args.ss))
     args.scene = args.scene or c_scene
@@ -336,8 +379,6 @@ def main():
     args.depth = args.depth or c_depth
     args.ss = args.ss or c_ss
     local = 0 if args.one_device else int(os.environ.get("LOCAL_RANK", str(rank)))
-    if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
 
     import torch
     import torch.distributed as dist
@@ -422,6 +463,7 @@ def main():
         first_argb = argb[: H * W].view(H, W).cpu().numpy().view(np.uint32)
         man = json.load(open(os.path.join(ROOT, "tests", "golden", "manifest.json")))["cases"]
         key = f"hash_{args.scene}_{W}x{H}_d{depth}" + (f"_ss{ss}" if ss != 1 else "")
+        key = PARITY_CASE.get(cfg_name, key) if not custom else key
         if key in man:
             ok_f = sha(first_rgb.tobytes()) == man[key]["sha_f32"]
             ok_a = sha(first_argb.tobytes()) == man[key]["sha_argb"]
@@ -688,8 +730,8 @@ def main():
     if world == 1 and not args.no_cpu_baseline:
         log("cpu_baseline: reference CPU path on a row sample of the same frame ...")
         if ss != 1:
-            cb, delta = cpu_baseline_band(desc, W, H, depth, ss, first_rgb, first_argb,
-                                          CPU_BAND_ROWS.get(cfg_name, 16) if not custom else 16)
+            y0b, nrows = CPU_BAND_ROWS.get(cfg_name, (None, 16)) if not custom else (None, 16)
+            cb, delta = cpu_baseline_band(desc, W, H, depth, ss, first_rgb, first_argb, nrows, y0b)
         else:
             stride = args.cpu_stride or (2 if custom else CPU_STRIDE[cfg_name])
             cb, delta = cpu_baseline(desc, W, H, depth, first_rgb, first_argb, stride)
@@ -707,4 +749,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -65,3 +65,34 @@ def test_no_committed_line_has_frac_above_one():
                 f = d["roofline"].get("frac")
                 assert f is None or 0 <= f <= 1, (p, f)
     assert seen > 0
+
+
+def test_gpus_n_without_launcher_starts_the_ranks(monkeypatch):
+    """`bench.py --gpus N` (N > 1) with no WORLD_SIZE runs N ranks as a torch.distributed.run child job (rendezvous on
+    127.0.0.1, the same arguments) and returns its exit code -- it never measures one GPU and calls it N."""
+    import subprocess
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    seen = {}
+
+    class Done:
+        returncode = 7
+
+    def fake_run(cmd, *a, **k):
+        seen["cmd"] = cmd
+        return Done()
+
+    monkeypatch.setattr(subprocess, "run", fake_run)
+    argv = ["--gpus", "2", "--steps", "3", "--one-device", "--backend", "gloo"]
+    assert bench.main(argv) == 7
+    cmd = seen["cmd"]
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=2" in cmd and "--master-addr=127.0.0.1" in cmd and "--nnodes=1" in cmd
+    assert cmd[-len(argv) - 1:] == [os.path.abspath(bench.__file__)] + argv
+    port = [c for c in cmd if c.startswith("--master-port=")]
+    assert len(port) == 1 and 0 < int(port[0].split("=")[1]) < 65536
+
+
+def test_gpus_must_match_the_launchers_world(monkeypatch):
+    """Under a launcher, --gpus must equal WORLD_SIZE: a mismatch exits 2 before anything is measured."""
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    assert bench.main(["--gpus", "4"]) == 2

@@ -77,6 +77,7 @@ VARIANTS = {
     "nocullsmall": ["RFX_NOCULL_MAX_TILES=8192"],
     "large6": ["RFX_WAVES_PER_EU_LARGE=6"],
     "large5": ["RFX_WAVES_PER_EU_LARGE=5"],
+    "scanall": ["RFX_SCAN_EMIT_BLOCKS=0"],
 }
 
 
