@@ -44,6 +44,11 @@ typedef struct rfx_renderer rfx_renderer;
 
 int rfx_abi_version(void);
 const char *rfx_last_error(void);
+/* Compile-time options of this build (A/B variants, tools/ab.py), as bits: per-view chunk lists of large scenes
+ * (RFX_PRIM_LARGE, off by default), per-view masks of per-pixel-loop SSAA frames (RFX_PRIM_SSAA, off), of the
+ * one-lane-per-sample SSAA modes (RFX_PRIM_LANES, on), one-light kernel instantiations (RFX_ONE_LIGHT, on). */
+enum { RFX_BUILD_PRIM_LARGE = 1, RFX_BUILD_PRIM_SSAA = 2, RFX_BUILD_PRIM_LANES = 4, RFX_BUILD_ONE_LIGHT = 8 };
+int rfx_build_options(void);
 
 /* ---------------------------------------------------------------- Scene */
 /* Scene(const Color & diffLightColor, float diffLightPower)  -- Scene.cpp:10-15 */
@@ -298,6 +303,12 @@ int rfx_kat_texels(rfx_renderer *r, int texture, const float *in, uint64_t n, fl
 int rfx_kat_powf(rfx_renderer *r, const float *xy, uint64_t n, float *out);
 int rfx_kat_argb(rfx_renderer *r, const float *rgb, uint64_t n, uint32_t *out);
 int rfx_kat_powf_cube(rfx_renderer *r, uint64_t counts[2]);
+/* The kernel-argument layout the bounce loops rely on (rfx_trace.h launder_scene / kernarg_params: DevScene at kernarg
+ * offset 0, FrameParams after it): a one-lane kernel of the trace kernels' signature compares the records read through
+ * the kernarg segment pointer with its by-value arguments.  out[0] / out[1] = differing words of the scene record / the
+ * frame parameters (0 expected), out[2] = 1 if the build reads the scene record that way.  swapped = 1 runs the same
+ * check in a kernel declared (FrameParams, DevScene): the check must report differences there. */
+int rfx_kat_kernarg(rfx_renderer *r, int swapped, uint32_t out[3]);
 
 #ifdef __cplusplus
 }

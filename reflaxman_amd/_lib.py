@@ -42,6 +42,7 @@ class Frame(C.Structure):
 SIGNATURES = [
     ("rfx_abi_version", C.c_int, []),
     ("rfx_last_error", C.c_char_p, []),
+    ("rfx_build_options", C.c_int, []),
     ("rfx_scene_create", C.c_void_p, [C.c_float] * 4),
     ("rfx_scene_destroy", None, [C.c_void_p]),
     ("rfx_scene_add_sphere", C.c_int, [C.c_void_p, _fp, C.c_float, C.c_int, _fp, C.c_float, C.c_float]),
@@ -112,6 +113,7 @@ SIGNATURES = [
     ("rfx_kat_powf", C.c_int, [C.c_void_p, _fp, C.c_uint64, _fp]),
     ("rfx_kat_argb", C.c_int, [C.c_void_p, _fp, C.c_uint64, _u32p]),
     ("rfx_kat_powf_cube", C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
+    ("rfx_kat_kernarg", C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_uint32)]),
 ]
 
 _lib = None

@@ -49,6 +49,7 @@ hipError_t launch_bounce_lds(int cfg, uint32_t groups, const DevScene &S, const 
 hipError_t launch_kat(int what, const DevScene &S, int tex, const void *in, const int32_t *objs, uint32_t n, void *out,
                       hipStream_t st);
 hipError_t launch_kat_powf_cube(uint32_t first, uint32_t n, unsigned long long *counts, hipStream_t st);
+hipError_t launch_kat_kernarg(const DevScene &S, const FrameParams &P, int swapped, uint32_t *out, hipStream_t st);
 }  // namespace rfx
 
 using namespace rfx;
@@ -456,6 +457,9 @@ constexpr size_t kPrimLargeWords = 12;  // per wave tile, large scenes (rfx_trac
 #ifndef RFX_PRIM_LARGE
 #define RFX_PRIM_LARGE 0
 #endif
+#ifndef RFX_ONE_LIGHT
+#define RFX_ONE_LIGHT 1  // one-light kernel instantiations (rfx_trace.h kCfgOneLight; -DRFX_ONE_LIGHT=0 turns them off)
+#endif
 #ifndef RFX_BOUNCE_GROUPS_PER_CU
 #define RFX_BOUNCE_GROUPS_PER_CU 14
 #endif
@@ -683,6 +687,12 @@ extern "C" void rfx_renderer_destroy(rfx_renderer *r)
     if (e) (void)hipEventDestroy(e);
   if (r->own_stream) (void)hipStreamDestroy(r->own_stream);
   delete r;
+}
+
+extern "C" int rfx_build_options(void)
+{
+  return (RFX_PRIM_LARGE ? RFX_BUILD_PRIM_LARGE : 0) | (RFX_PRIM_SSAA ? RFX_BUILD_PRIM_SSAA : 0) |
+         (RFX_PRIM_LANES ? RFX_BUILD_PRIM_LANES : 0) | (RFX_ONE_LIGHT ? RFX_BUILD_ONE_LIGHT : 0);
 }
 
 extern "C" int rfx_renderer_set_launch_traces(rfx_renderer *r, uint64_t max_traces)
@@ -1506,7 +1516,7 @@ static int trace_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *rd, float
     const uint64_t waves = (pl.traces + 63) / 64;
     const uint32_t groups = (uint32_t)std::min<uint64_t>((waves + 1) / 2, (uint64_t)r->cus * RFX_BOUNCE_GROUPS_PER_CU);
     const int cfg = 1 | (r->dev.n_light > 32 ? 2 : 0) | (small ? 4 : 0) | (r->dev.n_pln ? 8 : 0) |  // rfx_trace.h kCfg*
-                    (r->dev.n_light == 1 ? 32 : 0);  // kCfgOneLight (rfx_trace_plain_park.hip: else the general form)
+                    (RFX_ONE_LIGHT && r->dev.n_light == 1 ? 32 : 0);  // kCfgOneLight (rfx_trace_plain_park.hip)
     if (sort_queue) HIP_CHECK(launch_queue_sort(r->d_qctr, r->d_qkey, r->d_qctr + 2, r->d_qorder, st));
     // a BVH whose nodes fit the workgroup's LDS (56 B each beside the stacks: up to ~2,100 nodes, i.e. 4,200 spheres):
     // the LDS-staged bounce kernel, one 16-wave workgroup per CU (C5 trace + bounce -4..6%, tools/ab.py); else the
@@ -2075,6 +2085,26 @@ extern "C" int rfx_kat_argb(rfx_renderer *r, const float *rgb, uint64_t n, uint3
 {
   if (!r || (n && (!rgb || !out))) return fail(RFX_ERR_ARG, "kat_argb: bad args");
   return kat_run(r, 3, 0, rgb, (size_t)n * 3, nullptr, n, out, (size_t)n);
+}
+
+extern "C" int rfx_kat_kernarg(rfx_renderer *r, int swapped, uint32_t out[3])
+{
+  if (!r || !out) return fail(RFX_ERR_ARG, "kat_kernarg: bad args");
+  if (!r->has_scene) return fail(RFX_ERR_STATE, "kat_kernarg: no scene uploaded");
+  int rc;
+  if ((rc = set_dev(r)) != RFX_OK) return rc;
+  FrameParams P;
+  uint32_t *w = (uint32_t *)&P;  // every word distinct, so a shifted read cannot match by accident
+  for (size_t i = 0; i < sizeof(P) / 4; ++i) w[i] = 0x9E3779B9u * (uint32_t)(i + 1);
+  uint32_t *d = nullptr;
+  hipError_t e = hipMalloc(&d, 3 * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMemsetAsync(d, 0xFF, 3 * sizeof(uint32_t), r->stream);
+  if (e == hipSuccess) e = launch_kat_kernarg(r->dev, P, swapped, d, r->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(r->stream);
+  if (e == hipSuccess) e = hipMemcpy(out, d, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  if (e != hipSuccess) return fail(RFX_ERR_HIP, "kat_kernarg: %s", hipGetErrorString(e));
+  return RFX_OK;
 }
 
 // ============================================================== internals shared with rfx_group.cpp (rfx_internal.h)

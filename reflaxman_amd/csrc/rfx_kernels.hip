@@ -606,6 +606,36 @@ __global__ __launch_bounds__(kKatThreads) void kat_powf_cube(uint32_t first, uin
   }
 }
 
+// The kernel-argument layout the bounce loops read through the kernarg segment pointer (rfx_trace.h launder_scene,
+// kernarg_params): the laundered DevScene and FrameParams against the by-value arguments, word by word.  out[0] / out[1]:
+// words of the DevScene / FrameParams that differ (0 expected), out[2]: 1 when the build reads the record laundered.
+// kat_kernarg_swapped takes the arguments the other way round -- what a kernel with a swapped signature would read --
+// so the test can show the check catches it.
+template <bool SWAPPED>
+__device__ __forceinline__ void kernarg_compare(const DevScene &S, const FrameParams &P, uint32_t *out)
+{
+  const uint32_t *ps = (const uint32_t *)&P, *qs = (const uint32_t *)&kernarg_params();
+  uint32_t bad_p = 0, bad_s = 0;
+  for (size_t i = 0; i < sizeof(FrameParams) / 4; ++i) bad_p += ps[i] != qs[i] ? 1u : 0u;
+#ifdef RFX_LAUNDER_SCENE
+  const uint32_t *a = (const uint32_t *)&S, *b = (const uint32_t *)&launder_scene<true>(S);
+  for (size_t i = 0; i < sizeof(DevScene) / 4; ++i) bad_s += a[i] != b[i] ? 1u : 0u;
+  out[2] = 1;
+#else
+  out[2] = 0;
+#endif
+  out[0] = bad_s;
+  out[1] = bad_p;
+}
+__global__ void kat_kernarg(DevScene S, FrameParams P, uint32_t *out)
+{
+  if (threadIdx.x == 0 && blockIdx.x == 0) kernarg_compare<false>(S, P, out);
+}
+__global__ void kat_kernarg_swapped(FrameParams P, DevScene S, uint32_t *out)
+{
+  if (threadIdx.x == 0 && blockIdx.x == 0) kernarg_compare<true>(S, P, out);
+}
+
 // Color::argb (Color.cpp:114-117) as the epilogue evaluates it: rgb n x 3 -> out n
 __global__ __launch_bounds__(kKatThreads) void kat_argb(const float *rgb, uint32_t n, uint32_t *out)
 {
@@ -705,6 +735,13 @@ static void launch_mode_cfg(bool stats, int mode, int cfg, dim3 grid, const DevS
 }
 
 static dim3 kat_grid(uint32_t n) { return dim3((n + kKatThreads - 1) / kKatThreads); }
+
+hipError_t launch_kat_kernarg(const DevScene &S, const FrameParams &P, int swapped, uint32_t *out, hipStream_t st)
+{
+  if (swapped) hipLaunchKernelGGL(kat_kernarg_swapped, dim3(1), dim3(64), 0, st, P, S, out);
+  else hipLaunchKernelGGL(kat_kernarg, dim3(1), dim3(64), 0, st, S, P, out);
+  return hipGetLastError();
+}
 
 hipError_t launch_kat(int what, const DevScene &S, int tex, const void *in, const int32_t *objs, uint32_t n, void *out,
                       hipStream_t st)

@@ -22,6 +22,9 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <cstddef>
+#include <type_traits>
+
 #include "rfx_math.h"
 #include "rfx_powf.h"
 #include "rfx_types.h"
@@ -1489,6 +1492,15 @@ __device__ __forceinline__ const DevScene &launder_scene(const DevScene &S)
 // by an empty asm: every use reloads them with scalar loads where it stands, so their values are not held in SGPRs
 // across a bounce loop (with RFX_LAUNDER_PARAMS: the epilogue and the park ids; the RFX_SSAA_LDS_STATE sample loop)
 constexpr size_t kParamsOff = (sizeof(DevScene) + alignof(FrameParams) - 1) / alignof(FrameParams) * alignof(FrameParams);
+// The layout both readers assume, checked where it is defined (host and device passes): by-value kernel arguments are
+// laid out like the members of a struct, so (DevScene, FrameParams, ...) puts the record at 0 and the parameters at
+// kParamsOff.  Every kernel that reads them this way asserts its own signature (kKernargSig, in its body), and
+// tests/test_gpu_kat.py::test_kernarg_layout compares the laundered reads with the by-value arguments on the device.
+struct KernargPair { DevScene S; FrameParams P; };
+static_assert(offsetof(KernargPair, S) == 0 && offsetof(KernargPair, P) == kParamsOff,
+              "kernel-argument layout: DevScene at offset 0, FrameParams at kParamsOff");
+template <class F>
+constexpr bool kKernargSig = std::is_same<F, void (*)(DevScene, FrameParams)>::value;
 template <bool LAUNDER = true>  // false: the plain kernarg reference, which the compiler may keep in registers
 __device__ __forceinline__ const FrameParams &kernarg_params()
 {
@@ -1966,6 +1978,7 @@ template <bool STATS, int MODE, int CFG>
 __global__ __launch_bounds__(kWgThreads) __attribute__((amdgpu_waves_per_eu(
     (CFG & kCfgSmall) ? RFX_WAVES_PER_EU : RFX_WAVES_PER_EU_LARGE))) void trace_kernel(DevScene S, FrameParams P)
 {
+  static_assert(kKernargSig<decltype(&trace_kernel<STATS, MODE, CFG>)>, "launder_scene / kernarg_params layout");
   constexpr bool CULL = (CFG & kCfgCull) != 0, MANYL = (CFG & kCfgManyLights) != 0, SMALL = (CFG & kCfgSmall) != 0;
   constexpr bool PLANES = (CFG & kCfgPlanes) != 0, PARK = MODE == kModePlain && !STATS && (CFG & kCfgPark) != 0;
   constexpr bool ONEL = (CFG & kCfgOneLight) != 0;  // exactly one light: the light loops unrolled
@@ -2537,6 +2550,7 @@ struct Refill {
 template <int CFG>
 __global__ RFX_TRACE_BOUNDS void bounce_kernel(DevScene S, FrameParams P)
 {
+  static_assert(kKernargSig<decltype(&bounce_kernel<CFG>)>, "launder_scene / kernarg_params layout");
   constexpr bool CULL = (CFG & kCfgCull) != 0, MANYL = (CFG & kCfgManyLights) != 0, SMALL = (CFG & kCfgSmall) != 0;
   constexpr bool PLANES = (CFG & kCfgPlanes) != 0;
   __shared__ float lut[256];
@@ -2568,6 +2582,7 @@ template <int CFG>
 __global__ __launch_bounds__(kLdsBvhThreads) __attribute__((amdgpu_waves_per_eu(4)))
 void bounce_kernel_lds(DevScene S, FrameParams P)
 {
+  static_assert(kKernargSig<decltype(&bounce_kernel_lds<CFG>)>, "launder_scene / kernarg_params layout");
   constexpr bool CULL = (CFG & kCfgCull) != 0, MANYL = (CFG & kCfgManyLights) != 0, SMALL = (CFG & kCfgSmall) != 0;
   constexpr bool PLANES = (CFG & kCfgPlanes) != 0;
   static_assert(!SMALL, "large scenes only");

@@ -47,6 +47,7 @@ def kept(lo, hi, o, d, ref, mt, rng, fused):
             t0 = np.fmax(np.fmax(mn[:, 0], mn[:, 1]), np.fmax(mn[:, 2], F(0)))
             t1 = np.fmin(np.fmin(mx[:, 0], mx[:, 1]), mx[:, 2])
             return ~(t0 > t1 * F(1.00001) + F(1e-30))
+        elif fused:  # RFX_BVH_FMA without pre-widening (RFX_BVH_PREWIDE=0)
             m = fmaf(np.full_like(mt, K_CULL_REL), mt, dm)
             oi = o * inv
             a = fmaf(lo - m[:, None], inv, -oi)

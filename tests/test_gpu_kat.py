@@ -189,3 +189,24 @@ def test_triangle_reject_before_divide_decides_like_the_divide():
     r.close()
     assert not np.isnan(out[:, 14]).any(), int(np.isnan(out[:, 14]).sum())
     assert 0.2 * n < out[:, 14].sum() < 0.9 * n  # both outcomes well represented
+
+
+@pytest.mark.parametrize("scene_name", ["default", "stress4096"])
+def test_kernarg_layout(scene_name):
+    """The bounce loops read the scene record and the frame parameters through the kernarg segment pointer
+    (rfx_trace.h launder_scene / kernarg_params), assuming DevScene at offset 0 and FrameParams after it.  A kernel of
+    the trace kernels' signature finds every word of both equal to its by-value arguments; one declared with the two
+    arguments swapped finds differences, so the check would catch a kernel whose signature moved them."""
+    import ctypes as C
+    from reflaxman_amd import _lib, scenes
+    from reflaxman_amd.render import build_scene
+    scene, _ = build_scene(scenes.get_scene(scene_name))
+    r = Renderer()
+    r.set_scene(scene)
+    L = _lib.load()
+    good, swapped = (C.c_uint32 * 3)(), (C.c_uint32 * 3)()
+    _lib.check(L.rfx_kat_kernarg(r._h, 0, good), "kat_kernarg")
+    _lib.check(L.rfx_kat_kernarg(r._h, 1, swapped), "kat_kernarg")
+    assert list(good) == [0, 0, 1], list(good)  # (1: this build reads the record laundered)
+    assert swapped[0] > 0 and swapped[1] > 0, list(swapped)
+    r.close()
