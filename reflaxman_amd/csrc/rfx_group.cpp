@@ -106,15 +106,18 @@ std::vector<uint32_t> balanced_bounds(const std::vector<uint32_t> &bounds, const
 struct rfx_group {
   std::vector<int> dev;
   std::vector<rfx_renderer *> r;
-  std::vector<hipStream_t> own;                  // members 1..n-1: their streams (member 0: the caller's)
+  std::vector<hipStream_t> own;                  // per member: the stream its counts, emits and traces run on
+  std::vector<hipStream_t> cp;                   // per member: the stream its band copies to the caller's frame run on
   std::vector<uint32_t *> cnt[2];                // per member: n x bps count words, double-buffered by frame parity
   uint64_t cnt_words = 0, bps = 0;
-  std::vector<float *> rgb;                      // members 1..n-1: whole-frame scratch (their band rows written)
-  std::vector<uint32_t *> argb;
+  std::vector<float *> rgb[2];                   // per member: whole-frame scratch (its band rows written), double-
+  std::vector<uint32_t *> argb[2];               // buffered by pass parity: pass k traces while pass k - 1's copy runs
   size_t px_cap = 0;
-  float *rgb0 = nullptr;                         // member 0's float frame of ARGB8-only frames (d_rgb NULL)
+  float *rgb0 = nullptr;                         // a one-member frame's floats when the caller wants ARGB8 only
   size_t rgb0_cap = 0;
-  std::vector<hipEvent_t> ev_start, ev_cnt, ev_emit[2], ev_t1, ev_done;
+  std::vector<hipEvent_t> ev_start, ev_cnt, ev_emit[2], ev_t1, ev_copied[2];
+  std::vector<uint64_t> seq;                     // members' random-stream state counters after the group's last pass
+  bool seq_ok = false;
   std::vector<uint32_t> bounds;
   bool fixed = false;
   uint32_t W = 0, H = 0;
@@ -132,17 +135,22 @@ static void destroy(rfx_group *g)
   {
     (void)hipSetDevice(g->dev[i]);
     if (i < g->own.size() && g->own[i]) (void)hipStreamSynchronize(g->own[i]);
+    if (i < g->cp.size() && g->cp[i]) (void)hipStreamSynchronize(g->cp[i]);
   }
   for (size_t i = 0; i < g->dev.size(); ++i)
   {
     (void)hipSetDevice(g->dev[i]);
     for (int b = 0; b < 2; ++b)
+    {
       if (i < g->cnt[b].size()) (void)hipFree(g->cnt[b][i]);
-    if (i < g->rgb.size()) (void)hipFree(g->rgb[i]);
-    if (i < g->argb.size()) (void)hipFree(g->argb[i]);
-    for (std::vector<hipEvent_t> *v : {&g->ev_start, &g->ev_cnt, &g->ev_emit[0], &g->ev_emit[1], &g->ev_t1, &g->ev_done})
+      if (i < g->rgb[b].size()) (void)hipFree(g->rgb[b][i]);
+      if (i < g->argb[b].size()) (void)hipFree(g->argb[b][i]);
+    }
+    for (std::vector<hipEvent_t> *v : {&g->ev_start, &g->ev_cnt, &g->ev_emit[0], &g->ev_emit[1], &g->ev_t1,
+                                       &g->ev_copied[0], &g->ev_copied[1]})
       if (i < v->size() && (*v)[i]) (void)hipEventDestroy((*v)[i]);
     if (i < g->own.size() && g->own[i]) (void)hipStreamDestroy(g->own[i]);
+    if (i < g->cp.size() && g->cp[i]) (void)hipStreamDestroy(g->cp[i]);
   }
   if (g->rgb0)
   {
@@ -183,27 +191,32 @@ static int create(rfx_group *g, const int *devices, int n)
   for (int i = 0; i < n; ++i)
   {
     GCHECK(hipSetDevice(g->dev[i]));
-    hipStream_t s = nullptr;
-    if (i > 0) GCHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    hipStream_t s = nullptr, c = nullptr;
+    GCHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     g->own.push_back(s);
-    hipEvent_t e[6];
+    GCHECK(hipStreamCreateWithFlags(&c, hipStreamNonBlocking));
+    g->cp.push_back(c);
+    hipEvent_t e[7];
     for (hipEvent_t &x : e) GCHECK(hipEventCreate(&x));
     g->ev_start.push_back(e[0]);
     g->ev_cnt.push_back(e[1]);
     g->ev_emit[0].push_back(e[2]);
     g->ev_emit[1].push_back(e[3]);
     g->ev_t1.push_back(e[4]);
-    g->ev_done.push_back(e[5]);
-    // the double-buffer waits of the first two frames find recorded events
-    hipStream_t st = i > 0 ? s : rfx_detail_stream(g->r[0]);
-    GCHECK(hipEventRecord(e[2], st));
-    GCHECK(hipEventRecord(e[3], st));
-    g->cnt[0].push_back(nullptr);
-    g->cnt[1].push_back(nullptr);
-    g->rgb.push_back(nullptr);
-    g->argb.push_back(nullptr);
+    g->ev_copied[0].push_back(e[5]);
+    g->ev_copied[1].push_back(e[6]);
+    // the double-buffer waits of the first two passes find recorded events
+    for (int k = 2; k < 7; ++k)
+      if (k != 4) GCHECK(hipEventRecord(e[k], s));
+    for (int b = 0; b < 2; ++b)
+    {
+      g->cnt[b].push_back(nullptr);
+      g->rgb[b].push_back(nullptr);
+      g->argb[b].push_back(nullptr);
+    }
   }
   g->acc.assign(n, 0.0);
+  g->seq.assign(n, 0);
   return RFX_OK;
 }
 
@@ -314,14 +327,17 @@ static int ensure_buffers(rfx_group *g, const rfx_frame &f0, size_t m)
   const size_t px = (size_t)f0.width * f0.height;
   if (px > g->px_cap)
   {
-    for (size_t i = 1; i < n; ++i)
+    for (size_t i = 0; i < n; ++i)
     {
       GCHECK(hipSetDevice(g->dev[i]));
-      GCHECK(hipStreamSynchronize(g->own[i]));
-      (void)hipFree(g->rgb[i]); (void)hipFree(g->argb[i]);
-      g->rgb[i] = nullptr; g->argb[i] = nullptr;
-      GCHECK(hipMalloc(&g->rgb[i], px * 3 * sizeof(float)));
-      GCHECK(hipMalloc(&g->argb[i], px * sizeof(uint32_t)));
+      GCHECK(hipDeviceSynchronize());  // traces and copies still in flight use the old scratch
+      for (int b = 0; b < 2; ++b)
+      {
+        (void)hipFree(g->rgb[b][i]); (void)hipFree(g->argb[b][i]);
+        g->rgb[b][i] = nullptr; g->argb[b][i] = nullptr;
+        GCHECK(hipMalloc(&g->rgb[b][i], px * 3 * sizeof(float)));
+        GCHECK(hipMalloc(&g->argb[b][i], px * sizeof(uint32_t)));
+      }
     }
     g->px_cap = px;
   }
@@ -332,8 +348,14 @@ static int ensure_buffers(rfx_group *g, const rfx_frame &f0, size_t m)
 // within [y0, y1)), the random stream runs over the pass's rows (rfx_frame span_begin / span_end).  A frame is one pass
 // over all rows, or -- 2^31 traces or more -- consecutive passes of row spans (the stream continues from pass to pass on
 // every member, as Render.cpp:136-215's cursor does).
+//
+// Each member counts, emits and traces on its own stream into its own scratch frame (double-buffered by pass parity), and
+// copies its band rows into the caller's frame on a copy stream: so member i's copy of pass k overlaps its trace of pass
+// k + 1.  Only the copies wait for the caller's stream (its work before the call may still read or write the frame); the
+// traces wait for it only when a member's random stream may differ from member 0's (a frame rendered on member 0 alone,
+// a rewind, set_rng: the stream-state counters moved) or the frame accumulates onto the caller's pixels.
 static int group_pass(rfx_group *g, const rfx_frame *f, uint32_t y0, uint32_t y1, const std::vector<uint32_t> &bd,
-                      float *d_rgb, uint32_t *d_argb, float *img0, hipStream_t s0)
+                      float *d_rgb, uint32_t *d_argb, hipStream_t s0)
 {
   const size_t m = bd.size() - 1;
   const uint32_t W = f->width;
@@ -351,19 +373,23 @@ static int group_pass(rfx_group *g, const rfx_frame *f, uint32_t y0, uint32_t y1
   RCHECK(ensure_buffers(g, fr[0], m));
   const int b = (int)(g->frames & 1);
   const bool accumulate = f->additive_counter > 1;
-  std::vector<hipStream_t> st(m);
-  for (size_t i = 0; i < m; ++i) st[i] = i ? g->own[i] : s0;
-  // 0. after the caller's work on its stream; member 0's stream state is the group's
+  const std::vector<hipStream_t> &st = g->own;
+  // 0. the caller's work on its stream before this pass
   GCHECK(hipSetDevice(g->dev[0]));
   GCHECK(hipEventRecord(g->ev_start[0], s0));
+  bool handoff = !g->seq_ok;
+  for (size_t i = 0; i < g->n(); ++i) handoff = handoff || rfx_detail_state_seq(g->r[i]) != g->seq[i];
   const uint32_t jitter = rfx_detail_jitter(g->r[0]);
-  for (size_t i = 1; i < m; ++i)
+  for (size_t i = 0; i < m; ++i)
   {
     GCHECK(hipSetDevice(g->dev[i]));
-    GCHECK(hipStreamWaitEvent(st[i], g->ev_start[0], 0));
-    GCHECK(hipMemcpyPeerAsync(rfx_detail_seed_word(g->r[i]), g->dev[i], rfx_detail_seed_word(g->r[0]), g->dev[0],
-                              sizeof(uint32_t), st[i]));
+    if (handoff || accumulate) GCHECK(hipStreamWaitEvent(st[i], g->ev_start[0], 0));
+    // member 0's stream state is the group's: handed to the others when theirs may differ
+    if (handoff && i)
+      GCHECK(hipMemcpyPeerAsync(rfx_detail_seed_word(g->r[i]), g->dev[i], rfx_detail_seed_word(g->r[0]), g->dev[0],
+                                sizeof(uint32_t), st[i]));
     rfx_detail_set_jitter(g->r[i], jitter);
+    GCHECK(hipStreamWaitEvent(st[i], g->ev_copied[b][i], 0));  // the copy of two passes ago has read scratch b
   }
   // 1. each member counts its slice of the pass's random stream and pushes it to every other member
   const size_t sl = g->bps * sizeof(uint32_t);
@@ -379,35 +405,37 @@ static int group_pass(rfx_group *g, const rfx_frame *f, uint32_t y0, uint32_t y1
     }
     GCHECK(hipEventRecord(g->ev_cnt[i], st[i]));
   }
-  // 2. every slice arrived: emit the band's randDirs and trace the band; 3. bands to the caller's frame
+  // 2. every slice arrived: emit the band's randDirs and trace the band into scratch; 3. the band rows to the caller's
+  // frame on the member's copy stream
   for (size_t i = 0; i < m; ++i)
   {
     GCHECK(hipSetDevice(g->dev[i]));
     for (size_t j = 0; j < m; ++j)
       if (j != i) GCHECK(hipStreamWaitEvent(st[i], g->ev_cnt[j], 0));
     const uint64_t r0 = bd[i], rows = bd[i + 1] - r0;
-    float *img = i ? g->rgb[i] : img0;
-    uint32_t *a = i ? (d_argb ? g->argb[i] : nullptr) : d_argb;
-    if (accumulate && i)  // the accumulated rows this member adds to (Render.cpp:191-194)
+    float *img = g->rgb[b][i];
+    uint32_t *a = g->argb[b][i];
+    if (accumulate)  // the accumulated rows this member adds to (Render.cpp:191-194)
       GCHECK(hipMemcpyPeerAsync(img + r0 * W * 3, g->dev[i], d_rgb + r0 * W * 3, g->dev[0], rows * W * 12, st[i]));
     const uint32_t j0 = rfx_detail_jitter(g->r[i]);
-    RCHECK(rfx_render_frame_counted_ev(g->r[i], &fr[i], (uint32_t)m, g->cnt[b][i], img, a, nullptr, st[i],
-                                       g->ev_emit[b][i]));
+    RCHECK(rfx_render_frame_counted_ev(g->r[i], &fr[i], (uint32_t)m, g->cnt[b][i], img, d_argb ? a : nullptr, nullptr,
+                                       st[i], g->ev_emit[b][i]));
     rfx_detail_set_rewindable(g->r[i], j0);
     GCHECK(hipSetDevice(g->dev[i]));
     GCHECK(hipEventRecord(g->ev_t1[i], st[i]));
-    if (i)
-    {
-      if (d_rgb)
-        GCHECK(hipMemcpyPeerAsync(d_rgb + r0 * W * 3, g->dev[0], img + r0 * W * 3, g->dev[i], rows * W * 12, st[i]));
-      if (d_argb)
-        GCHECK(hipMemcpyPeerAsync(d_argb + r0 * W, g->dev[0], a + r0 * W, g->dev[i], rows * W * 4, st[i]));
-      GCHECK(hipEventRecord(g->ev_done[i], st[i]));
-    }
+    GCHECK(hipStreamWaitEvent(g->cp[i], g->ev_t1[i], 0));
+    GCHECK(hipStreamWaitEvent(g->cp[i], g->ev_start[0], 0));  // the caller's frame is free to be written
+    if (d_rgb)
+      GCHECK(hipMemcpyPeerAsync(d_rgb + r0 * W * 3, g->dev[0], img + r0 * W * 3, g->dev[i], rows * W * 12, g->cp[i]));
+    if (d_argb)
+      GCHECK(hipMemcpyPeerAsync(d_argb + r0 * W, g->dev[0], a + r0 * W, g->dev[i], rows * W * 4, g->cp[i]));
+    GCHECK(hipEventRecord(g->ev_copied[b][i], g->cp[i]));
   }
   GCHECK(hipSetDevice(g->dev[0]));
-  for (size_t i = 1; i < m; ++i) GCHECK(hipStreamWaitEvent(s0, g->ev_done[i], 0));
+  for (size_t i = 0; i < m; ++i) GCHECK(hipStreamWaitEvent(s0, g->ev_copied[b][i], 0));
   ++g->frames;
+  for (size_t i = 0; i < g->n(); ++i) g->seq[i] = rfx_detail_state_seq(g->r[i]);
+  g->seq_ok = true;
   return RFX_OK;
 }
 
@@ -425,18 +453,21 @@ extern "C" int rfx_group_render_frame(rfx_group *g, const rfx_frame *f, float *d
       !((f->pixel_begin == 0 && f->pixel_end == 0) || (f->pixel_begin == 0 && f->pixel_end == npx)))
     return rfx_detail_fail(RFX_ERR_ARG, "group_render_frame: a whole frame with sample_num > 0 (no partition fields)");
   hipStream_t s0 = stream ? (hipStream_t)stream : rfx_detail_stream(g->r[0]);
-  if (argb_only && npx > g->rgb0_cap)
+  if (n == 1 || H < n)  // one member renders the frame (and splits a large one itself)
   {
-    GCHECK(hipSetDevice(g->dev[0]));
-    GCHECK(hipDeviceSynchronize());  // any earlier frame on any stream may still write the old buffer
-    (void)hipFree(g->rgb0);
-    g->rgb0 = nullptr;
-    g->rgb0_cap = 0;
-    GCHECK(hipMalloc(&g->rgb0, npx * 3 * sizeof(float)));
-    g->rgb0_cap = npx;
+    if (argb_only && npx > g->rgb0_cap)
+    {
+      GCHECK(hipSetDevice(g->dev[0]));
+      GCHECK(hipDeviceSynchronize());  // any earlier frame on any stream may still write the old buffer
+      (void)hipFree(g->rgb0);
+      g->rgb0 = nullptr;
+      g->rgb0_cap = 0;
+      GCHECK(hipMalloc(&g->rgb0, npx * 3 * sizeof(float)));
+      g->rgb0_cap = npx;
+    }
+    g->seq_ok = false;
+    return rfx_render_frame(g->r[0], f, argb_only ? g->rgb0 : d_rgb, d_argb, nullptr, s0);
   }
-  float *img0 = argb_only ? g->rgb0 : d_rgb;
-  if (n == 1 || H < n) return rfx_render_frame(g->r[0], f, img0, d_argb, nullptr, s0);  // (splits a large frame itself)
   // a frame of more traces than one pass takes -- every member's band at most its launch limit, the pass under the band
   // scan's 2^31 -- runs as passes over consecutive row spans, each cut into equal bands (no balancing)
   const uint64_t spp = (uint64_t)f->sample_num * (uint64_t)f->sample_num;
@@ -447,14 +478,18 @@ extern "C" int rfx_group_render_frame(rfx_group *g, const rfx_frame *f, float *d
     if (!per) return rfx_detail_fail(RFX_ERR_ARG, "group_render_frame: one row exceeds 2^31 traces");
     GCHECK(hipSetDevice(g->dev[0]));
     const uint32_t jitter0 = rfx_detail_jitter(g->r[0]);
-    RCHECK(rfx_detail_save_start(g->r[0], s0));
+    // the frame's start state for a rewind, saved on member 0's stream after the caller's work (the first pass hands
+    // member 0's state over when it differs)
+    GCHECK(hipEventRecord(g->ev_start[0], s0));
+    GCHECK(hipStreamWaitEvent(g->own[0], g->ev_start[0], 0));
+    RCHECK(rfx_detail_save_start(g->r[0], g->own[0]));
     for (uint64_t y = 0; y < H; y += per)
     {
       const uint32_t y0 = (uint32_t)y, y1 = (uint32_t)std::min<uint64_t>(H, y + per);
       const size_t m = std::min<size_t>(n, y1 - y0);
       std::vector<uint32_t> bd(m + 1);
       for (size_t i = 0; i <= m; ++i) bd[i] = y0 + (uint32_t)(((uint64_t)(y1 - y0) * i) / m);
-      RCHECK(group_pass(g, f, y0, y1, bd, d_rgb, d_argb, img0, s0));
+      RCHECK(group_pass(g, f, y0, y1, bd, d_rgb, d_argb, s0));
     }
     g->timing_pending = false;  // the bands of a split frame are not the frame's bands
     rfx_detail_set_rewindable_saved(g->r[0], jitter0, s0);
@@ -472,7 +507,7 @@ extern "C" int rfx_group_render_frame(rfx_group *g, const rfx_frame *f, float *d
   }
   RCHECK(collect_times(g));
   const int parity = (int)(g->frames & 1);
-  RCHECK(group_pass(g, f, 0, H, g->bounds, d_rgb, d_argb, img0, s0));
+  RCHECK(group_pass(g, f, 0, H, g->bounds, d_rgb, d_argb, s0));
   g->timing_parity = parity;
   g->timing_pending = true;
   return RFX_OK;

@@ -479,6 +479,9 @@ constexpr size_t kPrimLargeWords = 12;  // per wave tile, large scenes (rfx_trac
 #ifndef RFX_LAUNCH_TRACES
 #define RFX_LAUNCH_TRACES (1ull << 30)  // traces per launch of a split frame (rfx_renderer_set_launch_traces)
 #endif
+#ifndef RFX_SPLIT_STREAMS
+#define RFX_SPLIT_STREAMS 2  // split frames: spans alternate between two streams (1: one stream, no overlap)
+#endif
 constexpr uint64_t kMaxLaunchTraces = 1ull << 31;  // the band scan's 32-bit offsets (rfx_kernels.hip rng_band_range)
 #ifndef RFX_SCAN_EMIT_BLOCKS
 // one-device emits of more RNG blocks than this scan the counts first (rng_band_range) instead of summing them per
@@ -515,6 +518,9 @@ struct rfx_renderer {
   // frames of more traces than launch_traces: consecutive spans alternate between the caller's stream and split_stream
   // (randDirs in d_rd / d_rd_alt); split_ev[k] marks span k's emit (the next span's pre-pass starts from its state)
   uint64_t launch_traces = RFX_LAUNCH_TRACES;
+  // bumped whenever the random streams move or are set (emits, set_rng, rewinds): a device group compares it with the
+  // value after its own last frame to know whether the members' streams still equal member 0's
+  uint64_t state_seq = 0;
   hipStream_t split_stream = nullptr;
   hipEvent_t split_ev[3] = {nullptr, nullptr, nullptr};
   uint32_t *d_blk_cnt = nullptr; uint64_t blk_cap = 0;
@@ -1201,6 +1207,7 @@ extern "C" int rfx_renderer_set_rng(rfx_renderer *r, uint32_t sphere_seed, uint3
   HIP_CHECK(hipStreamSynchronize(r->stream));
   r->jitter_seed = jitter_seed;
   r->rewind_ok = false;
+  ++r->state_seq;
   return RFX_OK;
 }
 
@@ -1281,6 +1288,7 @@ static int enqueue_rng(rfx_renderer *r, uint64_t traces, hipStream_t st)
   HIP_CHECK(launch_rng_finish(seed_cur(r), r->d_jump, seed_next(r), r->d_blk_cnt, r->d_rng_masks, nblk, traces,
                               r->d_rd, r->d_err, 1, 1, 1, 0, 1, st));
   r->seed_idx ^= 1u;
+  ++r->state_seq;
   r->rewind_ok = false;
   return RFX_OK;
 }
@@ -1387,6 +1395,7 @@ static int emit_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *d_counts, 
     HIP_CHECK(launch_rng_finish(seed_cur(r), r->d_jump, seed_next(r), d_counts, d_masks, nblk, pl.traces, rd,
                                 r->d_err, ss2, P.W, P.row_block, P.rank, P.nranks, st));
   r->seed_idx ^= 1u;
+  ++r->state_seq;
   // the caller's event: the randDirs are written and the next frame's stream state is known (the next frame's
   // RNG count may start on another stream while this frame traces)
   if (emitted) HIP_CHECK(hipEventRecord(emitted, st));
@@ -1642,6 +1651,7 @@ extern "C" int rfx_frame_rng_discard(rfx_renderer *r)
   if (r->emit_pending >= 0)
   {
     r->seed_idx ^= 1u;
+    ++r->state_seq;
     r->emit_pending = -1;
   }
   return RFX_OK;
@@ -1745,7 +1755,7 @@ static int render_split(rfx_renderer *r, const rfx_frame *f, uint64_t p0, uint64
     rfx_frame fk = *f;
     fk.pixel_begin = a;
     fk.pixel_end = b;
-    const int side = (int)(k & 1);
+    const int side = RFX_SPLIT_STREAMS > 1 ? (int)(k & 1) : 0;
     FramePlan pl;
     if ((rc = plan_frame(r, &fk, s2[side], pl)) != RFX_OK) return rc;
     pl.split = true;
@@ -1782,11 +1792,13 @@ extern "C" int rfx_frame_rng_rewind(rfx_renderer *r)
   if (!r) return fail(RFX_ERR_ARG, "frame_rng_rewind: null renderer");
   if (!r->rewind_ok) return fail(RFX_ERR_STATE, "frame_rng_rewind: the last call was not rfx_render_frame");
   if (r->rewind_flip) r->seed_idx ^= 1u;
+  ++r->state_seq;
   if (r->rewind_saved)
   {
     int rc;
     if ((rc = set_dev(r)) != RFX_OK) return rc;
     HIP_CHECK(hipMemcpyAsync(seed_cur(r), r->d_seed + 2, sizeof(uint32_t), hipMemcpyDeviceToDevice, r->rewind_stream));
+    ++r->state_seq;
   }
   r->jitter_seed = r->rewind_jitter;
   r->rewind_ok = false;
@@ -2137,3 +2149,4 @@ void rfx_detail_set_rewindable_saved(rfx_renderer *r, uint32_t jitter0, hipStrea
   r->rewind_jitter = jitter0;
 }
 uint64_t rfx_detail_launch_traces(const rfx_renderer *r) { return r->launch_traces; }
+uint64_t rfx_detail_state_seq(const rfx_renderer *r) { return r->state_seq; }

@@ -15,3 +15,4 @@ void rfx_detail_set_rewindable(rfx_renderer *r, uint32_t jitter0);
 int rfx_detail_save_start(rfx_renderer *r, hipStream_t st);
 void rfx_detail_set_rewindable_saved(rfx_renderer *r, uint32_t jitter0, hipStream_t st);
 uint64_t rfx_detail_launch_traces(const rfx_renderer *r);
+uint64_t rfx_detail_state_seq(const rfx_renderer *r);  // moves whenever the random streams move or are set

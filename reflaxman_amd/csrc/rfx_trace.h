@@ -1049,15 +1049,29 @@ __device__ __forceinline__ void closest_spheres_bvh(const DevScene &S, v3 origin
   }
 }
 
-// any sphere but skip_sph occludes the shadow ray (Scene.cpp:129-141 restricted to the spheres)
+// any sphere but skip_sph occludes the shadow ray (Scene.cpp:129-141 restricted to the spheres): the occluding pair's
+// index, or -1.  hint (wave-uniform, RFX_OCC_HINT): a pair that occluded a lane of this wave before, tested first -- an
+// occluder is an occluder whatever the order (Scene.cpp:132-141 breaks at the first), so a lane it occludes skips its walk.
+#ifndef RFX_OCC_HINT
+#define RFX_OCC_HINT 1
+#endif
 template <bool STATS, class NS>
-__device__ __forceinline__ bool occluded_spheres_bvh(const DevScene &S, v3 o, v3 ray, const RayConst &k, int skip_sph,
-                                                     Cnt &cnt, const NS &ns)
+__device__ __forceinline__ int occluded_spheres_bvh(const DevScene &S, v3 o, v3 ray, const RayConst &k, int skip_sph,
+                                                    Cnt &cnt, const NS &ns, int hint = -1)
 {
+  float t, sq;
+  if (RFX_OCC_HINT && hint >= 0)
+  {
+    f2 b, d;
+    pair_bd(S.sph_pair[hint], o, k, b, d);
+    if (pair_may_hit(b, d) &&
+        ((sphere_tail<STATS, true, true>(b.x, d.x, ray, k, t, sq, cnt) && 2 * hint != skip_sph) ||
+         (sphere_tail<STATS, true, true>(b.y, d.y, ray, k, t, sq, cnt) && 2 * hint + 1 != skip_sph)))
+      return hint;
+  }
   const RayInv ri = ray_inv(S, o, ray);
   BvhSlot *stack = ns.stack();
   int sp = 0, node = 0;
-  float t, sq;
   for (;;)
   {
     if (node >= 0)
@@ -1086,9 +1100,9 @@ __device__ __forceinline__ bool occluded_spheres_bvh(const DevScene &S, v3 o, v3
       if (pair_may_hit(b, d) &&
           ((sphere_tail<STATS, true, true>(b.x, d.x, ray, k, t, sq, cnt) && 2 * j != skip_sph) ||
            (sphere_tail<STATS, true, true>(b.y, d.y, ray, k, t, sq, cnt) && 2 * j + 1 != skip_sph)))
-        return true;
+        return j;
     }
-    if (sp == 0) return false;
+    if (sp == 0) return -1;
     node = stack[NS::kStride * --sp];
   }
 }
@@ -1345,14 +1359,25 @@ __device__ __forceinline__ bool occluded_small(const DevScene &S, v3 o, v3 ray, 
 // when the first did not occlude.)
 template <bool STATS, bool PLANES, class NS = BvhGlobal>
 __device__ __forceinline__ bool occluded(const DevScene &S, v3 o, v3 ray, bool live, int skip_sph, int skip_tri,
-                                         int skip_pln, const Bundle *B, Cnt &cnt, const NS &ns = NS{})
+                                         int skip_pln, const Bundle *B, Cnt &cnt, const NS &ns = NS{}, int *hint = nullptr)
 {
   const RayConst k = ray_const(ray);
   const bool cull = B && B->ok;
   bool occ = false;
   float t, sq, u, v;
   const bool use_bvh = !STATS && S.bvh != nullptr;
-  if (use_bvh && live) occ = occluded_spheres_bvh<STATS>(S, o, ray, k, skip_sph, cnt, ns);
+  if (use_bvh)
+  {
+    int found = -1;
+    if (live) found = occluded_spheres_bvh<STATS>(S, o, ray, k, skip_sph, cnt, ns, hint ? *hint : -1);
+    occ = found >= 0;
+    if (RFX_OCC_HINT && hint)
+    {
+      // the next query's hint: the occluder of this wave's lowest occluded lane
+      const uint64_t fm = __ballot(found >= 0);
+      if (fm) *hint = __builtin_amdgcn_readlane(found, (int)__builtin_ctzll(fm));
+    }
+  }
   for (int cfirst = 0; !use_bvh && cfirst < S.n_chunk; cfirst += 64)
   {
     if (__ballot(live && !occ) == 0) return occ;
@@ -1525,6 +1550,7 @@ __device__ __forceinline__ col trace_from(const DevScene &RFX_SCENE_PARAM, v3 or
   if (valid && refl == 0) RFX_CNT(C_RAYS);
   const Tabs<SMALL> T{S};
   bool alive = valid && refl < depth;
+  int occ_hint = -1;  // large scenes: the shadow rays' occluder hint (occluded_spheres_bvh)
 #ifdef RFX_DEBUG_SEGS
   int nseg = 0;  // diagnostic build only (tools/segstats.py): the trace's segment count replaces its colour
 #endif
@@ -1654,7 +1680,7 @@ __device__ __forceinline__ col trace_from(const DevScene &RFX_SCENE_PARAM, v3 or
             Bundle SB;
             if constexpr (CULL) SB = make_bundle(drop, sray, facing);
             const bool occ = occluded<STATS, PLANES>(S, drop, sray, facing, skip_sph, skip_tri, skip_pln,
-                                                     CULL ? &SB : nullptr, cnt, park.bvh());
+                                                     CULL ? &SB : nullptr, cnt, park.bvh(), &occ_hint);
             if (facing && !occ) lit |= 1u << q;
           }
         }
@@ -1974,6 +2000,9 @@ constexpr int kCfgCull = 1, kCfgManyLights = 2, kCfgSmall = 4, kCfgPlanes = 8, k
 #ifndef RFX_WAVES_PER_EU_LARGE
 #define RFX_WAVES_PER_EU_LARGE RFX_WAVES_PER_EU  // large-scene (BVH) trace kernels' occupancy target (experiment)
 #endif
+#ifndef RFX_SSAA_CHANNEL_SUM
+#define RFX_SSAA_CHANNEL_SUM 1  // SSAA epilogues: one lane per colour channel runs the ordered sample sum
+#endif
 template <bool STATS, int MODE, int CFG>
 __global__ __launch_bounds__(kWgThreads) __attribute__((amdgpu_waves_per_eu(
     (CFG & kCfgSmall) ? RFX_WAVES_PER_EU : RFX_WAVES_PER_EU_LARGE))) void trace_kernel(DevScene S, FrameParams P)
@@ -2084,6 +2113,40 @@ __global__ __launch_bounds__(kWgThreads) __attribute__((amdgpu_waves_per_eu(
         sm[3 * le + 2] = c.b;
         __builtin_amdgcn_wave_barrier();
         const uint32_t first = bw == 1 ? 64 * chunk : 0;  // the pixel's sum starts at its sample 0
+#if RFX_SSAA_CHANNEL_SUM
+        // Color::operator+= adds the three channels independently (r += c.r, ...), so the pixel's first three lanes
+        // each run one channel's chain of adds in the reference's order -- a third of the serial sum one lane ran.
+        // The final channels wait in the pixel's first sample's words (only lane ch reads word 3 lead + ch), where the
+        // pixel's first lane assembles the ARGB word.
+        if (ss2 >= 3)
+        {
+          const uint32_t lead = bw == 1 ? 0u : le - kk, ch = le - lead;  // kk: the lane's sample in its pixel
+          const uint32_t n = min(ss2 - first, bw == 1 ? 64u : ss2);
+          const bool last = first + n >= ss2;
+          if (pvalid && ch < 3)
+          {
+            float fc = first ? sm[192 + ch] : 0.0f;
+#pragma unroll 8
+            for (uint32_t j = 0; j < n; ++j) fc = fc + sm[3 * (lead + j) + ch];
+            if (!last)
+              sm[192 + ch] = fc;  // more chunks to come: the running sum waits in LDS
+            else
+            {
+              const float sq = (float)(int)ss2;                                    // Render.cpp:189
+              if (fabsf(sq) > kVerySmall) fc = fc / sq;
+              const size_t o = (size_t)(P.nranks > 1 ? ly : y) * P.W + x;
+              float *d = P.img + o * 3;
+              if (P.accumulate) fc = d[ch] + fc;                                   // Render.cpp:191-194
+              d[ch] = fc;
+              sm[3 * lead + ch] = fc;
+            }
+          }
+          __builtin_amdgcn_wave_barrier();
+          if (last && pvalid && ch == 0 && P.argb)                                 // Render::copyImage
+            P.argb[(size_t)(P.nranks > 1 ? ly : y) * P.W + x] = argb(mkc(sm[3 * lead], sm[3 * lead + 1], sm[3 * lead + 2]));
+        }
+        else
+#endif
         if (pvalid && (bw == 1 ? le == 0 : kk == 0))
         {
           col fin = first ? mkc(sm[192], sm[193], sm[194]) : mkc(0.0f, 0.0f, 0.0f);

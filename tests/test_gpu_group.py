@@ -195,3 +195,34 @@ def test_group_on_distinct_devices():
         assert torch.equal(rgb, rgb1) and torch.equal(argb, argb1), i
     g.close()
     one.close()
+
+
+def test_group_frames_ordered_with_the_callers_stream():
+    """Members trace into double-buffered scratch on their own streams and copy their bands on copy streams, so a
+    member's copy of frame k overlaps its trace of frame k + 1.  The caller's stream must still see each frame whole
+    right after the call and must not have a frame overwritten under its later work: 10 frames enqueued back to back on
+    a torch stream, each followed on that stream by a clone of the frame (no host sync in between), equal the single
+    renderer's frames one by one."""
+    import torch
+    from reflaxman_amd.render import build_scene, make_frame
+    scene, cam = build_scene(scenes.get_scene("synth16"))
+    W, H = 640, 360
+    g, one = Group(3, scene), _single(scene)
+    f = make_frame(cam, W, H, 8, 1)
+    rgb, argb = _bufs(torch, W, H)
+    rgb1, argb1 = _bufs(torch, W, H)
+    s = torch.cuda.Stream()
+    got = []
+    with torch.cuda.stream(s):
+        for _ in range(10):
+            _lib.check(g.L.rfx_group_render_frame(g.g, C.byref(f), C.c_void_p(rgb.data_ptr()),
+                                                  C.c_void_p(argb.data_ptr()), C.c_void_p(s.cuda_stream)))
+            got.append((rgb.clone(), argb.clone()))
+            rgb.fill_(-1.0)  # the caller's own writes between frames: the next frame's copies come after them
+    torch.cuda.synchronize()
+    for i, (a, b) in enumerate(got):
+        one.render_frame(f, rgb1.data_ptr(), argb1.data_ptr())
+        torch.cuda.synchronize()
+        assert torch.equal(a, rgb1) and torch.equal(b, argb1), i
+    g.close()
+    one.close()

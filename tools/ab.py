@@ -78,6 +78,11 @@ VARIANTS = {
     "large6": ["RFX_WAVES_PER_EU_LARGE=6"],
     "large5": ["RFX_WAVES_PER_EU_LARGE=5"],
     "scanall": ["RFX_SCAN_EMIT_BLOCKS=0"],
+    "chsum0": ["RFX_SSAA_CHANNEL_SUM=0"],
+    "nohint": ["RFX_OCC_HINT=0"],
+    "split1": ["RFX_SPLIT_STREAMS=1"],
+    "lt28": ["RFX_LAUNCH_TRACES=(1ull<<28)"],
+    "lt31": ["RFX_LAUNCH_TRACES=(1ull<<31)"],
 }
 
 

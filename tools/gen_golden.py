@@ -381,7 +381,8 @@ def main():
             _, a2 = banded_frame(tmp, "default", 800, 600, 20, 2, 0, ref["RFX_SPHERE_SEED"])
             assert sha(shot_bmp(a2, 800, 600)) == ref["sha_bmp"], "banded frame + savetex != the reference Pulse's BMP"
             t0 = time.time()
-            rgb, argb = banded_frame(tmp, "default", W, H, 20, ss, 0, ref["RFX_SPHERE_SEED"])
+            workers = int(os.environ.get("RFX_GEN_WORKERS", "0")) or None  # leave cores free for other work
+            rgb, argb = banded_frame(tmp, "default", W, H, 20, ss, 0, ref["RFX_SPHERE_SEED"], workers=workers)
             data = shot_bmp(argb, W, H)
             cases[key] = dict(kind="pulse", res_key=res_key, ss_key=ss_key, W=W, H=H, ss=ss, depth=20, bytes=len(data),
                               sha_bmp=sha(data), file=ref["file"], RFX_SPHERE_SEED=ref["RFX_SPHERE_SEED"],
