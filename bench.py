@@ -300,6 +300,21 @@ class SingleGpu:
         self.r.close()
 
 
+LAUNCH_TRACES = 1 << 30  # rfx_host.cpp RFX_LAUNCH_TRACES (the library's default launch limit)
+
+
+def split_launches(W: int, H: int, ss: int) -> int:
+    """Launches rfx_render_frame makes of a W x H frame at ss x ss samples (rfx_host.cpp render_split)."""
+    spp = ss * ss
+    if W * H * spp <= LAUNCH_TRACES:
+        return 1
+    per = max(1, LAUNCH_TRACES // spp)
+    if per >= W:
+        per = per // W * W
+        return -(-H // (per // W))
+    return -(-(W * H) // per)
+
+
 def launcher_command(n: int, argv: list, port: int) -> list:
     """The command that runs this bench as n ranks of one node (torch.distributed.run, rendezvous on 127.0.0.1)."""
     return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
@@ -683,11 +698,21 @@ def main(argv=None):
     px_launch = rows * W
     # HBM traffic and executed VALU work of the trace kernel: rocprofv3 --pmc passes of this very workload
     # and library build (tools/prof_round.sh -> profiles/pmc/), per launch; null when no such record exists
-    pmc = metrics.pmc_record(os.path.join(ROOT, "profiles", "pmc"), [args.scene, W, H, depth, world],
+    pmc = metrics.pmc_record(os.path.join(ROOT, "profiles", "pmc"), [args.scene, W, H, depth, world, ss],
                              _lib.lib_sha256(), _lib.device_sha256())
     traffic = pmc["hbm_bytes_per_launch"] if pmc else None
+    launches = split_launches(W, H, ss) if world == 1 else 1
+    if launches > 1:
+        # a frame of several launches on two overlapping streams: a launch's HIP-event span includes the other stream's
+        # work, so the per-launch time is the frame's wall time shared out over its launches
+        trace_avg = ms_step / launches
+        flops_launch = flops_frame / launches
+        px_launch = W * H // launches
     executed = metrics.executed_work(pmc, trace_avg)
     roofline = metrics.roofline(executed, traffic, flops_launch, trace_avg, px_launch)
+    if launches > 1:
+        roofline["launches_per_frame"] = launches
+        roofline["launch_time_kind"] = "frame wall time / launches (the split frame's launches overlap on two streams)"
     roofline["kernel"] = ("rfx::trace_kernel (plain pixel mode, wave-bundle culling)" if ss == 1 else
                           "rfx::trace_kernel (SSAA pixel mode, wave-bundle culling)")
     if baseline is not None:

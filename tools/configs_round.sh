@@ -11,4 +11,5 @@ $B --config c3 --steps 20 --warmup 3 > $O/c3_synth16_3840x2160_d8.json 2> $O/c3.
 $B --config c4 --steps 10 --warmup 2 --cpu-stride 16 > $O/c4_synth16_7680x4320_d8_1gpu.json 2> $O/c4.err || exit 5
 $B --config c5 --steps 5 --warmup 1 --cpu-stride 270 > $O/c5_stress4096_3840x2160_d12.json 2> $O/c5.err || exit 6
 $B --config shot --steps 10 --warmup 2 > $O/shot_default_1920x1080_d20_ss4.json 2> $O/shot.err || exit 7
+$B --config shot128 > $O/shot128_default_1920x1080_d20_ss128.json 2> $O/shot128.err || exit 8
 exit 0

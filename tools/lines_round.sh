@@ -9,6 +9,6 @@ bash tools/configs_round.sh ${1:-lines}/configs || exit 2
 timeout -k 10 300 python -u tools/pulse_session_time.py --reps 5 --out $O/pulse_session_640x480.json > $O/pulse.log 2>&1 || exit 3
 timeout -k 10 200 python -u tools/group_copy_cost.py > $O/group_copy_cost_c4_8members_one_device.json 2> $O/group_copy.err || exit 4
 for n in 2 4; do
-  timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 --master-port $((29500 + n)) bench.py --gpus $n --backend gloo --one-device --steps 20 --warmup 3 --no-cpu-baseline > $O/rehearsal_c4_n${n}_bands_gloo_one_device.json 2> $O/rehearsal_n$n.err || exit 5
+  timeout -k 10 400 python bench.py --gpus $n --backend gloo --one-device --steps 20 --warmup 3 --no-cpu-baseline > $O/rehearsal_c4_n${n}_bands_gloo_one_device.json 2> $O/rehearsal_n$n.err || exit 5
 done
 exit 0
