@@ -46,7 +46,8 @@ int rfx_abi_version(void);
 const char *rfx_last_error(void);
 /* Compile-time options of this build (A/B variants, tools/ab.py), as bits: per-view chunk lists of large scenes
  * (RFX_PRIM_LARGE, off by default), per-view masks of per-pixel-loop SSAA frames (RFX_PRIM_SSAA, off), of the
- * one-lane-per-sample SSAA modes (RFX_PRIM_LANES, on), one-light kernel instantiations (RFX_ONE_LIGHT, on). */
+ * one-lane-per-sample SSAA modes (RFX_PRIM_LANES, on), one-light kernel instantiations (RFX_ONE_LIGHT, on); bits 8-15:
+ * sphere pairs per leaf of the large scenes' BVH. */
 enum { RFX_BUILD_PRIM_LARGE = 1, RFX_BUILD_PRIM_SSAA = 2, RFX_BUILD_PRIM_LANES = 4, RFX_BUILD_ONE_LIGHT = 8 };
 int rfx_build_options(void);
 

@@ -698,7 +698,8 @@ extern "C" void rfx_renderer_destroy(rfx_renderer *r)
 extern "C" int rfx_build_options(void)
 {
   return (RFX_PRIM_LARGE ? RFX_BUILD_PRIM_LARGE : 0) | (RFX_PRIM_SSAA ? RFX_BUILD_PRIM_SSAA : 0) |
-         (RFX_PRIM_LANES ? RFX_BUILD_PRIM_LANES : 0) | (RFX_ONE_LIGHT ? RFX_BUILD_ONE_LIGHT : 0);
+         (RFX_PRIM_LANES ? RFX_BUILD_PRIM_LANES : 0) | (RFX_ONE_LIGHT ? RFX_BUILD_ONE_LIGHT : 0) |
+         (RFX_BVH_LEAF_PAIRS << 8);
 }
 
 extern "C" int rfx_renderer_set_launch_traces(rfx_renderer *r, uint64_t max_traces)
@@ -939,7 +940,11 @@ extern "C" int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *s)
     si.push_back(sp.obj);
     si.push_back(sp.mat.dielectric);
   }
-  std::vector<SpherePair> sp((sg.size() + 1) / 2);
+  // (large scenes: a whole number of BVH leaves of RFX_BVH_LEAF_PAIRS pairs; the padding pairs never hit)
+  const size_t npair_dev = sg.size() > 32 ? ((sg.size() + 1) / 2 + RFX_BVH_LEAF_PAIRS - 1) / RFX_BVH_LEAF_PAIRS *
+                                                RFX_BVH_LEAF_PAIRS
+                                          : (sg.size() + 1) / 2;
+  std::vector<SpherePair> sp(npair_dev);
   for (size_t i = 0; i < 2 * sp.size(); ++i)
   {
     SpherePair &p = sp[i / 2];
@@ -1083,13 +1088,15 @@ extern "C" int rfx_renderer_set_scene(rfx_renderer *r, const rfx_scene *s)
   double bvh_ref[3] = {0.0, 0.0, 0.0};
   if (nsph > 32)
   {
-    const size_t npairs = (nsph + 1) / 2;
+    // leaves: groups of RFX_BVH_LEAF_PAIRS consecutive pairs (compact clusters of the median-split order)
+    const size_t npairs = ((nsph + 1) / 2 + RFX_BVH_LEAF_PAIRS - 1) / RFX_BVH_LEAF_PAIRS;
+    constexpr size_t kLeafSph = 2 * RFX_BVH_LEAF_PAIRS;
     std::vector<PairBox> box(npairs);
     for (size_t j = 0; j < npairs; ++j)
     {
       PairBox &b = box[j];
       for (int k = 0; k < 3; ++k) { b.lo[k] = INFINITY; b.hi[k] = -INFINITY; }
-      for (size_t q = 2 * j; q < std::min(nsph, 2 * j + 2); ++q)
+      for (size_t q = kLeafSph * j; q < std::min(nsph, kLeafSph * j + kLeafSph); ++q)
       {
         const double c[3] = {bd[q].x, bd[q].y, bd[q].z}, rr = bd[q].r;
         for (int k = 0; k < 3; ++k) { b.lo[k] = fmin(b.lo[k], c[k] - rr); b.hi[k] = fmax(b.hi[k], c[k] + rr); }

@@ -1023,25 +1023,29 @@ __device__ __forceinline__ void closest_spheres_bvh(const DevScene &S, v3 origin
     }
     else
     {
-      const int j = ~node;
-      f2 b, d;
-      pair_bd(S.sph_pair[j], origin, k, b, d);
-      if (pair_may_hit(b, d))
+#pragma unroll
+      for (int e = 0; e < RFX_BVH_LEAF_PAIRS; ++e)
       {
-        float t, sq;
-        if (sphere_tail<STATS, false, true>(b.x, d.x, ray, k, t, sq, cnt))
+        const int j = RFX_BVH_LEAF_PAIRS * ~node + e;
+        f2 b, d;
+        pair_bd(S.sph_pair[j], origin, k, b, d);
+        if (pair_may_hit(b, d))
         {
-          const int obj = S.sph_info[4 * j];
-          if (tri_takes(sq, h.sq, obj, h.obj)) { h.sq = sq; h.obj = obj; h.i = 2 * j; h.t = t; }
-        }
-        if (sphere_tail<STATS, false, true>(b.y, d.y, ray, k, t, sq, cnt))
-        {
-          const int obj = S.sph_info[4 * j + 2];
-          if (tri_takes(sq, h.sq, obj, h.obj)) { h.sq = sq; h.obj = obj; h.i = 2 * j + 1; h.t = t; }
-        }
+          float t, sq;
+          if (sphere_tail<STATS, false, true>(b.x, d.x, ray, k, t, sq, cnt))
+          {
+            const int obj = S.sph_info[4 * j];
+            if (tri_takes(sq, h.sq, obj, h.obj)) { h.sq = sq; h.obj = obj; h.i = 2 * j; h.t = t; }
+          }
+          if (sphere_tail<STATS, false, true>(b.y, d.y, ray, k, t, sq, cnt))
+          {
+            const int obj = S.sph_info[4 * j + 2];
+            if (tri_takes(sq, h.sq, obj, h.obj)) { h.sq = sq; h.obj = obj; h.i = 2 * j + 1; h.t = t; }
+          }
 #if RFX_BVH_TLIM
-        tlim = __builtin_amdgcn_sqrtf(h.sq * 1.001f * ia) * 1.0001f;
+          tlim = __builtin_amdgcn_sqrtf(h.sq * 1.001f * ia) * 1.0001f;
 #endif
+        }
       }
     }
     if (sp == 0) break;
@@ -1093,14 +1097,18 @@ __device__ __forceinline__ int occluded_spheres_bvh(const DevScene &S, v3 o, v3 
     }
     else
     {
-      const int j = ~node;
-      f2 b, d;
-      pair_bd(S.sph_pair[j], o, k, b, d);
-      // the hit object is filtered out after its test, which does not change the boolean
-      if (pair_may_hit(b, d) &&
-          ((sphere_tail<STATS, true, true>(b.x, d.x, ray, k, t, sq, cnt) && 2 * j != skip_sph) ||
-           (sphere_tail<STATS, true, true>(b.y, d.y, ray, k, t, sq, cnt) && 2 * j + 1 != skip_sph)))
-        return j;
+#pragma unroll
+      for (int e = 0; e < RFX_BVH_LEAF_PAIRS; ++e)
+      {
+        const int j = RFX_BVH_LEAF_PAIRS * ~node + e;
+        f2 b, d;
+        pair_bd(S.sph_pair[j], o, k, b, d);
+        // the hit object is filtered out after its test, which does not change the boolean
+        if (pair_may_hit(b, d) &&
+            ((sphere_tail<STATS, true, true>(b.x, d.x, ray, k, t, sq, cnt) && 2 * j != skip_sph) ||
+             (sphere_tail<STATS, true, true>(b.y, d.y, ray, k, t, sq, cnt) && 2 * j + 1 != skip_sph)))
+          return j;
+      }
     }
     if (sp == 0) return -1;
     node = stack[NS::kStride * --sp];

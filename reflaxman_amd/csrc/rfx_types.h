@@ -63,6 +63,11 @@ struct alignas(16) CullTri { float v0x, v0y, v0z, nu, gux, guy, guz, nv, gvx, gv
 #define RFX_BVH_PREWIDE 1
 #endif
 struct alignas(16) BvhNode { float lx[2], ly[2], lz[2], hx[2], hy[2], hz[2]; int32_t child[2]; float mt[2]; };
+// Sphere pairs per BVH leaf (rfx_host.cpp build_pair_bvh, rfx_trace.h leaf tests): leaf ~g holds the pairs
+// [RFX_BVH_LEAF_PAIRS g, RFX_BVH_LEAF_PAIRS (g + 1)) of the device order (sph_pair padded with never-hit pairs)
+#ifndef RFX_BVH_LEAF_PAIRS
+#define RFX_BVH_LEAF_PAIRS 4
+#endif
 // Plane(pos, norm, material) (Plane.h:6-14): the normal as given (the reference never normalises it)
 struct alignas(16) PlaneGeo { float px, py, pz, nx, ny, nz; int32_t obj, dielectric; };
 struct alignas(16) LightRec { float ox, oy, oz, radius, r, g, b, power; }; // OmniLight.h

@@ -512,11 +512,15 @@ def test_stress_band_chunk_lists(key):
     r.close()
 
 
-@pytest.mark.parametrize("n_spheres", [4096, 4600])
-def test_regrouped_large_scene_equals_unregrouped(n_spheres):
-    """The bounce kernel's two forms on large scenes: with the BVH staged in LDS (4096 spheres: 2,047 nodes fit) and
-    walking it in global memory (4600 spheres: 2,299 nodes do not).  Regrouped frames (park after 1 and 2) equal the
-    frame traced without regrouping, bit for bit, over two frames of the random stream."""
+@pytest.mark.parametrize("big", [False, True])
+def test_regrouped_large_scene_equals_unregrouped(big):
+    """The bounce kernel's two forms on large scenes: with the BVH staged in LDS (4096 spheres fit) and walking it in
+    global memory (a scene whose BVH has more than the ~2,100 nodes the LDS holds: 4,400 spheres per sphere pair of a
+    leaf, rfx_build_options).  Regrouped frames (park after 1 and 2) equal the frame traced without regrouping, bit for
+    bit, over two frames of the random stream."""
+    from reflaxman_amd import _lib
+    leaf_pairs = (_lib.load().rfx_build_options() >> 8) & 0xFF
+    n_spheres = 4400 * leaf_pairs if big else 4096
     desc = scenes.stress_scene(n_spheres)
     ref, _, r0 = gpu_render(desc, 320, 180, 12, frames=2, regroup=0)
     assert r0._r.bounce_form() == 0
@@ -525,7 +529,7 @@ def test_regrouped_large_scene_equals_unregrouped(n_spheres):
         rgb, _, r = gpu_render(desc, 320, 180, 12, frames=2, regroup=park)
         assert rgb.tobytes() == ref.tobytes(), (n_spheres, park)
         # the form the test is about ran (a refused LDS launch falls back to the global form silently otherwise)
-        assert r._r.bounce_form() == (2 if n_spheres == 4096 else 1), (n_spheres, park)
+        assert r._r.bounce_form() == (1 if big else 2), (n_spheres, park)
         r.close()
 
 

@@ -81,6 +81,9 @@ VARIANTS = {
     "chsum0": ["RFX_SSAA_CHANNEL_SUM=0"],
     "nohint": ["RFX_OCC_HINT=0"],
     "split1": ["RFX_SPLIT_STREAMS=1"],
+    "leaf1": ["RFX_BVH_LEAF_PAIRS=1"],
+    "leaf2": ["RFX_BVH_LEAF_PAIRS=2"],
+    "leaf8": ["RFX_BVH_LEAF_PAIRS=8"],
     "lt28": ["RFX_LAUNCH_TRACES=(1ull<<28)"],
     "lt31": ["RFX_LAUNCH_TRACES=(1ull<<31)"],
 }
