@@ -1,7 +1,7 @@
 """Summarise rocprofv3 --pmc CSVs of the trace kernel (+ its bounce kernel): per-frame means of each counter.
 
     python tools/pmc_summary.py [--kernel SUBSTR[,SUBSTR..]] [--out profiles/pmc/<name>.json
-                                 --config SCENE W H DEPTH NGPUS [SS]] CSV...
+                                 --config SCENE W H DEPTH NGPUS SS] CSV...
 
 With --out, also writes the HBM traffic record bench.py reads for `roofline.traffic`:
 FETCH_SIZE and WRITE_SIZE are reported by rocprofv3 in KiB per dispatch; the bytes are
@@ -38,7 +38,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--kernel", default="trace_kernel<false,bounce_kernel")
     ap.add_argument("--out")
-    ap.add_argument("--config", nargs="+", help="SCENE W H DEPTH NGPUS [SS] (samples per axis, default 1)")
+    ap.add_argument("--config", nargs=6, help="SCENE W H DEPTH NGPUS SS (SS: samples per axis)")
     ap.add_argument("--lib-sha256", default=None, help="build the counters came from (default: the in-tree librfx.so)")
     ap.add_argument("csv", nargs="+")
     a = ap.parse_args()
@@ -47,10 +47,9 @@ def main():
         s["valu_lane_util"] = s["SQ_THREAD_CYCLES_VALU"] / (64 * s["SQ_ACTIVE_INST_VALU"])
     print(json.dumps(s, indent=1))
     if a.out:
-        scene, W, H, depth, n = a.config[:5]
-        ss = int(a.config[5]) if len(a.config) > 5 else 1
+        scene, W, H, depth, n, ss = a.config
         rec = {
-            "kernel": a.kernel, "config": [scene, int(W), int(H), int(depth), int(n), ss],
+            "kernel": a.kernel, "config": [scene, int(W), int(H), int(depth), int(n), int(ss)],
             "lib_sha256": a.lib_sha256 or _lib.lib_sha256(),
             "device_sha256": None if a.lib_sha256 else _lib.device_sha256(),
             "fetch_bytes_per_launch": int(s["FETCH_SIZE"] * 1024), "write_bytes_per_launch": int(s["WRITE_SIZE"] * 1024),
