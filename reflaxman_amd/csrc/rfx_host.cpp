@@ -42,6 +42,7 @@ hipError_t launch_prim_cull(const DevScene &S, const FrameParams &P, uint64_t *m
 hipError_t launch_queue_sort(const uint32_t *count, const uint32_t *key, uint32_t *hist, uint32_t *order, hipStream_t st);
 uint32_t trace_tiles(const FrameParams &P);
 bool trace_lanes(const FrameParams &P);
+bool trace_chunks(const FrameParams &P);
 size_t tile_order_scratch();
 hipError_t launch_tile_order(const uint32_t *cost, uint32_t n, uint32_t *order, uint32_t *scratch, hipStream_t st);
 void launch_bounce(int cfg, dim3 grid, const DevScene &S, const FrameParams &P, hipStream_t st);
@@ -454,6 +455,9 @@ constexpr size_t kPrimLargeWords = 12;  // per wave tile, large scenes (rfx_trac
 #ifndef RFX_PRIM_LANES
 #define RFX_PRIM_LANES 1  // masks of kModeSsaaLanes frames (the lanes' own small pixel blocks)
 #endif
+#ifndef RFX_PRIM_CHUNKS
+#define RFX_PRIM_CHUNKS 1  // closest-hit masks of kModeSsaaChunks frames (a pixel's sample rectangle), every launch
+#endif
 #ifndef RFX_PRIM_LARGE
 #define RFX_PRIM_LARGE 0
 #endif
@@ -548,6 +552,9 @@ struct rfx_renderer {
   // primary-bundle cull masks (small scenes, plain frames): one u64 per wave tile, valid for prim_key
   uint64_t *d_prim_mask = nullptr;
   size_t prim_cap = 0;
+  // split frames in the chunk mode: each span's pixel masks, in the buffer of its stream side (render_split)
+  uint64_t *d_split_mask[2] = {nullptr, nullptr};
+  size_t split_mask_cap[2] = {0, 0};
   std::vector<uint8_t> prim_key;   // the view the masks hold (empty: none)
   std::vector<uint8_t> prim_seen;  // the view of the last plain small-scene launch
   uint64_t scene_gen = 0;  // bumped by every set_scene
@@ -677,6 +684,7 @@ extern "C" void rfx_renderer_destroy(rfx_renderer *r)
   (void)hipFree(r->d_rng_range);
   (void)hipFree(r->d_img); (void)hipFree(r->d_argb); (void)hipFree(r->d_cnt);
   (void)hipFree(r->d_queue); (void)hipFree(r->d_qctr); (void)hipFree(r->d_prim_mask);
+  (void)hipFree(r->d_split_mask[0]); (void)hipFree(r->d_split_mask[1]);
   (void)hipFree(r->d_qkey); (void)hipFree(r->d_qorder);
   for (hipEvent_t e : r->events) (void)hipEventDestroy(e);
   if (r->tile_stream) (void)hipStreamSynchronize(r->tile_stream);
@@ -1312,6 +1320,7 @@ struct FramePlan {
   // one span of a split frame (rfx_render_frame): launches on two streams overlap, so the per-renderer state of
   // single launches (tile schedule, per-view masks, regroup queue) stays out
   bool split = false;
+  int split_side = 0;  // the span's stream (0: the caller's, 1: the renderer's second)
   uint64_t rd_traces() const { return band ? band_hi - band_lo : traces; }  // randDir words the plan writes and reads
 };
 
@@ -1479,9 +1488,30 @@ static int trace_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *rd, float
   // primary-bundle cull masks: small scenes, plain and SSAA frames (not block previews), culling launches; large scenes,
   // plain frames: the primary bundles' chunk lists.  Recomputed only when the camera, the frame geometry, the sampling
   // or the scene changed (the bench's frames all reuse one set)
-  if (((small && (plain || (RFX_PRIM_LANES && trace_lanes(P)) || (RFX_PRIM_SSAA && P.ss >= 1)) && !park) ||
-       (RFX_PRIM_LARGE && !small && plain)) &&
-      !d_counters && P.grid_rows && r->prim_mode && !pl.split)
+  // The chunk mode (sampleNum > 8: a wave per pixel) takes closest-hit masks only, over each pixel's sample rectangle:
+  // one cheap cull per pixel that every chunk of its samples reuses, so they are built for every view and every span
+  // of a split frame (into the span's stream side's buffer: the spans of the two streams overlap).
+  const bool chunks = RFX_PRIM_CHUNKS && RFX_PRIM_LANES && small && trace_chunks(P);
+  if (chunks && pl.split && !d_counters && P.grid_rows && r->prim_mode)
+  {
+    const int sd = pl.split_side;
+    const size_t nwords = (size_t)trace_tiles(P) * kPrimWords;
+    if (nwords > r->split_mask_cap[sd])
+    {
+      (void)hipFree(r->d_split_mask[sd]);
+      r->d_split_mask[sd] = nullptr;
+      r->split_mask_cap[sd] = 0;
+      HIP_CHECK(hipMalloc(&r->d_split_mask[sd], nwords * sizeof(uint64_t)));
+      r->split_mask_cap[sd] = nwords;
+    }
+    HIP_CHECK(launch_prim_cull(r->dev, P, r->d_split_mask[sd], st));
+    P.prim_mask = r->d_split_mask[sd];
+    P.prim_shadow = 0;
+  }
+  else if (((small && (plain || (RFX_PRIM_LANES && (trace_lanes(P) || chunks)) || (RFX_PRIM_SSAA && P.ss >= 1)) &&
+             !park) ||
+            (RFX_PRIM_LARGE && !small && plain)) &&
+           !d_counters && P.grid_rows && r->prim_mode && !pl.split)
   {
     struct Key { float cam[15]; uint32_t W, H, grid_rows, row0, row_block, rank, nranks; int32_t depth, ss, additive;
                  uint64_t p_begin, p_end, gen; } k;
@@ -1511,7 +1541,7 @@ static int trace_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *rd, float
       const bool repeat = kb == r->prim_seen;
       r->prim_seen = kb;
       r->prim_key.clear();
-      if (repeat || r->prim_mode == 2)
+      if (repeat || r->prim_mode == 2 || chunks)
       {
         HIP_CHECK(launch_prim_cull(r->dev, P, r->d_prim_mask, st));
         r->prim_key = kb;
@@ -1520,7 +1550,7 @@ static int trace_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *rd, float
     if (!r->prim_key.empty())
     {
       P.prim_mask = r->d_prim_mask;
-      P.prim_shadow = P.additive ? 0 : 1;  // jittered frames: closest-hit masks only (prim_cull_kernel)
+      P.prim_shadow = P.additive || chunks ? 0 : 1;  // jittered frames, chunks: closest-hit masks only (prim_cull_kernel)
     }
   }
   if (P.grid_rows) HIP_CHECK(launch_trace(r->dev, P, d_counters != nullptr, st));
@@ -1766,6 +1796,7 @@ static int render_split(rfx_renderer *r, const rfx_frame *f, uint64_t p0, uint64
     FramePlan pl;
     if ((rc = plan_frame(r, &fk, s2[side], pl)) != RFX_OK) return rc;
     pl.split = true;
+    pl.split_side = side;
     const uint64_t nblk = rng_layout(pl.traces, 1, nullptr);
     if (k > 0) HIP_CHECK(hipStreamWaitEvent(s2[side], r->split_ev[side ^ 1], 0));  // span k - 1's end state
     if ((rc = timing_start(r, pl.st)) != RFX_OK) return rc;

@@ -802,6 +802,13 @@ bool trace_lanes(const FrameParams &P)
   return trace_mode(P) == kModeSsaaLanes;
 }
 
+// the frame runs kModeSsaaChunks (one pixel per wave; its per-view masks are prim_cull_kernel<., true>'s closest-hit
+// masks over the pixel's sample rectangle)
+bool trace_chunks(const FrameParams &P)
+{
+  return trace_mode(P) == kModeSsaaChunks;
+}
+
 // the per-view masks of a small scene's plain or SSAA frame (prim_cull_kernel, kPrimStride words per wave tile), or
 // a large scene's chunk lists (prim_cull_large_kernel, kPrimLargeStride words)
 hipError_t launch_prim_cull(const DevScene &S, const FrameParams &P, uint64_t *masks, hipStream_t st)
@@ -809,7 +816,7 @@ hipError_t launch_prim_cull(const DevScene &S, const FrameParams &P, uint64_t *m
   const dim3 grid = trace_grid(P);
   if (!(S.n_sph <= 32 && S.n_tri <= 32))  // large scenes: the primary bundles' chunk lists
     hipLaunchKernelGGL(prim_cull_large_kernel<0>, grid, dim3(kWgThreads), 0, st, S, P, masks);
-  else if (trace_lanes(P))
+  else if (trace_lanes(P) || trace_chunks(P))
   {
     if (S.n_pln > 0)
       hipLaunchKernelGGL((prim_cull_kernel<true, true>), grid, dim3(kWgThreads), 0, st, S, P, masks);

@@ -2096,8 +2096,8 @@ __global__ __launch_bounds__(kWgThreads) __attribute__((amdgpu_waves_per_eu(
       const v3 ray = mmul(view, mk(rx + ox + rndx, ry + oy + rndy, P.rz));         // Render.cpp:183-184
       v3 rd = mk(0.0f, 0.0f, 0.0f);
       if (valid) rd = load_rd(P, pr * (uint64_t)ss2 + kk);
-      // the tile's per-view masks (prim_cull_kernel<., true>), not for the chunk loop
-      const uint64_t *pm = RFX_PRIM_LANES && !CHUNKS && SMALL && CULL && !STATS && P.prim_mask
+      // the tile's per-view masks (prim_cull_kernel<., true>; chunks: the pixel's closest-hit mask, every chunk)
+      const uint64_t *pm = RFX_PRIM_LANES && SMALL && CULL && !STATS && P.prim_mask
                                ? P.prim_mask + (size_t)kPrimStride * t8 : nullptr;
       const col c = trace<STATS, CULL, MANYL, SMALL, PLANES, ONEL>(S, eye, ray, P.depth, rd, lut, cnt, valid, pm,
                                                                   P.prim_shadow != 0);
@@ -2379,7 +2379,9 @@ __global__ __launch_bounds__(kWgThreads) __attribute__((amdgpu_waves_per_eu(
 // masks depend only on the view (camera, frame geometry, scene), so the host builds them once per view.
 // LANES: the tiles of a kModeSsaaLanes frame (sampleNum 1 jittered, 2, 4, 8): wave t8 covers bw x bw pixels, one sample
 // per lane, exactly as trace_kernel's lanes branch maps them; its masks cover the lanes' own rays (jittered: each lane's
-// unit jitter square), so the shadow masks need one primary hit per lane.
+// unit jitter square), so the shadow masks need one primary hit per lane.  A kModeSsaaChunks frame (sampleNum > 8, the
+// wave is one pixel): the closest-hit mask of the pixel's whole sample rectangle, which every chunk of its samples reuses;
+// no shadow masks (they would need the primary hit of every sample).
 template <bool PLANES, bool LANES = false>
 __global__ RFX_TRACE_BOUNDS void prim_cull_kernel(DevScene S, FrameParams P, uint64_t *masks)
 {
@@ -2392,11 +2394,12 @@ __global__ RFX_TRACE_BOUNDS void prim_cull_kernel(DevScene S, FrameParams P, uin
   const uint32_t t8 = (blockIdx.y * kTileWavesY + wv / kTileWavesX) * w8 + blockIdx.x * kTileWavesX + wv % kTileWavesX;
   uint32_t gx, gy, kk = 0;
   float lox = 0.0f, loy = 0.0f;  // LANES: the lane's sample offsets (Render.cpp:183), as trace_kernel forms them
+  const bool chunks = LANES && P.ss > 8;
   if constexpr (LANES)
   {
     const uint32_t ss = (uint32_t)P.ss, ss2 = ss * ss, bw = ss_lane_block(P.ss);
     const uint32_t q = bw == 1 ? 0 : lane / ss2;
-    kk = bw == 1 ? lane : lane - q * ss2;
+    kk = chunks ? 0 : bw == 1 ? lane : lane - q * ss2;
     const uint32_t sx = kk / ss, sy = kk - sx * ss;
     gx = (t8 % w8) * bw + q % bw;
     gy = (t8 / w8) * bw + q / bw;
@@ -2425,7 +2428,7 @@ __global__ RFX_TRACE_BOUNDS void prim_cull_kernel(DevScene S, FrameParams P, uin
   // the pixel's sample rectangle [rx, rx + omax] x [ry, ry + omax] (Render.cpp:177-183: offsets (ss - 1) / ss at most,
   // plus a jitter of at most 1 in additive frames), through its four corners
   const int ss = P.ss;
-  const bool exact = (LANES || ss == 1) && !P.additive;
+  const bool exact = (LANES || ss == 1) && !P.additive && !chunks;
   uint64_t om = 0;
   if (__ballot(valid))
   {
@@ -2434,8 +2437,9 @@ __global__ RFX_TRACE_BOUNDS void prim_cull_kernel(DevScene S, FrameParams P, uin
       B = make_bundle(eye, mmul(view, mk(rx + lox + 0.0f, ry + loy + 0.0f, P.rz)), valid);
     else
     {
-      const float bx = rx + lox, by = ry + loy;  // LANES: the lane's jitter square; else the pixel's sample rectangle
-      const float omax = LANES ? 1.0f : (float)(ss - 1) / (float)ss + (P.additive ? 1.0f : 0.0f);
+      // LANES: the lane's jitter square; else (and chunks) the pixel's sample rectangle
+      const float bx = rx + lox, by = ry + loy;
+      const float omax = LANES && !chunks ? 1.0f : (float)(ss - 1) / (float)ss + (P.additive ? 1.0f : 0.0f);
       const v3 q[4] = {mmul(view, mk(bx, by, P.rz)), mmul(view, mk(bx + omax, by, P.rz)),
                        mmul(view, mk(bx, by + omax, P.rz)), mmul(view, mk(bx + omax, by + omax, P.rz))};
       B = make_bundle_quad(eye, q, valid);
@@ -2446,7 +2450,7 @@ __global__ RFX_TRACE_BOUNDS void prim_cull_kernel(DevScene S, FrameParams P, uin
   // the primary hits of every sample, as trace_from's first segment finds them with this mask (Scene.cpp:86-106), and
   // per light the union of their shadow bundles' masks.  Jittered frames: the hits are not known ahead, no shadow masks
   // (FrameParams::prim_shadow; the trace kernel builds those bundles itself).
-  const int nl = P.additive ? 0 : min(S.n_light, kPrimLights);
+  const int nl = P.additive || chunks ? 0 : min(S.n_light, kPrimLights);
   uint64_t sm[kPrimLights] = {0, 0, 0, 0};
   const float ssf = (float)ss;
   const int nss = LANES ? 1 : ss;  // LANES: the lane's one sample
