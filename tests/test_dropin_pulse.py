@@ -89,13 +89,18 @@ def test_pulse_screenshot_on_a_device_group(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("devices,policy", [(None, "frame"), (None, "span"), ("0,0,0", "frame")])
-def test_pulse_screenshot_128x128_samples(tmp_path, devices, policy):
-    """Pulse's screenshot at 800x600 with 128x128 SSAA (menu keys 1 and 8; Pulse.cpp:10-34): 7.9e9 samples, more than
-    2^32, which the renderer splits into launches (rfx_render_frame) or row-span passes (a device group).  The BMP equals,
-    byte for byte, the reference's frame written by the reference's Texture::saveToFile (tools/gen_golden.py
-    pulse_screenshot_800x600_ss128; the route is pinned to the reference Pulse's own BMP at 2x2)."""
-    c = manifest()["cases"]["pulse_screenshot_800x600_ss128"]
+@pytest.mark.parametrize("case,devices,policy", [("pulse_screenshot_800x600_ss128", None, "frame"),
+                                                  ("pulse_screenshot_800x600_ss128", None, "span"),
+                                                  ("pulse_screenshot_800x600_ss128", "0,0,0", "frame"),
+                                                  ("pulse_screenshot_1920x1080_ss128", None, "frame"),
+                                                  ("pulse_screenshot_1920x1080_ss128", "0,0,0", "frame")])
+def test_pulse_screenshot_128x128_samples(tmp_path, case, devices, policy):
+    """Pulse's screenshot with 128x128 SSAA (menu key 8; Pulse.cpp:10-34) at 800x600 (7.9e9 samples) and at 1920x1080,
+    the reference's ReadMe image (ReadMe.md:30-32; 3.4e10 samples): more than 2^32, which the renderer splits into
+    launches (rfx_render_frame) or row-span passes (a device group).  The BMP equals, byte for byte, the reference's frame
+    written by the reference's Texture::saveToFile (tools/gen_golden.py; the route is pinned to the reference Pulse's own
+    BMP at 2x2)."""
+    c = manifest()["cases"][case]
     if not os.path.exists(DROPIN):
         pytest.fail("tests/native/_build/pulse_dropin missing: run __graft_entry__.build() where /root/reference exists")
     env = {k: v for k, v in os.environ.items() if k != "RFX_DEVICES"}

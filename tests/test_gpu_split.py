@@ -140,11 +140,12 @@ def test_split_frame_on_a_device_group():
     one.close()
 
 
-def test_screenshot_over_2_32_samples():
+@pytest.mark.parametrize("case", ["pulse_screenshot_800x600_ss128", "pulse_screenshot_1920x1080_ss128"])
+def test_screenshot_over_2_32_samples(case):
     """800x600 at 128x128 samples, depth 20 (Pulse's menu keys 1 and 8): 7.9e9 samples in one rfx_render_frame, split
-    into launches at the default limit; SHA-256 of the floats and the ARGB8 image equal the reference's frame
-    (tools/gen_golden.py, banded refharness)."""
-    c = CASES["pulse_screenshot_800x600_ss128"]
+    into launches at the default limit; and the reference's ReadMe screenshot, 1920x1080 at 128x128 (3.4e10 samples).
+    SHA-256 of the floats and the ARGB8 image equal the reference's frame (tools/gen_golden.py, banded refharness)."""
+    c = CASES[case]
     assert c["samples"] >= 1 << 32
     rgb, argb, r = gpu_render(scenes.get_scene("default"), c["W"], c["H"], c["depth"], c["ss"],
                               sphere_seed=c["RFX_SPHERE_SEED"])
