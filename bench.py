@@ -736,9 +736,10 @@ def main(argv=None):
                       **({"rng_prepass_kind": "look-ahead emit on the side stream, beside the previous trace (HIP "
                                               "events on that stream): off the critical path"}
                          if emit_side is not None else {}),
-                      **({"split_kind": f"{launches} launches per frame on two streams: rng_prepass sums the frame's "
-                                        "pre-passes (each timed on its stream while the other stream's trace runs); "
-                                        "trace is the frame's wall time / launches"}
+                      **({"split_kind": f"{launches} launches per frame on two streams: rng_prepass is the mean "
+                                        "pre-pass per launch, timed on its stream while the other stream's trace holds "
+                                        "the chip (so it spans most of that trace, off the critical path); trace is "
+                                        "the frame's wall time / launches"}
                          if launches > 1 else {})},
         "work_per_ray": {k: round(v, 3) for k, v in work.items() if k != "flops"},
         # SURVEY §8(d) secondary metric: bounce segments + shadow rays per second (counted, frame 0's rates)
