@@ -133,7 +133,9 @@ int rfx_renderer_bounce_form(const rfx_renderer *r);
 /* Primary-bundle cull masks of small-scene plain frames and of SSAA frames run one sample per lane (sampleNum 2, 4,
  * 8, and jittered sampleNum 1) (no pixel changes): the first segment's cull masks of every wave tile, computed by one
  * extra launch for a view (camera, frame geometry, sampling, scene) and reused while the view stays.  1 (default) = built when a view repeats (the second frame of a still camera on), so a camera that
- * moves every frame never pays for them; 2 = built before every launch; 0 = off (per-launch bundles). */
+ * moves every frame never pays for them; 2 = built before every launch; 0 = off (per-launch bundles).  SSAA frames of
+ * sampleNum > 8 (a wave per pixel) take one closest-hit mask per pixel, built for every view and every launch of a split
+ * frame under 1 and 2.  Any call forgets the views seen so far. */
 int rfx_renderer_set_prim_masks(rfx_renderer *r, int mode);
 /* The reference's two LCG streams (trace_math.h:34-39): Vector3.cpp's (randomInsideSphere) and
  * Render.cpp's (additive jitter).  Both persist across frames exactly as the reference's would. */

@@ -307,9 +307,9 @@ class Renderer:
         check(_lib.load().rfx_renderer_set_tile_order(self._h, int(mode)), "set_tile_order")
 
     def set_prim_masks(self, mode: int):
-        """Primary-bundle cull masks of small-scene plain and one-sample-per-lane SSAA frames
-        (rfx.h rfx_renderer_set_prim_masks): 1 built when
-        a view repeats (default), 2 before every launch, 0 off.  No pixel changes."""
+        """Primary-bundle cull masks of small-scene plain and SSAA frames (rfx.h rfx_renderer_set_prim_masks): 1 built
+        when a view repeats (default; sampleNum > 8: every view), 2 before every launch, 0 off.  No pixel changes.  Any
+        call forgets the views seen so far."""
         check(_lib.load().rfx_renderer_set_prim_masks(self._h, int(mode)), "set_prim_masks")
 
     def set_regroup(self, park_after: int):
