@@ -37,6 +37,9 @@ hipError_t launch_rng_finish_band(const uint32_t *d_seed, const uint32_t *d_jump
                                   const uint32_t *d_blk_cnt, const uint16_t *d_masks, uint64_t nblk, uint64_t traces,
                                   uint32_t *d_rd_state, int *d_err, uint64_t lo, uint64_t hi, uint64_t *d_off,
                                   uint32_t *d_range, hipStream_t st);
+hipError_t launch_rng_fused(const uint32_t *d_seed, const uint32_t *d_jump, uint32_t *d_next_seed, uint64_t nblk,
+                            uint64_t traces, uint32_t *d_rd_state, int *d_err, unsigned long long *d_status,
+                            unsigned long long *d_ticket, uint32_t epoch, hipStream_t st);
 hipError_t launch_trace(const DevScene &S, const FrameParams &P, bool stats, hipStream_t st);
 hipError_t launch_prim_cull(const DevScene &S, const FrameParams &P, uint64_t *masks, hipStream_t st);
 hipError_t launch_queue_sort(const uint32_t *count, const uint32_t *key, uint32_t *hist, uint32_t *order, hipStream_t st);
@@ -530,6 +533,9 @@ struct rfx_renderer {
   uint32_t *d_blk_cnt = nullptr; uint64_t blk_cap = 0;
   uint64_t *d_blk_off = nullptr;     // band emits: the scanned block offsets ...
   uint32_t *d_rng_range = nullptr;   // ... and the band's first / last / final block
+  // the one-pass pre-pass (rng_fused): per-block status words (blk_cap), the block ticket, the launch's epoch tag
+  unsigned long long *d_rng_status = nullptr, *d_rng_ticket = nullptr;
+  uint32_t rng_epoch = 0;
   uint16_t *d_rng_masks = nullptr;  // one device's accept flags per pre-pass thread (rng_count -> rng_emit)
   uint32_t *d_jump = nullptr;  // LCG jump table for blk_cap blocks (rng_jump_table)
   // host staging for rfx_render_frame_host
@@ -682,6 +688,7 @@ extern "C" void rfx_renderer_destroy(rfx_renderer *r)
   (void)hipFree(r->d_seed); (void)hipFree(r->d_err); (void)hipFree(r->d_rd); (void)hipFree(r->d_rd_alt);
   (void)hipFree(r->d_blk_cnt); (void)hipFree(r->d_jump); (void)hipFree(r->d_rng_masks); (void)hipFree(r->d_blk_off);
   (void)hipFree(r->d_rng_range);
+  (void)hipFree(r->d_rng_status); (void)hipFree(r->d_rng_ticket);
   (void)hipFree(r->d_img); (void)hipFree(r->d_argb); (void)hipFree(r->d_cnt);
   (void)hipFree(r->d_queue); (void)hipFree(r->d_qctr); (void)hipFree(r->d_prim_mask);
   (void)hipFree(r->d_split_mask[0]); (void)hipFree(r->d_split_mask[1]);
@@ -1236,7 +1243,8 @@ extern "C" int rfx_renderer_get_rng(rfx_renderer *r, uint32_t *sphere_seed, uint
   HIP_CHECK(hipMemcpyAsync(&s, seed_cur(r), sizeof(uint32_t), hipMemcpyDeviceToHost, r->stream));
   HIP_CHECK(hipMemcpyAsync(&err, r->d_err, sizeof(int), hipMemcpyDeviceToHost, r->stream));
   HIP_CHECK(hipStreamSynchronize(r->stream));
-  if (err) return fail(RFX_ERR_RNG, "RNG pre-pass ran short of accepted triples");
+  if (err) return fail(RFX_ERR_RNG, err == 2 ? "RNG pre-pass: a block's offset look-back gave up waiting"
+                                              : "RNG pre-pass ran short of accepted triples");
   if (sphere_seed) *sphere_seed = s;
   if (jitter_seed) *jitter_seed = r->jitter_seed;
   return RFX_OK;
@@ -1278,8 +1286,18 @@ static int ensure_rng_workspace(rfx_renderer *r, uint64_t traces, uint64_t nblk)
   if (nblk > r->blk_cap)
   {
     (void)hipFree(r->d_blk_cnt); (void)hipFree(r->d_jump); (void)hipFree(r->d_rng_masks); (void)hipFree(r->d_blk_off);
+    (void)hipFree(r->d_rng_status);
     r->d_blk_cnt = nullptr; r->d_jump = nullptr; r->d_rng_masks = nullptr; r->d_blk_off = nullptr; r->blk_cap = 0;
+    r->d_rng_status = nullptr;
     HIP_CHECK(hipMalloc(&r->d_blk_cnt, nblk * sizeof(uint32_t)));
+    HIP_CHECK(hipMalloc(&r->d_rng_status, nblk * sizeof(unsigned long long)));
+    HIP_CHECK(hipMemset(r->d_rng_status, 0, nblk * sizeof(unsigned long long)));  // epoch 0: no launch's
+    r->rng_epoch = 0;
+    if (!r->d_rng_ticket)
+    {
+      HIP_CHECK(hipMalloc(&r->d_rng_ticket, sizeof(unsigned long long)));
+      HIP_CHECK(hipMemset(r->d_rng_ticket, 0, sizeof(unsigned long long)));
+    }
     HIP_CHECK(hipMalloc(&r->d_blk_off, nblk * sizeof(uint64_t)));
     if (!r->d_rng_range) HIP_CHECK(hipMalloc(&r->d_rng_range, 4 * sizeof(uint32_t)));
     HIP_CHECK(hipMalloc(&r->d_rng_masks, nblk * 256 * sizeof(uint16_t)));
@@ -1415,6 +1433,32 @@ static int emit_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *d_counts, 
   // the caller's event: the randDirs are written and the next frame's stream state is known (the next frame's
   // RNG count may start on another stream while this frame traces)
   if (emitted) HIP_CHECK(hipEventRecord(emitted, st));
+  return RFX_OK;
+}
+
+// The whole pre-pass of a one-device launch in one kernel (rng_fused: count, look-back scan and scatter), with
+// emit_frame's bookkeeping.  RFX_RNG_FUSED=0 keeps the two-kernel form (rng_count, then emit_frame).
+// Launches of at most RFX_RNG_FUSED_MAX_BLOCKS pre-pass blocks take it: on larger ones (C3: 4,067 blocks) the look-back
+// chain costs what the second launch does (interleaved A/B, profiles/r05/ab/*_rng_fused.jsonl).
+#ifndef RFX_RNG_FUSED
+#define RFX_RNG_FUSED 1
+#endif
+#ifndef RFX_RNG_FUSED_MAX_BLOCKS
+#define RFX_RNG_FUSED_MAX_BLOCKS 2048
+#endif
+static bool fused_prepass(const FramePlan &pl, uint64_t nblk)
+{
+  return RFX_RNG_FUSED && !pl.band && pl.P.nranks <= 1 && nblk <= (uint64_t)RFX_RNG_FUSED_MAX_BLOCKS;
+}
+
+static int prepass_fused(rfx_renderer *r, FramePlan &pl, uint64_t nblk, uint32_t *rd, hipEvent_t emitted)
+{
+  r->rng_epoch = r->rng_epoch % ((1u << 28) - 1) + 1;  // 1 .. 2^28 - 1, a new tag per launch
+  HIP_CHECK(launch_rng_fused(seed_cur(r), r->d_jump, seed_next(r), nblk, pl.traces, rd, r->d_err, r->d_rng_status,
+                             r->d_rng_ticket, r->rng_epoch, pl.st));
+  r->seed_idx ^= 1u;
+  ++r->state_seq;
+  if (emitted) HIP_CHECK(hipEventRecord(emitted, pl.st));
   return RFX_OK;
 }
 
@@ -1738,9 +1782,19 @@ extern "C" int rfx_render_frame(rfx_renderer *r, const rfx_frame *f, float *d_rg
   if ((rc = timing_start(r, pl.st)) != RFX_OK) return rc;
   if (r->emit_pending >= 0)
     return fail(RFX_ERR_STATE, "render_frame: an emitted frame awaits rfx_render_frame_emitted (or rfx_frame_rng_discard)");
-  // one device counts every block, so the emit can take its accept flags instead of regenerating them
-  HIP_CHECK(launch_rng_count(seed_cur(r), r->d_jump, r->d_blk_cnt, 0, nblk, r->d_rng_masks, pl.st));
-  if ((rc = finish_frame(r, pl, r->d_blk_cnt, r->d_rng_masks, nblk, d_rgb, d_argb, d_counters)) != RFX_OK) return rc;
+  if (fused_prepass(pl, nblk))
+  {
+    if ((rc = prepass_fused(r, pl, nblk, r->d_rd, nullptr)) != RFX_OK) return rc;
+    r->trace_buf = 0;
+    if ((rc = timing_event(r, pl.st)) != RFX_OK) return rc;
+    if ((rc = trace_frame(r, pl, r->d_rd, d_rgb, d_argb, d_counters)) != RFX_OK) return rc;
+  }
+  else
+  {
+    // one device counts every block, so the emit can take its accept flags instead of regenerating them
+    HIP_CHECK(launch_rng_count(seed_cur(r), r->d_jump, r->d_blk_cnt, 0, nblk, r->d_rng_masks, pl.st));
+    if ((rc = finish_frame(r, pl, r->d_blk_cnt, r->d_rng_masks, nblk, d_rgb, d_argb, d_counters)) != RFX_OK) return rc;
+  }
   r->rewind_ok = true;
   r->rewind_flip = true;
   r->rewind_jitter = jitter0;
@@ -1800,9 +1854,16 @@ static int render_split(rfx_renderer *r, const rfx_frame *f, uint64_t p0, uint64
     const uint64_t nblk = rng_layout(pl.traces, 1, nullptr);
     if (k > 0) HIP_CHECK(hipStreamWaitEvent(s2[side], r->split_ev[side ^ 1], 0));  // span k - 1's end state
     if ((rc = timing_start(r, pl.st)) != RFX_OK) return rc;
-    HIP_CHECK(launch_rng_count(seed_cur(r), r->d_jump, r->d_blk_cnt, 0, nblk, r->d_rng_masks, pl.st));
     uint32_t *rd = side ? r->d_rd_alt : r->d_rd;
-    if ((rc = emit_frame(r, pl, r->d_blk_cnt, r->d_rng_masks, nblk, rd, r->split_ev[side])) != RFX_OK) return rc;
+    if (fused_prepass(pl, nblk))
+    {
+      if ((rc = prepass_fused(r, pl, nblk, rd, r->split_ev[side])) != RFX_OK) return rc;
+    }
+    else
+    {
+      HIP_CHECK(launch_rng_count(seed_cur(r), r->d_jump, r->d_blk_cnt, 0, nblk, r->d_rng_masks, pl.st));
+      if ((rc = emit_frame(r, pl, r->d_blk_cnt, r->d_rng_masks, nblk, rd, r->split_ev[side])) != RFX_OK) return rc;
+    }
     if ((rc = timing_event(r, pl.st)) != RFX_OK) return rc;
     if ((rc = trace_frame(r, pl, rd, d_rgb, d_argb, d_counters)) != RFX_OK) return rc;
     a = b;
@@ -1992,7 +2053,8 @@ extern "C" int rfx_synchronize(rfx_renderer *r)
   HIP_CHECK(hipStreamSynchronize(r->stream));
   int err = 0;
   HIP_CHECK(hipMemcpy(&err, r->d_err, sizeof(int), hipMemcpyDeviceToHost));
-  if (err) return fail(RFX_ERR_RNG, "RNG pre-pass ran short of accepted triples");
+  if (err) return fail(RFX_ERR_RNG, err == 2 ? "RNG pre-pass: a block's offset look-back gave up waiting"
+                                              : "RNG pre-pass ran short of accepted triples");
   return RFX_OK;
 }
 

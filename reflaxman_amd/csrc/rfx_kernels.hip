@@ -461,6 +461,149 @@ __global__ __launch_bounds__(kRngBlock) void rng_emit_band(const uint32_t *seed,
   }
 }
 
+// One-pass pre-pass (one device, no partition): count, scan and scatter in one launch.  Each workgroup generates its
+// 16 triples per thread once (states and accept flags), publishes its accept count, then finds its offset by decoupled
+// look-back over the published words of the blocks before it -- 64 at a time, one per lane of the first wave -- until
+// one holds an inclusive prefix; it publishes its own inclusive prefix and scatters as emit_block does.  A status word
+// is epoch << 36 | flag << 34 | value (flag 1: the block's count, 2: its inclusive prefix); a word of another launch's
+// epoch reads as not yet published, so the array is never cleared.  The waits are bounded: past kLookbackSpins polls
+// the launch flags an error (RFX_ERR_RNG) and goes on, so a broken invariant cannot hang the device.
+// RFX_RNG_TICKET=0 (default): the block number is blockIdx.x.  Each XCD dispatches its workgroups in index order, so
+// the oldest unfinished block is always resident and waits only on finished ones; the ticket (one device-scope atomic
+// per block, all on one word) serialised the launch's start.
+#ifndef RFX_RNG_TICKET
+#define RFX_RNG_TICKET 0
+#endif
+#ifndef RFX_LOOKBACK_SLEEP
+#define RFX_LOOKBACK_SLEEP 1  // s_sleep between polls of a not yet published status word (units of 64 cycles)
+#endif
+constexpr uint64_t kStatAgg = 1ull << 34, kStatPre = 2ull << 34, kStatVal = (1ull << 34) - 1;
+constexpr uint32_t kLookbackSpins = 1u << 22;
+
+// Relaxed device-scope accesses: a status word carries its own value, and no other data is handed over through it, so
+// no fence is needed (release / acquire at device scope would write back and invalidate the XCDs' L2s on every access).
+__device__ __forceinline__ unsigned long long status_load(const unsigned long long *p)
+{
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ void status_store(unsigned long long *p, unsigned long long v)
+{
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(kRngBlock) void rng_fused(const uint32_t *seed, const uint32_t *jump, uint32_t nblk,
+                                                       uint64_t need, uint32_t *rd_state, uint32_t *next_seed, int *err,
+                                                       unsigned long long *status, unsigned long long *ticket,
+                                                       uint32_t epoch)
+{
+  __shared__ uint32_t sst[kTriplesPerBlock];
+  __shared__ uint32_t wsum[kRngBlock / 64];
+  __shared__ uint64_t s_off;
+  uint32_t b = blockIdx.x;
+#if RFX_RNG_TICKET
+  __shared__ uint32_t s_b;
+  if (threadIdx.x == 0)
+  {
+    const uint32_t t = (uint32_t)atomicAdd(ticket, 1ull);
+    if (t == nblk - 1) atomicExch(ticket, 0ull);  // every block has its ticket: ready for the next launch
+    s_b = t;
+  }
+  __syncthreads();
+  b = s_b;
+#endif
+  // the block's triples, generated once: the state before each and its accept flag (rng_count / emit_block)
+  uint32_t s = thread_state(*seed, jump, b, threadIdx.x);
+  uint32_t s2 = kHalfJump.a * s + kHalfJump.c;
+  uint32_t st[kTriplesPerThread];
+  uint32_t acc = 0, c = 0;
+  {
+    float x, y, z;
+#pragma unroll
+    for (int j = 0; j < kHalfRun; ++j)
+    {
+      st[j] = s;
+      st[j + kHalfRun] = s2;
+      const bool a = triple(s, x, y, z), a2 = triple(s2, x, y, z);
+      acc |= (a ? 1u : 0u) << j | (a2 ? 1u : 0u) << (j + kHalfRun);
+      c += (a ? 1u : 0u) + (a2 ? 1u : 0u);
+    }
+  }
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t inc = c;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1)
+  {
+    const uint32_t v = __shfl_up(inc, o, 64);
+    if (lane >= (uint32_t)o) inc += v;
+  }
+  if (lane == 63) wsum[threadIdx.x >> 6] = inc;
+  __syncthreads();
+  uint32_t wbase = 0, tot = 0;
+  for (uint32_t w = 0; w < kRngBlock / 64; ++w)
+  {
+    if (w < (threadIdx.x >> 6)) wbase += wsum[w];
+    tot += wsum[w];
+  }
+  if (threadIdx.x < 64)
+  {
+    const unsigned long long tag = (unsigned long long)epoch << 36;
+    uint64_t excl = 0;
+    if (b == 0)
+    {
+      if (lane == 0) status_store(&status[0], tag | kStatPre | tot);
+    }
+    else
+    {
+      if (lane == 0) status_store(&status[b], tag | kStatAgg | tot);
+      int64_t j = (int64_t)b - 1 - (int64_t)lane;  // this lane's predecessor in the window
+      uint32_t spins = 0;
+      for (;;)
+      {
+        const unsigned long long w = j >= 0 ? status_load(&status[j]) : (tag | kStatPre);
+        const bool ready = (w >> 36) == (unsigned long long)epoch && (w & (3ull << 34)) != 0;
+        const uint64_t pre = __ballot(ready && (w & (3ull << 34)) == kStatPre);
+        const uint32_t first = pre ? (uint32_t)__builtin_ctzll(pre) : 64u;  // nearest predecessor with a prefix
+        const uint64_t upto = first >= 63 ? ~0ull : (2ull << first) - 1ull;
+        if (__ballot(!ready) & upto)
+        {
+          if (++spins > kLookbackSpins)
+          {
+            if (lane == 0) *err = 2;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(RFX_LOOKBACK_SLEEP);
+          continue;
+        }
+        uint64_t v = lane <= first ? (uint64_t)(w & kStatVal) : 0ull;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        excl += v;
+        if (first < 64) break;
+        j -= 64;
+      }
+      if (lane == 0) status_store(&status[b], tag | kStatPre | ((excl + tot) & kStatVal));
+    }
+    if (lane == 0) s_off = excl;
+  }
+  __syncthreads();
+  const uint64_t off = s_off;
+  if (b == nblk - 1 && threadIdx.x == 0 && off + tot < need) *err = 1;  // stream too short for the frame
+  if (off >= need) return;
+  const uint32_t cnt = (uint32_t)min((uint64_t)tot, need - off);
+  uint32_t li = wbase + (inc - c);                                               // block-local rank
+#pragma unroll
+  for (int j = 0; j < kTriplesPerThread; ++j)
+    if ((acc >> j) & 1u)
+    {
+      if (off + li == need - 1) *next_seed = lcg_step(lcg_step(lcg_step(st[j])));
+      if (li < cnt) sst[li] = st[j];
+      ++li;
+    }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < cnt; i += kRngBlock) rd_state[off + i] = sst[i];
+}
+
 // ------------------------------------------------------------- device known-answer kernels
 // Thread i runs the trace kernel's own device code on one case (rfx.h rfx_kat_*), so the reference's
 // known answers (tests/golden/kat_*.npz, outputs of the unmodified Sphere / Triangle / Plane / Skybox /
@@ -716,6 +859,17 @@ hipError_t launch_rng_finish_band(const uint32_t *d_seed, const uint32_t *d_jump
   hipLaunchKernelGGL(rng_emit_band, dim3((uint32_t)std::min<uint64_t>(est, nblk)), dim3(kRngBlock), 0, st, d_seed, d_jump,
                      d_blk_cnt, d_masks, (const uint64_t *)d_off, (const uint32_t *)d_range, nblk, traces, d_rd_state,
                      d_next_seed, flt);
+  return hipGetLastError();
+}
+
+// the one-pass pre-pass of a one-device launch (rng_fused); status: nblk words, ticket: one word, both zeroed once at
+// allocation; epoch: this launch's tag, distinct from every earlier launch's on the same status array (never 0)
+hipError_t launch_rng_fused(const uint32_t *d_seed, const uint32_t *d_jump, uint32_t *d_next_seed, uint64_t nblk,
+                            uint64_t traces, uint32_t *d_rd_state, int *d_err, unsigned long long *d_status,
+                            unsigned long long *d_ticket, uint32_t epoch, hipStream_t st)
+{
+  hipLaunchKernelGGL(rng_fused, dim3((uint32_t)nblk), dim3(kRngBlock), 0, st, d_seed, d_jump, (uint32_t)nblk, traces,
+                     d_rd_state, d_next_seed, d_err, d_status, d_ticket, epoch);
   return hipGetLastError();
 }
 

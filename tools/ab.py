@@ -80,6 +80,7 @@ VARIANTS = {
     "scanall": ["RFX_SCAN_EMIT_BLOCKS=0"],
     "chsum0": ["RFX_SSAA_CHANNEL_SUM=0"],
     "nochunkmask": ["RFX_PRIM_CHUNKS=0"],
+    "fused0": ["RFX_RNG_FUSED=0"],
     "nohint": ["RFX_OCC_HINT=0"],
     "split1": ["RFX_SPLIT_STREAMS=1"],
     "leaf1": ["RFX_BVH_LEAF_PAIRS=1"],
