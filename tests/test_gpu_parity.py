@@ -124,6 +124,22 @@ def test_rand_dirs_prepass():
     rr.close()
 
 
+@pytest.mark.parametrize("W,H,ss,frames", [(1, 1, 1, 3), (7, 9, 1, 2), (65, 63, 1, 2), (640, 480, 1, 2),
+                                           (1999, 2000, 1, 2), (2000, 2000, 1, 1), (2100, 2100, 1, 1), (333, 200, 8, 1),
+                                           (512, 511, 2, 2), (300, 200, 4, 1)])
+def test_rng_stream_state_per_frame_size(W, H, ss, frames):
+    """The render path's pre-pass -- the one-pass kernel (rng_fused: count, decoupled look-back scan, scatter) up to
+    RFX_RNG_FUSED_MAX_BLOCKS blocks, the two-kernel form beyond (2000x2000 is 1,969 blocks, 2100x2100 2,170) -- carries
+    the reference's randomInsideSphere stream: after each frame the renderer's sphere seed equals the serial stream
+    advanced by the frame's W*H*ss^2 accepted triples (oracle orc_rand_dirs), frame after frame; no error flag."""
+    import oracle as orc
+    desc = scene("default")
+    _, _, r = gpu_render(desc, W, H, 1, ss, frames=frames, sphere_seed=4242)
+    _, after = orc.rand_dirs(4242, W * H * ss * ss * frames)
+    assert r.getRng()[0] == after
+    r.close()
+
+
 @pytest.mark.parametrize("name,W,H,depth,ss,additive,chunks", [
     ("synth16", 640, 360, 8, 1, False, None),      # plain frames: record, reuse the sorted order, re-sort
     ("default", 200, 150, 4, 2, True, None),       # SSAA + additive accumulation
