@@ -300,6 +300,12 @@ class SingleGpu:
         self.r.close()
 
 
+def times_c4_denominator(world: int, cfg_name: str, custom: bool, no_c4: bool) -> bool:
+    """Does this line carry c4_1gpu -- the C4 frame timed on one GPU in the same run?  The driver's default N = 1 line
+    (C3) does, so that a scaling curve over the N > 1 lines (C4) has a same-config denominator."""
+    return world == 1 and cfg_name == "c3" and not custom and not no_c4
+
+
 LAUNCH_TRACES = 1 << 30  # rfx_host.cpp RFX_LAUNCH_TRACES (the library's default launch limit)
 
 
@@ -354,6 +360,7 @@ def main(argv=None):
     ap.add_argument("--depth", type=int, default=None)
     ap.add_argument("--ss", type=int, default=None, help="samples per pixel ss x ss (SSAA; default: the config's)")
     ap.add_argument("--no-first-view", action="store_true", help="N = 1: skip the first-view timing")
+    ap.add_argument("--no-c4", action="store_true", help="N = 1 (C3): skip the same-run C4 frame (c4_1gpu)")
     ap.add_argument("--gather-rgb", action="store_true", help="N > 1: gather the float RGB strips to rank 0 too")
     ap.add_argument("--regroup", type=int, default=None,
                     help="ray regrouping: park traces after n segments (0 off; default: the library's choice)")
@@ -411,8 +418,8 @@ def main(argv=None):
 
     W, H = frame_size(world, args.width, args.height, args.scaling)
     depth, rb, ss = args.depth, args.row_block, args.ss
-    if world > 1 and ss != 1:
-        raise SystemExit("bench.py: N > 1 renders one-sample frames (the SSAA screenshot is a single-GPU line)")
+    if world > 1 and args.partition == "strips" and W * H * ss * ss > (1 << 31):
+        raise SystemExit("bench.py: frames of more than 2^31 traces run as row-span passes of bands (--partition bands)")
     desc = scenes.get_scene(args.scene)
     scene, cam = build_scene(desc)
     rr = Renderer(device=local, sphere_seed=SEED)
@@ -436,7 +443,7 @@ def main(argv=None):
         common = dict(pipeline=False if args.no_pipeline else None, gather_rgb=args.gather_rgb,
                       count_ahead=False if args.no_count_ahead else None,
                       emit_ahead=False if args.no_emit_ahead else None)
-        sf = BandFrame(ops, W, H, rank, world, dev, **common) if bands else \
+        sf = BandFrame(ops, W, H, rank, world, dev, ss=ss, **common) if bands else \
             StripFrame(ops, W, H, rb, rank, world, dev, **common)
         rows, img, argb = sf.rows, sf.img, sf.argb
     else:
@@ -458,13 +465,14 @@ def main(argv=None):
     one = None  # rank 0 at N > 1: a single-GPU renderer of the same frame (parity checks, strong-scaling baseline)
     if world > 1 and rank == 0:
         # the assembled multi-rank frame must equal a single-GPU render of the same frame (untimed)
-        one = SingleGpu(Renderer, scene, make_frame(cam, W, H, depth, 1), W, H, dev, stream)
+        one = SingleGpu(Renderer, scene, make_frame(cam, W, H, depth, ss), W, H, dev, stream)
         img1, argb1 = one.render(SEED)
         parity["multi_rank_frame_equals_single_gpu"] = bool(torch.equal(full0.reshape(-1), argb1))
         if args.gather_rgb:
             parity["multi_rank_rgb_equals_single_gpu"] = bool(torch.equal(sf.rgb_full.reshape(-1), img1))
         man = json.load(open(os.path.join(ROOT, "tests", "golden", "manifest.json")))["cases"]
-        key = f"hash_{args.scene}_{W}x{H}_d{depth}"
+        key = f"hash_{args.scene}_{W}x{H}_d{depth}" + (f"_ss{ss}" if ss != 1 else "")
+        key = PARITY_CASE.get(cfg_name, key) if not custom else key
         if key in man:
             parity["multi_rank_frame_vs_reference_sha256"] = {
                 "argb8": sha(full0.reshape(-1).cpu().numpy().view(np.uint32).tobytes()) == man[key]["sha_argb"],
@@ -491,7 +499,10 @@ def main(argv=None):
         c = torch.zeros(_lib.RFX_NCOUNTERS, dtype=torch.int64, device=dev)
         if world > 1:
             sf.drop_lookahead()
-        rr.render_frame(frame, cimg.data_ptr(), cargb.data_ptr(), c.data_ptr(), stream.cuda_stream)
+        if world > 1 and bands and sf.passes:
+            sf.step(c.data_ptr())  # a frame of row-span passes: the counters sum the passes' band launches
+        else:
+            rr.render_frame(frame, cimg.data_ptr(), cargb.data_ptr(), c.data_ptr(), stream.cuda_stream)
         torch.cuda.synchronize()
         return c
 
@@ -665,6 +676,25 @@ def main(argv=None):
                       "note": "value (above) is the steady state of a still camera: masks built on its second frame, "
                               "longest-first schedule from earlier frames' tile costs"}
 
+    c4_1gpu = None
+    if times_c4_denominator(world, cfg_name, custom, args.no_c4):
+        # the denominator of a scaling curve: N > 1 lines render C4 (7680x4320), the N = 1 line C3 (3840x2160), so the
+        # C4 frame is also timed here on this GPU, same steps and warmup, and checked against the reference's hash
+        s4, w4, h4, d4, _, _ = CONFIGS["c4"]
+        sc4, cam4 = build_scene(scenes.get_scene(s4))
+        one4 = SingleGpu(Renderer, sc4, make_frame(cam4, w4, h4, d4, 1), w4, h4, dev, stream)
+        _, argb4 = one4.render(SEED)
+        man = json.load(open(os.path.join(ROOT, "tests", "golden", "manifest.json")))["cases"]
+        key4 = f"hash_{s4}_{w4}x{h4}_d{d4}"
+        ok4 = sha(argb4.cpu().numpy().view(np.uint32).tobytes()) == man[key4]["sha_argb"] if key4 in man else None
+        c4_1gpu = one4.time(args.steps, args.warmup, prewarm_s=args.prewarm_ms * 1e-3, traces=w4 * h4)
+        c4_1gpu.update({"config": f"C4 {s4} {w4}x{h4} d{d4}, 1 spp", "frame_vs_reference_sha256": {"argb8": ok4,
+                                                                                                  "case": key4},
+                        "kind": "the C4 frame (the N > 1 lines' fixed frame) on this GPU alone in this run: the "
+                                "same-config denominator of value(N) / (N value(1))"})
+        one4.close()
+        del one4
+
     rgb_gather = None
     if world > 1 and bands and not args.gather_rgb:
         # the drop-in's path reads the float image (Render::imagePixel): the same bands with the f32 RGB plane sent to
@@ -708,18 +738,24 @@ def main(argv=None):
     pmc = metrics.pmc_record(os.path.join(ROOT, "profiles", "pmc"), [args.scene, W, H, depth, world, ss],
                              _lib.lib_sha256(), _lib.device_sha256())
     traffic = pmc["hbm_bytes_per_launch"] if pmc else None
-    launches = split_launches(W, H, ss) if world == 1 else 1
-    if launches > 1:
+    passes = len(sf.passes) if world > 1 and bands and sf.passes else 0
+    launches = split_launches(W, H, ss) if world == 1 else max(1, passes)
+    if launches > 1 and world == 1:
         # a frame of several launches on two overlapping streams: a launch's HIP-event span includes the other stream's
         # work, so the per-launch time is the frame's wall time shared out over its launches
         trace_avg = ms_step / launches
         flops_launch = flops_frame / launches
         px_launch = W * H // launches
+    elif launches > 1:
+        # row-span passes (N > 1): rank 0 traces one band per pass, each timed by HIP events on its stream
+        flops_launch = flops_launch / launches
+        px_launch = sf.rows * W // launches
     executed = metrics.executed_work(pmc, trace_avg)
     roofline = metrics.roofline(executed, traffic, flops_launch, trace_avg, px_launch)
     if launches > 1:
         roofline["launches_per_frame"] = launches
-        roofline["launch_time_kind"] = "frame wall time / launches (the split frame's launches overlap on two streams)"
+        roofline["launch_time_kind"] = ("frame wall time / launches (the split frame's launches overlap on two streams)"
+                                        if world == 1 else "rank 0's band launch of each row-span pass (HIP events)")
     roofline["kernel"] = ("rfx::trace_kernel (plain pixel mode, wave-bundle culling)" if ss == 1 else
                           "rfx::trace_kernel (SSAA pixel mode, wave-bundle culling)")
     if baseline is not None:
@@ -737,7 +773,8 @@ def main(argv=None):
                    "parallelism": ((f"balanced-bands-x{world}" if bands else f"row-strips{rb}x{world}")
                                    + ("+pipelined-gather" if sf.pipeline else "")
                                    + ("+count-ahead" if sf.count_ahead else "")
-                                   + ("+emit-ahead" if sf.emit_ahead else "")) if world > 1 else "single-gpu"},
+                                   + ("+emit-ahead" if sf.emit_ahead else "")
+                                   + (f"+row-span-passes-x{passes}" if passes else "")) if world > 1 else "single-gpu"},
         "roofline": roofline,
         "phases_ms": {"rng_prepass": round(pre_avg, 4), "trace": round(trace_avg, 4), "timed_every_nth_frame": timing_every,
                       **({"rng_prepass_kind": "look-ahead emit on the side stream, beside the previous trace (HIP "
@@ -754,10 +791,14 @@ def main(argv=None):
                                            * args.steps / elapsed / 1e6, 1),
         "end_to_end_incl_d2h": e2e,
         **({"first_view": first_view} if first_view else {}),
+        **({"c4_1gpu": c4_1gpu} if c4_1gpu else {}),
         **({"with_rgb_gather": rgb_gather} if rgb_gather else {}),
         "parity": parity,
         **({"band_bounds": sf.bounds} if bands else {}),
         **({"steady_state_parity": steady,
+            "efficiency": baseline["efficiency"] if baseline else None,
+            "efficiency_kind": "value / (N x strong_scaling_baseline.value): the same C4 frame on one GPU of this run "
+                               "(the N = 1 line's c4_1gpu is the same measurement on the driver's N = 1 run)",
             "strong_scaling_baseline": baseline,
             "strong_scaling_baseline_committed": one_gpu_line(cfg_name, W, H, depth),
             "scale_note": "N > 1 renders C4 (7680x4320); the driver's N = 1 bench point is C3 (3840x2160), whose rate "

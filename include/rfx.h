@@ -299,13 +299,18 @@ int rfx_rand_dirs(rfx_renderer *r, uint32_t seed, uint64_t n, float *out3, uint3
  *   rfx_kat_powf_cube: the Fresnel site's powf(x, 3) (Scene.cpp:196) as the bounce loop evaluates it (the double
  *       cube where it provably rounds like glibc, rfx_powf.h powf_cube_fast) against glibc's algorithm on the device,
  *       for every float x in [0, 1]: counts[0] = mismatches (0 expected), counts[1] = inputs that took glibc's
- *       algorithm.
+ *       algorithm;
+ *   rfx_kat_div: the trace loop's division fast paths (rfx_math.h div_rn and the shared-divisor Vector3 / float)
+ *       against IEEE '/' on the operand pairs first .. first + n - 1 of a fixed hash (every float class, both edges
+ *       of the fast path's divisor and quotient bounds): counts[0] = quotients whose bits differ (0 expected),
+ *       counts[1] = pairs that took the fast path, counts[2] = quotients checked (4 per pair).
  */
 int rfx_kat_objects(rfx_renderer *r, const float *rays, const int32_t *objects, uint64_t n, float *out);
 int rfx_kat_texels(rfx_renderer *r, int texture, const float *in, uint64_t n, float *out);
 int rfx_kat_powf(rfx_renderer *r, const float *xy, uint64_t n, float *out);
 int rfx_kat_argb(rfx_renderer *r, const float *rgb, uint64_t n, uint32_t *out);
 int rfx_kat_powf_cube(rfx_renderer *r, uint64_t counts[2]);
+int rfx_kat_div(rfx_renderer *r, uint64_t first, uint64_t n, uint64_t counts[3]);
 /* The kernel-argument layout the bounce loops rely on (rfx_trace.h launder_scene / kernarg_params: DevScene at kernarg
  * offset 0, FrameParams after it): a one-lane kernel of the trace kernels' signature compares the records read through
  * the kernarg segment pointer with its by-value arguments.  out[0] / out[1] = differing words of the scene record / the

@@ -113,6 +113,7 @@ SIGNATURES = [
     ("rfx_kat_powf", C.c_int, [C.c_void_p, _fp, C.c_uint64, _fp]),
     ("rfx_kat_argb", C.c_int, [C.c_void_p, _fp, C.c_uint64, _u32p]),
     ("rfx_kat_powf_cube", C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
+    ("rfx_kat_div", C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64)]),
     ("rfx_kat_kernarg", C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_uint32)]),
 ]
 

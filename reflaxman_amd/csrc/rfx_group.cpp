@@ -435,7 +435,9 @@ static int group_pass(rfx_group *g, const rfx_frame *f, uint32_t y0, uint32_t y1
   for (size_t i = 0; i < m; ++i) GCHECK(hipStreamWaitEvent(s0, g->ev_copied[b][i], 0));
   ++g->frames;
   for (size_t i = 0; i < g->n(); ++i) g->seq[i] = rfx_detail_state_seq(g->r[i]);
-  g->seq_ok = true;
+  // members m..n-1 sat this pass out (a span of fewer rows than members): their streams stayed behind member 0's, so
+  // the next pass hands member 0's state over again
+  g->seq_ok = m == g->n();
   return RFX_OK;
 }
 

@@ -36,10 +36,10 @@ hipError_t launch_rng_finish(const uint32_t *d_seed, const uint32_t *d_jump, uin
 hipError_t launch_rng_finish_band(const uint32_t *d_seed, const uint32_t *d_jump, uint32_t *d_next_seed,
                                   const uint32_t *d_blk_cnt, const uint16_t *d_masks, uint64_t nblk, uint64_t traces,
                                   uint32_t *d_rd_state, int *d_err, uint64_t lo, uint64_t hi, uint64_t *d_off,
-                                  uint32_t *d_range, hipStream_t st);
+                                  uint32_t *d_range, uint32_t *d_tile_sum, hipStream_t st);
 hipError_t launch_rng_fused(const uint32_t *d_seed, const uint32_t *d_jump, uint32_t *d_next_seed, uint64_t nblk,
                             uint64_t traces, uint32_t *d_rd_state, int *d_err, unsigned long long *d_status,
-                            unsigned long long *d_ticket, uint32_t epoch, hipStream_t st);
+                            unsigned long long *d_ticket, unsigned long long base, uint32_t epoch, hipStream_t st);
 hipError_t launch_trace(const DevScene &S, const FrameParams &P, bool stats, hipStream_t st);
 hipError_t launch_prim_cull(const DevScene &S, const FrameParams &P, uint64_t *masks, hipStream_t st);
 hipError_t launch_queue_sort(const uint32_t *count, const uint32_t *key, uint32_t *hist, uint32_t *order, hipStream_t st);
@@ -53,6 +53,7 @@ hipError_t launch_bounce_lds(int cfg, uint32_t groups, const DevScene &S, const 
 hipError_t launch_kat(int what, const DevScene &S, int tex, const void *in, const int32_t *objs, uint32_t n, void *out,
                       hipStream_t st);
 hipError_t launch_kat_powf_cube(uint32_t first, uint32_t n, unsigned long long *counts, hipStream_t st);
+hipError_t launch_kat_div(uint64_t first, uint32_t n, unsigned long long *counts, hipStream_t st);
 hipError_t launch_kat_kernarg(const DevScene &S, const FrameParams &P, int swapped, uint32_t *out, hipStream_t st);
 }  // namespace rfx
 
@@ -515,6 +516,7 @@ struct rfx_renderer {
   uint32_t *d_rd_alt = nullptr; uint64_t rd_alt_cap = 0;  // emit-ahead: the second randDir buffer
   int emit_pending = -1;  // emit-ahead: buffer (0 d_rd, 1 d_rd_alt) of an emitted, untraced frame, or -1
   int trace_buf = 0;      // buffer the last enqueued trace read
+  bool split_alt_busy = false;  // a split frame's odd spans traced from d_rd_alt on split_stream (done at split_ev[2])
   uint64_t emit_key[10] = {};  // the emitted frame's plan (traces, band, geometry): rfx_render_frame_emitted must match it
   // rfx_frame_rng_rewind: the last call was an rfx_render_frame; its start states (the sphere stream's is the other
   // seed word while rewind_flip, or the saved word d_seed[2] while rewind_saved: a frame of several launches) can be
@@ -533,8 +535,11 @@ struct rfx_renderer {
   uint32_t *d_blk_cnt = nullptr; uint64_t blk_cap = 0;
   uint64_t *d_blk_off = nullptr;     // band emits: the scanned block offsets ...
   uint32_t *d_rng_range = nullptr;   // ... and the band's first / last / final block
-  // the one-pass pre-pass (rng_fused): per-block status words (blk_cap), the block ticket, the launch's epoch tag
+  uint32_t *d_tile_sum = nullptr;    // ... and the multi-workgroup scan's tile totals (one per 4096 blocks)
+  // the one-pass pre-pass (rng_fused): per-block status words (blk_cap), the block ticket word (counts up across
+  // launches, never reset), the tickets taken so far, the launch's epoch tag
   unsigned long long *d_rng_status = nullptr, *d_rng_ticket = nullptr;
+  unsigned long long rng_tickets = 0;
   uint32_t rng_epoch = 0;
   uint16_t *d_rng_masks = nullptr;  // one device's accept flags per pre-pass thread (rng_count -> rng_emit)
   uint32_t *d_jump = nullptr;  // LCG jump table for blk_cap blocks (rng_jump_table)
@@ -687,6 +692,7 @@ extern "C" void rfx_renderer_destroy(rfx_renderer *r)
   free_scene(r);
   (void)hipFree(r->d_seed); (void)hipFree(r->d_err); (void)hipFree(r->d_rd); (void)hipFree(r->d_rd_alt);
   (void)hipFree(r->d_blk_cnt); (void)hipFree(r->d_jump); (void)hipFree(r->d_rng_masks); (void)hipFree(r->d_blk_off);
+  (void)hipFree(r->d_tile_sum);
   (void)hipFree(r->d_rng_range);
   (void)hipFree(r->d_rng_status); (void)hipFree(r->d_rng_ticket);
   (void)hipFree(r->d_img); (void)hipFree(r->d_argb); (void)hipFree(r->d_cnt);
@@ -1243,8 +1249,7 @@ extern "C" int rfx_renderer_get_rng(rfx_renderer *r, uint32_t *sphere_seed, uint
   HIP_CHECK(hipMemcpyAsync(&s, seed_cur(r), sizeof(uint32_t), hipMemcpyDeviceToHost, r->stream));
   HIP_CHECK(hipMemcpyAsync(&err, r->d_err, sizeof(int), hipMemcpyDeviceToHost, r->stream));
   HIP_CHECK(hipStreamSynchronize(r->stream));
-  if (err) return fail(RFX_ERR_RNG, err == 2 ? "RNG pre-pass: a block's offset look-back gave up waiting"
-                                              : "RNG pre-pass ran short of accepted triples");
+  if (err & 1) return fail(RFX_ERR_RNG, "RNG pre-pass ran short of accepted triples");  // (bit 4: an exact fallback)
   if (sphere_seed) *sphere_seed = s;
   if (jitter_seed) *jitter_seed = r->jitter_seed;
   return RFX_OK;
@@ -1299,6 +1304,9 @@ static int ensure_rng_workspace(rfx_renderer *r, uint64_t traces, uint64_t nblk)
       HIP_CHECK(hipMemset(r->d_rng_ticket, 0, sizeof(unsigned long long)));
     }
     HIP_CHECK(hipMalloc(&r->d_blk_off, nblk * sizeof(uint64_t)));
+    (void)hipFree(r->d_tile_sum);
+    r->d_tile_sum = nullptr;
+    HIP_CHECK(hipMalloc(&r->d_tile_sum, (nblk / 4096 + 1) * sizeof(uint32_t)));
     if (!r->d_rng_range) HIP_CHECK(hipMalloc(&r->d_rng_range, 4 * sizeof(uint32_t)));
     HIP_CHECK(hipMalloc(&r->d_rng_masks, nblk * 256 * sizeof(uint16_t)));
     std::vector<uint32_t> jump(2 * (256 + nblk));
@@ -1421,10 +1429,11 @@ static int emit_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *d_counts, 
   const uint64_t ss2 = P.ss > 0 ? (uint64_t)(P.ss * P.ss) : 1;
   if (pl.band)  // the band's randDirs into a buffer of the band's size: index trace - band_lo
     HIP_CHECK(launch_rng_finish_band(seed_cur(r), r->d_jump, seed_next(r), d_counts, nullptr, nblk, pl.traces,
-                                     rd - pl.band_lo, r->d_err, pl.band_lo, pl.band_hi, r->d_blk_off, r->d_rng_range, st));
+                                     rd - pl.band_lo, r->d_err, pl.band_lo, pl.band_hi, r->d_blk_off, r->d_rng_range,
+                                     r->d_tile_sum, st));
   else if (P.nranks <= 1 && nblk > RFX_SCAN_EMIT_BLOCKS)
     HIP_CHECK(launch_rng_finish_band(seed_cur(r), r->d_jump, seed_next(r), d_counts, d_masks, nblk, pl.traces, rd,
-                                     r->d_err, 0, pl.traces, r->d_blk_off, r->d_rng_range, st));
+                                     r->d_err, 0, pl.traces, r->d_blk_off, r->d_rng_range, r->d_tile_sum, st));
   else
     HIP_CHECK(launch_rng_finish(seed_cur(r), r->d_jump, seed_next(r), d_counts, d_masks, nblk, pl.traces, rd,
                                 r->d_err, ss2, P.W, P.row_block, P.rank, P.nranks, st));
@@ -1453,9 +1462,17 @@ static bool fused_prepass(const FramePlan &pl, uint64_t nblk)
 
 static int prepass_fused(rfx_renderer *r, FramePlan &pl, uint64_t nblk, uint32_t *rd, hipEvent_t emitted)
 {
-  r->rng_epoch = r->rng_epoch % ((1u << 28) - 1) + 1;  // 1 .. 2^28 - 1, a new tag per launch
+  // 1 .. 2^28 - 1, a new tag per launch; when the tags wrap, the words earlier launches left are cleared first (a word
+  // of a wider launch could otherwise carry the new tag)
+  if (r->rng_epoch == (1u << 28) - 1)
+  {
+    HIP_CHECK(hipMemsetAsync(r->d_rng_status, 0, r->blk_cap * sizeof(unsigned long long), pl.st));
+    r->rng_epoch = 0;
+  }
+  ++r->rng_epoch;
   HIP_CHECK(launch_rng_fused(seed_cur(r), r->d_jump, seed_next(r), nblk, pl.traces, rd, r->d_err, r->d_rng_status,
-                             r->d_rng_ticket, r->rng_epoch, pl.st));
+                             r->d_rng_ticket, r->rng_tickets, r->rng_epoch, pl.st));
+  r->rng_tickets += nblk;  // every block of the launch takes one ticket
   r->seed_idx ^= 1u;
   ++r->state_seq;
   if (emitted) HIP_CHECK(hipEventRecord(emitted, pl.st));
@@ -1693,6 +1710,9 @@ extern "C" int rfx_frame_rng_emit(rfx_renderer *r, const rfx_frame *f, uint32_t 
   if ((rc = ensure_rng_workspace(r, pl.rd_traces(), nblk)) != RFX_OK) return rc;
   if ((rc = ensure_rd_alt(r, pl.rd_traces())) != RFX_OK) return rc;
   const int buf = r->trace_buf == 0 ? 1 : 0;  // not the buffer of the last enqueued trace
+  // nor one a split frame's spans on the renderer's second stream may still read (the emit may run on a third stream)
+  if (buf == 1 && r->split_alt_busy) HIP_CHECK(hipStreamWaitEvent(pl.st, r->split_ev[2], 0));
+  r->split_alt_busy = false;
   if ((rc = emit_frame(r, pl, d_blk_counts, nullptr, nblk, buf ? r->d_rd_alt : r->d_rd,
                        (hipEvent_t)emitted_event)) != RFX_OK)
     return rc;
@@ -1874,7 +1894,8 @@ static int render_split(rfx_renderer *r, const rfx_frame *f, uint64_t p0, uint64
     HIP_CHECK(hipEventRecord(r->split_ev[2], s2[1]));
     HIP_CHECK(hipStreamWaitEvent(s2[0], r->split_ev[2], 0));
   }
-  r->trace_buf = 0;
+  r->trace_buf = 0;            // the last span on the caller's stream read d_rd; the odd spans read d_rd_alt until
+  r->split_alt_busy = k > 1;   // split_ev[2], which the next emit-ahead into d_rd_alt waits for
   r->rewind_ok = true;
   r->rewind_flip = false;
   r->rewind_saved = true;
@@ -2053,8 +2074,7 @@ extern "C" int rfx_synchronize(rfx_renderer *r)
   HIP_CHECK(hipStreamSynchronize(r->stream));
   int err = 0;
   HIP_CHECK(hipMemcpy(&err, r->d_err, sizeof(int), hipMemcpyDeviceToHost));
-  if (err) return fail(RFX_ERR_RNG, err == 2 ? "RNG pre-pass: a block's offset look-back gave up waiting"
-                                              : "RNG pre-pass ran short of accepted triples");
+  if (err & 1) return fail(RFX_ERR_RNG, "RNG pre-pass ran short of accepted triples");  // (bit 4: an exact fallback)
   return RFX_OK;
 }
 
@@ -2190,6 +2210,25 @@ extern "C" int rfx_kat_powf_cube(rfx_renderer *r, uint64_t counts[2])
   if (e != hipSuccess) return fail(RFX_ERR_HIP, "kat_powf_cube: %s", hipGetErrorString(e));
   counts[0] = h[0];
   counts[1] = h[1];
+  return RFX_OK;
+}
+
+extern "C" int rfx_kat_div(rfx_renderer *r, uint64_t first, uint64_t n, uint64_t counts[3])
+{
+  if (!r || !counts) return fail(RFX_ERR_ARG, "kat_div: bad args");
+  int rc;
+  if ((rc = set_dev(r)) != RFX_OK) return rc;
+  unsigned long long *d = nullptr;
+  hipError_t e = hipMalloc(&d, 3 * sizeof(unsigned long long));
+  if (e == hipSuccess) e = hipMemsetAsync(d, 0, 3 * sizeof(unsigned long long), r->stream);
+  for (uint64_t k = 0; e == hipSuccess && k < n; k += 1ull << 28)  // launches of up to 2^28 pairs
+    e = launch_kat_div(first + k, (uint32_t)std::min<uint64_t>(1ull << 28, n - k), d, r->stream);
+  unsigned long long h[3] = {0, 0, 0};
+  if (e == hipSuccess) e = hipStreamSynchronize(r->stream);
+  if (e == hipSuccess) e = hipMemcpy(h, d, sizeof(h), hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  if (e != hipSuccess) return fail(RFX_ERR_HIP, "kat_div: %s", hipGetErrorString(e));
+  for (int i = 0; i < 3; ++i) counts[i] = h[i];
   return RFX_OK;
 }
 

@@ -442,6 +442,107 @@ __global__ __launch_bounds__(kScanThreads) void rng_band_range(const uint32_t *b
   if (tid == 0 && carry < need) *err = 1;  // stream too short for the frame
 }
 
+// The same scan over many workgroups (launches of many blocks: a split frame's 2^30-trace spans have 524K).  One
+// workgroup scanning 524K counts runs for milliseconds beside the other stream's trace, which holds the chip's issue
+// slots; two kernels of one workgroup per tile of kScanTileCounts counts do it in parallel:
+//   rng_tile_sums: each tile's total (coalesced 16-byte loads, a workgroup reduction);
+//   rng_tile_scan: each tile's prefix (the totals of the tiles before it, at most a few hundred words), then the tile's
+//   exclusive scan, the offsets, and the band's / the frame's range blocks found in the tile.
+constexpr uint32_t kScanTileCounts = 4096, kTileSumThreads = 256;
+__global__ __launch_bounds__(kTileSumThreads) void rng_tile_sums(const uint32_t *blk_cnt, uint64_t nblk,
+                                                                 uint32_t *tile_sum, uint32_t *range)
+{
+  __shared__ uint32_t wsum[kTileSumThreads / 64];
+  const uint64_t base = (uint64_t)blockIdx.x * kScanTileCounts;
+  const uint32_t n = (uint32_t)min((uint64_t)kScanTileCounts, nblk - base);
+  uint32_t sum = 0;
+  if (n == kScanTileCounts && ((uintptr_t)(blk_cnt + base) & 15u) == 0)
+  {
+    const uint4 *v = reinterpret_cast<const uint4 *>(blk_cnt + base);
+#pragma unroll
+    for (uint32_t k = 0; k < kScanTileCounts / 4 / kTileSumThreads; ++k)
+    {
+      const uint4 a = v[k * kTileSumThreads + threadIdx.x];
+      sum += a.x + a.y + a.z + a.w;
+    }
+  }
+  else
+    for (uint32_t i = threadIdx.x; i < n; i += kTileSumThreads) sum += blk_cnt[base + i];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+  if ((threadIdx.x & 63u) == 0) wsum[threadIdx.x >> 6] = sum;
+  __syncthreads();
+  if (threadIdx.x == 0)
+  {
+    uint32_t t = 0;
+    for (uint32_t w = 0; w < kTileSumThreads / 64; ++w) t += wsum[w];
+    tile_sum[blockIdx.x] = t;
+    if (blockIdx.x == 0) { range[0] = 0; range[1] = 0; range[2] = 0; }  // rng_tile_scan runs after every tile sum
+  }
+}
+
+__global__ __launch_bounds__(kScanThreads) void rng_tile_scan(const uint32_t *blk_cnt, uint64_t nblk, uint64_t need,
+                                                              uint64_t lo, uint64_t hi, const uint32_t *tile_sum,
+                                                              uint64_t *off, uint32_t *range, int *err)
+{
+  __shared__ uint32_t wsum[kScanThreads / 64];
+  __shared__ uint64_t s_pre;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+  // this tile's prefix: the totals of the tiles before it
+  unsigned long long pre = 0;
+  for (uint32_t t = tid; t < blockIdx.x; t += kScanThreads) pre += tile_sum[t];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) pre += __shfl_xor(pre, o, 64);
+  if (tid == 0) s_pre = 0;
+  __syncthreads();
+  if (lane == 0 && pre) atomicAdd((unsigned long long *)&s_pre, pre);
+  __syncthreads();
+  // four counts per thread: one 16-byte load where the tile is whole and aligned
+  const uint64_t base = (uint64_t)blockIdx.x * kScanTileCounts;
+  const uint64_t b0 = base + 4u * tid;
+  uint32_t c[4];
+  if (b0 + 3 < nblk && ((uintptr_t)(blk_cnt + b0) & 15u) == 0)
+  {
+    const uint4 a = *reinterpret_cast<const uint4 *>(blk_cnt + b0);
+    c[0] = a.x; c[1] = a.y; c[2] = a.z; c[3] = a.w;
+  }
+  else
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) c[k] = b0 + k < nblk ? blk_cnt[b0 + k] : 0u;
+  const uint32_t sum = c[0] + c[1] + c[2] + c[3];
+  uint32_t inc = sum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1)
+  {
+    const uint32_t v = __shfl_up(inc, o, 64);
+    if (lane >= (uint32_t)o) inc += v;
+  }
+  if (lane == 63) wsum[wv] = inc;
+  __syncthreads();
+  uint32_t wb = 0, tot = 0;
+  for (uint32_t w = 0; w < kScanThreads / 64; ++w)
+  {
+    wb += w < wv ? wsum[w] : 0u;
+    tot += wsum[w];
+  }
+  uint64_t run = s_pre + wb + (inc - sum);
+#pragma unroll
+  for (uint32_t k = 0; k < 4; ++k)
+  {
+    const uint64_t b = b0 + k, e = run + c[k];
+    if (b < nblk)
+    {
+      // block b holds traces [run, e): the band's first / last block and the frame's final one (one block each)
+      if (c[k] && run <= lo && lo < e) range[0] = (uint32_t)b;
+      if (c[k] && run <= hi - 1 && hi - 1 < e) range[1] = (uint32_t)b;
+      if (c[k] && run <= need - 1 && need - 1 < e) range[2] = (uint32_t)b;
+      off[b] = run;
+    }
+    run = e;
+  }
+  if (blockIdx.x == gridDim.x - 1 && tid == 0 && s_pre + tot < need) *err = 1;  // stream too short for the frame
+}
+
 __global__ __launch_bounds__(kRngBlock) void rng_emit_band(const uint32_t *seed, const uint32_t *jump,
                                                            const uint32_t *blk_cnt, const uint16_t *masks,
                                                            const uint64_t *off, const uint32_t *range, uint64_t nblk,
@@ -466,19 +567,27 @@ __global__ __launch_bounds__(kRngBlock) void rng_emit_band(const uint32_t *seed,
 // look-back over the published words of the blocks before it -- 64 at a time, one per lane of the first wave -- until
 // one holds an inclusive prefix; it publishes its own inclusive prefix and scatters as emit_block does.  A status word
 // is epoch << 36 | flag << 34 | value (flag 1: the block's count, 2: its inclusive prefix); a word of another launch's
-// epoch reads as not yet published, so the array is never cleared.  The waits are bounded: past kLookbackSpins polls
-// the launch flags an error (RFX_ERR_RNG) and goes on, so a broken invariant cannot hang the device.
-// RFX_RNG_TICKET=0 (default): the block number is blockIdx.x.  Each XCD dispatches its workgroups in index order, so
-// the oldest unfinished block is always resident and waits only on finished ones; the ticket (one device-scope atomic
-// per block, all on one word) serialised the launch's start.
+// epoch reads as not yet published, so the array is never cleared (the host clears it when the epoch wraps).
+// Block order: an ordered ticket, not blockIdx.x.  The hardware's workgroup dispatch order is not specified
+// (MI355X_MICROARCH.md: placement-independent protocols only), and with the ticket a block only ever waits on blocks that
+// took smaller tickets -- blocks already running, each waiting only on smaller tickets again -- so the look-back always
+// finishes, in any dispatch order and beside any other kernel (rocPRIM's ordered_block_id does the same).  The ticket
+// word counts up across launches and is never reset: the host passes the count of tickets its earlier launches took
+// (base), so no launch races another's reset.  The waits stay bounded as a guard against a broken invariant, never as a
+// path a correct launch takes: past kLookbackSpins polls the block recomputes its offset from the random stream itself
+// (below), so even then the frame's randDirs are exact and no later call is left to report a wrong frame.
+// RFX_RNG_TICKET=0 keeps the blockIdx.x order (timing builds only: it relies on in-order dispatch).
 #ifndef RFX_RNG_TICKET
-#define RFX_RNG_TICKET 0
+#define RFX_RNG_TICKET 1
 #endif
 #ifndef RFX_LOOKBACK_SLEEP
 #define RFX_LOOKBACK_SLEEP 1  // s_sleep between polls of a not yet published status word (units of 64 cycles)
 #endif
 constexpr uint64_t kStatAgg = 1ull << 34, kStatPre = 2ull << 34, kStatVal = (1ull << 34) - 1;
-constexpr uint32_t kLookbackSpins = 1u << 22;
+#ifndef RFX_LOOKBACK_SPINS
+#define RFX_LOOKBACK_SPINS (1u << 22)  // 0: every wait gives up at once (a timing build that exercises the fallback)
+#endif
+constexpr uint32_t kLookbackSpins = RFX_LOOKBACK_SPINS;
 
 // Relaxed device-scope accesses: a status word carries its own value, and no other data is handed over through it, so
 // no fence is needed (release / acquire at device scope would write back and invalidate the XCDs' L2s on every access).
@@ -495,7 +604,7 @@ __device__ __forceinline__ void status_store(unsigned long long *p, unsigned lon
 __global__ __launch_bounds__(kRngBlock) void rng_fused(const uint32_t *seed, const uint32_t *jump, uint32_t nblk,
                                                        uint64_t need, uint32_t *rd_state, uint32_t *next_seed, int *err,
                                                        unsigned long long *status, unsigned long long *ticket,
-                                                       uint32_t epoch)
+                                                       unsigned long long base, uint32_t epoch)
 {
   __shared__ uint32_t sst[kTriplesPerBlock];
   __shared__ uint32_t wsum[kRngBlock / 64];
@@ -503,12 +612,7 @@ __global__ __launch_bounds__(kRngBlock) void rng_fused(const uint32_t *seed, con
   uint32_t b = blockIdx.x;
 #if RFX_RNG_TICKET
   __shared__ uint32_t s_b;
-  if (threadIdx.x == 0)
-  {
-    const uint32_t t = (uint32_t)atomicAdd(ticket, 1ull);
-    if (t == nblk - 1) atomicExch(ticket, 0ull);  // every block has its ticket: ready for the next launch
-    s_b = t;
-  }
+  if (threadIdx.x == 0) s_b = (uint32_t)(atomicAdd(ticket, 1ull) - base);
   __syncthreads();
   b = s_b;
 #endif
@@ -538,6 +642,8 @@ __global__ __launch_bounds__(kRngBlock) void rng_fused(const uint32_t *seed, con
     if (lane >= (uint32_t)o) inc += v;
   }
   if (lane == 63) wsum[threadIdx.x >> 6] = inc;
+  __shared__ uint32_t s_gaveup;
+  if (threadIdx.x == 0) s_gaveup = 0;
   __syncthreads();
   uint32_t wbase = 0, tot = 0;
   for (uint32_t w = 0; w < kRngBlock / 64; ++w)
@@ -545,9 +651,9 @@ __global__ __launch_bounds__(kRngBlock) void rng_fused(const uint32_t *seed, con
     if (w < (threadIdx.x >> 6)) wbase += wsum[w];
     tot += wsum[w];
   }
+  const unsigned long long tag = (unsigned long long)epoch << 36;
   if (threadIdx.x < 64)
   {
-    const unsigned long long tag = (unsigned long long)epoch << 36;
     uint64_t excl = 0;
     if (b == 0)
     {
@@ -558,6 +664,7 @@ __global__ __launch_bounds__(kRngBlock) void rng_fused(const uint32_t *seed, con
       if (lane == 0) status_store(&status[b], tag | kStatAgg | tot);
       int64_t j = (int64_t)b - 1 - (int64_t)lane;  // this lane's predecessor in the window
       uint32_t spins = 0;
+      bool gaveup = false;
       for (;;)
       {
         const unsigned long long w = j >= 0 ? status_load(&status[j]) : (tag | kStatPre);
@@ -569,7 +676,7 @@ __global__ __launch_bounds__(kRngBlock) void rng_fused(const uint32_t *seed, con
         {
           if (++spins > kLookbackSpins)
           {
-            if (lane == 0) *err = 2;
+            gaveup = true;
             break;
           }
           __builtin_amdgcn_s_sleep(RFX_LOOKBACK_SLEEP);
@@ -582,11 +689,42 @@ __global__ __launch_bounds__(kRngBlock) void rng_fused(const uint32_t *seed, con
         if (first < 64) break;
         j -= 64;
       }
-      if (lane == 0) status_store(&status[b], tag | kStatPre | ((excl + tot) & kStatVal));
+      if (gaveup)
+      {
+        if (lane == 0) s_gaveup = 1;
+      }
+      else if (lane == 0)
+        status_store(&status[b], tag | kStatPre | ((excl + tot) & kStatVal));
     }
     if (lane == 0) s_off = excl;
   }
   __syncthreads();
+  if (s_gaveup)
+  {
+    // The look-back outwaited its bound (only a broken invariant gets here): the offset is recomputed from the random
+    // stream itself -- the accept counts of blocks 0 .. b - 1, regenerated by this workgroup -- so the frame's randDirs
+    // stay exact whatever the other blocks do.  Bit 4 of the error word records that it happened (not an error: the
+    // frame is exact; rfx_synchronize fails only on bits 1 and 2).
+    uint32_t part = 0;
+    for (uint32_t pb = 0; pb < b; ++pb)
+    {
+      uint32_t q = thread_state(*seed, jump, pb, threadIdx.x), q2 = kHalfJump.a * q + kHalfJump.c;
+      float x, y, z;
+#pragma unroll
+      for (int k = 0; k < kHalfRun; ++k) part += (triple(q, x, y, z) ? 1u : 0u) + (triple(q2, x, y, z) ? 1u : 0u);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+    if (threadIdx.x == 0) s_off = 0;
+    __syncthreads();
+    if (lane == 0) atomicAdd((unsigned long long *)&s_off, (unsigned long long)part);
+    __syncthreads();
+    if (threadIdx.x == 0)
+    {
+      status_store(&status[b], tag | kStatPre | ((s_off + tot) & kStatVal));
+      atomicOr(err, 4);
+    }
+  }
   const uint64_t off = s_off;
   if (b == nblk - 1 && threadIdx.x == 0 && off + tot < need) *err = 1;  // stream too short for the frame
   if (off >= need) return;
@@ -749,6 +887,90 @@ __global__ __launch_bounds__(kKatThreads) void kat_powf_cube(uint32_t first, uin
   }
 }
 
+// rfx_math.h's division fast paths (div_rn, the shared-divisor divv) against IEEE '/' on operand pairs drawn from a hash
+// of the pair index (first + i): raw bit patterns (every class: zeros, denormals, infinities, NaNs), divisors on both
+// edges of [2^-40, 2^100] (a few ulps either side), quotients on both edges of [2^-60, 2^60], zero and denormal
+// numerators, powers of two.  counts[0] += quotients whose bits differ from '/' (two NaNs compare equal), counts[1] +=
+// quotients that took the fast path, counts[2] += quotients checked.
+__device__ __forceinline__ uint32_t kat_mix(uint64_t x)
+{
+  x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull; x ^= x >> 33;
+  return (uint32_t)x;
+}
+__device__ __forceinline__ float kat_float(uint32_t sign, int32_t e, uint32_t mant)  // +-2^e (1 + mant 2^-23), e normal
+{
+  return __uint_as_float((sign & 1u) << 31 | (uint32_t)(e + 127) << 23 | (mant & 0x7FFFFFu));
+}
+__device__ __forceinline__ bool kat_same(float x, float y)
+{
+  return __float_as_uint(x) == __float_as_uint(y) || (x != x && y != y);
+}
+__global__ __launch_bounds__(kKatThreads) void kat_div(uint64_t first, uint32_t n, unsigned long long *counts)
+{
+  const uint32_t i = blockIdx.x * kKatThreads + threadIdx.x;
+  uint32_t bad = 0, fast = 0, seen = 0;
+  if (i < n)
+  {
+    const uint64_t k = first + i;
+    const uint32_t h0 = kat_mix(k), h1 = kat_mix(k ^ 0x9E3779B97F4A7C15ull), h2 = kat_mix(k * 3 + 1);
+    float a, b;
+    switch (h0 & 7u)
+    {
+      case 0: a = __uint_as_float(h1); b = __uint_as_float(h2); break;
+      case 1:  // divisor over [2^-45, 2^105], quotient exponent over [-66, 66]: both edges of both bounds
+      {
+        b = kat_float(h1 >> 31, (int32_t)(h1 % 151u) - 45, h2);
+        a = b * kat_float(h2 >> 31, (int32_t)((h0 >> 3) % 133u) - 66, h1 >> 5);
+        break;
+      }
+      case 2:  // divisor within 3 ulps of 2^-40 / 2^100, quotient near 2^-60 / 2^60 / 1
+      {
+        const float edge = (h1 & 1u) ? 0x1p100f : 0x1p-40f;
+        b = __uint_as_float(__float_as_uint(edge) + (int32_t)((h1 >> 1) % 7u) - 3) * ((h1 & 2u) ? -1.0f : 1.0f);
+        const int32_t qe = (h2 % 3u == 0) ? -60 : (h2 % 3u == 1) ? 60 : 0;
+        a = b * kat_float(h2 >> 31, qe + (int32_t)((h2 >> 2) % 5u) - 2, h0 >> 3);
+        break;
+      }
+      case 3:  // zero, denormal and tiny numerators
+      {
+        const uint32_t m = h1 % 3u;
+        a = m == 0 ? ((h1 & 8u) ? -0.0f : 0.0f) : m == 1 ? __uint_as_float((h1 & 0x807FFFFFu)) : kat_float(h1 >> 31, -126 + (int32_t)(h2 % 40u), h2);
+        b = kat_float(h2 >> 31, (int32_t)(h0 % 141u) - 40, h1 >> 3);
+        break;
+      }
+      case 4: b = kat_float(h1 >> 31, (int32_t)((h1 >> 1) % 3u) - 1, h2); a = kat_float(h2 >> 31, (int32_t)(h0 % 253u) - 126, h1 >> 4); break;
+      case 5: a = kat_float(h1 >> 31, (int32_t)(h0 % 253u) - 126, h2); b = kat_float(h2 >> 31, (int32_t)(h1 % 253u) - 126, h0); break;
+      case 6: b = kat_float(h1 >> 31, (int32_t)(h0 % 141u) - 40, h2); a = b * __uint_as_float(0x3f800000u + (h2 & 0xFu) - 8u); break;
+      default: b = kat_float(h1 >> 31, (int32_t)(h0 % 253u) - 126, 0u); a = kat_float(h2 >> 31, (int32_t)(h1 % 253u) - 126, h2 >> 1); break;
+    }
+    const float q = div_rn(a, b);
+    bool ok;
+    (void)div_fast(a, div_prep(b), ok);
+    // the shared-divisor form (normalize, Vector3 / float) on three numerators at once
+    const float a2 = __uint_as_float(__float_as_uint(a) ^ (h2 & 0x807F0000u)), a3 = a * -0.5f;
+    const v3 qv = divv(mk(a, a2, a3), b);
+    const bool sv = fabsf(b) > kVerySmall;  // divv divides only then (Vector3.cpp:143-151)
+    const float rx = sv ? a / b : a, ry = sv ? a2 / b : a2, rz = sv ? a3 / b : a3;
+    bad = (kat_same(q, a / b) ? 0u : 1u) + (kat_same(qv.x, rx) ? 0u : 1u) + (kat_same(qv.y, ry) ? 0u : 1u) +
+          (kat_same(qv.z, rz) ? 0u : 1u);
+    fast = ok ? 1u : 0u;
+    seen = 4;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+  {
+    bad += __shfl_xor(bad, o, 64);
+    fast += __shfl_xor(fast, o, 64);
+    seen += __shfl_xor(seen, o, 64);
+  }
+  if ((threadIdx.x & 63u) == 0 && seen)
+  {
+    if (bad) atomicAdd(&counts[0], (unsigned long long)bad);
+    atomicAdd(&counts[1], (unsigned long long)fast);
+    atomicAdd(&counts[2], (unsigned long long)seen);
+  }
+}
+
 // The kernel-argument layout the bounce loops read through the kernarg segment pointer (rfx_trace.h launder_scene,
 // kernarg_params): the laundered DevScene and FrameParams against the by-value arguments, word by word.  out[0] / out[1]:
 // words of the DevScene / FrameParams that differ (0 expected), out[2]: 1 when the build reads the record laundered.
@@ -843,17 +1065,29 @@ hipError_t launch_rng_finish(const uint32_t *d_seed, const uint32_t *d_jump, uin
   return hipGetLastError();
 }
 
-// the band partition's emit: traces [lo, hi) (and the frame's last trace's stream state); scratch: nblk offsets and
-// 3 range words.  Also the one-device emit of launches with many blocks (lo = 0, hi = traces, the count kernel's
+// the band partition's emit: traces [lo, hi) (and the frame's last trace's stream state); scratch: nblk offsets,
+// 3 range words and one word per tile of kScanTileCounts blocks (d_tile_sum; null: the one-workgroup scan).  Also the one-device emit of launches with many blocks (lo = 0, hi = traces, the count kernel's
 // accept flags in d_masks): rng_emit's per-block prefix sums cost O(nblk^2) reads, this scan O(nblk).
+#ifndef RFX_SCAN_TILES
+#define RFX_SCAN_TILES 2  // launches of at least this many tiles of kScanTileCounts blocks scan in many workgroups (0: never)
+#endif
 hipError_t launch_rng_finish_band(const uint32_t *d_seed, const uint32_t *d_jump, uint32_t *d_next_seed,
                                   const uint32_t *d_blk_cnt, const uint16_t *d_masks, uint64_t nblk, uint64_t traces,
                                   uint32_t *d_rd_state, int *d_err, uint64_t lo, uint64_t hi, uint64_t *d_off,
-                                  uint32_t *d_range, hipStream_t st)
+                                  uint32_t *d_range, uint32_t *d_tile_sum, hipStream_t st)
 {
   const EmitFilter flt{1, 1, 1, 0, 1, lo, hi};
-  hipLaunchKernelGGL(rng_band_range, dim3(1), dim3(kScanThreads), 0, st, d_blk_cnt, nblk, traces, lo, hi, d_off, d_range,
-                     d_err);
+  const uint64_t ntiles = (nblk + kScanTileCounts - 1) / kScanTileCounts;
+  if (RFX_SCAN_TILES && ntiles >= RFX_SCAN_TILES && d_tile_sum)
+  {
+    hipLaunchKernelGGL(rng_tile_sums, dim3((uint32_t)ntiles), dim3(kTileSumThreads), 0, st, d_blk_cnt, nblk, d_tile_sum,
+                       d_range);
+    hipLaunchKernelGGL(rng_tile_scan, dim3((uint32_t)ntiles), dim3(kScanThreads), 0, st, d_blk_cnt, nblk, traces, lo, hi,
+                       (const uint32_t *)d_tile_sum, d_off, d_range, d_err);
+  }
+  else
+    hipLaunchKernelGGL(rng_band_range, dim3(1), dim3(kScanThreads), 0, st, d_blk_cnt, nblk, traces, lo, hi, d_off,
+                       d_range, d_err);
   // about (hi - lo) / (accept rate pi/6 x 4096) blocks hold the band; the workgroups loop over however many there are
   const uint64_t est = (hi - lo) / 2048 + 4;
   hipLaunchKernelGGL(rng_emit_band, dim3((uint32_t)std::min<uint64_t>(est, nblk)), dim3(kRngBlock), 0, st, d_seed, d_jump,
@@ -863,13 +1097,14 @@ hipError_t launch_rng_finish_band(const uint32_t *d_seed, const uint32_t *d_jump
 }
 
 // the one-pass pre-pass of a one-device launch (rng_fused); status: nblk words, ticket: one word, both zeroed once at
-// allocation; epoch: this launch's tag, distinct from every earlier launch's on the same status array (never 0)
+// allocation; base: the tickets earlier launches took; epoch: this launch's tag, distinct from every earlier launch's on
+// the same status array since it was last cleared (never 0)
 hipError_t launch_rng_fused(const uint32_t *d_seed, const uint32_t *d_jump, uint32_t *d_next_seed, uint64_t nblk,
                             uint64_t traces, uint32_t *d_rd_state, int *d_err, unsigned long long *d_status,
-                            unsigned long long *d_ticket, uint32_t epoch, hipStream_t st)
+                            unsigned long long *d_ticket, unsigned long long base, uint32_t epoch, hipStream_t st)
 {
   hipLaunchKernelGGL(rng_fused, dim3((uint32_t)nblk), dim3(kRngBlock), 0, st, d_seed, d_jump, (uint32_t)nblk, traces,
-                     d_rd_state, d_next_seed, d_err, d_status, d_ticket, epoch);
+                     d_rd_state, d_next_seed, d_err, d_status, d_ticket, base, epoch);
   return hipGetLastError();
 }
 
@@ -908,6 +1143,13 @@ hipError_t launch_kat(int what, const DevScene &S, int tex, const void *in, cons
     case 2: hipLaunchKernelGGL(kat_powf, kat_grid(n), dim3(kKatThreads), 0, st, (const float *)in, n, (float *)out); break;
     default: hipLaunchKernelGGL(kat_argb, kat_grid(n), dim3(kKatThreads), 0, st, (const float *)in, n, (uint32_t *)out); break;
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_kat_div(uint64_t first, uint32_t n, unsigned long long *counts, hipStream_t st)
+{
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(kat_div, kat_grid(n), dim3(kKatThreads), 0, st, first, n, counts);
   return hipGetLastError();
 }
 

@@ -46,6 +46,77 @@ RFX_HD float sqrt_rn(float x)
   return sqrtf(x);
 }
 
+// Correctly rounded f32 division.  gfx950's IEEE lowering of a / b is eleven instructions:
+//   b' = v_div_scale(b), a' = v_div_scale(a) (VCC: a rescale is pending), r = v_rcp(b'), e = fma(-b', r, 1),
+//   r' = fma(e, r, r), q0 = a' r', t1 = fma(-b', q0, a'), q1 = fma(t1, r', q0), t2 = fma(-b', q1, a'),
+//   q2 = v_div_fmas(t2, r', q1) (an fma, scaled by 2^+-64 when VCC), v_div_fixup(q2, b, a) (special values, sign).
+// v_div_scale rescales an operand (or raises VCC) only for: a zero operand, b denormal, 1/b denormal, a/b denormal,
+// exponent(a) - exponent(b) >= 96, or exponent(a) <= 23; v_div_fixup departs from sign(a) sign(b) |q2| only for NaN /
+// infinite / zero operands and quotients beyond 2^+-150.  For b in [2^-40, 2^100] and a quotient in [2^-60, 2^60] none
+// of them holds (|a| = |a/b| |b| lies in [2^-100, 2^160]: exponent(a) > 23, and the quotient's bounds exclude the rest
+// with margins of 2^3 and more over the fast quotient's few-ulp error), so the scales and the fixup are identities and
+// v_div_fmas is an fma: the eight remaining instructions, run in the same order, give the same bits.  The divisor's
+// part (r, e, r') is shared by every quotient over one divisor (div_prep); a quotient outside the range is recomputed
+// with '/'.  tests/test_div_guard.py replays the range argument in float32; rfx_kat_div checks the device path against
+// IEEE '/' on 2^27+ operand pairs, both edges of every bound included.
+#ifndef RFX_DIV_FAST
+#define RFX_DIV_FAST 1  // 0: every quotient as the compiler lowers '/'; 2: no guard (timing builds only)
+#endif
+// the divisor and its refined reciprocal -- NaN when the divisor is outside [2^-40, 2^100], so that every fast quotient
+// by it is NaN and fails the quotient's range test (one register for the guard's divisor half, not two)
+struct DivRcp { float b, r; };
+RFX_HD DivRcp div_prep(float b)
+{
+  DivRcp d;
+  d.b = b;
+#if defined(__HIP_DEVICE_COMPILE__) && RFX_DIV_FAST
+  const float r = __builtin_amdgcn_rcpf(b);
+  const float e = __builtin_fmaf(-b, r, 1.0f);
+  const float r1 = __builtin_fmaf(e, r, r);
+  d.r = (RFX_DIV_FAST == 2 || (fabsf(b) >= 0x1p-40f && fabsf(b) <= 0x1p100f)) ? r1 : __builtin_nanf("");
+#else
+  d.r = 0.0f;
+#endif
+  return d;
+}
+// the quotient a / d.b by the shared reciprocal; ok: it is in the guarded range (else it must be recomputed)
+RFX_HD float div_fast(float a, const DivRcp &d, bool &ok)
+{
+#if defined(__HIP_DEVICE_COMPILE__) && RFX_DIV_FAST
+  const float q0 = a * d.r;
+  const float t1 = __builtin_fmaf(-d.b, q0, a);
+  const float q1 = __builtin_fmaf(t1, d.r, q0);
+  const float t2 = __builtin_fmaf(-d.b, q1, a);
+  const float q = __builtin_fmaf(t2, d.r, q1);
+  ok = RFX_DIV_FAST == 2 || (fabsf(q) >= 0x1p-60f && fabsf(q) <= 0x1p60f);  // false for NaN (an out-of-range divisor)
+  return q;
+#else
+  ok = false;
+  return a / d.b;
+#endif
+}
+RFX_HD float div_by(float a, const DivRcp &d)
+{
+  bool ok;
+  const float q = div_fast(a, d, ok);
+  if (__builtin_expect(!ok, 0)) return a / d.b;
+  return q;
+}
+RFX_HD float div_rn(float a, float b) { return div_by(a, div_prep(b)); }
+// a lone quotient (no divisor to share): the fast path saves three instructions and pays two compares and a branch for
+// it, so it is a build option (RFX_DIV_SINGLE, tools/ab.py)
+#ifndef RFX_DIV_SINGLE
+#define RFX_DIV_SINGLE 0
+#endif
+RFX_HD float qdiv(float a, float b)
+{
+#if RFX_DIV_SINGLE
+  return div_rn(a, b);
+#else
+  return a / b;
+#endif
+}
+
 struct v3 { float x, y, z; };
 struct col { float r, g, b; };
 // Matrix33 element order _11.._33 (Matrix33.h:13-22)
@@ -65,7 +136,17 @@ RFX_HD v3 cross(v3 a, v3 b)                                                     
 }
 RFX_HD v3 divv(v3 a, float f)                                                        // Vector3.cpp:143-151
 {
-  if (fabsf(f) > kVerySmall) return mk(a.x / f, a.y / f, a.z / f);
+  if (fabsf(f) > kVerySmall)
+  {
+#if defined(__HIP_DEVICE_COMPILE__) && RFX_DIV_FAST
+    // one reciprocal for the three quotients, one guard and one fallback branch for all three
+    const DivRcp d = div_prep(f);
+    bool ox, oy, oz;
+    const v3 q = mk(div_fast(a.x, d, ox), div_fast(a.y, d, oy), div_fast(a.z, d, oz));
+    if (__builtin_expect(ox && oy && oz, 1)) return q;
+#endif
+    return mk(a.x / f, a.y / f, a.z / f);
+  }
   return a;
 }
 // Vector3::normalized (Vector3.cpp:63-72) == Tracemath::normalize (trace_math.cpp:3-12)
@@ -79,7 +160,7 @@ RFX_HD v3 normalized(v3 a)
 RFX_HD v3 reflect(v3 v, v3 n)
 {
   const float dn = dot(n, n);
-  if (dn > kVerySmall) return sub(v, mul(mul(n, 2.0f), dot(v, n) / dn));
+  if (dn > kVerySmall) return sub(v, mul(mul(n, 2.0f), qdiv(dot(v, n), dn)));
   return v;
 }
 RFX_HD float clampf(float v, float lo, float hi) { return v < lo ? lo : v > hi ? hi : v; } // trace_math.h:24

@@ -265,22 +265,33 @@ __device__ __forceinline__ col skybox_texel(const DevScene &S, v3 ray, const flo
   const v3 n = normalized(ray);
   const float x = n.x, y = n.y, z = n.z;
   const float ax = fabsf(x) + kVerySmall, ay = fabsf(y) + kVerySmall, az = fabsf(z) + kVerySmall;
-  float u, v;
+  // the face's two quotients share their divisor (rfx_math.h div_prep): u0 -/+ p / den * hw, v0 -/+ q / den * hh
+  float u0, v0, p, q, den, su, sv;
   if (az >= ax && az >= ay)
   {
-    if (z > 0) { u = uFront + x / az * hw; v = vFront + y / az * hh; }
-    else { u = uBack - x / az * hw; v = vBack + y / az * hh; }
+    den = az;
+    if (z > 0) { u0 = uFront; v0 = vFront; p = x; q = y; su = 1.0f; sv = 1.0f; }
+    else { u0 = uBack; v0 = vBack; p = x; q = y; su = -1.0f; sv = 1.0f; }
   }
   else if (ax >= ay && ax >= az)
   {
-    if (x > 0) { u = uRight - z / ax * hw; v = vRight + y / ax * hh; }
-    else { u = uLeft + z / ax * hw; v = vLeft + y / ax * hh; }
+    den = ax;
+    if (x > 0) { u0 = uRight; v0 = vRight; p = z; q = y; su = -1.0f; sv = 1.0f; }
+    else { u0 = uLeft; v0 = vLeft; p = z; q = y; su = 1.0f; sv = 1.0f; }
   }
   else
   {
-    if (y > 0) { u = uTop + x / ay * hw; v = vTop - z / ay * hh; }
-    else { u = uBottom + x / ay * hw; v = vBottom + z / ay * hh; }
+    den = ay;
+    if (y > 0) { u0 = uTop; v0 = vTop; p = x; q = z; su = 1.0f; sv = -1.0f; }
+    else { u0 = uBottom; v0 = vBottom; p = x; q = z; su = 1.0f; sv = 1.0f; }
   }
+  const DivRcp d = div_prep(den);
+  bool okp, okq;
+  float pd = div_fast(p, d, okp), qd = div_fast(q, d, okq);
+  if (__builtin_expect(!(okp && okq), 0)) { pd = p / den; qd = q / den; }
+  // u0 + p / den * hw, or u0 - (p / den * hw): a subtraction of the product, as the reference writes it
+  const float pu = pd * hw, qv = qd * hh;
+  const float u = su > 0.0f ? u0 + pu : u0 - pu, v = sv > 0.0f ? v0 + qv : v0 - qv;
   return texel_uv<STATS>(S, S.skybox_tex, u, v, lut, cnt);
 }
 
@@ -301,6 +312,7 @@ struct RayConst {
   v3 ray2;      // 2.0f * ray
   float a4, a2; // 4.0f * a, 2.0f * a  with a = |ray|^2
   bool a_ok;    // a > VERY_SMALL_NUMBER
+  DivRcp a2d;   // the divisor 2a of every sphere's t, its reciprocal shared (rfx_math.h div_prep)
 };
 __device__ __forceinline__ RayConst ray_const(v3 ray)
 {
@@ -310,6 +322,7 @@ __device__ __forceinline__ RayConst ray_const(v3 ray)
   k.a4 = 4.0f * a;
   k.a2 = 2.0f * a;
   k.a_ok = a > kVerySmall;
+  k.a2d = div_prep(k.a2);
   return k;
 }
 
@@ -351,7 +364,7 @@ __device__ __forceinline__ bool sphere_tail(float b, float d, v3 ray, const RayC
   if constexpr (!STATS && SEL)
   {
     if (!(d >= 0.0f && k.a_ok && b < 0.0f)) return false;
-    const float t = (-b - sqrt_rn(d)) / k.a2;
+    const float t = div_by(-b - sqrt_rn(d), k.a2d);
     const float sq = sqlen(mul(ray, t));
     t_out = t;
     sq_out = sq;
@@ -363,7 +376,7 @@ __device__ __forceinline__ bool sphere_tail(float b, float d, v3 ray, const RayC
     if (!(b < 0.0f)) return false;
   if constexpr (STATS)
     if (!(b > 0.0f)) RFX_CNT(SHADOW ? C_SH_SPH_D : C_SPH_D);
-  const float t = (-b - sqrt_rn(d)) / k.a2;
+  const float t = div_by(-b - sqrt_rn(d), k.a2d);
   if (!(t > kVerySmall)) return false;
   RFX_CNT(SHADOW ? C_SH_SPH_T : C_SPH_T);
   const float sq = sqlen(mul(ray, t));
@@ -425,7 +438,7 @@ __device__ __forceinline__ bool tri_hit(const TriGeo &g, v3 o, v3 ray, float &t_
     const float mu = (fabsf(ao.x) + fabsf(pp.x)) * 0x1p-17f, mv = (fabsf(ao.y) + fabsf(pp.y)) * 0x1p-17f;
     if (uvp.x < -mu || uvp.y < -mv || uvp.x + uvp.y > 1.0f + (mu + mv) + 0x1p-20f) return false;
   }
-  const float t = nz / arz;
+  const float t = qdiv(nz, arz);
   if (!(t > kVerySmall)) return false;
   RFX_CNT(SHADOW ? C_SH_TRI_T : C_TRI_T);
   if constexpr (!(PRE && !STATS))
@@ -458,7 +471,7 @@ __device__ __forceinline__ bool plane_hit(const PlaneGeo &g, v3 o, v3 ray, float
   if (!((num > 0.0f && a > 0.0f) || (num < 0.0f && a < 0.0f))) return false;
   if constexpr (!SHADOW && !STATS)
     if (num * num * k.a2 > best_sq * (a * a) * 2.0000305f) return false;
-  const float t = num / a;
+  const float t = qdiv(num, a);
   if (!(t > kVerySmall)) return false;
   RFX_CNT(SHADOW ? C_SH_PLN_T : C_PLN_T);
   const float sq = sqlen(mul(ray, t));
@@ -1732,22 +1745,22 @@ __device__ __forceinline__ col trace_from(const DevScene &RFX_SCENE_PARAM, v3 or
           const v3 dtl = sub(mk(L.ox, L.oy, L.oz), drop);
           const float dlen = len(dtl);
           float aa = dlen * normLen;
-          const float cosl = (aa > kVerySmall) ? dot(dtl, norm) / aa : 0.0f;
+          const float cosl = (aa > kVerySmall) ? qdiv(dot(dtl, norm), aa) : 0.0f;
           const col lc = mkc(L.r, L.g, L.b);
           if (L.power > kVerySmall) sumL = cadd(sumL, cscale(cscale(lc, cosl), L.power));
           aa = sqlen(dtl);
-          const float ang = (aa > kVerySmall) ? 1.0f - L.radius * L.radius / aa : 0.0f;
+          const float ang = (aa > kVerySmall) ? 1.0f - qdiv(L.radius * L.radius, aa) : 0.0f;
           if (ang > 0)
           {
             RFX_CNT(C_L_SPEC);
             const v3 dlr = add(normalized(dtl), mul(rd, 1.0f - m.refl));
             aa = len(dlr) * reflectLen;
-            float sc = (aa > kVerySmall) ? dot(dlr, reflv) / aa : 0.0f;
+            float sc = (aa > kVerySmall) ? qdiv(dot(dlr, reflv), aa) : 0.0f;
             sc = clampf(sc + (1.0f - sqrt_rn(ang)), 0.0f, 1.0f);
             if (sc > kVerySmall && L.radius > kVerySmall)
             {
               RFX_CNT(C_L_POW);
-              const float sp = powf_dev(sc, 1 + 3 * m.refl * dlen / L.radius) * m.refl;
+              const float sp = powf_dev(sc, 1 + qdiv(3 * m.refl * dlen, L.radius)) * m.refl;
               sumS = cadd(sumS, cscale(lc, sp));
             }
           }
@@ -1766,7 +1779,7 @@ __device__ __forceinline__ col trace_from(const DevScene &RFX_SCENE_PARAM, v3 or
       {
         RFX_CNT(C_DIELECTRIC);
         const float aa = rayLen * normLen;
-        const float cosA = (aa > kVerySmall) ? clampf(dot(ray, neg(norm)) / aa, 0.0f, 1.0f) : 0.0f;
+        const float cosA = (aa > kVerySmall) ? clampf(qdiv(dot(ray, neg(norm)), aa), 0.0f, 1.0f) : 0.0f;
         const float r = 0.2f + 0.8f * powf3_dev(1.0f - cosA);
         fin = cadd(cmul(cscale(color, 1.0f - r), sumL), sumS);
         fin = cmul(fin, mulc);

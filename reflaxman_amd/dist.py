@@ -68,6 +68,18 @@ class RfxStripOps:
         self.frame.row_block = 0
         self.frame.pixel_begin, self.frame.pixel_end = y0 * self.frame.width, y1 * self.frame.width
 
+    def set_span(self, y0: int, y1: int):
+        """The rows [y0, y1) the random stream of the next band frames runs over (rfx.h span_begin / span_end; 0, 0:
+        the whole frame)."""
+        self.frame.span_begin, self.frame.span_end = y0 * self.frame.width, y1 * self.frame.width
+
+    def rng_state(self):
+        """(sphere stream state, jitter stream state) of the renderer (synchronises its stream)."""
+        return self.r.get_rng()
+
+    def set_rng_state(self, sphere: int, jitter: int):
+        self.r.set_rng(sphere, jitter)
+
     def blocks_per_slice(self, nslices: int) -> int:
         bps = C.c_uint64()
         _lib.check(self.L.rfx_frame_rng_blocks(self.r._h, C.byref(self.frame), nslices, C.byref(bps)), "rng_blocks")
@@ -272,23 +284,25 @@ class _CountedFrame:
         # gloo on device tensors (a multi-rank rehearsal on one GPU): stage the collectives through host memory
         return self.device.type == "cuda" and dist.get_backend() != "nccl"
 
-    def _all_gather_counts(self, group=None, async_op: bool = False):
-        mine = self.counts[self.rank * self.bps:(self.rank + 1) * self.bps]
+    def _all_gather_counts(self, group=None, async_op: bool = False, bps: Optional[int] = None):
+        """All-gather the ranks' slices of bps blocks (default self.bps) in the first world * bps words of counts."""
+        bps = bps or self.bps
+        counts = self.counts[:self.world * bps]
+        mine = counts[self.rank * bps:(self.rank + 1) * bps]
         if dist.get_backend() == "nccl":
-            return dist.all_gather_into_tensor(self.counts, mine.clone(), group=group, async_op=async_op)
+            return dist.all_gather_into_tensor(counts, mine.clone(), group=group, async_op=async_op)
         if self._host_staged():
             # gloo ranks on one GPU: through host memory on the current stream (the side stream of a look-ahead:
             # .cpu() waits for the count there, the copy back is ordered before the emit); completes here
-            h = self.counts.cpu()
-            dist.all_gather(list(h.split(self.bps)), h[self.rank * self.bps:(self.rank + 1) * self.bps].clone(),
-                            group=group)
-            self.counts.copy_(h, non_blocking=False)
+            h = counts.cpu()
+            dist.all_gather(list(h.split(bps)), h[self.rank * bps:(self.rank + 1) * bps].clone(), group=group)
+            counts.copy_(h, non_blocking=False)
             return None
         if async_op:  # gloo on CPU (the orchestration tests): the exchange completes here
-            dist.all_gather(list(self.counts.split(self.bps)), mine.clone(), group=group)
+            dist.all_gather(list(counts.split(bps)), mine.clone(), group=group)
             return None
         else:
-            dist.all_gather(list(self.counts.split(self.bps)), mine.clone())
+            dist.all_gather(list(counts.split(bps)), mine.clone())
 
 
 class StripFrame(_CountedFrame):
@@ -455,6 +469,37 @@ def balanced_bounds(bounds: List[int], times: List[float], H: int, grain: int = 
     return _fix_bounds(out, H, grain)
 
 
+LAUNCH_TRACES = 1 << 30  # rfx_host.cpp RFX_LAUNCH_TRACES: the library's default launch limit
+MAX_PASS_TRACES = 1 << 31  # rfx_host.cpp kMaxLaunchTraces: a band's span (its scan offsets are 32-bit)
+
+
+def pass_plan(W: int, H: int, ss: int, world: int, launch_traces: int = LAUNCH_TRACES) -> Optional[List[tuple]]:
+    """The row spans [y0, y1) a band frame of W x H pixels at ss x ss samples runs as, or None when one pass over the
+    whole frame takes it: at most min(world x launch_traces, 2^31) traces per pass (rfx_group.cpp does the same)."""
+    spp = max(1, ss) ** 2
+    cap = min(world * launch_traces, MAX_PASS_TRACES)
+    if W * H * spp <= cap:
+        return None
+    per = cap // (W * spp)  # rows per pass
+    if per == 0:
+        raise ValueError(f"one row of {W} x {spp} samples exceeds {cap} traces")
+    return [(y, min(H, y + per)) for y in range(0, H, per)]
+
+
+def pass_bands(y0: int, y1: int, world: int) -> List[int]:
+    """Equal bands of the span [y0, y1) for ranks 0 .. m - 1, m = min(world, rows): m + 1 bounds."""
+    m = min(world, y1 - y0)
+    return [y0 + ((y1 - y0) * i) // m for i in range(m + 1)]
+
+
+def pass_rows(bd: List[int], rank: int, y1: Optional[int]):
+    """Rank `rank`'s rows of a pass with bands bd; a rank without a band gets the span's last row when y1 is given (its
+    count of the span's stream needs a valid band frame; it traces nothing), else the empty range."""
+    if rank < len(bd) - 1:
+        return bd[rank], bd[rank + 1]
+    return (y1 - 1, y1) if y1 is not None else (0, 0)
+
+
 class BandFrame(_CountedFrame):
     """Rank `rank`'s band of a W x H frame rendered by `world` ranks: contiguous rows [bounds[rank],
     bounds[rank + 1]), traced into whole-frame buffers (rfx.h band partition), so that rank 0 receives every band
@@ -470,10 +515,21 @@ class BandFrame(_CountedFrame):
 
     def __init__(self, ops, W: int, H: int, rank: int, world: int, device: torch.device, gather_to_root: bool = True,
                  pipeline: Optional[bool] = None, gather_rgb: bool = False, count_ahead: Optional[bool] = None,
-                 bounds: Optional[List[int]] = None, grain: int = 8, emit_ahead: Optional[bool] = None):
+                 bounds: Optional[List[int]] = None, grain: int = 8, emit_ahead: Optional[bool] = None, ss: int = 1,
+                 launch_traces: int = LAUNCH_TRACES):
         self.W, self.H, self.grain = W, H, grain
-        b0 = bounds or equal_bounds(H, world, grain)
-        ops.set_rows(b0[rank], b0[rank + 1])  # the frame is a band frame from here on (the RNG layout below reads it)
+        # a frame of more traces than one pass takes (world x launch_traces, and at most 2^31 for the band scan's
+        # offsets: SSAA screenshots reach 2.2e12) runs as passes over row spans (pass_plan)
+        self.passes = pass_plan(W, H, ss, world, launch_traces)
+        if self.passes:
+            count_ahead = emit_ahead = False  # one pass's count exchange is negligible beside its trace
+            y0, y1 = self.passes[0]          # the largest pass: the count buffer is sized for it
+            ops.set_span(y0, y1)
+            bd = pass_bands(y0, y1, world)
+            ops.set_rows(*pass_rows(bd, rank, y1))
+        else:
+            b0 = bounds or equal_bounds(H, world, grain)
+            ops.set_rows(b0[rank], b0[rank + 1])  # a band frame from here on (the RNG layout below reads it)
         self._init_counts(ops, rank, world, device, count_ahead, emit_ahead)
         self.gather_to_root = gather_to_root and world > 1
         self.gather_rgb = bool(gather_rgb) and self.gather_to_root
@@ -490,12 +546,20 @@ class BandFrame(_CountedFrame):
         self.works: List[list] = [[] for _ in range(nbuf)]
         self.frame = 0
         self._events: Optional[list] = None  # (start, end) HIP events around each frame's render while balancing
-        self.set_bounds(b0)
+        if self.passes:
+            self.bounds = equal_bounds(H, world, grain) if H >= world else list(range(world)) + [H]
+            self.y0, self.y1 = self.bounds[rank], self.bounds[rank + 1]
+            self.rows = sum(max(0, b[1] - b[0]) for b in (pass_rows(pass_bands(a, e, world), rank, None)
+                                                           for a, e in self.passes))
+        else:
+            self.set_bounds(b0)
         self.full: Optional[torch.Tensor] = self.argb.view(H, W) if rank == 0 else None
         self.rgb_full: Optional[torch.Tensor] = self.img.view(H, W, 3) if rank == 0 and self.gather_rgb else None
 
     def set_bounds(self, bounds: List[int]):
         """Band bounds for the next frames (the same list on every rank)."""
+        if self.passes:
+            raise ValueError("BandFrame: a frame rendered in row-span passes takes equal bands per pass")
         assert len(bounds) == self.world + 1 and bounds[0] == 0 and bounds[-1] == self.H, bounds
         assert all(bounds[r] < bounds[r + 1] for r in range(self.world)), bounds
         if getattr(self, "emit_ready", False) and list(bounds) != self.bounds:
@@ -524,22 +588,25 @@ class BandFrame(_CountedFrame):
         if not on:
             self.rgb_full = None
 
-    def _sends(self, k: int):
-        """(tensor, peer, is_send) of frame buffer set k: every band to rank 0."""
+    def _sends(self, k: int, bounds: Optional[List[int]] = None):
+        """(tensor, peer, is_send) of frame buffer set k: every band to rank 0 (bounds: the bands of ranks
+        0 .. len(bounds) - 2, default the frame's; ranks beyond them send nothing)."""
         W, ops = self.W, []
+        bounds = self.bounds if bounds is None else bounds
+        n = len(bounds) - 1
         planes = [(self.argb_bufs[k], 1)]
         if self.gather_rgb:
             planes.append((self.img_bufs[k], 3))
         for buf, per in planes:
             if self.rank == 0:
-                for r in range(1, self.world):
-                    ops.append((buf[self.bounds[r] * W * per:self.bounds[r + 1] * W * per], r, False))
-            else:
-                ops.append((buf[self.y0 * W * per:self.y1 * W * per], 0, True))
+                for r in range(1, n):
+                    ops.append((buf[bounds[r] * W * per:bounds[r + 1] * W * per], r, False))
+            elif self.rank < n:
+                ops.append((buf[bounds[self.rank] * W * per:bounds[self.rank + 1] * W * per], 0, True))
         return ops
 
-    def _exchange(self, k: int):
-        todo = self._sends(k)
+    def _exchange(self, k: int, bounds: Optional[List[int]] = None):
+        todo = self._sends(k, bounds)
         if self._host_staged():  # gloo on device tensors (one-GPU rehearsal): through host memory, in order
             for t, peer, send in todo:
                 if send:
@@ -566,6 +633,8 @@ class BandFrame(_CountedFrame):
         argb = self.argb_bufs[k]
         img = self.img_bufs[k % len(self.img_bufs)]
         self.argb, self.img = argb, img
+        if self.passes:
+            return self._step_passes(k, img, argb, d_counters)
         self._frame_counts()
         ev = None
         if self._events is not None:
@@ -587,9 +656,58 @@ class BandFrame(_CountedFrame):
             self.rgb_full = img.view(self.H, self.W, 3)
         return self.full
 
+    def _step_passes(self, k: int, img: torch.Tensor, argb: torch.Tensor, d_counters: int) -> Optional[torch.Tensor]:
+        """One frame as passes over row spans (Render.cpp:136-215's cursor walks the same rows in order).  Per pass:
+        the span's rows are cut into equal bands of ranks 0 .. m - 1 (m = min(world, rows)); every rank counts its
+        1/world slice of the span's random stream and the counts are all-gathered; ranks with a band emit its
+        randDirs and trace it (the stream continues from pass to pass on every rank); the bands go to rank 0.  A pass
+        of fewer rows than ranks leaves ranks m .. world - 1 behind rank 0's stream: rank 0's state is broadcast to
+        them before the next pass counts."""
+        for y0, y1 in self.passes:
+            bd = pass_bands(y0, y1, self.world)
+            m = len(bd) - 1
+            self.ops.set_span(y0, y1)
+            self.ops.set_rows(*pass_rows(bd, self.rank, y1))
+            bps = self.ops.blocks_per_slice(self.world)
+            self.ops.rng_count(self.rank, self.world, self.counts.data_ptr())
+            if self.world > 1:
+                self._all_gather_counts(bps=bps)
+            if self.rank < m:
+                self.ops.render_counted(self.world, self.counts.data_ptr(), img.data_ptr(), argb.data_ptr(),
+                                        d_counters)
+            if m < self.world:
+                self._hand_over_rng_state()
+            if self.gather_to_root:
+                works = self._exchange(k, bd)
+                if self.pipeline and self.device.type == "cuda":
+                    self.works[k] += works
+                else:
+                    for w in works:
+                        w.wait()
+        if self.world == 1 or not self.gather_to_root:
+            return argb.view(self.H, self.W) if self.world == 1 else None
+        if self.rank != 0:
+            return None
+        self.full = argb.view(self.H, self.W)
+        if self.gather_rgb:
+            self.rgb_full = img.view(self.H, self.W, 3)
+        return self.full
+
+    def _hand_over_rng_state(self):
+        """Rank 0's random-stream states to every rank (the ranks that sat a pass out are behind it)."""
+        st = torch.tensor(list(self.ops.rng_state()) if self.rank == 0 else [0, 0], dtype=torch.int64)
+        if dist.get_backend() == "nccl":
+            st = st.to(self.device)
+        dist.broadcast(st, 0)
+        sphere, jitter = (int(v) for v in st.tolist())
+        if self.rank != 0:
+            self.ops.set_rng_state(sphere, jitter)
+
     def balance(self, rounds: int = 3, frames: int = 8, timer=None) -> List[int]:
         """Re-cut the bands `rounds` times from each rank's measured render time over `frames` frames (HIP events
         on the render stream, or `timer(step)` -> seconds per frame); returns the final bounds."""
+        if self.passes:
+            return self.bounds  # equal bands per pass: nothing to balance
         for _ in range(rounds):
             t = timer(self.step) if timer else self._time_render(frames)
             times = torch.tensor([t], dtype=torch.float64)

@@ -15,6 +15,18 @@ def test_strong_scaling_baseline_is_the_committed_one_gpu_c4_line():
     assert bench.one_gpu_line("c4", 640, 360, 8) is None  # another frame: no baseline
 
 
+def test_default_one_gpu_line_times_the_c4_denominator():
+    """The driver's N = 1 line (default config C3) carries c4_1gpu, the C4 frame every N > 1 line renders, timed on one
+    GPU in the same run; other configs, custom frames and --no-c4 do not."""
+    assert bench.times_c4_denominator(1, "c3", False, False)
+    assert not bench.times_c4_denominator(1, "c3", False, True)
+    assert not bench.times_c4_denominator(1, "c3", True, False)
+    assert not bench.times_c4_denominator(2, "c4", False, False)
+    assert not bench.times_c4_denominator(1, "c5", False, False)
+    ap_default = bench.CONFIGS["c4"]
+    assert ap_default[:4] == ("synth16", 7680, 4320, 8) and bench.CONFIGS["c3"][0] == ap_default[0]
+
+
 def test_cpu_sample_strides_cover_every_config():
     """Every config has a bounded CPU sample: a row stride (one-sample frames) or a band of rows (SSAA frames)."""
     one = {k for k, c in bench.CONFIGS.items() if c[4] == 1}

@@ -200,3 +200,95 @@ def test_balanced_bounds():
     assert b[0] == 0 and b[-1] == 4320 and all(x % 8 == 0 for x in b) and b == sorted(set(b))
     # degenerate inputs keep valid bands
     assert rdist.balanced_bounds([0, 8, 16, 24], [0.0, 1.0, 1e9], 24, 8) == [0, 8, 16, 24]
+
+
+class FakePassOps(FakeOps):
+    """A stand-in whose random stream is a counter: slice counts encode the counting rank's stream state, a band
+    emit checks that every slice of the all-gathered counts came from the same state and advances the state by the
+    span's rows, and band pixels are (frame << 24) | (y << 12) | x."""
+
+    def __init__(self, W, H, rank, world, bps=3):
+        super().__init__(W, H, 0, rank, world, bps)
+        self.state, self.jitter, self.span, self.fno = 7, 0, None, 0
+        self.consistent = True
+        self.passes_traced = 0
+
+    def set_span(self, y0, y1):
+        self.span = (y0, y1)
+
+    def rng_state(self):
+        return self.state, self.jitter
+
+    def set_rng_state(self, sphere, jitter):
+        self.state, self.jitter = sphere, jitter
+
+    def rng_count(self, slice_, nslices, d_counts, stream=0):
+        import ctypes
+        import numpy as np
+        t = np.ctypeslib.as_array((ctypes.c_int32 * (nslices * self.bps)).from_address(d_counts))
+        for b in range(self.bps):
+            t[slice_ * self.bps + b] = (self.state * 10 + slice_) * 100 + b
+
+    def render_counted(self, nslices, d_counts, d_img, d_argb, d_counters=0, emitted_event=0):
+        import ctypes
+        import numpy as np
+        cnt = np.ctypeslib.as_array((ctypes.c_int32 * (nslices * self.bps)).from_address(d_counts)).copy()
+        want = [(self.state * 10 + s) * 100 + b for s in range(nslices) for b in range(self.bps)]
+        self.consistent &= cnt.tolist() == want
+        y0, y1 = self.band
+        assert self.span[0] <= y0 < y1 <= self.span[1]
+        argb = np.ctypeslib.as_array((ctypes.c_int32 * (self.H * self.W)).from_address(d_argb))
+        for y in range(y0, y1):
+            argb[y * self.W:(y + 1) * self.W] = (self.fno << 24) | (y << 12) | np.arange(self.W)
+        self.state += self.span[1] - self.span[0]
+        self.jitter += 1
+        self.passes_traced += 1
+
+
+def _pass_worker(rank, world, port, W, H, ss, launch_traces, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ops = FakePassOps(W, H, rank, world)
+        sf = rdist.BandFrame(ops, W, H, rank, world, torch.device("cpu"), pipeline=False, ss=ss,
+                             launch_traces=launch_traces)
+        assert sf.passes and not sf.count_ahead and not sf.emit_ahead
+        ok = True
+        for frame in range(3):
+            ops.fno = frame
+            out = sf.step()
+            if rank == 0:
+                ys, xs = torch.meshgrid(torch.arange(H), torch.arange(W), indexing="ij")
+                ok &= bool(torch.equal(out, ((frame << 24) | (ys << 12) | xs).to(torch.int32)))
+            else:
+                ok &= out is None
+        q.put((rank, ok, ops.consistent, ops.state, ops.jitter, ops.passes_traced, len(sf.passes)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,W,H,ss,launch_traces", [
+    (2, 8, 10, 2, 8 * 4 * 3 // 2),   # passes of 3 rows (the last of 1): a rank sits out the last pass
+    (3, 8, 10, 2, 8 * 4 * 2 // 3),   # passes of 2 rows: every pass leaves one of 3 ranks out
+    (3, 6, 13, 3, 6 * 9 * 4 // 3),   # passes of 4 rows, the last of 1
+    (2, 5, 8, 4, 5 * 16 * 2),        # passes of 4 rows, 2 per rank: no rank sits out, no handover
+])
+def test_band_frame_row_span_passes_gloo(world, W, H, ss, launch_traces):
+    """The RCCL path's frames of more traces than one pass (SSAA screenshots): row-span passes with the count exchange
+    per pass, the stream continued across passes and frames, ranks that sit a pass out brought up to rank 0's stream
+    state, every band on rank 0 (reflaxman_amd/dist.py BandFrame._step_passes)."""
+    plan = rdist.pass_plan(W, H, ss, world, launch_traces)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pass_worker, args=(r, world, port, W, H, ss, launch_traces, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    res = sorted(q.get(timeout=10) for _ in range(world))
+    assert all(r[1] and r[2] for r in res), res  # whole frames on rank 0; every pass saw one stream state
+    assert {r[3] for r in res} == {7 + 3 * H}    # every rank ends where the serial stream does (3 frames x H rows)
+    assert len({r[4] for r in res}) == 1         # and with the same jitter state
+    assert res[0][5] == 3 * len(plan)            # rank 0 traced every pass

@@ -140,6 +140,39 @@ def test_rng_stream_state_per_frame_size(W, H, ss, frames):
     r.close()
 
 
+def test_concurrent_renderers_share_one_device():
+    """Three renderers render C1 frames (640x480 depth 4, the one-pass pre-pass: 166 blocks) on their own streams of one
+    device at once, beside a fourth renderer's C3 frame that holds the chip's slots, with no synchronisation between
+    them: the pre-pass's look-back takes its block order from an ordered ticket, so its blocks finish whatever order
+    the workgroups are dispatched in and whatever else is resident.  Each C1 frame hashes to the reference's frame and
+    no renderer reports an error."""
+    import torch
+    from reflaxman_amd.render import Renderer, build_scene, make_frame
+    c1 = CASES["hash_default_640x480_d4"]
+    s1, cam1 = build_scene(scene("default"))
+    s3, cam3 = build_scene(scene("synth16"))
+    big = Renderer()
+    big.set_scene(s3)
+    rs = [Renderer() for _ in range(3)]
+    for r in rs:
+        r.set_scene(s1)
+    W, H = 640, 480
+    f1, f3 = make_frame(cam1, W, H, 4), make_frame(cam3, 3840, 2160, 8)
+    bufs = [(torch.zeros(H * W * 3, device="cuda"), torch.zeros(H * W, dtype=torch.int32, device="cuda")) for _ in rs]
+    big_rgb = torch.zeros(3840 * 2160 * 3, device="cuda")
+    torch.cuda.synchronize()
+    big.render_frame(f3, big_rgb.data_ptr())
+    for r, (rgb, argb) in zip(rs, bufs):
+        r.render_frame(f1, rgb.data_ptr(), argb.data_ptr())
+    for r in rs + [big]:
+        r.synchronize()
+    for rgb, argb in bufs:
+        assert sha(rgb.cpu().numpy()) == c1["sha_f32"]
+        assert sha(argb.cpu().numpy().view(np.uint32)) == c1["sha_argb"]
+    for r in rs + [big]:
+        r.close()
+
+
 @pytest.mark.parametrize("name,W,H,depth,ss,additive,chunks", [
     ("synth16", 640, 360, 8, 1, False, None),      # plain frames: record, reuse the sorted order, re-sort
     ("default", 200, 150, 4, 2, True, None),       # SSAA + additive accumulation

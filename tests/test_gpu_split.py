@@ -140,6 +140,37 @@ def test_split_frame_on_a_device_group():
     one.close()
 
 
+def test_group_passes_narrower_than_the_group():
+    """Split group frames whose passes hold fewer rows than members (3 members, passes of 2 rows, the last of 1): the
+    members a pass leaves out keep an older stream state, so the next pass -- and the next whole frame, which takes
+    every member -- must hand member 0's state over again.  Two split frames, then two frames in one pass, each equal
+    to the single renderer's."""
+    import torch
+    from reflaxman_amd.render import build_scene, make_frame
+    scene, cam = build_scene(scenes.get_scene("default"))
+    W, H, ss = 40, 9, 4
+    L = _lib.load()
+    g = C.c_void_p()
+    devs = (C.c_int * 3)(0, 0, 0)
+    _lib.check(L.rfx_group_create(C.byref(g), devs, 3), "group_create")
+    _lib.check(L.rfx_group_set_scene(g, scene._h))
+    r0 = C.c_void_p(L.rfx_group_renderer(g, 0))
+    _lib.check(L.rfx_renderer_set_rng(r0, 1350490027, 99))
+    one = _renderer(scene)
+    rgb, argb = torch.zeros(H * W * 3, device="cuda"), torch.zeros(H * W, dtype=torch.int32, device="cuda")
+    rgb1, argb1 = torch.zeros_like(rgb), torch.zeros_like(argb)
+    for k, limit in enumerate([W * ss * ss * 2 // 3, W * ss * ss * 2 // 3, 0, 0]):
+        _lib.check(L.rfx_renderer_set_launch_traces(r0, limit))  # 3 x limit traces per pass: 2 rows, then 1 row
+        f = make_frame(cam, W, H, 6, ss)
+        _lib.check(L.rfx_group_render_frame(g, C.byref(f), C.c_void_p(rgb.data_ptr()), C.c_void_p(argb.data_ptr()),
+                                            None), "group_render_frame")
+        one.render_frame(f, rgb1.data_ptr(), argb1.data_ptr())
+        torch.cuda.synchronize()
+        assert torch.equal(rgb, rgb1) and torch.equal(argb, argb1), k
+    L.rfx_group_destroy(g)
+    one.close()
+
+
 @pytest.mark.parametrize("case", ["pulse_screenshot_800x600_ss128", "pulse_screenshot_1920x1080_ss128"])
 def test_screenshot_over_2_32_samples(case):
     """800x600 at 128x128 samples, depth 20 (Pulse's menu keys 1 and 8): 7.9e9 samples in one rfx_render_frame, split
@@ -152,3 +183,67 @@ def test_screenshot_over_2_32_samples(case):
     assert sha(argb) == c["sha_argb"]
     assert sha(rgb) == c["sha_f32"]
     r.close()
+
+
+@pytest.mark.parametrize("nranks,launch_traces", [(2, 0), (4, 0), (8, 800 * 128 * 128 * 3 // 8)])
+def test_rank_passes_assemble_the_screenshot(nranks, launch_traces):
+    """The multi-process path's SSAA frames (reflaxman_amd/dist.py BandFrame row-span passes) with the ranks emulated
+    in one process: the 800x600 128x128 screenshot (7.9e9 samples) as passes over row spans (dist.pass_plan: 2^31
+    traces per pass; with 8 ranks and a launch limit of 3/8 row, passes of 3 rows, so 5 of 8 ranks sit every pass out
+    and take rank 0's stream state), each span cut into equal bands (dist.pass_bands), every rank counting every slice
+    of the span's stream (the all-gather emulated), each band emitted and traced into its rank's whole-frame buffers
+    and copied into one frame as rank 0 receives it: SHA-256 of the f32 and ARGB8 frames equal the reference's."""
+    import torch
+    from reflaxman_amd import dist as rdist
+    from reflaxman_amd.render import Renderer, build_scene, make_frame
+    c = CASES["pulse_screenshot_800x600_ss128"]
+    W, H, depth, ss = c["W"], c["H"], c["depth"], c["ss"]
+    lt = launch_traces or rdist.LAUNCH_TRACES
+    plan = rdist.pass_plan(W, H, ss, nranks, lt)
+    assert plan and len(plan) > 1
+    s, cam = build_scene(scenes.get_scene("default"))
+    L = _lib.load()
+    rs = [Renderer(sphere_seed=c["RFX_SPHERE_SEED"]) for _ in range(nranks)]
+    for r in rs:
+        r.set_scene(s)
+    fr = [make_frame(cam, W, H, depth, ss, row_block=0, rank=k, nranks=nranks) for k in range(nranks)]
+    bufs = [(torch.zeros(H * W * 3, device="cuda"), torch.zeros(H * W, dtype=torch.int32, device="cuda"))
+            for _ in range(nranks)]
+    img = torch.zeros(H * W * 3, device="cuda")
+    argb = torch.zeros(H * W, dtype=torch.int32, device="cuda")
+    cnt = None
+    sat_out = 0
+    for y0, y1 in plan:
+        bd = rdist.pass_bands(y0, y1, nranks)
+        m = len(bd) - 1
+        for k in range(nranks):
+            fr[k].span_begin, fr[k].span_end = y0 * W, y1 * W
+            a, b = rdist.pass_rows(bd, k, y1)
+            fr[k].pixel_begin, fr[k].pixel_end = a * W, b * W
+        bps = C.c_uint64()
+        _lib.check(L.rfx_frame_rng_blocks(rs[0]._h, C.byref(fr[0]), nranks, C.byref(bps)))
+        if cnt is None:  # the first pass is the largest
+            cnt = [torch.zeros(nranks * bps.value, dtype=torch.int32, device="cuda") for _ in range(nranks)]
+        for k in range(nranks):
+            for sl in range(nranks):
+                _lib.check(L.rfx_frame_rng_count(rs[k]._h, C.byref(fr[k]), sl, nranks, C.c_void_p(cnt[k].data_ptr()),
+                                                 None), "rng_count")
+        for k in range(m):
+            _lib.check(L.rfx_render_frame_counted(rs[k]._h, C.byref(fr[k]), nranks, C.c_void_p(cnt[k].data_ptr()),
+                                                  C.c_void_p(bufs[k][0].data_ptr()), C.c_void_p(bufs[k][1].data_ptr()),
+                                                  None, None), "render_frame_counted")
+        if m < nranks:
+            sat_out += 1
+            st = rs[0].get_rng()
+            for k in range(m, nranks):
+                rs[k].set_rng(*st)
+        for k in range(m):
+            rs[k].synchronize()
+            img[bd[k] * W * 3:bd[k + 1] * W * 3] = bufs[k][0][bd[k] * W * 3:bd[k + 1] * W * 3]
+            argb[bd[k] * W:bd[k + 1] * W] = bufs[k][1][bd[k] * W:bd[k + 1] * W]
+    torch.cuda.synchronize()
+    assert (sat_out > 0) == (launch_traces != 0)
+    assert sha(argb.cpu().numpy().view(np.uint32)) == c["sha_argb"]
+    assert sha(img.cpu().numpy()) == c["sha_f32"]
+    for r in rs:
+        r.close()

@@ -41,7 +41,7 @@ def short(name: str) -> str:
 
 
 def usage(tu: str):
-    flags = [f for f in _build.FLAGS if f != "-fPIC"]
+    flags = [f for f in _build.FLAGS if f != "-fPIC"] + os.environ.get("RFX_RU_DEFINES", "").split()
     with tempfile.TemporaryDirectory() as tmp:
         cmd = [_build.hipcc(), *flags, "--cuda-device-only", "-c", os.path.join(_build.CSRC, tu), "-o",
                os.path.join(tmp, "x.o"), "-Rpass-analysis=kernel-resource-usage"]
