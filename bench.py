@@ -797,13 +797,14 @@ def main(argv=None):
         **({"band_bounds": sf.bounds} if bands else {}),
         **({"steady_state_parity": steady,
             "efficiency": baseline["efficiency"] if baseline else None,
-            "efficiency_kind": "value / (N x strong_scaling_baseline.value): the same C4 frame on one GPU of this run "
-                               "(the N = 1 line's c4_1gpu is the same measurement on the driver's N = 1 run)",
+            "efficiency_kind": "value / (N x strong_scaling_baseline.value): the same frame on one GPU of this run "
+                               "(for C4, the driver's N = 1 line carries the same measurement as c4_1gpu)",
             "strong_scaling_baseline": baseline,
             "strong_scaling_baseline_committed": one_gpu_line(cfg_name, W, H, depth),
-            "scale_note": "N > 1 renders C4 (7680x4320); the driver's N = 1 bench point is C3 (3840x2160), whose rate "
-                          "is ~5% below C4's on one GPU: efficiency here is against strong_scaling_baseline, the "
-                          "same C4 frame on one GPU of this run"} if world > 1 else {}),
+            "scale_note": (f"N > 1 renders {cfg_name.upper()} ({W}x{H}); the driver's N = 1 bench point is C3 "
+                           "(3840x2160), whose line carries c4_1gpu, the C4 frame on one GPU in that run: efficiency "
+                           "here is against strong_scaling_baseline, the same frame on one GPU of this run")}
+           if world > 1 else {}),
     }
     if world == 1 and not args.no_cpu_baseline:
         log("cpu_baseline: reference CPU path on a row sample of the same frame ...")

@@ -300,10 +300,11 @@ int rfx_rand_dirs(rfx_renderer *r, uint32_t seed, uint64_t n, float *out3, uint3
  *       cube where it provably rounds like glibc, rfx_powf.h powf_cube_fast) against glibc's algorithm on the device,
  *       for every float x in [0, 1]: counts[0] = mismatches (0 expected), counts[1] = inputs that took glibc's
  *       algorithm;
- *   rfx_kat_div: the trace loop's division fast paths (rfx_math.h div_rn and the shared-divisor Vector3 / float)
- *       against IEEE '/' on the operand pairs first .. first + n - 1 of a fixed hash (every float class, both edges
- *       of the fast path's divisor and quotient bounds): counts[0] = quotients whose bits differ (0 expected),
- *       counts[1] = pairs that took the fast path, counts[2] = quotients checked (4 per pair).
+ *   rfx_kat_div: the trace loop's division fast paths (rfx_math.h div_rn, normalized's shared reciprocal and the
+ *       skybox's div_fast_unit) against IEEE '/' on the operand pairs first .. first + n - 1 of a fixed hash (every
+ *       float class, both edges of the fast path's divisor and quotient bounds): counts[0] = quotients whose bits
+ *       differ (0 expected), counts[1] = pairs that took div_rn's fast path, counts[2] = quotients checked (5 per
+ *       pair).
  */
 int rfx_kat_objects(rfx_renderer *r, const float *rays, const int32_t *objects, uint64_t n, float *out);
 int rfx_kat_texels(rfx_renderer *r, int texture, const float *in, uint64_t n, float *out);

@@ -887,7 +887,8 @@ __global__ __launch_bounds__(kKatThreads) void kat_powf_cube(uint32_t first, uin
   }
 }
 
-// rfx_math.h's division fast paths (div_rn, the shared-divisor divv) against IEEE '/' on operand pairs drawn from a hash
+// rfx_math.h's division fast paths (div_rn, normalized's shared reciprocal, div_fast_unit) against IEEE '/' on operand
+// pairs drawn from a hash
 // of the pair index (first + i): raw bit patterns (every class: zeros, denormals, infinities, NaNs), divisors on both
 // edges of [2^-40, 2^100] (a few ulps either side), quotients on both edges of [2^-60, 2^60], zero and denormal
 // numerators, powers of two.  counts[0] += quotients whose bits differ from '/' (two NaNs compare equal), counts[1] +=
@@ -946,15 +947,22 @@ __global__ __launch_bounds__(kKatThreads) void kat_div(uint64_t first, uint32_t 
     const float q = div_rn(a, b);
     bool ok;
     (void)div_fast(a, div_prep(b), ok);
-    // the shared-divisor form (normalize, Vector3 / float) on three numerators at once
-    const float a2 = __uint_as_float(__float_as_uint(a) ^ (h2 & 0x807F0000u)), a3 = a * -0.5f;
-    const v3 qv = divv(mk(a, a2, a3), b);
-    const bool sv = fabsf(b) > kVerySmall;  // divv divides only then (Vector3.cpp:143-151)
-    const float rx = sv ? a / b : a, ry = sv ? a2 / b : a2, rz = sv ? a3 / b : a3;
-    bad = (kat_same(q, a / b) ? 0u : 1u) + (kat_same(qv.x, rx) ? 0u : 1u) + (kat_same(qv.y, ry) ? 0u : 1u) +
-          (kat_same(qv.z, rz) ? 0u : 1u);
+    // the normalize form (one reciprocal of the length, one range compare per component) on (a, a2, a3)
+    const float a2 = __uint_as_float(__float_as_uint(a) ^ (h2 & 0x807F0000u)), a3 = b * -0.5f;
+    const v3 v = mk(a, a2, a3), nv = normalized(v);
+    const float l = len(v);
+    const bool sv = l > kVerySmall;  // Vector3.cpp:63-72 divides only then
+    const float rx = sv ? v.x / l : v.x, ry = sv ? v.y / l : v.y, rz = sv ? v.z / l : v.z;
+    // the skybox form: a component over the largest one (|p| <= den, den = |b| + VERY_SMALL_NUMBER)
+    const float den = fabsf(b) + kVerySmall, p = fabsf(a) <= den ? a : copysignf(den, a) * 0.75f;
+    bool okp;
+    float pd = div_fast_unit(p, den, rcp_refined(den), okp);
+    const bool unit_ok = den <= 0x1p64f;  // div_fast_unit's precondition (the skybox's den is at most 1 + 2^-63)
+    if (!okp) pd = p / den;
+    bad = (kat_same(q, a / b) ? 0u : 1u) + (kat_same(nv.x, rx) ? 0u : 1u) + (kat_same(nv.y, ry) ? 0u : 1u) +
+          (kat_same(nv.z, rz) ? 0u : 1u) + (!unit_ok || kat_same(pd, p / den) ? 0u : 1u);
     fast = ok ? 1u : 0u;
-    seen = 4;
+    seen = 5;
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1)

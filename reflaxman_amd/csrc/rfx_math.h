@@ -136,24 +136,52 @@ RFX_HD v3 cross(v3 a, v3 b)                                                     
 }
 RFX_HD v3 divv(v3 a, float f)                                                        // Vector3.cpp:143-151
 {
-  if (fabsf(f) > kVerySmall)
-  {
-#if defined(__HIP_DEVICE_COMPILE__) && RFX_DIV_FAST
-    // one reciprocal for the three quotients, one guard and one fallback branch for all three
-    const DivRcp d = div_prep(f);
-    bool ox, oy, oz;
-    const v3 q = mk(div_fast(a.x, d, ox), div_fast(a.y, d, oy), div_fast(a.z, d, oz));
-    if (__builtin_expect(ox && oy && oz, 1)) return q;
-#endif
-    return mk(a.x / f, a.y / f, a.z / f);
-  }
+  if (fabsf(f) > kVerySmall) return mk(a.x / f, a.y / f, a.z / f);
   return a;
+}
+// q = a / b by the fast path where the caller has already bounded the operands: |b| in (2^-63, 2^64] and |a| <= |b| (1
+// + 2^-20) -- a vector component over the vector's length (a finite sum of squares is at most 2^128, so its root is at
+// most 2^64), a direction component over its largest one.  Then |q| <= 1 + 2^-20, 1/b is normal, and |q| >= 2^-38 gives
+// |a| >= 2^-102 (exponent(a) > 23) and a/b normal: the range test is one compare.  The reciprocal r is div_prep's.
+RFX_HD float div_fast_unit(float a, float b, float r, bool &ok)
+{
+#if defined(__HIP_DEVICE_COMPILE__) && RFX_DIV_FAST
+  const float q0 = a * r;
+  const float t1 = __builtin_fmaf(-b, q0, a);
+  const float q1 = __builtin_fmaf(t1, r, q0);
+  const float t2 = __builtin_fmaf(-b, q1, a);
+  const float q = __builtin_fmaf(t2, r, q1);
+  ok = RFX_DIV_FAST == 2 || fabsf(q) >= 0x1p-38f;  // false for NaN
+  return q;
+#else
+  ok = false;
+  return a / b;
+#endif
+}
+RFX_HD float rcp_refined(float b)  // div_prep's reciprocal, without its range test (div_fast_unit's callers bound b)
+{
+#if defined(__HIP_DEVICE_COMPILE__) && RFX_DIV_FAST
+  const float r = __builtin_amdgcn_rcpf(b);
+  return __builtin_fmaf(__builtin_fmaf(-b, r, 1.0f), r, r);
+#else
+  return 1.0f / b;
+#endif
 }
 // Vector3::normalized (Vector3.cpp:63-72) == Tracemath::normalize (trace_math.cpp:3-12)
 RFX_HD v3 normalized(v3 a)
 {
   const float l = len(a);
-  if (l > kVerySmall) return divv(a, l);
+  if (l > kVerySmall)
+  {
+#if defined(__HIP_DEVICE_COMPILE__) && RFX_DIV_FAST
+    // divv(a, l) with one reciprocal for the three quotients, one range compare each (div_fast_unit: |a_i| <= l <= 2^64)
+    const float r = rcp_refined(l);
+    bool ox, oy, oz;
+    const v3 q = mk(div_fast_unit(a.x, l, r, ox), div_fast_unit(a.y, l, r, oy), div_fast_unit(a.z, l, r, oz));
+    if (__builtin_expect(ox && oy && oz, 1)) return q;
+#endif
+    return divv(a, l);
+  }
   return a;
 }
 // Tracemath::reflect (trace_math.cpp:14-23): v - (2n) * ((v.n) / (n.n))

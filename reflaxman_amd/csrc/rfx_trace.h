@@ -265,7 +265,7 @@ __device__ __forceinline__ col skybox_texel(const DevScene &S, v3 ray, const flo
   const v3 n = normalized(ray);
   const float x = n.x, y = n.y, z = n.z;
   const float ax = fabsf(x) + kVerySmall, ay = fabsf(y) + kVerySmall, az = fabsf(z) + kVerySmall;
-  // the face's two quotients share their divisor (rfx_math.h div_prep): u0 -/+ p / den * hw, v0 -/+ q / den * hh
+  // the face's two quotients share their divisor (rfx_math.h div_fast_unit): u0 -/+ p / den * hw, v0 -/+ q / den * hh
   float u0, v0, p, q, den, su, sv;
   if (az >= ax && az >= ay)
   {
@@ -285,9 +285,10 @@ __device__ __forceinline__ col skybox_texel(const DevScene &S, v3 ray, const flo
     if (y > 0) { u0 = uTop; v0 = vTop; p = x; q = z; su = 1.0f; sv = -1.0f; }
     else { u0 = uBottom; v0 = vBottom; p = x; q = z; su = 1.0f; sv = 1.0f; }
   }
-  const DivRcp d = div_prep(den);
+  // den in [2^-63, 1 + 2^-63] and |p|, |q| <= den: div_fast_unit's bounds
+  const float rden = rcp_refined(den);
   bool okp, okq;
-  float pd = div_fast(p, d, okp), qd = div_fast(q, d, okq);
+  float pd = div_fast_unit(p, den, rden, okp), qd = div_fast_unit(q, den, rden, okq);
   if (__builtin_expect(!(okp && okq), 0)) { pd = p / den; qd = q / den; }
   // u0 + p / den * hw, or u0 - (p / den * hw): a subtraction of the product, as the reference writes it
   const float pu = pd * hw, qv = qd * hh;
@@ -354,6 +355,11 @@ __device__ __forceinline__ bool pair_may_hit(f2 b, f2 d)
 // SEL (large-scene loops): one branch, the rest computed and decided without branching.  tools/ab.py, trace ms: C5
 // 3.143 -> 3.067 (-2.4%); the small-scene kernel +9% with it (its SGPR spills 23 -> 51), so the small loops keep the
 // early outs.
+// The large scenes' sphere loops (SEL) keep '/': the shared reciprocal of 2a, live across the BVH walk, raised the C5
+// trace kernel's VGPR spills from 15 to 36 and its time by 5.9% (tools/ab.py, profiles/r06/ab/c5_div_sel_prefetch_r6c.jsonl)
+#ifndef RFX_DIV_SEL
+#define RFX_DIV_SEL 0
+#endif
 template <bool STATS, bool SHADOW, bool SEL = false>
 __device__ __forceinline__ bool sphere_tail(float b, float d, v3 ray, const RayConst &k, float &t_out,
                                             float &sq_out, Cnt &cnt)
@@ -364,7 +370,8 @@ __device__ __forceinline__ bool sphere_tail(float b, float d, v3 ray, const RayC
   if constexpr (!STATS && SEL)
   {
     if (!(d >= 0.0f && k.a_ok && b < 0.0f)) return false;
-    const float t = div_by(-b - sqrt_rn(d), k.a2d);
+    // (RFX_DIV_SEL 0: the large scenes' BVH loops divide with '/', and the shared reciprocal is not live across the walk)
+    const float t = RFX_DIV_SEL ? div_by(-b - sqrt_rn(d), k.a2d) : (-b - sqrt_rn(d)) / k.a2;
     const float sq = sqlen(mul(ray, t));
     t_out = t;
     sq_out = sq;

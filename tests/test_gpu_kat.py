@@ -149,7 +149,7 @@ def test_kat_powf_cube_every_float():
 def test_kat_division_fast_path():
     """The trace loop's division fast path (rfx_math.h: eight of the IEEE lowering's eleven instructions, for divisors
     in [2^-40, 2^100] and quotients in [2^-60, 2^60]; the shared-reciprocal form of Vector3 / float) equals IEEE '/'
-    bit for bit on 2^27 + 2^20 operand pairs (4 quotients each): raw bit patterns of every class, both edges of both
+    bit for bit on 2^27 + 2^20 operand pairs (5 quotients each: div_rn, normalize's three, the skybox's): raw bit patterns of every class, both edges of both
     bounds, zero and denormal numerators (tests/test_div_guard.py replays the range argument on the CPU)."""
     import ctypes as C
     from reflaxman_amd import _lib
@@ -158,10 +158,10 @@ def test_kat_division_fast_path():
     _lib.check(_lib.load().rfx_kat_div(r._h, 0, (1 << 27) + (1 << 20), counts), "kat_div")
     r.close()
     bad, fast, seen = counts
-    assert seen == 4 * ((1 << 27) + (1 << 20))
+    assert seen == 5 * ((1 << 27) + (1 << 20))
     assert bad == 0
     # the fast path is taken on most of the in-range classes and refused on the rest (NaN, zero, out-of-range pairs)
-    assert 0.2 * (seen // 4) < fast < 0.99 * (seen // 4), fast
+    assert 0.2 * (seen // 5) < fast < 0.99 * (seen // 5), fast
 
 
 def test_kat_argb():

@@ -93,6 +93,9 @@ VARIANTS = {
     "divall2": ["RFX_DIV_FAST=2", "RFX_DIV_SINGLE=1"],
     "ticket0": ["RFX_RNG_TICKET=0"],
     "lookback0": ["RFX_LOOKBACK_SPINS=0"],
+    "tiles0": ["RFX_SCAN_TILES=0"],
+    "divsel1": ["RFX_DIV_SEL=1"],
+    "divfast2": ["RFX_DIV_FAST=2"],
 }
 
 
