@@ -292,3 +292,29 @@ def test_band_frame_row_span_passes_gloo(world, W, H, ss, launch_traces):
     assert {r[3] for r in res} == {7 + 3 * H}    # every rank ends where the serial stream does (3 frames x H rows)
     assert len({r[4] for r in res}) == 1         # and with the same jitter state
     assert res[0][5] == 3 * len(plan)            # rank 0 traced every pass
+
+
+def test_pass_plan_matches_the_group_rule():
+    """dist.pass_plan cuts frames the way rfx_group_render_frame does (rfx_group.cpp: at most min(N x launch limit, 2^31)
+    traces per pass, whole rows), every pass within 2^31 traces; pass_bands gives min(N, rows) equal bands."""
+    assert rdist.pass_plan(3840, 2160, 1, 8) is None          # C3/C4-sized one-sample frames take one pass
+    assert rdist.pass_plan(7680, 4320, 1, 2) is None
+    for W, H, ss, N in [(1920, 1080, 128, 1), (1920, 1080, 128, 2), (1920, 1080, 128, 8), (800, 600, 128, 4),
+                        (7680, 4320, 256, 8), (1280, 720, 64, 2), (7680, 4320, 16, 8)]:
+        plan = rdist.pass_plan(W, H, ss, N)
+        assert plan, (W, H, ss, N)
+        cap = min(N * rdist.LAUNCH_TRACES, rdist.MAX_PASS_TRACES)
+        assert plan[0][0] == 0 and plan[-1][1] == H and all(a[1] == b[0] for a, b in zip(plan, plan[1:]))
+        assert all((y1 - y0) * W * ss * ss <= cap for y0, y1 in plan)
+        assert all(y1 - y0 == plan[0][1] for y0, y1 in plan[:-1])  # equal passes, the last one shorter
+        for y0, y1 in plan:
+            bd = rdist.pass_bands(y0, y1, N)
+            assert bd[0] == y0 and bd[-1] == y1 and len(bd) - 1 == min(N, y1 - y0)
+            assert all(b > a for a, b in zip(bd, bd[1:]))
+            for r in range(N):
+                a, b = rdist.pass_rows(bd, r, y1)
+                assert y0 <= a < b <= y1
+    # 7680 x 256^2 samples: 4 rows a pass, so 4 of 8 ranks sit every pass out
+    assert rdist.pass_plan(7680, 4320, 256, 8)[0] == (0, 4)
+    # 1280x720 at 64x64 (3.8e9 traces, between 2^31 and 2^32): passes, no longer refused (round-5 advice)
+    assert len(rdist.pass_plan(1280, 720, 64, 2)) == 2

@@ -8,10 +8,16 @@ R=$PWD
 O=$R/gpurun_out/${1:-pmc_configs}
 mkdir -p $O/records
 cd /tmp && export TMPDIR=/tmp
-run_cfg() {  # name  scene W H depth ss  bench args...
+run_cfg() {  # name  scene W H depth ss  bench args...   (PMC_ONLY="c3 c5 ..": only the configs whose name starts so)
   local name=$1 scene=$2 W=$3 H=$4 depth=$5 ss=$6
+  if [ -n "$PMC_ONLY" ]; then
+    local keep=0 p
+    for p in $PMC_ONLY; do case $name in ${p}_*) keep=1 ;; esac; done
+    [ $keep = 1 ] || return 0
+  fi
   shift 6
-  local args="$R/bench.py $* --no-cpu-baseline"
+  # steady-state frames only: no first-view frames and no same-run C4 frames in the per-dispatch means
+  local args="$R/bench.py $* --no-cpu-baseline --no-first-view --no-c4"
   timeout -s KILL ${PMC_T:-120} rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU --output-format csv -d $O/pmc1_$name -o run -- python3 $args > $O/pmc1_$name.log 2>&1 || return 7
   timeout -s KILL ${PMC_T:-120} rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmc2_$name -o run -- python3 $args > $O/pmc2_$name.log 2>&1 || return 8
   timeout -s KILL ${PMC_T:-120} rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmc3_$name -o run -- python3 $args > $O/pmc3_$name.log 2>&1 || return 9
@@ -26,7 +32,7 @@ run_cfg c2_default_1920x1080_d1 default 1920 1080 1 1 --config c2 --depth 1 --st
 run_cfg c2_default_1920x1080_d4 default 1920 1080 4 1 --config c2 --steps 10 --warmup 2 || exit $?
 run_cfg c4_synth16_7680x4320_d8 synth16 7680 4320 8 1 --config c4 --steps 3 --warmup 1 || exit $?
 run_cfg shot_default_1920x1080_d20 default 1920 1080 20 4 --config shot --steps 3 --warmup 1 || exit $?
-PMC_T=300 run_cfg shot128_default_1920x1080_d20 default 1920 1080 20 128 --config shot128 --steps 1 --warmup 0 --no-first-view || exit $?
+PMC_T=300 run_cfg shot128_default_1920x1080_d20 default 1920 1080 20 128 --config shot128 --steps 1 --warmup 0 || exit $?
 if [ "$2" = "--lines" ]; then
   cp $O/records/*.json $R/profiles/pmc/ || exit 12
   cd $R
