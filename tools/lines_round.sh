@@ -11,4 +11,6 @@ timeout -k 10 200 python -u tools/group_copy_cost.py > $O/group_copy_cost_c4_8me
 for n in 2 4; do
   timeout -k 10 400 python bench.py --gpus $n --backend gloo --one-device --steps 20 --warmup 3 --no-cpu-baseline > $O/rehearsal_c4_n${n}_bands_gloo_one_device.json 2> $O/rehearsal_n$n.err || exit 5
 done
+# the ReadMe screenshot over 2 ranks: row-span passes (dist.BandFrame), hashed against the reference's frame
+timeout -k 10 400 python bench.py --gpus 2 --backend gloo --one-device --config shot128 > $O/rehearsal_shot128_n2_bands_gloo_one_device.json 2> $O/rehearsal_shot128_n2.err || exit 6
 exit 0
