@@ -1447,13 +1447,15 @@ static int emit_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *d_counts, 
 
 // The whole pre-pass of a one-device launch in one kernel (rng_fused: count, look-back scan and scatter), with
 // emit_frame's bookkeeping.  RFX_RNG_FUSED=0 keeps the two-kernel form (rng_count, then emit_frame).
-// Launches of at most RFX_RNG_FUSED_MAX_BLOCKS pre-pass blocks take it: on larger ones (C3: 4,067 blocks) the look-back
-// chain costs what the second launch does (interleaved A/B, profiles/r05/ab/*_rng_fused.jsonl).
+// Launches of at most RFX_RNG_FUSED_MAX_BLOCKS pre-pass blocks take it.  Its block-order ticket (one atomic per
+// workgroup on one word) serialises the launch's start in proportion to the blocks, so it pays only on small launches
+// (interleaved A/B, frame ms, one-pass / two-kernel, profiles/r06/ab/prepass_limit_*_r6e.jsonl): 640x480 (166 blocks)
+// 0.0552 / 0.0565, 960x540 (269) 0.0657 / 0.0643, 1280x720 (466) 0.0841 / 0.0803, 1920x1080 (1,013) 0.0812 / 0.0679.
 #ifndef RFX_RNG_FUSED
 #define RFX_RNG_FUSED 1
 #endif
 #ifndef RFX_RNG_FUSED_MAX_BLOCKS
-#define RFX_RNG_FUSED_MAX_BLOCKS 2048
+#define RFX_RNG_FUSED_MAX_BLOCKS 256
 #endif
 static bool fused_prepass(const FramePlan &pl, uint64_t nblk)
 {

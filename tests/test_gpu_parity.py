@@ -129,7 +129,7 @@ def test_rand_dirs_prepass():
                                            (512, 511, 2, 2), (300, 200, 4, 1)])
 def test_rng_stream_state_per_frame_size(W, H, ss, frames):
     """The render path's pre-pass -- the one-pass kernel (rng_fused: count, decoupled look-back scan, scatter) up to
-    RFX_RNG_FUSED_MAX_BLOCKS blocks, the two-kernel form beyond (2000x2000 is 1,969 blocks, 2100x2100 2,170) -- carries
+    RFX_RNG_FUSED_MAX_BLOCKS = 256 blocks (640x480 is 166), the two-kernel form beyond -- carries
     the reference's randomInsideSphere stream: after each frame the renderer's sphere seed equals the serial stream
     advanced by the frame's W*H*ss^2 accepted triples (oracle orc_rand_dirs), frame after frame; no error flag."""
     import oracle as orc

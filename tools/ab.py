@@ -94,6 +94,8 @@ VARIANTS = {
     "ticket0": ["RFX_RNG_TICKET=0"],
     "lookback0": ["RFX_LOOKBACK_SPINS=0"],
     "tiles0": ["RFX_SCAN_TILES=0"],
+    "fmax256": ["RFX_RNG_FUSED_MAX_BLOCKS=256"],
+    "fmax512": ["RFX_RNG_FUSED_MAX_BLOCKS=512"],
     "divsel1": ["RFX_DIV_SEL=1"],
     "divfast2": ["RFX_DIV_FAST=2"],
 }
