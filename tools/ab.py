@@ -88,6 +88,7 @@ VARIANTS = {
     "leaf8": ["RFX_BVH_LEAF_PAIRS=8"],
     "lt28": ["RFX_LAUNCH_TRACES=(1ull<<28)"],
     "lt31": ["RFX_LAUNCH_TRACES=(1ull<<31)"],
+    "lt29": ["RFX_LAUNCH_TRACES=(1ull<<29)"],
     "div0": ["RFX_DIV_FAST=0"],
     "divsingle": ["RFX_DIV_SINGLE=1"],
     "divall2": ["RFX_DIV_FAST=2", "RFX_DIV_SINGLE=1"],
