@@ -169,16 +169,6 @@ __device__ __forceinline__ uint32_t thread_state(uint32_t s, const uint32_t *jum
   return tj[0] * (bj[0] * s + bj[1]) + tj[1];
 }
 
-__device__ __forceinline__ bool triple(uint32_t &s, float &x, float &y, float &z)
-{
-  const uint32_t s1 = lcg_step(s), s2 = lcg_step(s1), s3 = lcg_step(s2);
-  s = s3;
-  x = rand_component_dev(lcg_out(s1));
-  y = rand_component_dev(lcg_out(s2));
-  z = rand_component_dev(lcg_out(s3));
-  return !(x * x + y * y + z * z > 1.f);                                        // Vector3.cpp:185
-}
-
 // A thread's 16-triple run as two chains of 8 triples each (the second starts 24 draws later: one affine
 // jump), so two independent LCG dependency chains interleave -- the same states, half the serial latency.
 constexpr int kHalfRun = kTriplesPerThread / 2;
@@ -190,6 +180,99 @@ constexpr LcgJump lcg_jump_const(int draws)
   return LcgJump{a, c};
 }
 constexpr LcgJump kHalfJump = lcg_jump_const(3 * kHalfRun);
+struct TripleJumps { LcgJump m[kTriplesPerThread]; };
+constexpr TripleJumps triple_jumps()
+{
+  TripleJumps t{};
+  for (int j = 0; j < kTriplesPerThread; ++j) t.m[j] = lcg_jump_const(3 * j);
+  return t;
+}
+constexpr TripleJumps kTripleJump = triple_jumps();  // (A, C) of 3j draws, j < 16: triple j's state from the thread's
+
+// Vector3.cpp:182-185's accept test of one triple of draws k1..k3: !(x*x + y*y + z*z > 1) in float, x = k / 16383.5 - 1.
+__device__ __forceinline__ bool float_accept(uint32_t s1, uint32_t s2, uint32_t s3)
+{
+  const float x = rand_component_dev(lcg_out(s1)), y = rand_component_dev(lcg_out(s2)),
+              z = rand_component_dev(lcg_out(s3));
+  return !(x * x + y * y + z * z > 1.f);                                        // Vector3.cpp:185
+}
+
+// The same test in integers: x is within 2^-23 of v / 32767, v = 2k - 32767, so the float test agrees with
+// N = v1^2 + v2^2 + v3^2 <= 32767^2 except on a thin shell around the sphere.  tests/native/sphere_shell.c checks all
+// 2^45 triples: every accepted triple has N <= 32767^2 + 298 and every rejected one N >= 32767^2 - 174, so outside
+// |N - 32767^2| <= kSphereShell the integer answer is the float one.  A thread with a triple inside the shell (about 3
+// threads in 10^5) redoes its 16 in float.  Per draw: a bit-field extract and two 24-bit multiply-adds, not eight
+// operations.
+#ifndef RFX_RNG_INT_ACCEPT
+#define RFX_RNG_INT_ACCEPT 1
+#endif
+constexpr uint32_t kSphereN = 32767u * 32767u;
+constexpr uint32_t kSphereShell = 1024u;
+
+// N of draws k1..k3 from the k alone: N = 4 (k1^2 + k2^2 + k3^2) - 4 * 32767 (k1 + k2 + k3) + 3 * 32767^2, evaluated
+// mod 2^32 (N < 2^32), every product a 24-bit one.  The squares are v_mad_u32_u24 in inline asm: written in C (k * k or
+// __umul24), this compiler (ROCm 7.2, clang 22) folds two of them into v_perm + v_dot4_u32_u8 over one byte of each k
+// only, dropping bits 8..14 (tests/test_sphere_shell.py checks the built code object for that instruction).
+__device__ __forceinline__ uint32_t mad_u24(uint32_t a, uint32_t b, uint32_t c)
+{
+  uint32_t d;
+  asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+
+__device__ __forceinline__ uint32_t sphere_n(uint32_t k1, uint32_t k2, uint32_t k3)
+{
+  const uint32_t q = mad_u24(k3, k3, mad_u24(k2, k2, mad_u24(k1, k1, 0u))), t = k1 + k2 + k3;
+  return 4u * q - 131068u * t + 3u * kSphereN;
+}
+
+// one triple from state s (advanced past it): its accept flag into bit j of acc, and (integer test) bit j of und when
+// it lies inside the shell
+__device__ __forceinline__ void triple(uint32_t &s, int j, uint32_t &acc, uint32_t &und)
+{
+  const uint32_t s1 = lcg_step(s), s2 = lcg_step(s1), s3 = lcg_step(s2);
+  s = s3;
+#if RFX_RNG_INT_ACCEPT
+  const uint32_t n = sphere_n(lcg_out(s1), lcg_out(s2), lcg_out(s3));
+  acc |= (n < kSphereN ? 1u : 0u) << j;
+  und |= (n - (kSphereN - kSphereShell) <= 2u * kSphereShell ? 1u : 0u) << j;
+#else
+  acc |= (float_accept(s1, s2, s3) ? 1u : 0u) << j;
+#endif
+}
+
+// the 16 accept flags of the thread whose first triple starts at state s0 (bit j: triple j); st (optional): the state
+// before each triple
+template <bool kStates>
+__device__ __forceinline__ uint32_t thread_flags(uint32_t s0, uint32_t *st)
+{
+  uint32_t s = s0, s2 = kHalfJump.a * s0 + kHalfJump.c, acc = 0, und = 0;
+#pragma unroll
+  for (int j = 0; j < kHalfRun; ++j)
+  {
+    if (kStates)
+    {
+      st[j] = s;
+      st[j + kHalfRun] = s2;
+    }
+    triple(s, j, acc, und);
+    triple(s2, j + kHalfRun, acc, und);
+  }
+  if (__builtin_expect(und != 0u, 0))
+  {
+    // a triple on the shell: the thread's 16 in float, one chain (rare enough that its latency does not matter)
+    acc = 0u;
+    s = s0;
+#pragma nounroll
+    for (int j = 0; j < kTriplesPerThread; ++j)
+    {
+      const uint32_t s1 = lcg_step(s), s2b = lcg_step(s1), s3 = lcg_step(s2b);
+      s = s3;
+      acc |= (float_accept(s1, s2b, s3) ? 1u : 0u) << j;
+    }
+  }
+  return acc;
+}
 
 // accepted-triple count of blocks [blk0, blk0 + gridDim.x): one slice of the stream (multi-GPU: one per rank)
 // masks (optional, one device): each thread's 16 accept flags, so that rng_emit regenerates only the LCG states
@@ -197,17 +280,8 @@ __global__ __launch_bounds__(kRngBlock) void rng_count(const uint32_t *seed, con
                                                        uint64_t blk0, uint16_t *masks)
 {
   const uint64_t b = blk0 + blockIdx.x;
-  uint32_t s = thread_state(*seed, jump, b, threadIdx.x);
-  uint32_t s2 = kHalfJump.a * s + kHalfJump.c;
-  uint32_t c = 0, acc = 0;
-  float x, y, z;
-#pragma unroll
-  for (int j = 0; j < kHalfRun; ++j)
-  {
-    const bool a = triple(s, x, y, z), a2 = triple(s2, x, y, z);
-    acc |= (a ? 1u : 0u) << j | (a2 ? 1u : 0u) << (j + kHalfRun);
-    c += (a ? 1u : 0u) + (a2 ? 1u : 0u);
-  }
+  const uint32_t acc = thread_flags<false>(thread_state(*seed, jump, b, threadIdx.x), nullptr);
+  uint32_t c = (uint32_t)__popc(acc);
   if (masks) masks[b * kRngBlock + threadIdx.x] = (uint16_t)acc;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off, 64);
@@ -245,15 +319,30 @@ __device__ __forceinline__ bool owned(uint64_t idx, const EmitFilter &f)
 // LCG steps and three exact conversions.
 constexpr int kScanThreads = 1024;
 
-// One block of the emit: block b's accepted triples are the traces [off, off + blk_cnt[b]).  Every thread of the
-// workgroup calls it with the same b and off.
-__device__ __forceinline__ void emit_block(uint32_t b, uint64_t off, const uint32_t *seed, const uint32_t *jump,
-                                           const uint32_t *blk_cnt, const uint16_t *masks, uint64_t need,
+// The inputs of block b's emit: its accept count, the thread's first LCG state and (one device) its 16 accept flags.
+// Loaded together -- rng_emit issues them with the prefix sum's loads, so the block waits on memory once.
+struct EmitIn {
+  uint32_t cnt, s0, mask;
+};
+__device__ __forceinline__ EmitIn emit_in(uint32_t b, const uint32_t *seed, const uint32_t *jump, const uint32_t *blk_cnt,
+                                          const uint16_t *masks)
+{
+  EmitIn e;
+  e.cnt = blk_cnt[b];
+  e.s0 = thread_state(*seed, jump, b, threadIdx.x);
+  e.mask = masks ? (uint32_t)masks[(uint64_t)b * kRngBlock + threadIdx.x] : 0u;
+  return e;
+}
+
+// One block of the emit: block b's accepted triples are the traces [off, off + in.cnt).  Every thread of the workgroup
+// calls it with the same b and off.  have_masks: in.mask holds the thread's accept flags (rng_count's), so only the LCG
+// states are regenerated.
+__device__ __forceinline__ void emit_block(uint64_t off, const EmitIn &in, bool have_masks, uint64_t need,
                                            uint32_t *rd_state, uint32_t *next_seed, const EmitFilter &flt,
                                            uint32_t *sst, uint32_t *wsum)
 {
   if (off >= need) return;
-  const uint32_t cnt = (uint32_t)min((uint64_t)blk_cnt[b], need - off);  // triples this block emits
+  const uint32_t cnt = (uint32_t)min((uint64_t)in.cnt, need - off);  // triples this block emits
   const uint64_t last = off + cnt - 1;
   // block-uniform skip: a block whose accepted indices all belong to other ranks' strips (and do not
   // include the frame's last trace, whose stream state every rank carries forward) writes nothing
@@ -265,37 +354,18 @@ __device__ __forceinline__ void emit_block(uint32_t b, uint64_t off, const uint3
     for (uint64_t st = s_lo; st <= s_hi && !any; ++st) any = (st % flt.nranks) == flt.rank;
     if (!any) return;
   }
-  uint32_t s = thread_state(*seed, jump, b, threadIdx.x);
-  uint32_t s2 = kHalfJump.a * s + kHalfJump.c;
   uint32_t st[kTriplesPerThread];
-  uint32_t acc = 0, c = 0;
-  if (masks)
+  uint32_t acc;
+  if (have_masks)
   {
-    // the accept flags rng_count recorded: only the LCG states are regenerated (3 steps per triple)
-    acc = masks[(uint64_t)b * kRngBlock + threadIdx.x];
-    c = (uint32_t)__popc(acc);
+    acc = in.mask;
+    // each triple's state straight from the thread's: one affine jump of 3j draws (a multiply-add), not 3j steps
 #pragma unroll
-    for (int j = 0; j < kHalfRun; ++j)
-    {
-      st[j] = s;
-      st[j + kHalfRun] = s2;
-      s = lcg_step(lcg_step(lcg_step(s)));
-      s2 = lcg_step(lcg_step(lcg_step(s2)));
-    }
+    for (int j = 0; j < kTriplesPerThread; ++j) st[j] = kTripleJump.m[j].a * in.s0 + kTripleJump.m[j].c;
   }
   else
-  {
-    float x, y, z;
-#pragma unroll
-    for (int j = 0; j < kHalfRun; ++j)
-    {
-      st[j] = s;
-      st[j + kHalfRun] = s2;
-      const bool a = triple(s, x, y, z), a2 = triple(s2, x, y, z);
-      acc |= (a ? 1u : 0u) << j | (a2 ? 1u : 0u) << (j + kHalfRun);
-      c += (a ? 1u : 0u) + (a2 ? 1u : 0u);
-    }
-  }
+    acc = thread_flags<true>(in.s0, st);
+  const uint32_t c = (uint32_t)__popc(acc);
   // exclusive scan of c across the workgroup
   const uint32_t lane = threadIdx.x & 63;
   uint32_t inc = c;
@@ -310,12 +380,13 @@ __device__ __forceinline__ void emit_block(uint32_t b, uint64_t off, const uint3
   uint32_t wbase = 0;
   for (uint32_t w = 0; w < (threadIdx.x >> 6); ++w) wbase += wsum[w];
   uint32_t li = wbase + (inc - c);                                               // block-local rank
+  // trace need - 1's block-local rank when this block holds it (the stream state after its triple is the next frame's)
+  const uint32_t fin = last == need - 1 ? cnt - 1 : ~0u;
 #pragma unroll
   for (int j = 0; j < kTriplesPerThread; ++j)
     if ((acc >> j) & 1u)
     {
-      // trace need-1's triple: the stream state after it is the next frame's state
-      if (off + li == need - 1) *next_seed = lcg_step(lcg_step(lcg_step(st[j])));
+      if (li == fin) *next_seed = lcg_step(lcg_step(lcg_step(st[j])));
       if (li < cnt) sst[li] = st[j];
       ++li;
     }
@@ -333,6 +404,9 @@ __global__ __launch_bounds__(kRngBlock) void rng_emit(const uint32_t *seed, cons
 {
   __shared__ uint32_t sst[kTriplesPerBlock];
   __shared__ uint32_t wsum[kRngBlock / 64];
+  __shared__ uint32_t wpart[kRngBlock / 64];
+  // the block's own inputs first: their loads are in flight with the prefix sum's
+  const EmitIn in = emit_in(blockIdx.x, seed, jump, blk_cnt, masks);
   // this block's first trace: the accept counts of the blocks before it, summed by the block (the count
   // array is a few KB and L2-resident, so no separate scan pass)
   uint32_t part = 0;
@@ -359,15 +433,14 @@ __global__ __launch_bounds__(kRngBlock) void rng_emit(const uint32_t *seed, cons
     for (uint32_t k = threadIdx.x; k < blockIdx.x; k += kRngBlock) part += blk_cnt[k];
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
-  __shared__ uint64_t s_off;
-  if (threadIdx.x == 0) s_off = 0;
+  if ((threadIdx.x & 63) == 0) wpart[threadIdx.x >> 6] = part;
   __syncthreads();
-  if ((threadIdx.x & 63) == 0) atomicAdd((unsigned long long *)&s_off, (unsigned long long)part);
-  __syncthreads();
-  const uint64_t off = s_off;
+  uint64_t off = 0;  // (a launch has fewer than 2^32 traces, so each wave's partial fits 32 bits)
+#pragma unroll
+  for (int w = 0; w < kRngBlock / 64; ++w) off += wpart[w];
   // the last block flags a stream too short for the frame (host: RFX_ERR_RNG)
-  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0 && off + blk_cnt[blockIdx.x] < need) *err = 1;
-  emit_block(blockIdx.x, off, seed, jump, blk_cnt, masks, need, rd_state, next_seed, flt, sst, wsum);
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0 && off + in.cnt < need) *err = 1;
+  emit_block(off, in, masks != nullptr, need, rd_state, next_seed, flt, sst, wsum);
 }
 
 // Band emit (multi-GPU band partition): only the blocks holding the band's traces [flt.lo, flt.hi), and the block of
@@ -557,7 +630,8 @@ __global__ __launch_bounds__(kRngBlock) void rng_emit_band(const uint32_t *seed,
   {
     const uint32_t b = j <= last - first ? first + j : fin;
     if (b >= nblk) break;  // (a stream too short for the frame leaves the range unset: the error flag is raised)
-    emit_block(b, off[b], seed, jump, blk_cnt, masks, need, rd_state, next_seed, flt, sst, wsum);
+    emit_block(off[b], emit_in(b, seed, jump, blk_cnt, masks), masks != nullptr, need, rd_state, next_seed, flt, sst,
+               wsum);
     __syncthreads();  // sst / wsum are reused by the next block
   }
 }
@@ -617,22 +691,9 @@ __global__ __launch_bounds__(kRngBlock) void rng_fused(const uint32_t *seed, con
   b = s_b;
 #endif
   // the block's triples, generated once: the state before each and its accept flag (rng_count / emit_block)
-  uint32_t s = thread_state(*seed, jump, b, threadIdx.x);
-  uint32_t s2 = kHalfJump.a * s + kHalfJump.c;
   uint32_t st[kTriplesPerThread];
-  uint32_t acc = 0, c = 0;
-  {
-    float x, y, z;
-#pragma unroll
-    for (int j = 0; j < kHalfRun; ++j)
-    {
-      st[j] = s;
-      st[j + kHalfRun] = s2;
-      const bool a = triple(s, x, y, z), a2 = triple(s2, x, y, z);
-      acc |= (a ? 1u : 0u) << j | (a2 ? 1u : 0u) << (j + kHalfRun);
-      c += (a ? 1u : 0u) + (a2 ? 1u : 0u);
-    }
-  }
+  const uint32_t acc = thread_flags<true>(thread_state(*seed, jump, b, threadIdx.x), st);
+  const uint32_t c = (uint32_t)__popc(acc);
   const uint32_t lane = threadIdx.x & 63;
   uint32_t inc = c;
 #pragma unroll
@@ -708,10 +769,7 @@ __global__ __launch_bounds__(kRngBlock) void rng_fused(const uint32_t *seed, con
     uint32_t part = 0;
     for (uint32_t pb = 0; pb < b; ++pb)
     {
-      uint32_t q = thread_state(*seed, jump, pb, threadIdx.x), q2 = kHalfJump.a * q + kHalfJump.c;
-      float x, y, z;
-#pragma unroll
-      for (int k = 0; k < kHalfRun; ++k) part += (triple(q, x, y, z) ? 1u : 0u) + (triple(q2, x, y, z) ? 1u : 0u);
+      part += (uint32_t)__popc(thread_flags<false>(thread_state(*seed, jump, pb, threadIdx.x), nullptr));
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
@@ -730,11 +788,12 @@ __global__ __launch_bounds__(kRngBlock) void rng_fused(const uint32_t *seed, con
   if (off >= need) return;
   const uint32_t cnt = (uint32_t)min((uint64_t)tot, need - off);
   uint32_t li = wbase + (inc - c);                                               // block-local rank
+  const uint32_t fin = off + cnt == need ? cnt - 1 : ~0u;  // trace need - 1's block-local rank, if this block holds it
 #pragma unroll
   for (int j = 0; j < kTriplesPerThread; ++j)
     if ((acc >> j) & 1u)
     {
-      if (off + li == need - 1) *next_seed = lcg_step(lcg_step(lcg_step(st[j])));
+      if (li == fin) *next_seed = lcg_step(lcg_step(lcg_step(st[j])));
       if (li < cnt) sst[li] = st[j];
       ++li;
     }

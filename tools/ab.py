@@ -99,6 +99,9 @@ VARIANTS = {
     "fmax512": ["RFX_RNG_FUSED_MAX_BLOCKS=512"],
     "divsel1": ["RFX_DIV_SEL=1"],
     "divfast2": ["RFX_DIV_FAST=2"],
+    "intacc0": ["RFX_RNG_INT_ACCEPT=0"],
+    "fmax1024": ["RFX_RNG_FUSED_MAX_BLOCKS=1024"],
+    "fmax4096": ["RFX_RNG_FUSED_MAX_BLOCKS=4096"],
 }
 
 
