@@ -101,3 +101,36 @@ def test_pre_pass_code_has_no_byte_dot_products(tmp_path):
     asm = out.read_text()
     assert "v_mad_u32_u24" in asm
     assert "v_dot4_u32_u8" not in asm
+
+
+def _jump(n):
+    a, c, A, C = 214013, 2531011, 1, 0
+    while n:
+        if n & 1:
+            A, C = (a * A) & 0xFFFFFFFF, (a * C + c) & 0xFFFFFFFF
+        c, a, n = (a * c + c) & 0xFFFFFFFF, (a * a) & 0xFFFFFFFF, n >> 1
+    return np.uint32(A), np.uint32(C)
+
+
+def test_full_frame_streams_reach_the_shell():
+    """The float fallback is not dead code for the parity tests: the stream a renderer starts from its default seed
+    (1350490027, the C3 / C4 full-frame cases' frame 0) puts triples on the shell within the C3 frame's ~15.8 M
+    triples, so those frames' hashes check it.  Thread starts by doubling (jumps of 48 draws), then 16 triples each."""
+    seed, nthreads = 1350490027, 4054 * 256  # C3: 4,054 pre-pass blocks of 256 threads
+    S = np.empty(nthreads, np.uint32)
+    S[0] = seed
+    k = 1
+    with np.errstate(over="ignore"):
+        while k < nthreads:
+            A, C = _jump(48 * k)
+            m = min(k, nthreads - k)
+            S[k:k + m] = A * S[:m] + C
+            k *= 2
+        s, shell = S.copy(), 0
+        for _ in range(16):
+            n = np.zeros(nthreads, np.int64)
+            for _ in range(3):
+                s = np.uint32(214013) * s + np.uint32(2531011)
+                n += (2 * ((s >> 16) & 0x7FFF).astype(np.int64) - 32767) ** 2
+            shell += int((np.abs(n - R2) <= _device_shell()).sum())
+    assert shell >= 10, shell  # 19 for kSphereShell = 1024
