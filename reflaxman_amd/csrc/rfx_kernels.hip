@@ -335,7 +335,7 @@ __device__ __forceinline__ EmitIn emit_in(uint32_t b, const uint32_t *seed, cons
 }
 
 // One block of the emit: block b's accepted triples are the traces [off, off + in.cnt).  Every thread of the workgroup
-// calls it with the same b and off.  have_masks: in.mask holds the thread's accept flags (rng_count's), so only the LCG
+// calls it with the same off and b's inputs (emit_in).  have_masks: in.mask holds the thread's accept flags (rng_count's), so only the LCG
 // states are regenerated.
 __device__ __forceinline__ void emit_block(uint64_t off, const EmitIn &in, bool have_masks, uint64_t need,
                                            uint32_t *rd_state, uint32_t *next_seed, const EmitFilter &flt,
