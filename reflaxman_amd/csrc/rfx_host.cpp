@@ -481,8 +481,17 @@ constexpr size_t kPrimLargeWords = 12;  // per wave tile, large scenes (rfx_trac
 #ifndef RFX_PARK_AFTER
 #define RFX_PARK_AFTER 2  // large-scene plain frames: segments before a live trace is parked for the bounce kernel
 #endif
+// The tile sort: on the trace launch's own stream (RFX_TILE_SORT_MAIN=0: on a side stream beside the next frame's RNG
+// pre-pass, joined by an event pair) every RFX_TILE_SORT_EVERY-th launch.  Trace time against raster order (tools/ab.py,
+// C3): every launch -7.5%, every 4th -9.4%, every 16th -9.8%.  The side stream hid the sort but not its events: a kernel
+// trace shows ~20 us between two traces on a sorting frame beyond a plain one (fork before the count, join before the
+// trace).  Frame ms, interleaved A/B (profiles/r06/ab/*_tile_sort_r6q.jsonl): C3 every 4th beside 0.6556, on the stream
+// 0.6526, every 16th beside 0.6513, every 16th on the stream 0.6485 (-1.1%); C2 d4 -0.9%, the 4x4 screenshot -0.4%.
+#ifndef RFX_TILE_SORT_MAIN
+#define RFX_TILE_SORT_MAIN 1
+#endif
 #ifndef RFX_TILE_SORT_EVERY
-#define RFX_TILE_SORT_EVERY 4  // tools/ab.py, C3: every launch -7.5% trace time vs raster order, every 4th -9.4%, every 16th -9.8%
+#define RFX_TILE_SORT_EVERY 16
 #endif
 #ifndef RFX_LAUNCH_TRACES
 #define RFX_LAUNCH_TRACES (1ull << 30)  // traces per launch of a split frame (rfx_renderer_set_launch_traces)
@@ -545,9 +554,10 @@ struct rfx_renderer {
   uint32_t *d_jump = nullptr;  // LCG jump table for blk_cap blocks (rng_jump_table)
   // host staging for rfx_render_frame_host
   float *d_img = nullptr; uint32_t *d_argb = nullptr; uint64_t *d_cnt = nullptr; size_t img_cap = 0;
-  // tile schedule (rfx_renderer_set_tile_order): each trace launch records per-tile clock costs; a one-workgroup
-  // kernel on tile_stream sorts them into the next launch's order (longest first) while the next frame's RNG
-  // pre-pass runs; the next trace launch waits on tile_join.  tile_n: tiles of the launch the order is for.
+  // tile schedule (rfx_renderer_set_tile_order): a recording trace launch writes per-tile clock costs; a counting
+  // sort (lpt_*) turns them into the next launch's order (longest first), on the launch's stream (or, RFX_TILE_SORT_MAIN
+  // = 0, on tile_stream while the next frame's RNG pre-pass runs); a launch on another stream waits on tile_join.
+  // tile_n: tiles of the launch the order is for.
   int tile_mode = RFX_TILE_ORDER_DEFAULT;
   uint32_t *d_tile_cost = nullptr, *d_tile_order = nullptr, *d_tile_scratch = nullptr;
   uint32_t tile_cap = 0, tile_n = 0;
@@ -1393,6 +1403,7 @@ static int tile_schedule(rfx_renderer *r, FrameParams &P, hipStream_t st, uint64
   if (n > r->tile_cap)
   {
     HIP_CHECK(hipStreamSynchronize(r->tile_stream));  // a pending sort may still read the old buffers
+    if (r->tile_pending) HIP_CHECK(hipEventSynchronize(r->tile_join));  // (RFX_TILE_SORT_MAIN: on the launch's stream)
     HIP_CHECK(hipStreamSynchronize(st));
     (void)hipFree(r->d_tile_cost); (void)hipFree(r->d_tile_order);
     r->d_tile_cost = r->d_tile_order = nullptr;
@@ -1642,13 +1653,21 @@ static int trace_frame(rfx_renderer *r, FramePlan &pl, const uint32_t *rd, float
   }
   if (record)
   {
+#if RFX_TILE_SORT_MAIN
+    // sort this launch's tile costs into the next launch's order on the launch's own stream: no cross-stream events
+    // (tile_join only for a later launch on another stream)
+    HIP_CHECK(launch_tile_order(r->d_tile_cost, trace_tiles(P), r->d_tile_order, r->d_tile_scratch, st));
+    HIP_CHECK(hipEventRecord(r->tile_join, st));
+    r->tile_waited = st;
+#else
     // sort this launch's tile costs into the next launch's order beside the next frame's pre-pass
     HIP_CHECK(hipEventRecord(r->tile_fork, st));
     HIP_CHECK(hipStreamWaitEvent(r->tile_stream, r->tile_fork, 0));
     HIP_CHECK(launch_tile_order(r->d_tile_cost, trace_tiles(P), r->d_tile_order, r->d_tile_scratch, r->tile_stream));
     HIP_CHECK(hipEventRecord(r->tile_join, r->tile_stream));
-    r->tile_pending = true;
     r->tile_waited = nullptr;
+#endif
+    r->tile_pending = true;
     r->tile_n = trace_tiles(P);
     r->tile_key = key;
   }

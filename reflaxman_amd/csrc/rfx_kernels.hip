@@ -39,26 +39,30 @@ __global__ __launch_bounds__(kLptThreads) void lpt_hist(const uint32_t *cost, ui
   for (uint32_t b = threadIdx.x; b < kLptBuckets; b += kLptThreads) hist[blockIdx.x * kLptBuckets + b] = h[b];
 }
 
-// hist[g][b] <- first slot of group g's tiles of bucket b (buckets in order, groups in order within one)
+// hist[g][b] <- first slot of group g's tiles of bucket b (buckets in order, groups in order within one).  The bucket
+// totals' exclusive scan runs across the lanes (wave shuffles, then the four waves' totals), not in one thread: a
+// serial pass over 256 LDS words held the sort's critical path (18 us of the tile sort's 28, rocprofv3).
 __global__ __launch_bounds__(kLptBuckets) void lpt_scan(uint32_t *hist)
 {
-  __shared__ uint32_t tot[kLptBuckets];
-  const uint32_t b = threadIdx.x;
+  __shared__ uint32_t wtot[kLptBuckets / 64];
+  const uint32_t b = threadIdx.x, lane = b & 63u;
   uint32_t v[kLptGroups];  // all loads first (independent), then the running sum in registers
 #pragma unroll
   for (int g = 0; g < kLptGroups; ++g) v[g] = hist[g * kLptBuckets + b];
   uint32_t run = 0;
 #pragma unroll
   for (int g = 0; g < kLptGroups; ++g) { const uint32_t c = v[g]; v[g] = run; run += c; }
-  tot[b] = run;
-  __syncthreads();
-  if (b == 0)
+  uint32_t inc = run;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1)
   {
-    uint32_t acc = 0;
-    for (int k = 0; k < kLptBuckets; ++k) { const uint32_t v = tot[k]; tot[k] = acc; acc += v; }
+    const uint32_t t = __shfl_up(inc, o, 64);
+    if (lane >= (uint32_t)o) inc += t;
   }
+  if (lane == 63u) wtot[b >> 6] = inc;
   __syncthreads();
-  const uint32_t base = tot[b];
+  uint32_t base = inc - run;
+  for (uint32_t w = 0; w < (b >> 6); ++w) base += wtot[w];
 #pragma unroll
   for (int g = 0; g < kLptGroups; ++g) hist[g * kLptBuckets + b] = v[g] + base;
 }

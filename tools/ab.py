@@ -100,6 +100,10 @@ VARIANTS = {
     "divsel1": ["RFX_DIV_SEL=1"],
     "divfast2": ["RFX_DIV_FAST=2"],
     "intacc0": ["RFX_RNG_INT_ACCEPT=0"],
+    "sortside4": ["RFX_TILE_SORT_MAIN=0", "RFX_TILE_SORT_EVERY=4"],
+    "sortside16": ["RFX_TILE_SORT_MAIN=0", "RFX_TILE_SORT_EVERY=16"],
+    "sortmain4": ["RFX_TILE_SORT_EVERY=4"],
+    "sort32": ["RFX_TILE_SORT_EVERY=32"],
     "fmax1024": ["RFX_RNG_FUSED_MAX_BLOCKS=1024"],
     "fmax4096": ["RFX_RNG_FUSED_MAX_BLOCKS=4096"],
 }
