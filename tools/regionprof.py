@@ -29,10 +29,13 @@ def main():
     ap.add_argument("--lib", default="librfx_prof.so")
     ap.add_argument("--regroup", type=int, default=None,
                     help="rfx_renderer_set_regroup setting (large scenes: 0, since only the plain kernel is instrumented)")
+    ap.add_argument("--prim", type=int, default=None,
+                    help="rfx_renderer_set_prim_masks mode (0: no per-view masks, what a moving camera renders with)")
     a = ap.parse_args()
     path = os.path.join(_build.LIBDIR, "diag", a.lib)
     scene = a.scene
-    r = ab.Runner("prof", path, scenes.get_scene(scene), a.width, a.height, a.depth, 1350490027, regroup=a.regroup)
+    r = ab.Runner("prof", path, scenes.get_scene(scene), a.width, a.height, a.depth, 1350490027, regroup=a.regroup,
+                  prim=a.prim)
     r.render(2)
     assert r.L.rfx_synchronize(r.r) == 0
     buf = (C.c_ulonglong * 16)()
@@ -55,7 +58,7 @@ def main():
         cull["closest_large"] = {"bundles": v[0], "usable": round(v[1] / n, 3), "live_lanes": round(v[2] / n, 1),
                                  "kept_chunks": round(v[3] / n, 2), "kept_spheres": round(v[4] / n, 1),
                                  "pair_tests": round(v[5] / n, 1)}
-    print(json.dumps({"scene": scene, "lib": os.path.basename(path), "cycles": {k: int(v) for k, v in zip(REGIONS, buf[:8])},
+    print(json.dumps({"scene": scene, "lib": os.path.basename(path), "prim_masks": a.prim, "cycles": {k: int(v) for k, v in zip(REGIONS, buf[:8])},
                       "wave_executions": {k: int(v) for k, v in zip(REGIONS, buf[8:])},
                       "share_of_trace": {k: round(v / tot, 4) for k, v in zip(REGIONS, buf[:8])},
                       "cull": cull}))
