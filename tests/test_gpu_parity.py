@@ -641,3 +641,68 @@ def test_primary_masks_full_size_frames():
         hashes[mode] = out
     assert hashes[0][0] == (c["sha_f32"], c["sha_argb"])
     assert hashes[0] == hashes[1]
+
+
+def _float_accept_counts(seed, nthreads):
+    """Per pre-pass thread (16 triples, 48 draws from its jumped start), the accepted triples by the reference's float
+    test (Vector3.cpp:182-185: x = float(k) / (float(0x7FFF) / 2) - 1, rejected when x*x + y*y + z*z > 1), and the
+    number of triples that fall on the integer test's shell (where rng_count runs the float test itself)."""
+    def jump(n):
+        a, c, A, Cc = 214013, 2531011, 1, 0
+        while n:
+            if n & 1:
+                A, Cc = (a * A) & 0xFFFFFFFF, (a * Cc + c) & 0xFFFFFFFF
+            c, a, n = (a * c + c) & 0xFFFFFFFF, (a * a) & 0xFFFFFFFF, n >> 1
+        return np.uint32(A), np.uint32(Cc)
+    half = np.float32(np.float32(0x7FFF) / np.float32(2))
+    x_of = (np.arange(1 << 15, dtype=np.float32) / half - np.float32(1)).astype(np.float32)
+    S = np.empty(nthreads, np.uint32)
+    S[0] = seed
+    k = 1
+    cnt = np.zeros(nthreads, np.int64)
+    shell = 0
+    with np.errstate(over="ignore"):
+        while k < nthreads:
+            A, Cc = jump(48 * k)
+            m = min(k, nthreads - k)
+            S[k:k + m] = A * S[:m] + Cc
+            k *= 2
+        s = S
+        for _ in range(16):
+            acc = np.zeros(nthreads, np.float32)
+            n = np.zeros(nthreads, np.int64)
+            for d in range(3):
+                s = np.uint32(214013) * s + np.uint32(2531011)
+                kk = ((s >> 16) & 0x7FFF).astype(np.int64)
+                x = x_of[kk]
+                acc = (acc + x * x).astype(np.float32) if d else (x * x).astype(np.float32)
+                n += (2 * kk - 32767) ** 2
+            cnt += ~(acc > np.float32(1))
+            shell += int((np.abs(n - 32767 * 32767) <= 1024).sum())
+    return cnt, shell
+
+
+def test_rng_count_blocks_equal_the_float_test():
+    """rng_count's per-block accept counts (rfx_frame_rng_count, one slice) for the C3 frame from the default seed against
+    the reference's float test restated in numpy: every block of the launch (about 4,100) equal, with triples on the
+    integer test's shell among them (so its float fallback is what decided those)."""
+    import ctypes as C
+    from reflaxman_amd import _lib
+    from reflaxman_amd.render import Renderer, build_scene, make_frame
+    L = _lib.load()
+    s, cam = build_scene(scene("synth16"))
+    rr = Renderer(sphere_seed=1350490027)
+    rr.set_scene(s)
+    f = make_frame(cam, 3840, 2160, 8)
+    nblk = C.c_uint64()
+    _lib.check(L.rfx_frame_rng_blocks(rr._h, C.byref(f), 1, C.byref(nblk)))
+    d_cnt = C.c_void_p()
+    _lib.check(L.rfx_device_alloc(rr._h, nblk.value * 4, C.byref(d_cnt)))
+    _lib.check(L.rfx_frame_rng_count(rr._h, C.byref(f), 0, 1, d_cnt, None))
+    got = np.empty(nblk.value, np.uint32)
+    _lib.check(L.rfx_memcpy_d2h(rr._h, got.ctypes.data_as(C.c_void_p), d_cnt, got.nbytes))
+    rr.close()
+    per_thread, shell = _float_accept_counts(1350490027, nblk.value * 256)
+    want = per_thread.reshape(-1, 256).sum(1)
+    assert nblk.value >= 4054 and shell >= 10
+    assert np.array_equal(got.astype(np.int64), want)
