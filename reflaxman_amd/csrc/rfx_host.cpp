@@ -502,7 +502,9 @@ constexpr size_t kPrimLargeWords = 12;  // per wave tile, large scenes (rfx_trac
 constexpr uint64_t kMaxLaunchTraces = 1ull << 31;  // the band scan's 32-bit offsets (rfx_kernels.hip rng_band_range)
 #ifndef RFX_SCAN_EMIT_BLOCKS
 // one-device emits of more RNG blocks than this scan the counts first (rng_band_range) instead of summing them per
-// block (rng_emit: O(nblk^2) reads); C3 has 4,054 blocks, the 4x4 screenshot frame 16,219
+// block (rng_emit: O(nblk^2) reads); C3 has 4,066 blocks, the 4x4 screenshot frame 16,219.  Re-checked with the
+// multi-workgroup tile scan (round 6, profiles/r06/ab/*_scan_emit_threshold_r6x.jsonl): a threshold of 4,096 makes the C4
+// and screenshot pre-passes 0.093 -> 0.104 ms, so the per-block sums stay up to 16,384 blocks
 #define RFX_SCAN_EMIT_BLOCKS 16384
 #endif
 struct rfx_renderer {

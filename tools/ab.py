@@ -100,6 +100,7 @@ VARIANTS = {
     "divsel1": ["RFX_DIV_SEL=1"],
     "divfast2": ["RFX_DIV_FAST=2"],
     "intacc0": ["RFX_RNG_INT_ACCEPT=0"],
+    "se4096": ["RFX_SCAN_EMIT_BLOCKS=4096"],
     "sortside4": ["RFX_TILE_SORT_MAIN=0", "RFX_TILE_SORT_EVERY=4"],
     "sortside16": ["RFX_TILE_SORT_MAIN=0", "RFX_TILE_SORT_EVERY=16"],
     "sortmain4": ["RFX_TILE_SORT_EVERY=4"],
